@@ -1,0 +1,23 @@
+# Builds the MI355X (gfx950) shared library behind include/sv2n.h and the
+# oracle's C helpers.  `python -c "import __graft_entry__ as g; g.build()"`
+# runs the same recipe.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Wall -Wno-unused-result
+SRC := $(wildcard spotv2net_amd/csrc/*.hip)
+OBJ := $(patsubst spotv2net_amd/csrc/%.hip,build/%.o,$(SRC))
+LIB := spotv2net_amd/libsv2n.so
+
+all: $(LIB)
+
+build/%.o: spotv2net_amd/csrc/%.hip spotv2net_amd/csrc/sv2n_common.h include/sv2n.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean

@@ -1,0 +1,147 @@
+/*
+ * sv2n.h — C-ABI of the SpotV2Net GAT hot path on MI355X (gfx950).
+ *
+ * This is the drop-in boundary for the edge-featured GATConv layer that the
+ * reference stacks in GATModel (reference utils/models.py:86-117, called once
+ * per layer at utils/models.py:146).  The reference binds that layer through
+ * Python to the third-party PyG 2.3.0 `torch_geometric.nn.GATConv`
+ * (imported at utils/models.py:11; pinned by prose at README.md:88), which is
+ * not vendored.  Each entry point below replaces one group of PyG/ATen ops of
+ * `GATConv.forward` / its autograd backward:
+ *
+ *   sv2n_edge_logits_fwd   lin_edge(edge_attr) · att_edge            (row a8)
+ *                          folded to edge_attr · W̃ for ALL layers in one pass
+ *   sv2n_gat_attn_fwd      a_s[src]+a_d[dst]+a_e, add_self_loops('mean'),
+ *                          leaky_relu, softmax(index=dst), dropout, message
+ *                          passing scatter-add, concat/mean, bias, activation
+ *                          (rows a7, a9, a10, a11 and GATModel's act, a4)
+ *   sv2n_gat_attn_bwd      autograd backward of all of the above     (row a12)
+ *   sv2n_edge_logits_bwd   d(W̃) = edge_attrᵀ · d(a_e)                (row a12)
+ *   sv2n_gemm_f32          the dense projections lin_src(x) (row a6) and its
+ *                          backward products, on f32-input MFMA
+ *   sv2n_block_rowmask     edge_index -> per-target source bitmask for graph
+ *                          batches whose edges are not in canonical order
+ *
+ * Conventions
+ *  - Every pointer argument is a DEVICE pointer unless the comment says
+ *    "host".  The caller owns and pre-allocates every buffer; no entry point
+ *    allocates, frees or synchronises.  All work is enqueued on `stream`, so
+ *    the calls are capturable into a hipGraph.
+ *  - Return value: 0 on success, < 0 for an argument error (see
+ *    sv2n_strerror), > 0 is a hipError_t from the launch.
+ *  - Graph batches are a disjoint union of `num_graphs` graphs with `n`
+ *    nodes each (PyG Batch layout): node v of graph g is
+ *    row g*n+v.  Edge rows follow `edge_index` ([2, E], int64, row 0 =
+ *    source j, row 1 = target i).  When `edge_index` is NULL the canonical
+ *    CovarianceLaggedDataset order is implied (reference
+ *    utils/dataset.py:212-226: the n(n-1)/2 row-major upper-triangle pairs,
+ *    then the same pairs swapped), described by `canon` ([n(n-1)] uint16,
+ *    entry = target<<8 | source).
+ *  - Dense attention layout ("AE"): per layer, float [num_graphs][n][n][H],
+ *    entry [g][i][j][h] = edge logit of edge j->i for head h.  The diagonal
+ *    (self loop) is never stored: the attention kernel derives it as the
+ *    mean over i's incoming edges, which is PyG's add_self_loops
+ *    fill_value='mean' pushed through the linear edge projection.
+ *  - Activation codes: 0 identity, 1 relu, 2 tanh, 3 sigmoid
+ *    (reference utils/models.py:125-130).
+ */
+#ifndef SV2N_H
+#define SV2N_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SV2N_ABI_VERSION 1
+#define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
+#define SV2N_MAX_N 32       /* nodes per graph on the dense-block path     */
+#define SV2N_MAX_HEADS 8    /* attention heads per layer                   */
+
+/* argument errors (negative return codes) */
+#define SV2N_ERR_ARG       (-1)  /* null pointer / non-positive size        */
+#define SV2N_ERR_SHAPE     (-2)  /* unsupported n, heads, layers, widths     */
+#define SV2N_ERR_ALIGN     (-3)  /* pointer or leading dim not 16-B aligned  */
+#define SV2N_ERR_WORKSPACE (-4)  /* workspace too small                      */
+
+int sv2n_abi_version(void);
+const char* sv2n_strerror(int code);
+
+/* Edge logits for L layers at once (replaces PyG GATConv.edge_update's
+ * `lin_edge(edge_attr).view(-1,H,C)*att_edge).sum(-1)`).
+ *   edge_attr [E][D] row-major, 16-B aligned base.
+ *   wfold     [D][hl_pad] with column l*H+h = Σ_c W_edge[l][h*C+c][:]·att_edge[l][h][c];
+ *             hl_pad ∈ {4,8,16,32} and L*H <= hl_pad (padding columns are ignored).
+ *   ae_layers host array of L device pointers, each [num_graphs][n][n][H].
+ * Self loops present in edge_index are skipped (PyG remove_self_loops). */
+int sv2n_edge_logits_fwd(const float* edge_attr, int64_t num_edges, int edge_dim,
+                         const int64_t* edge_index, const uint16_t* canon,
+                         const float* wfold, int hl_pad,
+                         float* const* ae_layers, int num_layers, int heads,
+                         int64_t num_graphs, int n, hipStream_t stream);
+
+/* dW̃ = edge_attrᵀ·dAE over all layers: dwfold [D][hl_pad] (overwritten).
+ * workspace: sv2n_edge_logits_bwd_workspace(edge_dim, hl_pad) floats. */
+int64_t sv2n_edge_logits_bwd_workspace(int edge_dim, int hl_pad);
+int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, int edge_dim,
+                         const int64_t* edge_index, const uint16_t* canon,
+                         const float* const* dae_layers, int num_layers, int heads,
+                         int64_t num_graphs, int n,
+                         float* workspace, int64_t workspace_floats,
+                         float* dwfold, int hl_pad, hipStream_t stream);
+
+/* Fused per-graph attention forward for one layer.
+ *   xs      [N][ldx]: columns [0,H*C) = lin_src(x), [H*C, H*C+H) = a_src,
+ *           [H*C+H, H*C+2H) = a_dst (the projection GEMM emits all three).
+ *   ae      [num_graphs][n][n][H] or NULL (edge_attr=None: no edge term).
+ *   rowmask [N] uint32 (bit j of row g*n+i: edge j->i present) or NULL for
+ *           complete graphs.
+ *   bias    [H*C] (concat) or [C] (mean).
+ *   keep    [num_graphs][H][n][n] uint8 attention-dropout keep mask or NULL;
+ *           kept probabilities are scaled by keep_scale.
+ *   y       [N][concat ? H*C : C] = act(concat|mean(Σ_j p_ij·xs_j) + bias).
+ *   psave   [num_graphs][H][n][n] softmax probabilities (pre-dropout) whose
+ *           sign bit records leaky_relu's negative side (for the backward). */
+int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, const uint32_t* rowmask,
+                      const float* bias, const uint8_t* keep, float keep_scale,
+                      float* y, float* psave,
+                      int64_t num_graphs, int n, int heads, int channels, int concat,
+                      int act, float negative_slope, hipStream_t stream);
+
+/* Backward of sv2n_gat_attn_fwd.
+ *   dy, y   [N][OC] (OC = concat ? H*C : C); y is the forward output.
+ *   dxs     [N][ldx] gradient w.r.t. xs (all ldx columns written; padding 0).
+ *   dae     [num_graphs][n][n][H] gradient w.r.t. ae (diagonal / absent 0), or
+ *           NULL when the forward ran without ae.
+ *   dbias_partial [num_graphs][OC] per-graph bias-gradient partial sums. */
+int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* xs, int ldx,
+                      const float* psave, const uint8_t* keep, float keep_scale,
+                      const uint32_t* rowmask, float* dxs, float* dae, float* dbias_partial,
+                      int64_t num_graphs, int n, int heads, int channels, int concat,
+                      int act, float negative_slope, hipStream_t stream);
+
+/* C[M][N] = Σ_k A(m,k)·B(n,k), f32 in / f32 accumulate on MFMA (exact f32).
+ *   A(m,k) = A[m*lda+k] if a_kmajor else A[k*lda+m]
+ *   B(n,k) = B[n*ldb+k] if b_kmajor else B[k*ldb+n]
+ *   C[m*ldc+n] is overwritten.
+ * Replaces the lin_src projection GEMM (row a6: a_kmajor = b_kmajor = 1) and
+ * its backward products dX (a_kmajor=1, b_kmajor=0) and dWᵀ (0, 0).
+ * workspace: sv2n_gemm_f32_workspace(M,N,K) floats (split-K partial slabs;
+ * 0 => may be NULL). */
+int64_t sv2n_gemm_f32_workspace(int64_t M, int64_t N, int64_t K);
+int sv2n_gemm_f32(int a_kmajor, int b_kmajor, const float* A, int64_t lda,
+                  const float* B, int64_t ldb, float* C, int64_t ldc,
+                  int64_t M, int64_t N, int64_t K,
+                  float* workspace, int64_t workspace_floats, hipStream_t stream);
+
+/* rowmask[t] |= 1<<(s - g*n) for every non-self edge s->t (rowmask must be
+ * zeroed by the caller).  Edges must stay inside their n-node block. */
+int sv2n_block_rowmask(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
+                       int n, uint32_t* rowmask, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SV2N_H */

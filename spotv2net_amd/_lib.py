@@ -1,0 +1,90 @@
+"""ctypes binding of the C-ABI in ``include/sv2n.h`` (``libsv2n.so``).
+
+This is the one place the Python host side touches native code.  The library
+is built in-tree (``make`` / ``__graft_entry__.build()``) for gfx950; if it is
+missing or stale the import fails loudly — there is no CPU or eager-PyTorch
+fallback for the hot path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsv2n.so")
+ABI_VERSION = 1
+
+_c_f = ctypes.POINTER(ctypes.c_float)
+_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_f32 = ctypes.c_float
+
+# name -> (restype, argtypes); mirrors include/sv2n.h
+_SIGNATURES = {
+    "sv2n_abi_version": (_i32, []),
+    "sv2n_strerror": (ctypes.c_char_p, [_i32]),
+    "sv2n_edge_logits_fwd": (_i32, [_p, _i64, _i32, _p, _p, _p, _i32, _p, _i32, _i32, _i64, _i32, _p]),
+    "sv2n_edge_logits_bwd_workspace": (_i64, [_i32, _i32]),
+    "sv2n_edge_logits_bwd": (_i32, [_p, _i64, _i32, _p, _p, _p, _i32, _i32, _i64, _i32, _p, _i64, _p,
+                                    _i32, _p]),
+    "sv2n_gat_attn_fwd": (_i32, [_p, _i32, _p, _p, _p, _p, _f32, _p, _p, _i64, _i32, _i32, _i32, _i32,
+                                 _i32, _f32, _p]),
+    "sv2n_gat_attn_bwd": (_i32, [_p, _p, _p, _i32, _p, _p, _f32, _p, _p, _p, _p, _i64, _i32, _i32,
+                                 _i32, _i32, _i32, _f32, _p]),
+    "sv2n_gemm_f32_workspace": (_i64, [_i64, _i64, _i64]),
+    "sv2n_gemm_f32": (_i32, [_i32, _i32, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
+    "sv2n_block_rowmask": (_i32, [_p, _i64, _i64, _i32, _p, _p]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+_lib = None
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load libsv2n.so once; raise NativeLibraryError if it is absent/stale."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            f"{LIB_PATH} not found: build it with `make` (hipcc --offload-arch=gfx950) or "
+            "`python -c 'import __graft_entry__ as g; g.build()'`. The SpotV2Net GAT hot path "
+            "has no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError => stale library
+        fn.restype = res
+        fn.argtypes = args
+    if lib.sv2n_abi_version() != ABI_VERSION:
+        raise NativeLibraryError(f"libsv2n ABI {lib.sv2n_abi_version()} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().sv2n_strerror(rc).decode()
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    arr = (ctypes.c_void_p * len(ptrs))()
+    for k, p in enumerate(ptrs):
+        arr[k] = p
+    return arr

@@ -1,0 +1,82 @@
+// Shared device helpers for the SpotV2Net MI355X kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include "sv2n.h"
+
+#define SV2N_PSTR 36  // padded LDS row stride (floats) of a 32-wide attention row:
+                      // 144 B keeps ds_read_b128 16-B aligned and spreads the
+                      // transposed ds_write_b32 of a 32-lane half over 8 banks.
+
+namespace sv2n {
+
+enum Act { ACT_ID = 0, ACT_RELU = 1, ACT_TANH = 2, ACT_SIGMOID = 3 };
+
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float z) {
+  if constexpr (ACT == ACT_RELU) return z > 0.f ? z : 0.f;
+  else if constexpr (ACT == ACT_TANH) return tanhf(z);
+  else if constexpr (ACT == ACT_SIGMOID) return 1.f / (1.f + expf(-z));
+  else return z;
+}
+
+// d act / d z expressed through the forward output y (torch's *_backward forms:
+// relu: y>0, tanh: 1-y^2, sigmoid: y(1-y)).
+template <int ACT>
+__device__ __forceinline__ float act_bwd(float dy, float y) {
+  if constexpr (ACT == ACT_RELU) return y > 0.f ? dy : 0.f;
+  else if constexpr (ACT == ACT_TANH) return dy * (1.f - y * y);
+  else if constexpr (ACT == ACT_SIGMOID) return dy * (1.f - y) * y;
+  else return dy;
+}
+
+// quad (4-lane) butterflies through DPP quad_perm: lane^1 and lane^2.
+__device__ __forceinline__ float dpp_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+
+// reductions across one 32-lane half of the wave (a padded attention row)
+__device__ __forceinline__ float red32_sum(float v) {
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+__device__ __forceinline__ float red32_max(float v) {
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+  return v;
+}
+
+// rows i of graph g: bit j set <=> edge j->i present (self loop excluded)
+__device__ __forceinline__ uint32_t row_bits(const uint32_t* rowmask, int64_t row, int n, int i) {
+  if (rowmask) return rowmask[row] & ~(1u << i);
+  const uint32_t all = (n >= 32) ? 0xffffffffu : ((1u << n) - 1u);
+  return all & ~(1u << i);
+}
+
+// edge e -> (graph g, target i, source j); false for self loops / out-of-block
+__device__ __forceinline__ bool decode_edge(int64_t e, const int64_t* __restrict__ ei, int64_t E,
+                                            const uint16_t* __restrict__ canon, int E0, int n,
+                                            int64_t B, int64_t& g, int& i, int& j) {
+  if (ei) {
+    const int64_t s = ei[e], t = ei[E + e];
+    if (s == t) return false;
+    g = t / n;
+    i = (int)(t - g * n);
+    const int64_t jj = s - g * n;
+    if (jj < 0 || jj >= n || g >= B || g < 0) return false;
+    j = (int)jj;
+    return true;
+  }
+  g = e / E0;
+  const uint16_t c = canon[e - g * E0];
+  i = c >> 8;
+  j = c & 0xFF;
+  return g < B;
+}
+
+}  // namespace sv2n

@@ -1,0 +1,359 @@
+// Edge-feature streaming kernels: the folded lin_edge·att_edge logits for all
+// GAT layers in ONE pass over edge_attr, and the matching weight gradient.
+//
+// Reference semantics (PyG 2.3.0 GATConv.edge_update, used by
+// utils/models.py:146 for every layer):
+//     a_e[e,h] = Σ_c (edge_attr[e] · W_edge[h*C+c,:]) * att_edge[h,c]
+// which is linear in edge_attr, so it is evaluated as edge_attr[e] · W̃[:,h]
+// with W̃ = fold(W_edge, att_edge) built by the host (autograd-tracked).  The
+// fold removes the [E, H*C] intermediate (737 MB per layer at batch 512) and
+// divides the flops by C; what is left is an HBM stream of edge_attr.
+//
+// HBM layout: edge_attr [E][D] fp32 row-major (D = 3*seq_length), read once
+// per pass with 16-B loads into an LDS chunk of 64 edges.
+#include "sv2n_common.h"
+
+namespace sv2n {
+
+constexpr int EDGE_CHUNK = 64;
+constexpr int EDGE_THREADS = 256;
+
+struct LayerPtrs { float* p[SV2N_MAX_LAYERS]; };
+struct LayerCPtrs { const float* p[SV2N_MAX_LAYERS]; };
+
+// ---------------------------------------------------------------------------
+// forward: ae[l][g][i][j][h] = edge_attr[e] · wfold[:, l*H+h]
+// one block = one chunk of 64 edges; thread (el = t/4, q = t%4) sums d ≡ q (mod 4)
+// for all hl_pad columns, quad-reduced through DPP, then written per layer.
+// ---------------------------------------------------------------------------
+template <int HLP>
+__global__ __launch_bounds__(EDGE_THREADS) void k_edge_fwd(
+    const float* __restrict__ ea, int64_t E, int D, const int64_t* __restrict__ ei,
+    const uint16_t* __restrict__ canon, int E0, const float* __restrict__ wf, LayerPtrs ae,
+    int L, int H, int64_t B, int n) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_wf = smem;                            // [D][HLP]
+  float* s_ea = smem + D * HLP;                  // [64][D]
+  float* s_out = s_ea + EDGE_CHUNK * D;          // [64][HLP]
+  __shared__ float* s_ptr[SV2N_MAX_LAYERS];
+
+  const int t = threadIdx.x;
+  const int64_t e0 = (int64_t)blockIdx.x * EDGE_CHUNK;
+  const int ne = (int)min((int64_t)EDGE_CHUNK, E - e0);
+  if (t < SV2N_MAX_LAYERS) {
+#pragma unroll
+    for (int l = 0; l < SV2N_MAX_LAYERS; ++l)
+      if (l == t) s_ptr[l] = ae.p[l];
+  }
+  {
+    const float4* w4 = reinterpret_cast<const float4*>(wf);
+    float4* sw4 = reinterpret_cast<float4*>(s_wf);
+    for (int k = t; k < D * HLP / 4; k += EDGE_THREADS) sw4[k] = w4[k];
+    const float* src = ea + e0 * D;  // 64*D*4 bytes per chunk -> 16-B aligned
+    const int nf = ne * D, nf4 = nf >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(s_ea);
+#pragma unroll 4
+    for (int k = t; k < nf4; k += EDGE_THREADS) d4[k] = s4[k];
+    for (int k = (nf4 << 2) + t; k < nf; k += EDGE_THREADS) s_ea[k] = src[k];
+  }
+  __syncthreads();
+
+  const int el = t >> 2, q = t & 3;
+  float acc[HLP];
+#pragma unroll
+  for (int k = 0; k < HLP; ++k) acc[k] = 0.f;
+  if (el < ne) {
+    const float* row = s_ea + el * D;
+    for (int d = q; d < D; d += 4) {
+      const float v = row[d];
+      const float4* w4 = reinterpret_cast<const float4*>(s_wf + d * HLP);
+#pragma unroll
+      for (int k4 = 0; k4 < HLP / 4; ++k4) {
+        const float4 w = w4[k4];
+        acc[4 * k4 + 0] = fmaf(v, w.x, acc[4 * k4 + 0]);
+        acc[4 * k4 + 1] = fmaf(v, w.y, acc[4 * k4 + 1]);
+        acc[4 * k4 + 2] = fmaf(v, w.z, acc[4 * k4 + 2]);
+        acc[4 * k4 + 3] = fmaf(v, w.w, acc[4 * k4 + 3]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < HLP; ++k) {
+    acc[k] += dpp_xor1(acc[k]);
+    acc[k] += dpp_xor2(acc[k]);
+  }
+  // lane q of the quad parks columns k ≡ q (mod 4) in LDS (compile-time index)
+#pragma unroll
+  for (int k = 0; k < HLP; ++k)
+    if ((k & 3) == q) s_out[el * HLP + k] = acc[k];
+  __syncthreads();
+
+  const int HL = L * H;
+  for (int idx = t; idx < ne * HL; idx += EDGE_THREADS) {
+    const int le = idx / HL, k = idx - le * HL;
+    int64_t g;
+    int i, j;
+    if (!decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) continue;
+    const int l = k / H, h = k - l * H;
+    s_ptr[l][((g * n + i) * n + j) * H + h] = s_out[le * HLP + k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward: partial[b][d][k] = Σ_{e in block b's chunks} edge_attr[e][d] * dae_e[k]
+// thread tile = 4 d x 4 k outer products, ES edge-groups per tile; grid-stride
+// over chunks, block-level reduction at the end, then k_reduce_partials sums
+// the per-block partials in a fixed order (deterministic).
+// ---------------------------------------------------------------------------
+template <int HLP>
+__global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
+    const float* __restrict__ ea, int64_t E, int D, int DP, const int64_t* __restrict__ ei,
+    const uint16_t* __restrict__ canon, int E0, LayerCPtrs dae, int L, int H, int64_t B, int n,
+    float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_ea = smem;                        // [64][DP]
+  float* s_dae = smem + EDGE_CHUNK * DP;     // [64][HLP]
+  __shared__ const float* s_ptr[SV2N_MAX_LAYERS];
+
+  const int t = threadIdx.x;
+  if (t < SV2N_MAX_LAYERS) {
+#pragma unroll
+    for (int l = 0; l < SV2N_MAX_LAYERS; ++l)
+      if (l == t) s_ptr[l] = dae.p[l];
+  }
+  const int KG = HLP / 4;
+  const int T = (DP / 4) * KG;  // thread tiles
+  const int ES = EDGE_THREADS / T;
+  const int tile = t % T, es = t / T;
+  const bool active = es < ES;
+  const int dg = tile / KG, kg = tile - dg * KG;
+  const int HL = L * H;
+
+  float acc[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+
+  const int64_t nchunks = (E + EDGE_CHUNK - 1) / EDGE_CHUNK;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t e0 = c * EDGE_CHUNK;
+    const int ne = (int)min((int64_t)EDGE_CHUNK, E - e0);
+    __syncthreads();  // previous chunk fully consumed
+    const float* src = ea + e0 * D;
+    const int nf = ne * D;
+    if (DP == D) {
+      const int nf4 = nf >> 2;
+      const float4* s4 = reinterpret_cast<const float4*>(src);
+      float4* d4 = reinterpret_cast<float4*>(s_ea);
+#pragma unroll 4
+      for (int k = t; k < nf4; k += EDGE_THREADS) d4[k] = s4[k];
+      for (int k = (nf4 << 2) + t; k < nf; k += EDGE_THREADS) s_ea[k] = src[k];
+    } else {
+      const int nf4 = nf >> 2;
+      const float4* s4 = reinterpret_cast<const float4*>(src);
+#pragma unroll 2
+      for (int k = t; k < nf4; k += EDGE_THREADS) {
+        const float4 v = s4[k];
+        const int f = k << 2;
+        int r = f / D, d = f - r * D;
+        s_ea[r * DP + d] = v.x; if (++d == D) { d = 0; ++r; }
+        s_ea[r * DP + d] = v.y; if (++d == D) { d = 0; ++r; }
+        s_ea[r * DP + d] = v.z; if (++d == D) { d = 0; ++r; }
+        s_ea[r * DP + d] = v.w;
+      }
+      for (int f = (nf4 << 2) + t; f < nf; f += EDGE_THREADS) {
+        const int r = f / D;
+        s_ea[r * DP + (f - r * D)] = src[f];
+      }
+      // zero the row padding so the 4-wide tiles read finite values
+      for (int k = t; k < ne * (DP - D); k += EDGE_THREADS) {
+        const int r = k / (DP - D);
+        s_ea[r * DP + D + (k - r * (DP - D))] = 0.f;
+      }
+    }
+    for (int idx = t; idx < ne * HLP; idx += EDGE_THREADS) {
+      const int le = idx / HLP, k = idx - le * HLP;
+      float v = 0.f;
+      int64_t g;
+      int i, j;
+      if (k < HL && decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) {
+        const int l = k / H, h = k - l * H;
+        v = s_ptr[l][((g * n + i) * n + j) * H + h];
+      }
+      s_dae[idx] = v;
+    }
+    __syncthreads();
+    if (active) {
+      for (int le = es; le < ne; le += ES) {
+        const float4 a = *reinterpret_cast<const float4*>(s_ea + le * DP + 4 * dg);
+        const float4 b = *reinterpret_cast<const float4*>(s_dae + le * HLP + 4 * kg);
+        const float av[4] = {a.x, a.y, a.z, a.w};
+        const float bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 4; ++y) acc[4 * x + y] = fmaf(av[x], bv[y], acc[4 * x + y]);
+      }
+    }
+  }
+  // block reduction over the ES edge groups (reuse the chunk buffer)
+  __syncthreads();
+  float* s_red = smem;  // [ES][T][16] <= 256*16 floats
+  if (active) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s_red[(es * T + tile) * 16 + k] = acc[k];
+  }
+  __syncthreads();
+  const int O = D * HLP;
+  for (int o = t; o < O; o += EDGE_THREADS) {
+    const int d = o / HLP, k = o - d * HLP;
+    const int tl = (d >> 2) * KG + (k >> 2);
+    const int sub = (d & 3) * 4 + (k & 3);
+    float s = 0.f;
+    for (int g2 = 0; g2 < ES; ++g2) s += s_red[(g2 * T + tl) * 16 + sub];
+    partial[(int64_t)blockIdx.x * O + o] = s;
+  }
+}
+
+__global__ void k_reduce_partials(const float* __restrict__ partial, int nparts, int O,
+                                  float* __restrict__ out) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= O) return;
+  float s = 0.f;
+  for (int b = 0; b < nparts; ++b) s += partial[(int64_t)b * O + o];
+  out[o] = s;
+}
+
+__global__ void k_block_rowmask(const int64_t* __restrict__ ei, int64_t E, int64_t N, int n,
+                                uint32_t* __restrict__ rowmask) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int64_t s = ei[e], t = ei[E + e];
+  if (s == t || t < 0 || t >= N) return;
+  const int64_t g = t / n;
+  const int64_t j = s - g * n;
+  if (j < 0 || j >= n) return;
+  atomicOr(&rowmask[t], 1u << (int)j);
+}
+
+}  // namespace sv2n
+
+// ============================ C-ABI ========================================
+using namespace sv2n;
+
+static constexpr int EDGE_BWD_GRID = 1024;
+
+template <typename K>
+static void raise_lds_limit(K kernel, size_t bytes) {
+  if (bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+}
+
+extern "C" int sv2n_edge_logits_fwd(const float* edge_attr, int64_t num_edges, int edge_dim,
+                                    const int64_t* edge_index, const uint16_t* canon,
+                                    const float* wfold, int hl_pad, float* const* ae_layers,
+                                    int num_layers, int heads, int64_t num_graphs, int n,
+                                    hipStream_t stream) {
+  if (!edge_attr || !wfold || !ae_layers || num_edges < 0 || edge_dim <= 0 || num_graphs <= 0)
+    return SV2N_ERR_ARG;
+  if (num_edges == 0) return 0;  // nothing to project (e.g. single-node graphs)
+  if (!edge_index && !canon) return SV2N_ERR_ARG;
+  if (n < 1 || n > SV2N_MAX_N || heads < 1 || heads > SV2N_MAX_HEADS || num_layers < 1 ||
+      num_layers > SV2N_MAX_LAYERS || num_layers * heads > hl_pad)
+    return SV2N_ERR_SHAPE;
+  if (((uintptr_t)edge_attr & 15) || ((uintptr_t)wfold & 15)) return SV2N_ERR_ALIGN;
+  if (num_edges == 0) return 0;
+  LayerPtrs lp{};
+  for (int l = 0; l < num_layers; ++l) {
+    if (!ae_layers[l]) return SV2N_ERR_ARG;
+    lp.p[l] = ae_layers[l];
+  }
+  const int E0 = n * (n - 1);
+  const int64_t nblk = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
+  const size_t lds = sizeof(float) * ((size_t)edge_dim * hl_pad + (size_t)EDGE_CHUNK * edge_dim +
+                                      (size_t)EDGE_CHUNK * hl_pad);
+  if (lds > 160 * 1024) return SV2N_ERR_SHAPE;
+#define SV2N_LAUNCH_EF(HLP)                                                                         \
+  case HLP:                                                                                       \
+    raise_lds_limit(k_edge_fwd<HLP>, lds);                                                        \
+    hipLaunchKernelGGL(k_edge_fwd<HLP>, dim3((unsigned)nblk), dim3(EDGE_THREADS), lds, stream,    \
+                       edge_attr, num_edges, edge_dim, edge_index, canon, E0, wfold, lp,          \
+                       num_layers, heads, num_graphs, n);                                         \
+    break;
+  switch (hl_pad) {
+    SV2N_LAUNCH_EF(4)
+    SV2N_LAUNCH_EF(8)
+    SV2N_LAUNCH_EF(16)
+    SV2N_LAUNCH_EF(32)
+    default:
+      return SV2N_ERR_SHAPE;
+  }
+#undef SV2N_LAUNCH_EF
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t sv2n_edge_logits_bwd_workspace(int edge_dim, int hl_pad) {
+  return (int64_t)EDGE_BWD_GRID * edge_dim * hl_pad;
+}
+
+extern "C" int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, int edge_dim,
+                                    const int64_t* edge_index, const uint16_t* canon,
+                                    const float* const* dae_layers, int num_layers, int heads,
+                                    int64_t num_graphs, int n, float* workspace,
+                                    int64_t workspace_floats, float* dwfold, int hl_pad,
+                                    hipStream_t stream) {
+  if (!edge_attr || !dae_layers || !dwfold || !workspace || num_edges < 0 || edge_dim <= 0 ||
+      num_graphs <= 0)
+    return SV2N_ERR_ARG;
+  if (!edge_index && !canon) return SV2N_ERR_ARG;
+  if (n < 1 || n > SV2N_MAX_N || heads < 1 || heads > SV2N_MAX_HEADS || num_layers < 1 ||
+      num_layers > SV2N_MAX_LAYERS || num_layers * heads > hl_pad)
+    return SV2N_ERR_SHAPE;
+  if ((uintptr_t)edge_attr & 15) return SV2N_ERR_ALIGN;
+  const int DP = (edge_dim + 3) & ~3;
+  if ((DP / 4) * (hl_pad / 4) > EDGE_THREADS) return SV2N_ERR_SHAPE;
+  LayerCPtrs lp{};
+  for (int l = 0; l < num_layers; ++l) {
+    if (!dae_layers[l]) return SV2N_ERR_ARG;
+    lp.p[l] = dae_layers[l];
+  }
+  const int O = edge_dim * hl_pad;
+  const int64_t nchunks = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(EDGE_BWD_GRID, nchunks));
+  if (workspace_floats < (int64_t)grid * O) return SV2N_ERR_WORKSPACE;
+  const int E0 = n * (n - 1);
+  size_t lds = sizeof(float) * ((size_t)EDGE_CHUNK * DP + (size_t)EDGE_CHUNK * hl_pad);
+  lds = std::max(lds, sizeof(float) * (size_t)EDGE_THREADS * 16);
+  if (lds > 160 * 1024) return SV2N_ERR_SHAPE;
+  if (num_edges == 0) return (int)hipMemsetAsync(dwfold, 0, sizeof(float) * O, stream);
+#define SV2N_LAUNCH_EB(HLP)                                                                       \
+  case HLP:                                                                                     \
+    raise_lds_limit(k_edge_bwd<HLP>, lds);                                                      \
+    hipLaunchKernelGGL(k_edge_bwd<HLP>, dim3(grid), dim3(EDGE_THREADS), lds, stream, edge_attr, \
+                       num_edges, edge_dim, DP, edge_index, canon, E0, lp, num_layers, heads,   \
+                       num_graphs, n, workspace);                                               \
+    break;
+  switch (hl_pad) {
+    SV2N_LAUNCH_EB(4)
+    SV2N_LAUNCH_EB(8)
+    SV2N_LAUNCH_EB(16)
+    SV2N_LAUNCH_EB(32)
+    default:
+      return SV2N_ERR_SHAPE;
+  }
+#undef SV2N_LAUNCH_EB
+  hipLaunchKernelGGL(k_reduce_partials, dim3((O + 255) / 256), dim3(256), 0, stream, workspace,
+                     grid, O, dwfold);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_block_rowmask(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
+                                  int n, uint32_t* rowmask, hipStream_t stream) {
+  if (!edge_index || !rowmask || num_edges < 0 || num_nodes <= 0) return SV2N_ERR_ARG;
+  if (n < 1 || n > SV2N_MAX_N) return SV2N_ERR_SHAPE;
+  if (num_edges == 0) return 0;
+  hipLaunchKernelGGL(k_block_rowmask, dim3((unsigned)((num_edges + 255) / 256)), dim3(256), 0,
+                     stream, edge_index, num_edges, num_nodes, n, rowmask);
+  return (int)hipGetLastError();
+}

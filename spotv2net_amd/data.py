@@ -1,0 +1,205 @@
+"""PyG-free graph containers and the SpotV2Net window-graph builder.
+
+* ``Data`` / ``Batch`` / ``collate`` reproduce the PyG ``Data`` + DataLoader
+  collation the reference relies on (5_train_SpotV2Net.py:90-91, :142-143):
+  x rows concatenated, ``edge_index`` shifted by each graph's node offset,
+  edge_attr and y_x concatenated, plus ``batch`` / ``ptr`` vectors.
+  Real PyG ``Batch`` objects also work with GATModel (duck-typed).
+* ``window_graph`` restates ``CovarianceLaggedDataset.process`` for one
+  window (reference utils/dataset.py:200-282): node features are the rows of
+  the S vol matrices (x[v, c*S+t] = vol_t[v, c]); edges are the canonical
+  fully connected order; edge_attr[e, k*S+t] = (covol_t[u,v], var_t[src],
+  var_t[tgt]) from the vol-of-vol matrix; y_x = diag(vol_{S}).
+* ``window_batch`` builds B such windows on the device in one shot from a
+  matrix series (the device-resident replacement of the per-window Python loop
+  and the pickled InMemoryDataset cache).
+* ``synthetic_series`` draws standardized symmetric matrices
+  ((G+Gᵀ)/2, G ~ N(0,1)) matching 4_standardize_data.py's zero-mean data.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from .layout import canonical_edge_index, canonical_pairs
+
+_FIELDS = ("x", "edge_index", "edge_attr", "y_x")
+
+
+class Data:
+    """Minimal ``torch_geometric.data.Data`` stand-in with the fields the
+    reference uses."""
+
+    def __init__(self, x=None, edge_index=None, edge_attr=None, y_x=None, **kw):
+        self.x = x
+        self.edge_index = edge_index
+        self.edge_attr = edge_attr
+        self.y_x = y_x
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+    @property
+    def num_nodes(self) -> int:
+        return int(self.x.size(0))
+
+    @property
+    def num_edges(self) -> int:
+        return int(self.edge_index.size(1))
+
+    def to(self, device, non_blocking: bool = False):
+        out = self.__class__.__new__(self.__class__)
+        for k, v in self.__dict__.items():
+            if isinstance(v, torch.Tensor):
+                v = v.to(device, non_blocking=non_blocking)
+            setattr(out, k, v)
+        out.__dict__.pop("sv2n_layout", None)
+        return out
+
+    def __repr__(self) -> str:
+        parts = [f"{k}={list(v.shape)}" for k, v in self.__dict__.items()
+                 if isinstance(v, torch.Tensor)]
+        return f"{self.__class__.__name__}({', '.join(parts)})"
+
+
+class Batch(Data):
+    """A disjoint union of graphs (PyG ``Batch`` layout)."""
+
+    @property
+    def num_graphs(self) -> int:
+        return int(self.ptr.numel() - 1)
+
+
+def collate(graphs: Sequence[Data]) -> Batch:
+    """PyG DataLoader collation: x/edge_attr/y_x concatenated, edge_index +=
+    cumulative node count, ``batch`` and ``ptr`` added."""
+    xs, eis, eas, ys, sizes = [], [], [], [], []
+    off = 0
+    for g in graphs:
+        xs.append(g.x)
+        eis.append(g.edge_index + off)
+        if g.edge_attr is not None:
+            eas.append(g.edge_attr)
+        if g.y_x is not None:
+            ys.append(g.y_x)
+        sizes.append(g.num_nodes)
+        off += g.num_nodes
+    dev = graphs[0].x.device
+    sizes_t = torch.tensor(sizes, dtype=torch.long, device=dev)
+    ptr = torch.zeros(len(sizes) + 1, dtype=torch.long, device=dev)
+    ptr[1:] = torch.cumsum(sizes_t, 0)
+    b = Batch(x=torch.cat(xs, 0), edge_index=torch.cat(eis, 1),
+              edge_attr=torch.cat(eas, 0) if eas else None,
+              y_x=torch.cat(ys, 0) if ys else None,
+              batch=torch.repeat_interleave(torch.arange(len(sizes), device=dev), sizes_t),
+              ptr=ptr)
+    if len(set(sizes)) == 1:
+        b.nodes_per_graph = sizes[0]
+    return b
+
+
+def window_graph(vol: torch.Tensor, volvol: torch.Tensor) -> Data:
+    """One CovarianceLaggedDataset sample from S+1 consecutive matrices.
+
+    vol, volvol: [S+1, n, n] (the window's S matrices plus the next one, whose
+    diagonal is the target).  Restates utils/dataset.py:202-282 step by step."""
+    S = vol.shape[0] - 1
+    n = vol.shape[1]
+    src, tgt = canonical_pairs(n)
+    src_t = torch.tensor(src, dtype=torch.long)
+    tgt_t = torch.tensor(tgt, dtype=torch.long)
+    P = len(src) // 2
+    xs, eas = [], []
+    for t in range(S):
+        cov = vol[t].float()
+        covol = volvol[t]
+        variances = torch.diagonal(covol).float()                  # :236
+        cv = covol[src_t[:P], tgt_t[:P]].float()                  # adj_matrix[mask] :243
+        cv = torch.cat([cv, cv])                                  # :245
+        eas.append(torch.stack([cv, variances[src_t], variances[tgt_t]], dim=1))  # :247
+        xs.append(cov)                                            # :254
+    x = torch.stack(xs, dim=2).reshape(n, -1)                     # :279
+    ea = torch.stack(eas, dim=2).reshape(len(src), -1)            # :281
+    y = torch.diagonal(vol[S]).float()                            # :262
+    return Data(x=x, edge_index=torch.stack([src_t, tgt_t]), edge_attr=ea, y_x=y)
+
+
+def synthetic_series(T: int, n: int = 30, seed: int = 1234, device=None,
+                     dtype=torch.float32) -> tuple[torch.Tensor, torch.Tensor]:
+    """T standardized symmetric vol and vol-of-vol matrices [T, n, n]."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    G1 = torch.randn(T, n, n, generator=g, dtype=dtype)
+    G2 = torch.randn(T, n, n, generator=g, dtype=dtype)
+    V = (G1 + G1.transpose(1, 2)) / 2
+    W = (G2 + G2.transpose(1, 2)) / 2
+    if device is not None:
+        V, W = V.to(device), W.to(device)
+    return V, W
+
+
+def window_batch(vol: torch.Tensor, volvol: torch.Tensor, starts: torch.Tensor,
+                 seq_length: int) -> Batch:
+    """Collated batch of the windows beginning at ``starts`` (window k uses
+    matrices starts[k] .. starts[k]+S-1 and the target diag(vol[starts[k]+S])),
+    built with gathers on the series' device; identical to
+    ``collate([window_graph(...) for ...])``."""
+    S = seq_length
+    n = vol.shape[1]
+    dev = vol.device
+    B = int(starts.numel())
+    starts = starts.to(dev)
+    tidx = starts.view(B, 1) + torch.arange(S, device=dev).view(1, S)       # [B, S]
+    V = vol[tidx].float()                                                    # [B, S, n, n]
+    W = volvol[tidx].float()
+    x = V.permute(0, 2, 3, 1).reshape(B * n, n * S)                          # x[v, c*S+t]
+    src, tgt = canonical_pairs(n)
+    src_t = torch.tensor(src, dtype=torch.long, device=dev)
+    tgt_t = torch.tensor(tgt, dtype=torch.long, device=dev)
+    P = len(src) // 2
+    cv = W[:, :, src_t[:P], tgt_t[:P]]                                       # [B, S, P]
+    cv = torch.cat([cv, cv], dim=2)                                          # [B, S, E0]
+    var = torch.diagonal(W, dim1=2, dim2=3)                                  # [B, S, n]
+    ea = torch.stack([cv, var[:, :, src_t], var[:, :, tgt_t]], dim=2)       # [B, S, 3, E0]
+    ea = ea.permute(0, 3, 2, 1).reshape(B * len(src), 3 * S)                 # ea[e, k*S+t]
+    y = torch.diagonal(vol[starts + S].float(), dim1=1, dim2=2).reshape(B * n)
+    ei = canonical_edge_index(n, B, dev)
+    ptr = torch.arange(B + 1, device=dev) * n
+    b = Batch(x=x.contiguous(), edge_index=ei, edge_attr=ea.contiguous(), y_x=y,
+              batch=torch.arange(B, device=dev).repeat_interleave(n), ptr=ptr)
+    b.nodes_per_graph = n
+    return b
+
+
+def synthetic_batch(num_graphs: int, seq_length: int, n: int = 30, seed: int = 1234,
+                    device=None) -> Batch:
+    """B independent windows (each from its own S+1 random matrices)."""
+    T = num_graphs * (seq_length + 1)
+    V, W = synthetic_series(T, n, seed, device)
+    starts = torch.arange(num_graphs, device=V.device) * (seq_length + 1)
+    return window_batch(V, W, starts, seq_length)
+
+
+class WindowDataset:
+    """Sliding windows over a matrix series, like CovarianceLaggedDataset
+    (window i = matrices i .. i+S-1, target diag(vol[i+S]);
+    utils/dataset.py:200-262), kept on the series' device; ``cut`` drops the
+    first windows like the reference's ``data_list[8357:]`` (:287-288)."""
+
+    def __init__(self, vol: torch.Tensor, volvol: torch.Tensor, seq_length: int, cut: int = 0):
+        self.vol, self.volvol, self.S = vol, volvol, seq_length
+        self.starts = torch.arange(cut, vol.shape[0] - seq_length, device=vol.device)
+
+    def __len__(self) -> int:
+        return int(self.starts.numel())
+
+    def batch(self, idx: torch.Tensor) -> Batch:
+        return window_batch(self.vol, self.volvol, self.starts[idx.to(self.starts.device)],
+                            self.S)
+
+    def loader(self, batch_size: int, shuffle: bool, generator: Optional[torch.Generator] = None,
+               subset: Optional[torch.Tensor] = None):
+        idx = subset if subset is not None else torch.arange(len(self))
+        if shuffle:
+            idx = idx[torch.randperm(idx.numel(), generator=generator)]
+        for k in range(0, idx.numel(), batch_size):
+            yield self.batch(idx[k:k + batch_size])

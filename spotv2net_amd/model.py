@@ -1,0 +1,98 @@
+"""``GATModel`` — drop-in for reference utils/models.py:61-152 on MI355X.
+
+Same constructor signature and layer-stacking rules (utils/models.py:86-117),
+same attributes (``gat_layers``, ``linear``, ``a``, ``dropout``,
+``activation``, ``standardize``, ``bnorm_node``/``bnorm_edge``), same
+``forward(data)`` contract (reads ``data.x``, ``data.edge_index``,
+``data.edge_attr``; returns ``[N * output_node_channels]``), same state_dict
+keys, so reference checkpoints load and 5_train_SpotV2Net.py runs unchanged.
+
+The forward is fused across layers:
+* one edge pass computes the folded edge logits of EVERY layer
+  (edge_attr is the same tensor for all layers, utils/models.py:145-146);
+* per layer: projection GEMM (f32 MFMA) -> fused attention kernel with the
+  model's activation in its epilogue; dropout (utils/models.py:147-148) and
+  the final ``nn.Linear`` (:150) stay PyTorch ops.
+Documented deviation: an unknown activation raises ValueError instead of
+printing and calling ``sys.exit()`` (utils/models.py:131-133).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import ops
+from .conv import GATConv
+from .layout import GraphLayout, analyze_edge_index
+
+
+def _layout_of(data, x: torch.Tensor, edge_index: torch.Tensor) -> GraphLayout:
+    lay = getattr(data, "sv2n_layout", None)
+    if isinstance(lay, GraphLayout) and lay.num_nodes == x.size(0):
+        return lay
+    hint = getattr(data, "nodes_per_graph", None)
+    return analyze_edge_index(edge_index, x.size(0), hint)
+
+
+class GATModel(nn.Module):
+    def __init__(self, num_node_features, num_edge_features, num_heads, output_node_channels,
+                 dim_hidden_layers=[100], dropout_att=0.0, dropout=0.0, activation="relu",
+                 concat_heads=False, negative_slope=0.2, standardize=False):
+        super().__init__()
+        self.dropout = dropout
+        self.activation = activation
+        self.standardize = standardize
+        if self.standardize:
+            self.bnorm_node = nn.BatchNorm1d(num_node_features, affine=False)
+            self.bnorm_edge = nn.BatchNorm1d(num_edge_features, affine=False)
+
+        kw = dict(heads=num_heads, dropout=dropout_att, edge_dim=num_edge_features,
+                  negative_slope=negative_slope)
+        L = len(dim_hidden_layers)
+        # utils/models.py:86-91 — first layer concatenates only if more layers follow
+        first = [GATConv(num_node_features, dim_hidden_layers[0],
+                         concat=(False if L == 1 else concat_heads), **kw)]
+        stacked = []
+        # utils/models.py:95-113 — later layers; the last one never concatenates
+        for i in range(L - 1):
+            in_ch = dim_hidden_layers[i] * num_heads if (concat_heads and num_heads > 1) \
+                else dim_hidden_layers[i]
+            last = (i + 1 == L - 1)
+            stacked.append(GATConv(in_ch, dim_hidden_layers[i + 1],
+                                   concat=(False if last else concat_heads), **kw))
+        self.gat_layers = nn.ModuleList(first + stacked)
+        self.linear = nn.Linear(dim_hidden_layers[-1], output_node_channels)
+
+        acts = {"relu": F.relu, "tanh": F.tanh, "sigmoid": F.sigmoid}
+        if activation not in acts:
+            raise ValueError("Choose an available activation function")
+        self.a = acts[activation]
+        self._act_code = ops.ACT_CODES[activation]
+
+    def forward(self, data):
+        x, edge_index, edge_attr = data.x, data.edge_index, data.edge_attr
+        if self.standardize:
+            x = self.bnorm_node(x)
+            if edge_attr is not None:
+                edge_attr = self.bnorm_edge(edge_attr)
+        layout = _layout_of(data, x, edge_index)
+        layers = list(self.gat_layers)
+
+        # one pass over edge_attr for the edge logits of all layers
+        ae = [None] * len(layers)
+        with_edge = [l for l in layers if l.lin_edge is not None]
+        if edge_attr is not None and len(with_edge) == len(layers):
+            H = layers[0].heads
+            wf = torch.cat([l.edge_fold() for l in layers], dim=1)  # [D, L*H]
+            ae = list(ops.edge_logits(edge_attr, wf, layout, len(layers), H))
+
+        for l, conv in enumerate(layers):
+            xs = ops.linear(x, conv.projection_weight())
+            x = conv.attend(xs, ae[l], layout, self._act_code)
+            if self.dropout:
+                x = F.dropout(x, p=self.dropout, training=self.training)
+        x = self.linear(x)
+        return x.view(-1)
