@@ -1,0 +1,322 @@
+"""SpotV2Net GAT hot-path benchmark (BASELINE.json metric, config C2).
+
+Workload: one training step (forward + MSELoss + backward + Adam, reference
+5_train_SpotV2Net.py:150-159) of GATModel with the C2 configuration — 30-node
+fully connected graphs, seq_length 42 (F = 1260 node / D = 126 edge
+features), 2 GAT layers [100, 50], 4 heads, concat_heads — over a
+device-resident synthetic batch of 512 window graphs per GPU, fp32.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+value = graphs processed by ALL ranks / max-over-ranks wall time (weak
+scaling: 512 graphs per GPU).  The JSON line also carries the fwd-only rate,
+the dominant kernel's roofline point (HIP events on its launch stream) and the
+CPU baseline (oracle restatement of PyG GATConv, rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "graphs/sec (30-node dense GAT, batch=512) at 1/2/4/8 MI355X vs PyG-CPU"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32, dense
+
+S, N_NODES, HEADS, HIDDEN, BATCH = 42, 30, 4, [100, 50], 512
+
+
+def build_model(dev):
+    from spotv2net_amd import GATModel
+    torch.manual_seed(5154)  # config/GNN_param.yaml:23
+    return GATModel(N_NODES * S, 3 * S, HEADS, 1, HIDDEN, concat_heads=True,
+                    activation="relu", negative_slope=0.2).to(dev)
+
+
+def time_replays(fn, k, sync_group=True):
+    if sync_group and dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        fn()
+    torch.cuda.synchronize()
+    if sync_group and dist.is_initialized():
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(x: float, dev) -> float:
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# --------------------------------------------------------------------------
+# per-kernel timing (HIP events on the stream the kernels are launched on)
+# --------------------------------------------------------------------------
+def kernel_table(model, data, reps=50):
+    from spotv2net_amd import ops
+    from spotv2net_amd.layout import analyze_edge_index
+    dev = data.x.device
+    stream = torch.cuda.current_stream(dev)
+    B = data.x.shape[0] // N_NODES
+    layout = analyze_edge_index(data.edge_index, data.x.shape[0], N_NODES)
+    L = len(model.gat_layers)
+    with torch.no_grad():
+        W = [c.projection_weight().contiguous() for c in model.gat_layers]
+        wf = torch.cat([c.edge_fold() for c in model.gat_layers], 1)
+    x0 = data.x
+    N0 = x0.shape[0]
+    xs0 = ops.gemm_f32(x0, True, W[0], True, N0, W[0].shape[0], x0.shape[1])
+    conv0 = model.gat_layers[0]
+    ae = ops._EdgeLogits.apply(data.edge_attr, wf, layout, L, HEADS)
+    y0 = torch.empty(N0, conv0.out_dim, device=dev)
+    ps0 = torch.empty(B, HEADS, N_NODES, N_NODES, device=dev)
+    lib = ops._lib.load()
+    sh = stream.cuda_stream
+    E, D = data.edge_attr.shape
+
+    def attn_fwd():
+        lib.sv2n_gat_attn_fwd(xs0.data_ptr(), xs0.stride(0), ae[0].data_ptr(), None,
+                              conv0.bias.data_ptr(), None, 1.0, y0.data_ptr(), ps0.data_ptr(),
+                              B, N_NODES, HEADS, conv0.out_channels, 1, 1, 0.2, sh)
+
+    dy0 = torch.randn_like(y0)
+    dxs0 = torch.empty_like(xs0)
+    dae0 = torch.empty_like(ae[0])
+    dbp = torch.empty(B, conv0.out_dim, device=dev)
+
+    def attn_bwd():
+        lib.sv2n_gat_attn_bwd(dy0.data_ptr(), y0.data_ptr(), xs0.data_ptr(), xs0.stride(0),
+                              ps0.data_ptr(), None, 1.0, None, dxs0.data_ptr(), dae0.data_ptr(),
+                              dbp.data_ptr(), B, N_NODES, HEADS, conv0.out_channels, 1, 1, 0.2,
+                              sh)
+
+    wfp, hp = ops.pad_columns(wf)
+    aeb = [torch.empty_like(a) for a in ae]
+    ptrs = ops._lib.ptr_array([a.data_ptr() for a in aeb])
+
+    def edge_fwd():
+        lib.sv2n_edge_logits_fwd(data.edge_attr.data_ptr(), E, D, None, layout.canon.data_ptr(),
+                                 wfp.data_ptr(), hp, ptrs, L, HEADS, B, N_NODES, sh)
+
+    ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hp)
+    ws = torch.empty(ws_n, device=dev)
+    dwf = torch.empty(D, hp, device=dev)
+
+    def edge_bwd():
+        lib.sv2n_edge_logits_bwd(data.edge_attr.data_ptr(), E, D, None, layout.canon.data_ptr(),
+                                 ptrs, L, HEADS, B, N_NODES, ws.data_ptr(), ws_n,
+                                 dwf.data_ptr(), hp, sh)
+
+    out0 = torch.empty_like(xs0)
+
+    def gemm_fwd():
+        ops.gemm_f32(x0, True, W[0], True, N0, W[0].shape[0], x0.shape[1], out=out0)
+
+    def gemm_dwt():
+        ops.gemm_f32(x0, False, dxs0, False, x0.shape[1], W[0].shape[0], N0)
+
+    M0, N0c, K0 = N0, W[0].shape[0], x0.shape[1]
+    rows = {
+        "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * N0c * K0, 4.0 * (M0 * K0 + N0c * K0 + M0 * N0c)),
+        "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * N0c * K0, 4.0 * (M0 * K0 + M0 * N0c + N0c * K0)),
+        "edge_logits_fwd": (edge_fwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS)),
+        "edge_logits_bwd": (edge_bwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS)),
+        "gat_attn_fwd_l0": (attn_fwd, "hbm", 2.0 * B * N_NODES * N_NODES * HEADS * conv0.out_channels,
+                            4.0 * (xs0.numel() + ae[0].numel() + y0.numel() + ps0.numel())),
+        "gat_attn_bwd_l0": (attn_bwd, "hbm", 4.0 * B * N_NODES * N_NODES * HEADS * conv0.out_channels,
+                            4.0 * (2 * y0.numel() + 2 * xs0.numel() + 2 * ps0.numel() + ae[0].numel())),
+    }
+    res = {}
+    for name, (fn, bound, flops, nbytes) in rows.items():
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        res[name] = dict(avg_us=us, bound=bound, flops=flops, bytes=nbytes,
+                         tflops=flops / us / 1e6, gbs=nbytes / us / 1e3)
+    return res
+
+
+def roofline_entry(table, traffic=None):
+    # dominant = largest time per training step (gemm rows run once per step at L0)
+    name = max(table, key=lambda k: table[k]["avg_us"])
+    r = table[name]
+    if r["bound"] == "mfma":
+        ach, peak, unit = r["tflops"], F32_MFMA_PEAK_TFLOPS, "TFLOP/s"
+    else:
+        ach, peak, unit = r["gbs"], HBM_PEAK_GBS, "GB/s"
+    return name, {"kernel": name, "bound": r["bound"], "achieved": round(ach, 2), "peak": peak,
+                  "unit": unit, "frac": round(ach / peak, 4), "avg_us": round(r["avg_us"], 2),
+                  "traffic": traffic}
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch from a committed rocprofv3 --pmc pass
+    (tools/pmc_traffic.py writes profiles/pmc_traffic.json), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+# --------------------------------------------------------------------------
+# CPU baseline: PyG-semantics oracle, same model/config, host cores
+# --------------------------------------------------------------------------
+def cpu_baseline(model, budget_s: float, batch: int):
+    from oracle.pyg_gatconv import OracleGATModel
+    from spotv2net_amd import Data, synthetic_batch
+    cores = min(os.cpu_count() or 1, int(os.environ.get("SV2N_CPU_THREADS", "16")))
+    torch.set_num_threads(cores)
+    ref = OracleGATModel(N_NODES * S, 3 * S, HEADS, 1, HIDDEN, concat_heads=True)
+    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    data = synthetic_batch(batch, S, seed=4321)
+    d = Data(x=data.x, edge_index=data.edge_index, edge_attr=data.edge_attr)
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+
+    def step():
+        out = ref(d)
+        loss = torch.nn.functional.mse_loss(out, data.y_x)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    step()  # warm-up
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or steps >= 20:
+            break
+    gps = steps * batch / el
+    cpu_name = platform.processor() or "cpu"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(gps, 2), "unit": "graphs/s", "cores": cores, "kind": "port",
+            "sample": f"oracle PyG-2.3.0-semantics GATModel (unfolded lin_edge, scatter softmax), "
+                      f"same C2 model, {steps} train steps (fwd+bwd+Adam) x {batch} graphs, "
+                      f"{el:.1f}s, torch {torch.__version__} CPU, {cpu_name}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=BATCH, help="graphs per GPU")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches (no hipGraph)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-table", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from spotv2net_amd import synthetic_batch
+    from spotv2net_amd.train import ForwardStep, TrainStep
+
+    model = build_model(dev)
+    if world > 1:  # identical replicas: broadcast rank 0's weights
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    data = synthetic_batch(args.batch, S, n=N_NODES, seed=1234 + rank, device=dev)
+
+    step = TrainStep(model, data, lr=1e-3, use_graph=not args.no_graph)
+    for _ in range(args.warmup):
+        step()
+    el = time_replays(step, args.steps)
+    el = max_over_ranks(el, dev)
+    value = world * args.batch * args.steps / el
+    loss = float(step.loss.item())
+
+    model.eval()
+    fstep = ForwardStep(model, data, use_graph=not args.no_graph)
+    for _ in range(max(1, args.warmup)):
+        fstep()
+    fel = max_over_ranks(time_replays(fstep, args.steps), dev)
+    fwd_value = world * args.batch * args.steps / fel
+    model.train()
+
+    result = None
+    if rank == 0:
+        table = {}
+        roof = None
+        if not args.no_kernel_table:
+            table = kernel_table(model, data)
+            kname, roof = roofline_entry(table)
+            roof["traffic"] = load_traffic(kname)
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(model, args.cpu_seconds, args.batch)
+        result = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "graphs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (standardized symmetric vol / vol-of-vol matrices, "
+                    "CovarianceLaggedDataset layout), device-resident, random-init weights",
+            "config": {"workload": "C2 train step (fwd+MSE+bwd+Adam): 30-node dense GAT graphs, "
+                                   "870 edges + self loops, seq_length 42 (F=1260, D=126), "
+                                   "GAT [100,50] x 4 heads concat, relu",
+                       "graphs_per_gpu": args.batch, "global_batch": args.batch * world,
+                       "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
+            "fwd_graphs_per_s": round(fwd_value, 1),
+            "final_loss": loss,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "speedup_vs_cpu": (round(value / cpu["value"], 1) if cpu else None),
+            "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv)
+                            for kk, vv in v.items() if kk in ("avg_us", "tflops", "gbs", "bound")}
+                        for k, v in table.items()},
+            "peaks_assumed": {"hbm_GBs": HBM_PEAK_GBS, "f32_mfma_TFLOPs": F32_MFMA_PEAK_TFLOPS},
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -19,6 +19,9 @@
  *   sv2n_edge_logits_bwd   d(W̃) = edge_attrᵀ · d(a_e)                (row a12)
  *   sv2n_gemm_f32          the dense projections lin_src(x) (row a6) and its
  *                          backward products, on f32-input MFMA
+ *   sv2n_gat_prep_*        per-step weight folding (a_src/a_dst rows, W̃_edge)
+ *                          and its backward straight into the parameter grads
+ *   sv2n_adam_f32          the reference's Adam step over flat buffers (a13)
  *   sv2n_block_rowmask     edge_index -> per-target source bitmask for graph
  *                          batches whose edges are not in canonical order
  *
@@ -135,6 +138,43 @@ int sv2n_gemm_f32(int a_kmajor, int b_kmajor, const float* A, int64_t lda,
                   const float* B, int64_t ldb, float* C, int64_t ldc,
                   int64_t M, int64_t N, int64_t K,
                   float* workspace, int64_t workspace_floats, hipStream_t stream);
+
+/* Weight preparation for one GAT layer (replaces, per step, PyG's separate
+ * (x_src*att_src).sum(-1) / (x_dst*att_dst).sum(-1) and lin_edge·att_edge
+ * reductions by folded weights):
+ *   waug [ldx][F] = [ W (H*C rows) ; W_hᵀatt_src_h (H rows) ; W_hᵀatt_dst_h (H rows) ; 0 ]
+ *   wfold[d][col0+h] = Σ_c att_edge[h*C+c] · W_edge[h*C+c][d]   (skipped if W_edge NULL) */
+int sv2n_gat_prep_fwd(const float* W, const float* att_src, const float* att_dst,
+                      int heads, int channels, int in_features, float* waug, int ldx,
+                      const float* W_edge, const float* att_edge, int edge_dim,
+                      float* wfold, int hl_pad, int col0, hipStream_t stream);
+
+/* Backward of the node half of sv2n_gat_prep_fwd plus the bias: from
+ * dwaug_t = dWaugᵀ [F][ldx] ACCUMULATE (+=) into gW [H*C][F], g_att_src /
+ * g_att_dst [H*C] and g_bias[o] += Σ_b dbias_partial[b][o] (any output NULL
+ * = skipped; dwaug_t/W/att_* may be NULL when gW, g_att_src, g_att_dst are).
+ * workspace: sv2n_gat_prep_bwd_workspace(heads, in_features) floats (needed
+ * when g_att_src or g_att_dst is requested). */
+int64_t sv2n_gat_prep_bwd_workspace(int heads, int in_features);
+int sv2n_gat_prep_bwd_node(const float* dwaug_t, int ldx, const float* W,
+                           const float* att_src, const float* att_dst, int heads,
+                           int channels, int in_features, const float* dbias_partial,
+                           int num_parts, int bias_len, float* gW, float* g_att_src,
+                           float* g_att_dst, float* g_bias, float* workspace,
+                           int64_t workspace_floats, hipStream_t stream);
+
+/* Backward of the edge fold: ACCUMULATE gW_edge[h*C+c][d] += dwfold[d][col0+h]·att_edge[h*C+c]
+ * and g_att_edge[h*C+c] += Σ_d W_edge[h*C+c][d]·dwfold[d][col0+h]. */
+int sv2n_gat_prep_bwd_edge(const float* dwfold, int hl_pad, int col0,
+                           const float* W_edge, const float* att_edge, int heads,
+                           int channels, int edge_dim, float* gW_edge,
+                           float* g_att_edge, hipStream_t stream);
+
+/* torch.optim.Adam step (amsgrad=False) over flat buffers of n floats
+ * (16-B aligned); *step is the already-incremented device step count. */
+int sv2n_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                  int64_t n, const float* step, float lr, float beta1, float beta2,
+                  float eps, float weight_decay, hipStream_t stream);
 
 /* rowmask[t] |= 1<<(s - g*n) for every non-self edge s->t (rowmask must be
  * zeroed by the caller).  Edges must stay inside their n-node block. */

@@ -23,9 +23,10 @@ published source:
 Execution differs from PyG, not the math: the node projection carries two extra
 GEMM columns per head (W_srcᵀatt_src and W_srcᵀatt_dst, so a_src/a_dst come out
 of the projection), and the edge projection is folded to W̃ = W_edgeᵀatt_edge
-(one D x H matrix), so ``lin_edge(edge_attr)`` is never materialised.  Both
-folds are ordinary autograd ops on the parameters, so gradients reach the
-original parameters exactly as PyG's would.
+(one D x H matrix), so ``lin_edge(edge_attr)`` is never materialised.  The
+forward and backward run as one fused node (``stack.gat_stack``) whose
+backward undoes the folds in-kernel and accumulates into each parameter's
+``.grad``.
 """
 from __future__ import annotations
 
@@ -37,6 +38,7 @@ from torch import Tensor, nn
 
 from . import ops
 from .layout import GraphLayout, analyze_edge_index
+from .stack import gat_stack
 
 
 def glorot_(t: Tensor) -> None:
@@ -173,11 +175,7 @@ class GATConv(nn.Module):
             raise ValueError("x must be [N, in_channels]")
         if layout is None:
             layout = analyze_edge_index(edge_index, x.size(0))
-        xs = ops.linear(x, self.projection_weight())
-        ae = None
-        if edge_attr is not None and self.lin_edge is not None:
-            (ae,) = ops.edge_logits(edge_attr, self.edge_fold(), layout, 1, self.heads)
-        return self.attend(xs, ae, layout, ops.ACT_CODES[None])
+        return gat_stack(x, edge_attr, (self,), layout, ops.ACT_CODES[None], 0.0, self.training)
 
     def __repr__(self) -> str:
         return (f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, "

@@ -215,13 +215,29 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
   }
 }
 
-__global__ void k_reduce_partials(const float* __restrict__ partial, int nparts, int O,
-                                  float* __restrict__ out) {
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= O) return;
-  float s = 0.f;
-  for (int b = 0; b < nparts; ++b) s += partial[(int64_t)b * O + o];
-  out[o] = s;
+// out[o] = Σ_b partial[b][o] in a fixed order: a block owns 64 outputs, its
+// four waves sum interleaved quarters of the partials (4 loads in flight per
+// lane), then combine through LDS.
+__global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ partial,
+                                                         int nparts, int O,
+                                                         float* __restrict__ out) {
+  __shared__ float s_red[4][64];
+  const int lo = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int o = blockIdx.x * 64 + lo;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (o < O) {
+    int b = grp;
+    for (; b + 12 < nparts; b += 16) {
+      a0 += partial[(int64_t)b * O + o];
+      a1 += partial[(int64_t)(b + 4) * O + o];
+      a2 += partial[(int64_t)(b + 8) * O + o];
+      a3 += partial[(int64_t)(b + 12) * O + o];
+    }
+    for (; b < nparts; b += 4) a0 += partial[(int64_t)b * O + o];
+  }
+  s_red[grp][lo] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (grp == 0 && o < O) out[o] = (s_red[0][lo] + s_red[1][lo]) + (s_red[2][lo] + s_red[3][lo]);
 }
 
 __global__ void k_block_rowmask(const int64_t* __restrict__ ei, int64_t E, int64_t N, int n,
@@ -241,7 +257,7 @@ __global__ void k_block_rowmask(const int64_t* __restrict__ ei, int64_t E, int64
 // ============================ C-ABI ========================================
 using namespace sv2n;
 
-static constexpr int EDGE_BWD_GRID = 1024;
+static constexpr int EDGE_BWD_GRID = 512;
 
 template <typename K>
 static void raise_lds_limit(K kernel, size_t bytes) {
@@ -343,7 +359,7 @@ extern "C" int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, i
       return SV2N_ERR_SHAPE;
   }
 #undef SV2N_LAUNCH_EB
-  hipLaunchKernelGGL(k_reduce_partials, dim3((O + 255) / 256), dim3(256), 0, stream, workspace,
+  hipLaunchKernelGGL(k_reduce_partials, dim3((O + 63) / 64), dim3(256), 0, stream, workspace,
                      grid, O, dwfold);
   return (int)hipGetLastError();
 }

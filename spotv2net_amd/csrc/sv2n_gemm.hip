@@ -190,10 +190,16 @@ __global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int6
                                 float* __restrict__ C, int64_t ldc) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= M * N) return;
-  float s = 0.f;
-  for (int z = 0; z < nsplit; ++z) s += part[(int64_t)z * M * N + idx];
+  const int64_t MN = M * N;
+  float s0 = 0.f, s1 = 0.f;
+  int z = 0;
+  for (; z + 1 < nsplit; z += 2) {
+    s0 += part[(int64_t)z * MN + idx];
+    s1 += part[(int64_t)(z + 1) * MN + idx];
+  }
+  if (z < nsplit) s0 += part[(int64_t)z * MN + idx];
   const int64_t m = idx / N, n = idx - m * N;
-  C[m * ldc + n] = s;
+  C[m * ldc + n] = s0 + s1;
 }
 
 struct GemmPlan {

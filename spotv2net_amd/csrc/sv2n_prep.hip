@@ -1,0 +1,263 @@
+// Weight preparation for the fused GAT stack, and its backward.
+//
+// Forward (one launch per layer):
+//   Waug[ldx][F] = [ W_src ; W_srcᵀatt_src (H rows) ; W_srcᵀatt_dst (H rows) ; 0 ]
+//   wfold[d][col0+h] = Σ_c att_edge[h,c] · W_edge[h*C+c][d]
+// so the projection GEMM also emits PyG's alpha_src / alpha_dst
+// ((x_src*att_src).sum(-1), GATConv.forward) and the edge pass needs one D x H
+// matrix per layer instead of lin_edge's [E, H*C] output.
+//
+// Backward: the projection GEMM produces T = dWaugᵀ [F][ldx]; the fold is
+// undone here and the parameter gradients are ACCUMULATED into p.grad:
+//   gW[hC+c][f]   += T[f][hC+c] + T[f][HC+h]·att_src[h,c] + T[f][HC+H+h]·att_dst[h,c]
+//   g_att_src[h,c] += Σ_f T[f][HC+h] · W[hC+c][f]       (same for dst)
+//   gW_e[hC+c][d] += dwfold[d][col0+h] · att_edge[h,c]
+//   g_att_edge[h,c] += Σ_d W_e[hC+c][d] · dwfold[d][col0+h]
+//   g_bias[o]     += Σ_g dbias_partial[g][o]
+#include "sv2n_common.h"
+
+namespace sv2n {
+
+// grid (ceil(max(F, D)/64), 2H), block 256 = 64 columns x 4 row groups
+__global__ __launch_bounds__(256) void k_prep_fwd(const float* __restrict__ W,
+                                                  const float* __restrict__ att_s,
+                                                  const float* __restrict__ att_d, int H, int C,
+                                                  int F, float* __restrict__ waug, int ldx,
+                                                  const float* __restrict__ We,
+                                                  const float* __restrict__ att_e, int D,
+                                                  float* __restrict__ wfold, int hlp, int col0) {
+  __shared__ float s_red[2][4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const int y = blockIdx.y;
+  if (y < H) {
+    const int h = y;
+    float ss = 0.f, sd = 0.f;
+    if (col < F) {
+      for (int c = grp; c < C; c += 4) {
+        const int row = h * C + c;
+        const float w = W[(int64_t)row * F + col];
+        waug[(int64_t)row * F + col] = w;
+        ss = fmaf(att_s[row], w, ss);
+        sd = fmaf(att_d[row], w, sd);
+      }
+    }
+    s_red[0][grp][lane] = ss;
+    s_red[1][grp][lane] = sd;
+    __syncthreads();
+    if (grp == 0 && col < F) {
+      waug[(int64_t)(H * C + h) * F + col] =
+          (s_red[0][0][lane] + s_red[0][1][lane]) + (s_red[0][2][lane] + s_red[0][3][lane]);
+      waug[(int64_t)(H * C + H + h) * F + col] =
+          (s_red[1][0][lane] + s_red[1][1][lane]) + (s_red[1][2][lane] + s_red[1][3][lane]);
+    }
+    if (h == 0 && col < F) {  // zero padding rows
+      for (int r = H * C + 2 * H + grp; r < ldx; r += 4) waug[(int64_t)r * F + col] = 0.f;
+    }
+  } else {
+    if (!We) return;
+    const int h = y - H;
+    float s = 0.f;
+    if (col < D) {
+      for (int c = grp; c < C; c += 4) {
+        const int row = h * C + c;
+        s = fmaf(att_e[row], We[(int64_t)row * D + col], s);
+      }
+    }
+    s_red[0][grp][lane] = s;
+    __syncthreads();
+    if (grp == 0 && col < D)
+      wfold[(int64_t)col * hlp + col0 + h] =
+          (s_red[0][0][lane] + s_red[0][1][lane]) + (s_red[0][2][lane] + s_red[0][3][lane]);
+  }
+}
+
+// gW[o][f] += T[f][o] + T[f][HC+h]·att_s[o] + T[f][HC+H+h]·att_d[o], o = h*C+c
+// 64(f) x 64(o) tiles transposed through LDS; grid (ceil(F/64), ceil(HC/64)).
+__global__ __launch_bounds__(256) void k_prep_bwd_w(const float* __restrict__ T, int ldx,
+                                                    const float* __restrict__ att_s,
+                                                    const float* __restrict__ att_d, int H, int C,
+                                                    int F, float* __restrict__ gW,
+                                                    float* __restrict__ g2) {
+  __shared__ float tile[64][65];
+  __shared__ float sfold[64][2 * SV2N_MAX_HEADS];
+  const int HC = H * C;
+  const int f0 = blockIdx.x * 64, o0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+  for (int idx = t; idx < 64 * 64; idx += 256) {
+    const int fr = idx >> 6, oc = idx & 63;
+    const int f = f0 + fr, o = o0 + oc;
+    tile[fr][oc] = (f < F && o < HC) ? T[(int64_t)f * ldx + o] : 0.f;
+  }
+  for (int idx = t; idx < 64 * 2 * H; idx += 256) {
+    const int fr = idx / (2 * H), k = idx - fr * 2 * H;
+    const int f = f0 + fr;
+    sfold[fr][k] = (f < F) ? T[(int64_t)f * ldx + HC + k] : 0.f;
+  }
+  __syncthreads();
+  if (blockIdx.y == 0 && g2) {  // compact fold gradients for k_prep_bwd_att: g2[k][f]
+    for (int idx = t; idx < 64 * 2 * H; idx += 256) {
+      const int k = idx >> 6, fc = idx & 63;
+      if (f0 + fc < F) g2[(int64_t)k * F + f0 + fc] = sfold[fc][k];
+    }
+  }
+  if (!gW) return;
+  for (int idx = t; idx < 64 * 64; idx += 256) {
+    const int orow = idx >> 6, fc = idx & 63;
+    const int o = o0 + orow, f = f0 + fc;
+    if (o < HC && f < F) {
+      const int h = o / C;
+      const float v = tile[fc][orow] + sfold[fc][h] * att_s[o] + sfold[fc][H + h] * att_d[o];
+      gW[(int64_t)o * F + f] += v;
+    }
+  }
+}
+
+// one wave per row o = h*C+c (grid ceil(HC/4)): g_att_src[o] += Σ_f g2[h][f]·W[o][f],
+// g_att_dst[o] += Σ_f g2[H+h][f]·W[o][f]
+__global__ __launch_bounds__(256) void k_prep_bwd_att(const float* __restrict__ g2,
+                                                      const float* __restrict__ W, int H, int C,
+                                                      int F, float* __restrict__ g_att_s,
+                                                      float* __restrict__ g_att_d) {
+  const int lane = threadIdx.x & 63;
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (o >= H * C) return;
+  const int h = o / C;
+  const float* wr = W + (int64_t)o * F;
+  const float* fs = g2 + (int64_t)h * F;
+  const float* fd = g2 + (int64_t)(H + h) * F;
+  float a = 0.f, b = 0.f;
+  for (int f = lane; f < F; f += 64) {
+    const float w = wr[f];
+    a = fmaf(fs[f], w, a);
+    b = fmaf(fd[f], w, b);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    a += __shfl_xor(a, m, 64);
+    b += __shfl_xor(b, m, 64);
+  }
+  if (lane == 0) {
+    if (g_att_s) g_att_s[o] += a;
+    if (g_att_d) g_att_d[o] += b;
+  }
+}
+
+// one wave per row o = h*C+c (grid ceil(HC/4)): gW_e[o][d] += dwfold[d][col0+h]·att_e[o],
+// g_att_edge[o] += Σ_d W_e[o][d]·dwfold[d][col0+h]
+__global__ __launch_bounds__(256) void k_prep_bwd_edge(const float* __restrict__ dwfold, int hlp,
+                                                       int col0, const float* __restrict__ We,
+                                                       const float* __restrict__ att_e, int H,
+                                                       int C, int D, float* __restrict__ gWe,
+                                                       float* __restrict__ g_att_e) {
+  const int lane = threadIdx.x & 63;
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (o >= H * C) return;
+  const int h = o / C;
+  const float ae = att_e[o];
+  float a = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float g = dwfold[(int64_t)d * hlp + col0 + h];
+    a = fmaf(We[(int64_t)o * D + d], g, a);
+    if (gWe) gWe[(int64_t)o * D + d] += g * ae;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) a += __shfl_xor(a, m, 64);
+  if (lane == 0 && g_att_e) g_att_e[o] += a;
+}
+
+// g[o] += Σ_b part[b][o] (fixed order): block = 16 columns x 16 row groups
+__global__ __launch_bounds__(256) void k_colsum_accum(const float* __restrict__ part, int nparts,
+                                                      int O, float* __restrict__ g) {
+  __shared__ float s_red[16][17];
+  const int lo = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int o = blockIdx.x * 16 + lo;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (o < O) {
+    int b = grp;
+    for (; b + 48 < nparts; b += 64) {
+      a0 += part[(int64_t)b * O + o];
+      a1 += part[(int64_t)(b + 16) * O + o];
+      a2 += part[(int64_t)(b + 32) * O + o];
+      a3 += part[(int64_t)(b + 48) * O + o];
+    }
+    for (; b < nparts; b += 16) a0 += part[(int64_t)b * O + o];
+  }
+  s_red[grp][lo] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (grp == 0 && o < O) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += s_red[k][lo];
+    g[o] += s;
+  }
+}
+
+}  // namespace sv2n
+
+using namespace sv2n;
+
+extern "C" int sv2n_gat_prep_fwd(const float* W, const float* att_src, const float* att_dst,
+                                 int heads, int channels, int in_features, float* waug, int ldx,
+                                 const float* W_edge, const float* att_edge, int edge_dim,
+                                 float* wfold, int hl_pad, int col0, hipStream_t stream) {
+  if (!W || !att_src || !att_dst || !waug || heads < 1 || channels < 1 || in_features < 1)
+    return SV2N_ERR_ARG;
+  if (heads > SV2N_MAX_HEADS || ldx < heads * channels + 2 * heads) return SV2N_ERR_SHAPE;
+  const bool edge = W_edge && att_edge && wfold;
+  if (edge && (edge_dim < 1 || col0 + heads > hl_pad)) return SV2N_ERR_SHAPE;
+  const int cols = std::max(in_features, edge ? edge_dim : 0);
+  dim3 grid((cols + 63) / 64, edge ? 2 * heads : heads);
+  hipLaunchKernelGGL(k_prep_fwd, grid, dim3(256), 0, stream, W, att_src, att_dst, heads, channels,
+                     in_features, waug, ldx, edge ? W_edge : nullptr, att_edge, edge_dim, wfold,
+                     hl_pad, col0);
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t sv2n_gat_prep_bwd_workspace(int heads, int in_features) {
+  return (int64_t)2 * heads * in_features;
+}
+
+extern "C" int sv2n_gat_prep_bwd_node(const float* dwaug_t, int ldx, const float* W,
+                                      const float* att_src, const float* att_dst, int heads,
+                                      int channels, int in_features, const float* dbias_partial,
+                                      int num_parts, int bias_len, float* gW, float* g_att_src,
+                                      float* g_att_dst, float* g_bias, float* workspace,
+                                      int64_t workspace_floats, hipStream_t stream) {
+  const bool weights = gW || g_att_src || g_att_dst;
+  if (weights && (!dwaug_t || !W || !att_src || !att_dst)) return SV2N_ERR_ARG;
+  if (heads < 1 || channels < 1 || in_features < 1) return SV2N_ERR_ARG;
+  if (heads > SV2N_MAX_HEADS || (weights && ldx < heads * channels + 2 * heads))
+    return SV2N_ERR_SHAPE;
+  const int HC = heads * channels;
+  const bool att = g_att_src || g_att_dst;
+  if (att && (!workspace || workspace_floats < (int64_t)2 * heads * in_features))
+    return SV2N_ERR_WORKSPACE;
+  if (gW || att) {
+    dim3 grid((in_features + 63) / 64, gW ? (HC + 63) / 64 : 1);
+    hipLaunchKernelGGL(k_prep_bwd_w, grid, dim3(256), 0, stream, dwaug_t, ldx, att_src, att_dst,
+                       heads, channels, in_features, gW, att ? workspace : nullptr);
+  }
+  if (att) {
+    hipLaunchKernelGGL(k_prep_bwd_att, dim3((HC + 3) / 4), dim3(256), 0, stream, workspace, W,
+                       heads, channels, in_features, g_att_src, g_att_dst);
+  }
+  if (g_bias && dbias_partial && bias_len > 0 && num_parts > 0) {
+    hipLaunchKernelGGL(k_colsum_accum, dim3((bias_len + 15) / 16), dim3(256), 0, stream,
+                       dbias_partial, num_parts, bias_len, g_bias);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_gat_prep_bwd_edge(const float* dwfold, int hl_pad, int col0,
+                                      const float* W_edge, const float* att_edge, int heads,
+                                      int channels, int edge_dim, float* gW_edge,
+                                      float* g_att_edge, hipStream_t stream) {
+  if (!dwfold || !W_edge || !att_edge || heads < 1 || channels < 1 || edge_dim < 1)
+    return SV2N_ERR_ARG;
+  if (col0 + heads > hl_pad) return SV2N_ERR_SHAPE;
+  const int HC = heads * channels;
+  hipLaunchKernelGGL(k_prep_bwd_edge, dim3((HC + 3) / 4), dim3(256), 0, stream, dwfold, hl_pad,
+                     col0, W_edge, att_edge, heads, channels, edge_dim, gW_edge, g_att_edge);
+  return (int)hipGetLastError();
+}

@@ -7,12 +7,12 @@ same attributes (``gat_layers``, ``linear``, ``a``, ``dropout``,
 ``data.edge_attr``; returns ``[N * output_node_channels]``), same state_dict
 keys, so reference checkpoints load and 5_train_SpotV2Net.py runs unchanged.
 
-The forward is fused across layers:
+The GAT layers run as ONE fused autograd node (``stack.gat_stack``):
 * one edge pass computes the folded edge logits of EVERY layer
   (edge_attr is the same tensor for all layers, utils/models.py:145-146);
 * per layer: projection GEMM (f32 MFMA) -> fused attention kernel with the
-  model's activation in its epilogue; dropout (utils/models.py:147-148) and
-  the final ``nn.Linear`` (:150) stay PyTorch ops.
+  model's activation in its epilogue, then the inter-layer dropout
+  (utils/models.py:147-148); the final ``nn.Linear`` (:150) stays a PyTorch op.
 Documented deviation: an unknown activation raises ValueError instead of
 printing and calling ``sys.exit()`` (utils/models.py:131-133).
 """
@@ -27,6 +27,7 @@ from torch import nn
 from . import ops
 from .conv import GATConv
 from .layout import GraphLayout, analyze_edge_index
+from .stack import gat_stack
 
 
 def _layout_of(data, x: torch.Tensor, edge_index: torch.Tensor) -> GraphLayout:
@@ -79,20 +80,7 @@ class GATModel(nn.Module):
             if edge_attr is not None:
                 edge_attr = self.bnorm_edge(edge_attr)
         layout = _layout_of(data, x, edge_index)
-        layers = list(self.gat_layers)
-
-        # one pass over edge_attr for the edge logits of all layers
-        ae = [None] * len(layers)
-        with_edge = [l for l in layers if l.lin_edge is not None]
-        if edge_attr is not None and len(with_edge) == len(layers):
-            H = layers[0].heads
-            wf = torch.cat([l.edge_fold() for l in layers], dim=1)  # [D, L*H]
-            ae = list(ops.edge_logits(edge_attr, wf, layout, len(layers), H))
-
-        for l, conv in enumerate(layers):
-            xs = ops.linear(x, conv.projection_weight())
-            x = conv.attend(xs, ae[l], layout, self._act_code)
-            if self.dropout:
-                x = F.dropout(x, p=self.dropout, training=self.training)
+        x = gat_stack(x, edge_attr, tuple(self.gat_layers), layout, self._act_code,
+                      float(self.dropout or 0.0), self.training)
         x = self.linear(x)
         return x.view(-1)

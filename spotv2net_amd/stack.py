@@ -1,0 +1,254 @@
+"""Fused GAT stack: all GATConv layers of a GATModel (or one standalone
+GATConv) as ONE autograd node whose forward and backward are sequences of
+sv2n kernel launches.
+
+Forward (reference utils/models.py:145-148 with PyG GATConv inside):
+  per layer  sv2n_gat_prep_fwd   W -> [W ; Wᵀatt_src ; Wᵀatt_dst] and W̃_edge columns
+  once       sv2n_edge_logits_fwd  edge_attr · W̃ for every layer (one HBM pass)
+  per layer  sv2n_gemm_f32       xs = x · Waugᵀ  (f32 MFMA)
+             sv2n_gat_attn_fwd   loops/leaky/softmax/dropout/aggregate/bias/act
+             dropout between layers (model-level, torch RNG mask)
+Backward, layers in reverse:
+  sv2n_gat_attn_bwd  -> d xs, d ae, bias partials
+  sv2n_gemm_f32      -> dWaugᵀ = xᵀ·dxs (split-K), and dx = dxs·Waug (if needed)
+  sv2n_gat_prep_bwd_node -> ACCUMULATES into W/att_src/att_dst/bias .grad
+  then one sv2n_edge_logits_bwd for all layers + sv2n_gat_prep_bwd_edge.
+
+Parameter gradients are written straight into ``p.grad`` (allocated as zeros
+when None), so no per-parameter autograd glue (copies, adds, fold backward)
+runs; the node returns None for the parameters.  Gradient hooks registered on
+these parameters therefore do not fire for this path (documented deviation).
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+from .layout import GraphLayout
+from .ops import _aligned, _require_device, gemm_f32, pad_columns
+
+
+def _grad_buf(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    if p is None or not p.requires_grad:
+        return None
+    if p.grad is None:
+        p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
+    elif not p.grad.is_contiguous():
+        p.grad = p.grad.contiguous()
+    return p.grad
+
+
+def layer_params(conv) -> list:
+    ps = [conv.lin_src.weight, conv.att_src, conv.att_dst]
+    if conv.lin_edge is not None:
+        ps += [conv.lin_edge.weight, conv.att_edge]
+    if conv.bias is not None:
+        ps.append(conv.bias)
+    return ps
+
+
+def _ldx(conv) -> int:
+    return (conv.heads * conv.out_channels + 2 * conv.heads + 3) // 4 * 4
+
+
+class _GATStack(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, edge_attr, convs, layout: GraphLayout, act: int, post_dropout: float,
+                training: bool, *params):
+        lib = _lib.load()
+        dev = x.device
+        st = _lib.stream_handle(dev)
+        L = len(convs)
+        B, n, N = layout.num_graphs, layout.n, layout.num_nodes
+        use_edge = edge_attr is not None and all(c.lin_edge is not None for c in convs)
+        H = convs[0].heads
+        if use_edge and any(c.heads != H for c in convs):
+            raise NotImplementedError("fused edge pass needs equal head counts across layers")
+
+        ea = None
+        wf = None
+        hp = 0
+        if use_edge:
+            ea = edge_attr.view(-1, 1) if edge_attr.dim() == 1 else edge_attr
+            ea = _aligned(ea)
+            if ea.size(0) != layout.num_edges:
+                raise ValueError("edge_attr rows must match edge_index columns")
+            D = ea.size(1)
+            _, hp = pad_columns(torch.empty(0, L * H))
+            wf = torch.empty(D, hp, device=dev, dtype=torch.float32)
+
+        # 1) weight preparation
+        waugs = []
+        for l, c in enumerate(convs):
+            F = c.in_channels
+            waug = torch.empty(_ldx(c), F, device=dev, dtype=torch.float32)
+            We = c.lin_edge.weight if use_edge else None
+            _lib.check(lib.sv2n_gat_prep_fwd(
+                c.lin_src.weight.data_ptr(), c.att_src.data_ptr(), c.att_dst.data_ptr(), c.heads,
+                c.out_channels, F, waug.data_ptr(), waug.size(0), _lib.ptr(We),
+                _lib.ptr(c.att_edge if use_edge else None), ea.size(1) if use_edge else 0,
+                _lib.ptr(wf), hp, l * H, st), "sv2n_gat_prep_fwd")
+            waugs.append(waug)
+
+        # 2) edge logits of every layer in one pass over edge_attr
+        aes = [None] * L
+        if use_edge:
+            aes = [torch.empty(B, n, n, H, device=dev, dtype=torch.float32) for _ in range(L)]
+            E = ea.size(0)
+            if E > 0:
+                ptrs = _lib.ptr_array([a.data_ptr() for a in aes])
+                ei = layout.edge_index if layout.kind == "block" else None
+                _lib.check(lib.sv2n_edge_logits_fwd(ea.data_ptr(), E, ea.size(1), _lib.ptr(ei),
+                                                    layout.canon.data_ptr(), wf.data_ptr(), hp,
+                                                    ptrs, L, H, B, n, st), "sv2n_edge_logits_fwd")
+
+        # 3) layers
+        xin = _aligned(x)
+        saved_x, saved_xs, saved_y, saved_p, saved_keep, saved_drop = [], [], [], [], [], []
+        for l, c in enumerate(convs):
+            Hc, C = c.heads, c.out_channels
+            F = c.in_channels
+            if xin.size(1) != F:
+                raise ValueError(f"layer {l}: expected {F} input features, got {xin.size(1)}")
+            xs = gemm_f32(xin, True, waugs[l], True, N, waugs[l].size(0), F)
+            keep, kscale = None, 1.0
+            if training and c.dropout > 0.0:
+                if c.dropout >= 1.0:
+                    keep = torch.zeros(B, Hc, n, n, device=dev, dtype=torch.uint8)
+                    kscale = 0.0
+                else:
+                    keep = (torch.rand(B, Hc, n, n, device=dev) >= c.dropout).to(torch.uint8)
+                    kscale = 1.0 / (1.0 - c.dropout)
+            OC = Hc * C if c.concat else C
+            y = torch.empty(N, OC, device=dev, dtype=torch.float32)
+            ps = torch.empty(B, Hc, n, n, device=dev, dtype=torch.float32)
+            _lib.check(lib.sv2n_gat_attn_fwd(
+                xs.data_ptr(), xs.stride(0), _lib.ptr(aes[l]), _lib.ptr(layout.rowmask),
+                _lib.ptr(c.bias), _lib.ptr(keep), kscale, y.data_ptr(), ps.data_ptr(), B, n, Hc, C,
+                int(c.concat), act, float(c.negative_slope), st), "sv2n_gat_attn_fwd")
+            out = y
+            dmask = None
+            if training and post_dropout > 0.0:
+                if post_dropout >= 1.0:
+                    dmask = torch.zeros_like(y)
+                else:
+                    dmask = (torch.rand_like(y) >= post_dropout).to(torch.float32) * \
+                        (1.0 / (1.0 - post_dropout))
+                out = y * dmask
+            saved_x.append(xin)
+            saved_xs.append(xs)
+            saved_y.append(y)
+            saved_p.append(ps)
+            saved_keep.append(keep)
+            saved_drop.append(dmask)
+            xin = out
+
+        ctx.convs = convs
+        ctx.layout = layout
+        ctx.meta = (L, act, use_edge, hp, H)
+        ctx.kscales = [(1.0 / (1.0 - c.dropout)) if (training and 0.0 < c.dropout < 1.0) else
+                       (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs]
+        ctx.save_for_backward(ea, *saved_x, *saved_xs, *saved_y, *saved_p, *saved_keep,
+                              *saved_drop, *waugs)
+        return xin
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = _lib.load()
+        convs = ctx.convs
+        layout: GraphLayout = ctx.layout
+        L, act, use_edge, hp, H = ctx.meta
+        sv = ctx.saved_tensors
+        ea = sv[0]
+        k = 1
+        xs_in = sv[k:k + L]; k += L
+        xss = sv[k:k + L]; k += L
+        ys = sv[k:k + L]; k += L
+        pss = sv[k:k + L]; k += L
+        keeps = sv[k:k + L]; k += L
+        drops = sv[k:k + L]; k += L
+        waugs = sv[k:k + L]
+        dev = dout.device
+        st = _lib.stream_handle(dev)
+        B, n, N = layout.num_graphs, layout.n, layout.num_nodes
+
+        dy = dout.contiguous()
+        daes = [None] * L
+        need_x0 = ctx.needs_input_grad[0]
+        for l in range(L - 1, -1, -1):
+            c = convs[l]
+            Hc, C = c.heads, c.out_channels
+            F = c.in_channels
+            OC = Hc * C if c.concat else C
+            if drops[l] is not None:
+                dy = dy * drops[l]
+            xs = xss[l]
+            dxs = torch.empty_like(xs)
+            dae = torch.empty(B, n, n, Hc, device=dev, dtype=torch.float32) if use_edge else None
+            dbp = torch.empty(B, OC, device=dev, dtype=torch.float32)
+            _lib.check(lib.sv2n_gat_attn_bwd(
+                dy.data_ptr(), ys[l].data_ptr(), xs.data_ptr(), xs.stride(0), pss[l].data_ptr(),
+                _lib.ptr(keeps[l]), ctx.kscales[l], _lib.ptr(layout.rowmask), dxs.data_ptr(),
+                _lib.ptr(dae), dbp.data_ptr(), B, n, Hc, C, int(c.concat), act,
+                float(c.negative_slope), st), "sv2n_gat_attn_bwd")
+            daes[l] = dae
+            gW = _grad_buf(c.lin_src.weight)
+            gas = _grad_buf(c.att_src)
+            gad = _grad_buf(c.att_dst)
+            gb = _grad_buf(c.bias)
+            T = None
+            if gW is not None or gas is not None or gad is not None:
+                T = gemm_f32(xs_in[l], False, dxs, False, F, xs.size(1), N)  # dWaugᵀ [F][ldx]
+            if T is not None or gb is not None:
+                ws_n = lib.sv2n_gat_prep_bwd_workspace(Hc, F)
+                ws = torch.empty(ws_n, device=dev, dtype=torch.float32)
+                _lib.check(lib.sv2n_gat_prep_bwd_node(
+                    _lib.ptr(T), xs.size(1), c.lin_src.weight.data_ptr(), c.att_src.data_ptr(),
+                    c.att_dst.data_ptr(), Hc, C, F, dbp.data_ptr(), B, OC, _lib.ptr(gW),
+                    _lib.ptr(gas), _lib.ptr(gad), _lib.ptr(gb), ws.data_ptr(), ws_n, st),
+                    "sv2n_gat_prep_bwd_node")
+            if l > 0 or need_x0:
+                dy = gemm_f32(dxs, True, waugs[l], False, N, F, xs.size(1))
+
+        if use_edge and ea is not None:
+            # grads exist (zeros) even without edges, as in PyG
+            need_e = [(_grad_buf(c.lin_edge.weight), _grad_buf(c.att_edge)) for c in convs]
+            if ea.size(0) > 0 and any(a is not None or b is not None for a, b in need_e):
+                E, D = ea.shape
+                ptrs = _lib.ptr_array([d.data_ptr() for d in daes])
+                ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hp)
+                ws = torch.empty(ws_n, device=dev, dtype=torch.float32)
+                dwf = torch.empty(D, hp, device=dev, dtype=torch.float32)
+                ei = layout.edge_index if layout.kind == "block" else None
+                _lib.check(lib.sv2n_edge_logits_bwd(ea.data_ptr(), E, D, _lib.ptr(ei),
+                                                    layout.canon.data_ptr(), ptrs, L, H, B, n,
+                                                    ws.data_ptr(), ws_n, dwf.data_ptr(), hp, st),
+                           "sv2n_edge_logits_bwd")
+                for l, c in enumerate(convs):
+                    gWe, gae = need_e[l]
+                    _lib.check(lib.sv2n_gat_prep_bwd_edge(
+                        dwf.data_ptr(), hp, l * H, c.lin_edge.weight.data_ptr(),
+                        c.att_edge.data_ptr(), c.heads, c.out_channels, D, _lib.ptr(gWe),
+                        _lib.ptr(gae), st), "sv2n_gat_prep_bwd_edge")
+        dx0 = dy if need_x0 else None
+        n_params = len(ctx.needs_input_grad) - 7
+        return (dx0, None, None, None, None, None, None) + (None,) * n_params
+
+
+def gat_stack(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs: Sequence,
+              layout: GraphLayout, act: int, post_dropout: float, training: bool) -> torch.Tensor:
+    """Run ``convs`` (GATConv modules) as one fused autograd node."""
+    _require_device(x, edge_attr)
+    if edge_attr is not None and edge_attr.requires_grad:
+        raise NotImplementedError("gradients w.r.t. edge_attr are not supported (the reference "
+                                  "treats edge_attr as data)")
+    params = []
+    for c in convs:
+        params += layer_params(c)
+    for p in params:
+        if p.device != x.device:
+            raise RuntimeError("parameters and data must be on the same device")
+    return _GATStack.apply(x, edge_attr, tuple(convs), layout, int(act), float(post_dropout),
+                           bool(training), *params)
