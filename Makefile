@@ -10,7 +10,7 @@ LIB := spotv2net_amd/libsv2n.so
 
 all: $(LIB)
 
-build/%.o: spotv2net_amd/csrc/%.hip spotv2net_amd/csrc/sv2n_common.h include/sv2n.h
+build/%.o: spotv2net_amd/csrc/%.hip $(wildcard spotv2net_amd/csrc/*.h) include/sv2n.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -102,11 +102,13 @@ int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, int edge_dim
  *   rowmask [N] uint32 (bit j of row g*n+i: edge j->i present) or NULL for
  *           complete graphs.
  *   bias    [H*C] (concat) or [C] (mean).
- *   keep    [num_graphs][H][n][n] uint8 attention-dropout keep mask or NULL;
- *           kept probabilities are scaled by keep_scale.
+ *   keep    [num_graphs][H][32][32] uint8 attention-dropout keep mask (entry
+ *           [g][h][i][j] for edge j->i) or NULL; kept probabilities are
+ *           scaled by keep_scale.
  *   y       [N][concat ? H*C : C] = act(concat|mean(Σ_j p_ij·xs_j) + bias).
- *   psave   [num_graphs][H][n][n] softmax probabilities (pre-dropout) whose
- *           sign bit records leaky_relu's negative side (for the backward). */
+ *   psave   [num_graphs][H][32][32] softmax probabilities (pre-dropout; rows
+ *           padded to 32, absent edges 0) whose sign bit records leaky_relu's
+ *           negative side (for the backward). */
 int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, const uint32_t* rowmask,
                       const float* bias, const uint8_t* keep, float keep_scale,
                       float* y, float* psave,

@@ -6,21 +6,36 @@
 // One workgroup (256 threads = 4 waves) owns one graph g.  Per head h the
 // incoming edges of target i form row i of a 32-padded n x n matrix, so
 // PyG's per-target softmax (scatter_max / scatter_sum over edge_index[1]) is a
-// row softmax reduced inside one 32-lane half of a wave, the self loop with
+// row softmax reduced inside one 32-lane half of a wave, and the self loop with
 // fill_value='mean' is the mean of the row's stored edge logits (linearity of
-// lin_edge), and the scatter-add aggregation is the row-by-column product
-// P(n x n) · xs_h(n x C) with P broadcast from LDS.
+// lin_edge).  The message passing products are 32x32 MFMA tiles
+// (v_mfma_f32_32x32x2_f32: exact f32, k-ordered fma chains):
+//   forward    out_h   = P_h (n x n) · xs_h (n x C)             (scatter-add, a10)
+//   backward   dP_hᵀ   = xs_h · dOut_hᵀ                        (message bwd)
+//              dxs_h   = P_hᵀ · dOut_h                         (gather bwd)
+// with P in LDS as [h][i][j] (row stride 33 floats: conflict-free for row and
+// column fragment reads) and xs / dOut rows read coalesced from HBM.
 //
-// HBM traffic per graph (fwd): xs rows n*ldx*4 B read once, ae slab n*n*H*4 B,
-// y rows written once, P saved (n*n*H*4 B).
+// Saved probabilities / keep masks use a padded [g][h][32][32] layout
+// (16-B aligned rows); the sign bit of a saved probability records
+// leaky_relu's negative side for the backward.
 #include "sv2n_common.h"
 
 namespace sv2n {
 
 constexpr int ATT_THREADS = 256;
+constexpr int TS = 33;  // LDS tile row stride (floats)
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// C/D row of accumulator register r for lane half hf (32x32 MFMA layout)
+__device__ __forceinline__ int crow(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
+
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // ---------------------------------------------------------------------------
 // forward
+// LDS: sP[H][32][TS] | sA[H][32] | sD[H][32]
 // ---------------------------------------------------------------------------
 template <int ACT, bool CONCAT>
 __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
@@ -28,12 +43,14 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
     const uint32_t* __restrict__ rowmask, const float* __restrict__ bias,
     const uint8_t* __restrict__ keep, float keep_scale, float* __restrict__ y,
     float* __restrict__ psave, int n, int H, int C, float slope) {
-  __shared__ __attribute__((aligned(16))) float sPT[SV2N_MAX_HEADS][32][SV2N_PSTR];  // [h][j][i]
-  __shared__ float sA[SV2N_MAX_HEADS][32];
-  __shared__ float sD[SV2N_MAX_HEADS][32];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sP = smem;
+  float* sA = sP + H * 32 * TS;
+  float* sD = sA + H * 32;
 
   const int g = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
   const int64_t row0 = (int64_t)g * n;
   const int HC = H * C;
 
@@ -45,23 +62,21 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
       as = r[h];
       ad = r[H + h];
     }
-    sA[h][j] = as;
-    sD[h][j] = ad;
+    sA[idx] = as;
+    sD[idx] = ad;
   }
   __syncthreads();
 
-  // ---- per-target softmax, two rows per wave instruction ----
-  const int R = H * n;
-  const int half = lane >> 5, j = lane & 31;
-  for (int rb = wave * 2; rb < R; rb += 8) {  // wave-uniform trip count
+  // ---- per-target softmax over all 32 (padded) rows of every head ----
+  const int j = l32;
+  for (int rb = wave * 2; rb < H * 32; rb += 8) {
     const int r = rb + half;
-    const bool rv = r < R;
-    const int h = rv ? r / n : 0;
-    const int i = rv ? r - h * n : 0;
-    const uint32_t bits = row_bits(rowmask, row0 + i, n, i);
+    const int h = r >> 5, i = r & 31;
+    const bool rv = i < n;
+    const uint32_t bits = rv ? row_bits(rowmask, row0 + i, n, i) : 0u;
     const bool off = rv && j < n && j != i && ((bits >> j) & 1u);
     const bool valid = rv && j < n && (j == i || off);
-    float s = sA[h][j] + sD[h][i];
+    float s = sA[h * 32 + j] + sD[h * 32 + i];
     if (ae) {
       const float e = off ? ae[((row0 + i) * n + j) * H + h] : 0.f;
       const float esum = red32_sum(e);
@@ -76,54 +91,51 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
     const float den = red32_sum(ex);
     const float p = ex / (den + 1e-16f);
     float pd = valid ? p : 0.f;
-    if (rv && j < n) {  // absent edges store 0 so the backward reads finite P
-      const int64_t pidx = (((int64_t)g * H + h) * n + i) * n + j;
+    if (rv) {
+      const int64_t pidx = (((int64_t)g * H + h) * 32 + i) * 32 + j;
       psave[pidx] = valid ? (neg ? -p : p) : 0.f;
       if (keep && valid) pd = keep[pidx] ? p * keep_scale : 0.f;
     }
-    if (rv) sPT[h][j][i] = pd;
+    sP[(h * 32 + i) * TS + j] = pd;
   }
   __syncthreads();
 
-  // ---- aggregation + head combine + bias + activation ----
+  // ---- aggregation on MFMA: acc[i][c] = Σ_j P[h][i][j] · xs[j][h*C + c] ----
+  const int nck = (C + 31) / 32;
+  const int items = CONCAT ? H * nck : nck;
   const int OC = CONCAT ? HC : C;
-  for (int oc = t; oc < OC; oc += ATT_THREADS) {
-    float sum[32];
+  const float invH = 1.f / (float)H;
+  for (int it = wave; it < items; it += 4) {
+    const int hb = CONCAT ? it / nck : 0;
+    const int c0 = 32 * (CONCAT ? it - hb * nck : it);
+    const int he = CONCAT ? hb + 1 : H;
+    const int c = c0 + l32;
+    const bool cok = c < C;
+    floatx16 acc;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) sum[i] = 0.f;
-    const int h0 = CONCAT ? oc / C : 0;
-    const int h1 = CONCAT ? h0 + 1 : H;
-    for (int h = h0; h < h1; ++h) {
-      const int col = CONCAT ? oc : h * C + oc;
-      float xv[32];
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int h = hb; h < he; ++h) {
+      float bv[16];
 #pragma unroll
-      for (int jj = 0; jj < 32; ++jj) xv[jj] = (jj < n) ? xs[(row0 + jj) * ldx + col] : 0.f;
-      float acc[32];
-#pragma unroll
-      for (int i = 0; i < 32; ++i) acc[i] = 0.f;
-#pragma unroll
-      for (int jj = 0; jj < 32; ++jj) {
-        if (jj < n) {
-          const float4* pr = reinterpret_cast<const float4*>(&sPT[h][jj][0]);
-#pragma unroll
-          for (int i4 = 0; i4 < 8; ++i4) {
-            const float4 pv = pr[i4];
-            acc[4 * i4 + 0] = fmaf(pv.x, xv[jj], acc[4 * i4 + 0]);
-            acc[4 * i4 + 1] = fmaf(pv.y, xv[jj], acc[4 * i4 + 1]);
-            acc[4 * i4 + 2] = fmaf(pv.z, xv[jj], acc[4 * i4 + 2]);
-            acc[4 * i4 + 3] = fmaf(pv.w, xv[jj], acc[4 * i4 + 3]);
-          }
-        }
+      for (int kk = 0; kk < 16; ++kk) {
+        const int jj = 2 * kk + half;
+        bv[kk] = (jj < n && cok) ? xs[(row0 + jj) * ldx + h * C + c] : 0.f;
       }
+      const float* prow = sP + (h * 32 + l32) * TS + half;
 #pragma unroll
-      for (int i = 0; i < 32; ++i) sum[i] += acc[i];
+      for (int kk = 0; kk < 16; ++kk)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(prow[2 * kk], bv[kk], acc, 0, 0, 0);
     }
-    const float b = bias ? bias[oc] : 0.f;
+    if (cok) {
+      const int oc = CONCAT ? hb * C + c : c;
+      const float b = bias ? bias[oc] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      if (i < n) {
-        const float z = (CONCAT ? sum[i] : sum[i] / (float)H) + b;
-        y[(row0 + i) * OC + oc] = act_fwd<ACT>(z);
+      for (int r = 0; r < 16; ++r) {
+        const int i = crow(r, half);
+        if (i < n) {
+          const float z = (CONCAT ? acc[r] : acc[r] * invH) + b;
+          y[(row0 + i) * OC + oc] = act_fwd<ACT>(z);
+        }
       }
     }
   }
@@ -131,10 +143,9 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
 
 // ---------------------------------------------------------------------------
 // backward
-// dynamic LDS (floats): sPd[H][32][PSTR] | sG[H][32][PSTR] | sO[H][CK][PSTR] | sX[H][CK][PSTR]
+// LDS: sP[H][32][TS] (post-dropout P) | per wave: tO[32][TS] (dOut chunk, [i][c]),
+//      tX[32][TS] (xs chunk [j][c], later dLᵀ [j][i])
 // ---------------------------------------------------------------------------
-constexpr int BWD_CK = 16;
-
 template <int ACT, bool CONCAT>
 __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ xs,
@@ -142,172 +153,154 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
     const uint32_t* __restrict__ rowmask, float* __restrict__ dxs, float* __restrict__ dae,
     float* __restrict__ dbias_part, int n, int H, int C, float slope) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int PS = 32 * SV2N_PSTR;
-  float* sPd = smem;                       // post-dropout P   [h][i][j]
-  float* sG = sPd + H * PS;                // dP, then dL      [h][i][j]
-  float* sO = sG + H * PS;                 // dOut chunk       [h][c][i]
-  float* sX = sO + H * BWD_CK * SV2N_PSTR; // xs chunk         [h][c][j]
-
   const int g = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
   const int64_t row0 = (int64_t)g * n;
   const int HC = H * C;
   const int OC = CONCAT ? HC : C;
   const float invH = 1.f / (float)H;
-  const int64_t pbase = (int64_t)g * H * n * n;
+  const int64_t pbase = (int64_t)g * H * 1024;
+  float* sP = smem;
+  float* tO = sP + H * 32 * TS + wave * 2 * 32 * TS;
+  float* tX = tO + 32 * TS;
 
-  // phase 1: post-dropout probabilities
-  for (int idx = t; idx < H * n * n; idx += ATT_THREADS) {
-    const int h = idx / (n * n);
-    const int rem = idx - h * n * n;
-    const int i = rem / n, j = rem - i * n;
-    const float p = fabsf(psave[pbase + idx]);
-    float pd = p;
-    if (keep) pd = keep[pbase + idx] ? p * keep_scale : 0.f;
-    sPd[h * PS + i * SV2N_PSTR + j] = pd;
-  }
-
-  // phase 2: dP[h][i][j] = Σ_c dOut[i][h][c] · xs[j][h][c], 4x4 register tiles
-  const int ntile = H * 64;
-  float acc0[16], acc1[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) { acc0[k] = 0.f; acc1[k] = 0.f; }
-  for (int c0 = 0; c0 < C; c0 += BWD_CK) {
-    const int ck = min(BWD_CK, C - c0);
-    __syncthreads();
-    for (int idx = t; idx < H * 32 * BWD_CK; idx += ATT_THREADS) {
-      const int c = idx % BWD_CK;
-      const int i = (idx / BWD_CK) & 31;
-      const int h = idx / (BWD_CK * 32);
-      float vo = 0.f, vx = 0.f;
-      if (i < n && c < ck) {
-        const int col = h * C + c0 + c;
-        vx = xs[(row0 + i) * ldx + col];
-        const int oc = CONCAT ? col : c0 + c;
-        const float dz = act_bwd<ACT>(dy[(row0 + i) * OC + oc], y[(row0 + i) * OC + oc]);
-        vo = CONCAT ? dz : dz * invH;
-      }
-      sO[(h * BWD_CK + c) * SV2N_PSTR + i] = vo;
-      sX[(h * BWD_CK + c) * SV2N_PSTR + i] = vx;
+  for (int idx = t; idx < H * 1024; idx += ATT_THREADS) {
+    const int h = idx >> 10, i = (idx >> 5) & 31, jj = idx & 31;
+    float pd = 0.f;
+    if (i < n) {
+      pd = fabsf(psave[pbase + idx]);
+      if (keep) pd = keep[pbase + idx] ? pd * keep_scale : 0.f;
     }
-    __syncthreads();
+    sP[(h * 32 + i) * TS + jj] = pd;
+  }
+  __syncthreads();
+
+  for (int h = wave; h < H; h += 4) {
+    floatx16 G;  // dPᵀ: G[j][i] = Σ_c xs[j][c] · dOut[i][c]
 #pragma unroll
-    for (int rep = 0; rep < 2; ++rep) {
-      const int tt = t + rep * ATT_THREADS;
-      if (tt < ntile) {
-        const int h = tt >> 6, ib = (tt >> 3) & 7, jb = tt & 7;
-        float* acc = rep == 0 ? acc0 : acc1;
-        for (int c = 0; c < ck; ++c) {
-          const float4 a = *reinterpret_cast<const float4*>(sO + (h * BWD_CK + c) * SV2N_PSTR + 4 * ib);
-          const float4 b = *reinterpret_cast<const float4*>(sX + (h * BWD_CK + c) * SV2N_PSTR + 4 * jb);
-          const float av[4] = {a.x, a.y, a.z, a.w};
-          const float bv[4] = {b.x, b.y, b.z, b.w};
+    for (int r = 0; r < 16; ++r) G[r] = 0.f;
+    for (int c0 = 0; c0 < C; c0 += 32) {
+      const int c = c0 + l32;
+      const bool cok = c < C;
+      const int ycol = CONCAT ? h * C + c : c;
+      float bsum = 0.f;
+#pragma unroll 4
+      for (int s = 0; s < 16; ++s) {
+        const int rr = half + 2 * s;
+        const bool ok = rr < n && cok;
+        const float dz = ok ? act_bwd<ACT>(dy[(row0 + rr) * OC + ycol], y[(row0 + rr) * OC + ycol])
+                            : 0.f;
+        bsum += dz;
+        tO[rr * TS + l32] = CONCAT ? dz : dz * invH;
+        tX[rr * TS + l32] = ok ? xs[(row0 + rr) * ldx + h * C + c] : 0.f;
+      }
+      bsum += __shfl_xor(bsum, 32, 64);
+      if (half == 0 && cok && (CONCAT || h == 0)) dbias_part[(int64_t)g * OC + ycol] = bsum;
+      lds_fence();
+      // G += X · Oᵀ   (A[j][c] = tX[j][c], B[c][i] = tO[i][c])
+      const float* xr = tX + l32 * TS + half;
+      const float* orow = tO + l32 * TS + half;
 #pragma unroll
-          for (int x = 0; x < 4; ++x)
+      for (int kk = 0; kk < 16; ++kk)
+        G = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[2 * kk], orow[2 * kk], G, 0, 0, 0);
+      // dxs chunk = Pdᵀ · O   (A[j][i] = sP[h][i][j], B[i][c] = tO[i][c])
+      floatx16 D2;
 #pragma unroll
-            for (int z = 0; z < 4; ++z) acc[4 * x + z] = fmaf(av[x], bv[z], acc[4 * x + z]);
+      for (int r = 0; r < 16; ++r) D2[r] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const int ii = 2 * kk + half;
+        D2 = __builtin_amdgcn_mfma_f32_32x32x2f32(sP[(h * 32 + ii) * TS + l32], tO[ii * TS + l32],
+                                                  D2, 0, 0, 0);
+      }
+      if (cok) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int jr = crow(r, half);
+          if (jr < n) dxs[(row0 + jr) * ldx + h * C + c] = D2[r];
         }
       }
+      lds_fence();  // tile reads retired before the next chunk overwrites them
     }
-  }
-#pragma unroll
-  for (int rep = 0; rep < 2; ++rep) {
-    const int tt = t + rep * ATT_THREADS;
-    if (tt < ntile) {
-      const int h = tt >> 6, ib = (tt >> 3) & 7, jb = tt & 7;
-      const float* acc = rep == 0 ? acc0 : acc1;
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int z = 0; z < 4; ++z) sG[h * PS + (4 * ib + x) * SV2N_PSTR + 4 * jb + z] = acc[4 * x + z];
-    }
-  }
-  __syncthreads();
 
-  // phase 3: softmax + leaky_relu backward per target row, self-loop share,
-  //          dAE, d a_dst
-  const int R = H * n;
-  const int half = lane >> 5, j = lane & 31;
-  for (int rb = wave * 2; rb < R; rb += 8) {
-    const int r = rb + half;
-    const bool rv = r < R;
-    const int h = rv ? r / n : 0;
-    const int i = rv ? r - h * n : 0;
-    const uint32_t bits = row_bits(rowmask, row0 + i, n, i);
-    const bool off = rv && j < n && j != i && ((bits >> j) & 1u);
-    const bool valid = rv && j < n && (j == i || off);
-    const int64_t pidx = pbase + ((int64_t)h * n + i) * n + j;
-    const float ps = valid ? psave[pidx] : 0.f;
-    const float p = fabsf(ps);
-    const bool neg = signbit(ps);
-    float dp = valid ? sG[h * PS + i * SV2N_PSTR + j] : 0.f;
-    if (keep) dp = (valid && keep[pidx]) ? dp * keep_scale : 0.f;
-    const float tsum = red32_sum(p * dp);
-    const float ds = p * (dp - tsum);
-    const float dl = valid ? (neg ? ds * slope : ds) : 0.f;
-    const float dad = red32_sum(dl);
-    const float dlii = __shfl(dl, (lane & 32) | i, 64);
-    if (dae && rv && j < n) {
+    // ---- softmax + leaky_relu backward on G: lane column i, rows j = crow(r, half) ----
+    const int i = l32;
+    const bool iv = i < n;
+    const uint32_t bits = iv ? row_bits(rowmask, row0 + i, n, i) : 0u;
+    const int64_t prow = pbase + ((int64_t)h * 32 + i) * 32;
+    float ps[16];
+    uint32_t kp[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int jb = 8 * q + 4 * half;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (iv) v = *reinterpret_cast<const float4*>(psave + prow + jb);
+      ps[4 * q + 0] = v.x;
+      ps[4 * q + 1] = v.y;
+      ps[4 * q + 2] = v.z;
+      ps[4 * q + 3] = v.w;
+      kp[q] = (keep && iv) ? *reinterpret_cast<const uint32_t*>(keep + prow + jb) : 0u;
+    }
+    float dp[16];
+    float tl = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jr = crow(r, half);
+      const bool valid = iv && jr < n && (jr == i || ((bits >> jr) & 1u));
+      float d = valid ? G[r] : 0.f;
+      if (keep) d = ((kp[r >> 2] >> (8 * (r & 3))) & 0xffu) ? d * keep_scale : 0.f;
+      dp[r] = d;
+      tl += fabsf(ps[r]) * d;
+    }
+    tl += __shfl_xor(tl, 32, 64);
+    float dl[16];
+    float dad = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jr = crow(r, half);
+      const bool valid = iv && jr < n && (jr == i || ((bits >> jr) & 1u));
+      const float p = fabsf(ps[r]);
+      const float ds = p * (dp[r] - tl);
+      dl[r] = valid ? (signbit(ps[r]) ? ds * slope : ds) : 0.f;
+      dad += dl[r];
+    }
+    dad += __shfl_xor(dad, 32, 64);
+    if (half == 0 && iv) dxs[(row0 + i) * ldx + HC + H + h] = dad;
+    // dl[i][i] sits in half (i>>2)&1, register (i&3) + 4*(i>>3)
+    const int hi = (i >> 2) & 1, ri = (i & 3) + 4 * (i >> 3);
+    float mine = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mine = (r == ri) ? dl[r] : mine;
+    const float other = __shfl_xor(mine, 32, 64);
+    const float dlii = (half == hi) ? mine : other;
+    if (dae && iv) {
       const int cnt = __popc(bits);
       const float share = cnt > 0 ? dlii / (float)cnt : 0.f;
-      dae[((row0 + i) * n + j) * H + h] = off ? dl + share : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int jr = crow(r, half);
+        if (jr < n)
+          dae[((row0 + i) * n + jr) * H + h] =
+              (jr != i && ((bits >> jr) & 1u)) ? dl[r] + share : 0.f;
+      }
     }
-    if (rv && j == 0) dxs[(row0 + i) * ldx + HC + H + h] = dad;
-    if (rv) sG[h * PS + i * SV2N_PSTR + j] = dl;
-  }
-  __syncthreads();
-
-  // phase 4: d a_src[j][h] = Σ_i dL[h][i][j]; zero the padding columns
-  for (int idx = t; idx < H * 32; idx += ATT_THREADS) {
-    const int h = idx >> 5, jj = idx & 31;
-    if (jj < n) {
+    // d a_src[j] = Σ_i dL[i][j]: transpose through LDS (tX as [j][i])
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tX[crow(r, half) * TS + i] = dl[r];
+    lds_fence();
+    if (lane < 32 && lane < n) {
       float s = 0.f;
-      for (int i = 0; i < n; ++i) s += sG[h * PS + i * SV2N_PSTR + jj];
-      dxs[(row0 + jj) * ldx + HC + h] = s;
+      for (int ii = 0; ii < 32; ++ii) s += tX[lane * TS + ii];
+      dxs[(row0 + lane) * ldx + HC + h] = s;
     }
+    lds_fence();
   }
+
   const int npad = ldx - (HC + 2 * H);
   for (int idx = t; idx < n * npad; idx += ATT_THREADS) {
     const int rr = idx / npad;
     dxs[(row0 + rr) * ldx + HC + 2 * H + (idx - rr * npad)] = 0.f;
-  }
-
-  // phase 5: dxs[j][h*C+c] = Σ_i Pd[h][i][j] · dOut[i][h][c]; bias partials
-  for (int oc = t; oc < HC; oc += ATT_THREADS) {
-    const int h = oc / C;
-    const int c = oc - h * C;
-    const int ycol = CONCAT ? oc : c;
-    float dz[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i)
-      dz[i] = (i < n) ? act_bwd<ACT>(dy[(row0 + i) * OC + ycol], y[(row0 + i) * OC + ycol]) : 0.f;
-    if (CONCAT || h == 0) {
-      float bsum = 0.f;
-#pragma unroll
-      for (int i = 0; i < 32; ++i) bsum += dz[i];
-      dbias_part[(int64_t)g * OC + ycol] = bsum;
-    }
-    float acc[32];
-#pragma unroll
-    for (int jj = 0; jj < 32; ++jj) acc[jj] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      if (i < n) {
-        const float d = CONCAT ? dz[i] : dz[i] * invH;
-        const float4* pr = reinterpret_cast<const float4*>(sPd + h * PS + i * SV2N_PSTR);
-#pragma unroll
-        for (int j4 = 0; j4 < 8; ++j4) {
-          const float4 pv = pr[j4];
-          acc[4 * j4 + 0] = fmaf(pv.x, d, acc[4 * j4 + 0]);
-          acc[4 * j4 + 1] = fmaf(pv.y, d, acc[4 * j4 + 1]);
-          acc[4 * j4 + 2] = fmaf(pv.z, d, acc[4 * j4 + 2]);
-          acc[4 * j4 + 3] = fmaf(pv.w, d, acc[4 * j4 + 3]);
-        }
-      }
-    }
-#pragma unroll
-    for (int jj = 0; jj < 32; ++jj)
-      if (jj < n) dxs[(row0 + jj) * ldx + oc] = acc[jj];
   }
 }
 
@@ -316,25 +309,33 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
 // ============================ C-ABI ========================================
 using namespace sv2n;
 
+static size_t fwd_lds(int H) { return sizeof(float) * ((size_t)H * 32 * TS + 2 * (size_t)H * 32); }
+static size_t bwd_lds(int H) { return sizeof(float) * ((size_t)H * 32 * TS + 4 * 2 * 32 * TS); }
+
+template <typename K>
+static void raise_lds(K kernel, size_t bytes) {
+  if (bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+}
+
 template <int ACT, bool CONCAT>
 static void launch_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
                        const uint32_t* rowmask, const float* bias, const uint8_t* keep,
                        float keep_scale, float* y, float* psave, int n, int H, int C, float slope) {
-  hipLaunchKernelGGL((k_attn_fwd<ACT, CONCAT>), dim3((unsigned)B), dim3(ATT_THREADS), 0, st, xs,
+  const size_t lds = fwd_lds(H);
+  raise_lds(k_attn_fwd<ACT, CONCAT>, lds);
+  hipLaunchKernelGGL((k_attn_fwd<ACT, CONCAT>), dim3((unsigned)B), dim3(ATT_THREADS), lds, st, xs,
                      ldx, ae, rowmask, bias, keep, keep_scale, y, psave, n, H, C, slope);
 }
 
 template <int ACT, bool CONCAT>
-static void launch_bwd(int64_t B, hipStream_t st, size_t lds, const float* dy, const float* y,
+static void launch_bwd(int64_t B, hipStream_t st, const float* dy, const float* y,
                        const float* xs, int ldx, const float* psave, const uint8_t* keep,
                        float keep_scale, const uint32_t* rowmask, float* dxs, float* dae,
                        float* dbias, int n, int H, int C, float slope) {
-  static bool raised = false;
-  if (!raised && lds > 65536) {
-    (void)hipFuncSetAttribute((const void*)k_attn_bwd<ACT, CONCAT>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    raised = true;
-  }
+  const size_t lds = bwd_lds(H);
+  raise_lds(k_attn_bwd<ACT, CONCAT>, lds);
   hipLaunchKernelGGL((k_attn_bwd<ACT, CONCAT>), dim3((unsigned)B), dim3(ATT_THREADS), lds, st, dy,
                      y, xs, ldx, psave, keep, keep_scale, rowmask, dxs, dae, dbias, n, H, C, slope);
 }
@@ -380,14 +381,12 @@ extern "C" int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* x
                                  hipStream_t stream) {
   if (!dy || !y || !xs || !psave || !dxs || !dbias_partial) return SV2N_ERR_ARG;
   if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
-  const size_t lds = sizeof(float) * (size_t)heads * (2 * 32 * SV2N_PSTR + 2 * BWD_CK * SV2N_PSTR);
-  if (lds > 160 * 1024) return SV2N_ERR_SHAPE;
   if (concat) {
-    SV2N_DISPATCH_ACT(launch_bwd, true, num_graphs, stream, lds, dy, y, xs, ldx, psave, keep,
+    SV2N_DISPATCH_ACT(launch_bwd, true, num_graphs, stream, dy, y, xs, ldx, psave, keep,
                       keep_scale, rowmask, dxs, dae, dbias_partial, n, heads, channels,
                       negative_slope)
   } else {
-    SV2N_DISPATCH_ACT(launch_bwd, false, num_graphs, stream, lds, dy, y, xs, ldx, psave, keep,
+    SV2N_DISPATCH_ACT(launch_bwd, false, num_graphs, stream, dy, y, xs, ldx, psave, keep,
                       keep_scale, rowmask, dxs, dae, dbias_partial, n, heads, channels,
                       negative_slope)
   }

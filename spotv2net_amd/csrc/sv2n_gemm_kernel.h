@@ -1,0 +1,261 @@
+// f32-MFMA GEMM kernel template shared by the library (sv2n_gemm.hip) and the
+// standalone tuner (tools/gemm_tune.hip).
+//
+//   C[M][N] = Σ_k A(m,k) · B(n,k)
+//   A(m,k) = A[m*lda + k] (AK) or A[k*lda + m];  B(n,k) = B[n*ldb + k] (BK) or B[k*ldb + n]
+//
+// v_mfma_f32_16x16x4_f32 (exact f32, 157 TF chip peak): lane l supplies
+// A[l&15][k = l>>4] and B[k = l>>4][l&15]; C/D: col = l&15, row = 4*(l>>4)+reg.
+// Workgroup = NW waves; wave w owns rows [16*MT*w, 16*MT*(w+1)) of the block
+// tile and all NT 16-column tiles (BM = 16*MT*NW, BN = 16*NT).  K-steps of KB
+// are staged through two LDS buffers in k-major [k][row] images (row stride
+// ≡ 16 mod 32 dwords => conflict-free ds_read_b32 fragments); PF register
+// sets prefetch the next PF tiles from global memory while the MFMAs of the
+// current one run; one barrier per K-step.  gridDim.z = split-K slices, whose
+// partial slabs are summed in fixed order by k_splitk_reduce.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sv2n {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ constexpr int gemm_lds_stride(int rows) {
+  return rows + ((16 - rows % 32) + 32) % 32;  // smallest stride >= rows, ≡ 16 (mod 32)
+}
+
+template <int ROWS, int KB, bool KMAJOR, int THREADS>
+struct GemmTile {
+  static constexpr int NV = ROWS * KB / 4;  // float4 slots per tile
+  static constexpr int PER = (NV + THREADS - 1) / THREADS;
+  static constexpr int STRIDE = gemm_lds_stride(ROWS);
+  float4 v[PER];
+
+  __device__ __forceinline__ void load(const float* __restrict__ base, int64_t ld, int64_t r0,
+                                       int64_t rmax, int64_t k0, int64_t kmax, bool vec, int t) {
+#pragma unroll
+    for (int s = 0; s < PER; ++s) {
+      const int idx = t + s * THREADS;
+      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (NV % THREADS == 0 || idx < NV) {
+        if constexpr (KMAJOR) {
+          const int64_t r = r0 + idx / (KB / 4);
+          const int64_t k = k0 + 4 * (idx % (KB / 4));
+          if (r < rmax) {
+            const float* p = base + r * ld + k;
+            if (vec && k + 3 < kmax) {
+              x = *reinterpret_cast<const float4*>(p);
+            } else {
+              if (k + 0 < kmax) x.x = p[0];
+              if (k + 1 < kmax) x.y = p[1];
+              if (k + 2 < kmax) x.z = p[2];
+              if (k + 3 < kmax) x.w = p[3];
+            }
+          }
+        } else {
+          const int64_t k = k0 + idx / (ROWS / 4);
+          const int64_t r = r0 + 4 * (idx % (ROWS / 4));
+          if (k < kmax) {
+            const float* p = base + k * ld + r;
+            if (vec && r + 3 < rmax) {
+              x = *reinterpret_cast<const float4*>(p);
+            } else {
+              if (r + 0 < rmax) x.x = p[0];
+              if (r + 1 < rmax) x.y = p[1];
+              if (r + 2 < rmax) x.z = p[2];
+              if (r + 3 < rmax) x.w = p[3];
+            }
+          }
+        }
+      }
+      v[s] = x;
+    }
+  }
+
+  __device__ __forceinline__ void store(float* __restrict__ lds, int t) const {
+#pragma unroll
+    for (int s = 0; s < PER; ++s) {
+      const int idx = t + s * THREADS;
+      if (NV % THREADS == 0 || idx < NV) {
+        if constexpr (KMAJOR) {
+          const int r = idx / (KB / 4), k = 4 * (idx % (KB / 4));
+          lds[(k + 0) * STRIDE + r] = v[s].x;
+          lds[(k + 1) * STRIDE + r] = v[s].y;
+          lds[(k + 2) * STRIDE + r] = v[s].z;
+          lds[(k + 3) * STRIDE + r] = v[s].w;
+        } else {
+          const int k = idx / (ROWS / 4), r = 4 * (idx % (ROWS / 4));
+          *reinterpret_cast<float4*>(lds + k * STRIDE + r) = v[s];
+        }
+      }
+    }
+  }
+};
+
+template <int NW, int MT, int NT, int KB, bool AK, bool BK, int PF>
+struct GemmCfg {
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int BM = 16 * MT * NW, BN = 16 * NT;
+  using TA = GemmTile<BM, KB, AK, THREADS>;
+  using TB = GemmTile<BN, KB, BK, THREADS>;
+  static constexpr int SA = TA::STRIDE, SB = TB::STRIDE;
+  static constexpr int BUF = KB * (SA + SB);
+  static constexpr int LDS_BYTES = 2 * BUF * 4;
+};
+
+template <int NW, int MT, int NT, int KB, bool AK, bool BK, int PF>
+__global__ __launch_bounds__(64 * NW) void k_gemm_f32(
+    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
+    float* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int64_t kslice,
+    bool avec, bool bvec, float* __restrict__ part) {
+  using Cfg = GemmCfg<NW, MT, NT, KB, AK, BK, PF>;
+  using TA = typename Cfg::TA;
+  using TB = typename Cfg::TB;
+  constexpr int SA = Cfg::SA, SB = Cfg::SB, BUF = Cfg::BUF, T = Cfg::THREADS;
+  __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * Cfg::BM, n0 = (int64_t)blockIdx.y * Cfg::BN;
+  const int64_t kb = (int64_t)blockIdx.z * kslice;
+  const int64_t ke = min(K, kb + kslice);
+  const int nk = (int)((ke - kb + KB - 1) / KB);
+
+  floatx4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int li = lane & 15, lk = lane >> 4;
+  auto compute = [&](const float* sa, const float* sb) {
+#pragma unroll
+    for (int ks = 0; ks < KB / 4; ++ks) {
+      const int k = 4 * ks + lk;
+      float af[MT];
+#pragma unroll
+      for (int a = 0; a < MT; ++a) af[a] = sa[k * SA + wave * 16 * MT + 16 * a + li];
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        const float bf = sb[k * SB + 16 * b + li];
+#pragma unroll
+        for (int a = 0; a < MT; ++a)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a], bf, acc[a][b], 0, 0, 0);
+      }
+    }
+  };
+
+  TA ra0, ra1;
+  TB rb0, rb1;
+  if (nk > 0) {
+    ra0.load(A, lda, m0, M, kb, ke, avec, t);
+    rb0.load(B, ldb, n0, N, kb, ke, bvec, t);
+    ra0.store(lds, t);
+    rb0.store(lds + KB * SA, t);
+    if (PF == 2 && nk > 1) {
+      ra1.load(A, lda, m0, M, kb + KB, ke, avec, t);
+      rb1.load(B, ldb, n0, N, kb + KB, ke, bvec, t);
+    }
+  }
+  __syncthreads();
+
+  if constexpr (PF == 1) {
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) {
+        const int64_t k0 = kb + (int64_t)(kt + 1) * KB;
+        ra0.load(A, lda, m0, M, k0, ke, avec, t);
+        rb0.load(B, ldb, n0, N, k0, ke, bvec, t);
+      }
+      const float* sa = lds + cur * BUF;
+      compute(sa, sa + KB * SA);
+      if (more) {
+        float* nxt = lds + (cur ^ 1) * BUF;
+        ra0.store(nxt, t);
+        rb0.store(nxt + KB * SA, t);
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
+    // two register sets: tile kt+1 is already in (ra1, rb1) when step kt starts
+    for (int kt = 0; kt < nk; kt += 2) {
+      {  // even step: compute buf 0, refill set 0 with tile kt+2, store set 1 -> buf 1
+        if (kt + 2 < nk) {
+          const int64_t k0 = kb + (int64_t)(kt + 2) * KB;
+          ra0.load(A, lda, m0, M, k0, ke, avec, t);
+          rb0.load(B, ldb, n0, N, k0, ke, bvec, t);
+        }
+        compute(lds, lds + KB * SA);
+        if (kt + 1 < nk) {
+          ra1.store(lds + BUF, t);
+          rb1.store(lds + BUF + KB * SA, t);
+        }
+        __syncthreads();
+      }
+      if (kt + 1 < nk) {  // odd step: compute buf 1, refill set 1 with tile kt+3, store set 0 -> buf 0
+        if (kt + 3 < nk) {
+          const int64_t k0 = kb + (int64_t)(kt + 3) * KB;
+          ra1.load(A, lda, m0, M, k0, ke, avec, t);
+          rb1.load(B, ldb, n0, N, k0, ke, bvec, t);
+        }
+        compute(lds + BUF, lds + BUF + KB * SA);
+        if (kt + 2 < nk) {
+          ra0.store(lds, t);
+          rb0.store(lds + KB * SA, t);
+        }
+        __syncthreads();
+      }
+    }
+  }
+
+  float* out = part ? part + (int64_t)blockIdx.z * M * N : C;
+  const int64_t ldo = part ? N : ldc;
+#pragma unroll
+  for (int a = 0; a < MT; ++a) {
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int64_t col = n0 + 16 * b + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wave * 16 * MT + 16 * a + 4 * lk + r;
+        if (row < M && col < N) out[row * ldo + col] = acc[a][b][r];
+      }
+    }
+  }
+}
+
+__global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int64_t M, int64_t N,
+                                float* __restrict__ C, int64_t ldc) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * N) return;
+  const int64_t MN = M * N;
+  float s0 = 0.f, s1 = 0.f;
+  int z = 0;
+  for (; z + 1 < nsplit; z += 2) {
+    s0 += part[(int64_t)z * MN + idx];
+    s1 += part[(int64_t)(z + 1) * MN + idx];
+  }
+  if (z < nsplit) s0 += part[(int64_t)z * MN + idx];
+  const int64_t m = idx / N, n = idx - m * N;
+  C[m * ldc + n] = s0 + s1;
+}
+
+template <int NW, int MT, int NT, int KB, bool AK, bool BK, int PF>
+inline void launch_gemm_cfg(int splitk, int64_t kslice, hipStream_t st, const float* A,
+                            int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                            int64_t M, int64_t N, int64_t K, bool avec, bool bvec, float* part) {
+  using Cfg = GemmCfg<NW, MT, NT, KB, AK, BK, PF>;
+  dim3 grid((unsigned)((M + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN),
+            (unsigned)splitk);
+  hipLaunchKernelGGL((k_gemm_f32<NW, MT, NT, KB, AK, BK, PF>), grid, dim3(Cfg::THREADS), 0, st, A,
+                     lda, B, ldb, C, ldc, M, N, K, kslice, avec, bvec, splitk > 1 ? part : nullptr);
+  if (splitk > 1) {
+    const int64_t tot = M * N;
+    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, part,
+                       splitk, M, N, C, ldc);
+  }
+}
+
+}  // namespace sv2n

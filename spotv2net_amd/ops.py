@@ -197,7 +197,7 @@ class _GatAttention(torch.autograd.Function):
         N = layout.num_nodes
         OC = heads * channels if concat else channels
         y = torch.empty(N, OC, device=dev, dtype=torch.float32)
-        psave = torch.empty(B, heads, n, n, device=dev, dtype=torch.float32)
+        psave = torch.empty(B, heads, 32, 32, device=dev, dtype=torch.float32)
         ae_c = ae.contiguous() if ae is not None else None
         _lib.check(lib.sv2n_gat_attn_fwd(xs.data_ptr(), xs.stride(0), _lib.ptr(ae_c),
                                          _lib.ptr(layout.rowmask), _lib.ptr(bias), _lib.ptr(keep),
@@ -245,10 +245,10 @@ def gat_attention(xs: torch.Tensor, ae: Optional[torch.Tensor], bias: Optional[t
     if training and attn_dropout > 0.0:
         B, n = layout.num_graphs, layout.n
         if attn_dropout >= 1.0:
-            keep = torch.zeros(B, heads, n, n, device=xs.device, dtype=torch.uint8)
+            keep = torch.zeros(B, heads, 32, 32, device=xs.device, dtype=torch.uint8)
             scale = 0.0
         else:
-            keep = (torch.rand(B, heads, n, n, device=xs.device) >= attn_dropout).to(torch.uint8)
+            keep = (torch.rand(B, heads, 32, 32, device=xs.device) >= attn_dropout).to(torch.uint8)
             scale = 1.0 / (1.0 - attn_dropout)
     return _GatAttention.apply(xs, ae, bias, layout, heads, channels, bool(concat), int(act),
                                float(negative_slope), keep, float(scale))

@@ -116,14 +116,14 @@ class _GATStack(torch.autograd.Function):
             keep, kscale = None, 1.0
             if training and c.dropout > 0.0:
                 if c.dropout >= 1.0:
-                    keep = torch.zeros(B, Hc, n, n, device=dev, dtype=torch.uint8)
+                    keep = torch.zeros(B, Hc, 32, 32, device=dev, dtype=torch.uint8)
                     kscale = 0.0
                 else:
-                    keep = (torch.rand(B, Hc, n, n, device=dev) >= c.dropout).to(torch.uint8)
+                    keep = (torch.rand(B, Hc, 32, 32, device=dev) >= c.dropout).to(torch.uint8)
                     kscale = 1.0 / (1.0 - c.dropout)
             OC = Hc * C if c.concat else C
             y = torch.empty(N, OC, device=dev, dtype=torch.float32)
-            ps = torch.empty(B, Hc, n, n, device=dev, dtype=torch.float32)
+            ps = torch.empty(B, Hc, 32, 32, device=dev, dtype=torch.float32)
             _lib.check(lib.sv2n_gat_attn_fwd(
                 xs.data_ptr(), xs.stride(0), _lib.ptr(aes[l]), _lib.ptr(layout.rowmask),
                 _lib.ptr(c.bias), _lib.ptr(keep), kscale, y.data_ptr(), ps.data_ptr(), B, n, Hc, C,
