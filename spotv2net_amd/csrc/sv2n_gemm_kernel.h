@@ -22,54 +22,79 @@ namespace sv2n {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __host__ __device__ constexpr int gemm_lds_stride(int rows) {
-  return rows + ((16 - rows % 32) + 32) % 32;  // smallest stride >= rows, ≡ 16 (mod 32)
+  return rows + ((16 - rows % 32) + 32) % 32;  // [k][row] image: stride ≡ 16 (mod 32)
+}
+__host__ __device__ constexpr int gemm_kmajor_stride(int kb) {
+  return kb == 16 ? 24 : 40;  // [row][k] image: conflict-free ds_read_b128 fragments
 }
 
+// One operand tile (ROWS x KB) of the block.  k-major operands (global [row][k])
+// are kept as a [row][k] LDS image (16-B copies, no transpose); the others
+// (global [k][row]) as a [k][row] image.  frag() returns, for lane (li, lk),
+// X(row rb+li, k = 16*kc + 4*lk + c), c = 0..3 — the k-permuted order in which
+// MFMA step c of lane group lk consumes k (A and B agree, so the sum is exact).
 template <int ROWS, int KB, bool KMAJOR, int THREADS>
 struct GemmTile {
   static constexpr int NV = ROWS * KB / 4;  // float4 slots per tile
   static constexpr int PER = (NV + THREADS - 1) / THREADS;
-  static constexpr int STRIDE = gemm_lds_stride(ROWS);
+  static constexpr int STRIDE = KMAJOR ? gemm_kmajor_stride(KB) : gemm_lds_stride(ROWS);
+  static constexpr int FLOATS = KMAJOR ? ROWS * STRIDE : KB * STRIDE;
   float4 v[PER];
 
+  // VEC (host-checked: 16-B aligned base, ld % 4 == 0 and the 4-wide extent —
+  // k for k-major, rows otherwise — a multiple of 4): branch-free 16-B loads
+  // from clamped in-bounds addresses (also for the surplus slots of the last
+  // pass, idx >= NV), with the out-of-matrix float4s (wholly outside, the
+  // extent being a multiple of 4) zeroed at STORE time so no wait is forced
+  // between the load and the MFMAs that run before the store.  Otherwise a
+  // guarded scalar path.
+  uint32_t okm;
+
+  template <bool VEC>
   __device__ __forceinline__ void load(const float* __restrict__ base, int64_t ld, int64_t r0,
-                                       int64_t rmax, int64_t k0, int64_t kmax, bool vec, int t) {
+                                       int64_t rmax, int64_t k0, int64_t kmax, int t) {
+    okm = 0u;
 #pragma unroll
     for (int s = 0; s < PER; ++s) {
-      const int idx = t + s * THREADS;
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (NV % THREADS == 0 || idx < NV) {
+      const int idx0 = t + s * THREADS;
+      const int idx = (NV % THREADS == 0) ? idx0 : min(idx0, NV - 1);
+      int64_t r, k;
+      if constexpr (KMAJOR) {
+        r = r0 + idx / (KB / 4);
+        k = k0 + 4 * (idx % (KB / 4));
+      } else {
+        k = k0 + idx / (ROWS / 4);
+        r = r0 + 4 * (idx % (ROWS / 4));
+      }
+      if constexpr (VEC) {
+        const bool ok = r < rmax && k < kmax;
+        const int64_t rc = KMAJOR ? min(r, rmax - 1) : min(r, rmax - 4);
+        const int64_t kc = KMAJOR ? min(k, kmax - 4) : min(k, kmax - 1);
+        const float* p = KMAJOR ? base + rc * ld + kc : base + kc * ld + rc;
+        v[s] = *reinterpret_cast<const float4*>(p);
+        okm |= (ok ? 1u : 0u) << s;
+      } else {
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (KMAJOR) {
-          const int64_t r = r0 + idx / (KB / 4);
-          const int64_t k = k0 + 4 * (idx % (KB / 4));
           if (r < rmax) {
             const float* p = base + r * ld + k;
-            if (vec && k + 3 < kmax) {
-              x = *reinterpret_cast<const float4*>(p);
-            } else {
-              if (k + 0 < kmax) x.x = p[0];
-              if (k + 1 < kmax) x.y = p[1];
-              if (k + 2 < kmax) x.z = p[2];
-              if (k + 3 < kmax) x.w = p[3];
-            }
+            if (k + 0 < kmax) x.x = p[0];
+            if (k + 1 < kmax) x.y = p[1];
+            if (k + 2 < kmax) x.z = p[2];
+            if (k + 3 < kmax) x.w = p[3];
           }
         } else {
-          const int64_t k = k0 + idx / (ROWS / 4);
-          const int64_t r = r0 + 4 * (idx % (ROWS / 4));
           if (k < kmax) {
             const float* p = base + k * ld + r;
-            if (vec && r + 3 < rmax) {
-              x = *reinterpret_cast<const float4*>(p);
-            } else {
-              if (r + 0 < rmax) x.x = p[0];
-              if (r + 1 < rmax) x.y = p[1];
-              if (r + 2 < rmax) x.z = p[2];
-              if (r + 3 < rmax) x.w = p[3];
-            }
+            if (r + 0 < rmax) x.x = p[0];
+            if (r + 1 < rmax) x.y = p[1];
+            if (r + 2 < rmax) x.z = p[2];
+            if (r + 3 < rmax) x.w = p[3];
           }
         }
+        v[s] = x;
+        okm |= 1u << s;
       }
-      v[s] = x;
     }
   }
 
@@ -78,17 +103,30 @@ struct GemmTile {
     for (int s = 0; s < PER; ++s) {
       const int idx = t + s * THREADS;
       if (NV % THREADS == 0 || idx < NV) {
+        const bool ok = (okm >> s) & 1u;
+        float4 x;
+        x.x = ok ? v[s].x : 0.f;
+        x.y = ok ? v[s].y : 0.f;
+        x.z = ok ? v[s].z : 0.f;
+        x.w = ok ? v[s].w : 0.f;
         if constexpr (KMAJOR) {
           const int r = idx / (KB / 4), k = 4 * (idx % (KB / 4));
-          lds[(k + 0) * STRIDE + r] = v[s].x;
-          lds[(k + 1) * STRIDE + r] = v[s].y;
-          lds[(k + 2) * STRIDE + r] = v[s].z;
-          lds[(k + 3) * STRIDE + r] = v[s].w;
+          *reinterpret_cast<float4*>(lds + r * STRIDE + k) = x;
         } else {
           const int k = idx / (ROWS / 4), r = 4 * (idx % (ROWS / 4));
-          *reinterpret_cast<float4*>(lds + k * STRIDE + r) = v[s];
+          *reinterpret_cast<float4*>(lds + k * STRIDE + r) = x;
         }
       }
+    }
+  }
+
+  __device__ __forceinline__ static floatx4 frag(const float* __restrict__ lds, int rb, int kc,
+                                                 int li, int lk) {
+    if constexpr (KMAJOR) {
+      return *reinterpret_cast<const floatx4*>(lds + (rb + li) * STRIDE + 16 * kc + 4 * lk);
+    } else {
+      const float* p = lds + (16 * kc + 4 * lk) * STRIDE + rb + li;
+      return floatx4{p[0], p[STRIDE], p[2 * STRIDE], p[3 * STRIDE]};
     }
   }
 };
@@ -99,20 +137,21 @@ struct GemmCfg {
   static constexpr int BM = 16 * MT * NW, BN = 16 * NT;
   using TA = GemmTile<BM, KB, AK, THREADS>;
   using TB = GemmTile<BN, KB, BK, THREADS>;
-  static constexpr int SA = TA::STRIDE, SB = TB::STRIDE;
-  static constexpr int BUF = KB * (SA + SB);
+  static constexpr int AOFF = TA::FLOATS;  // B image follows A's in each buffer
+  static constexpr int BUF = TA::FLOATS + TB::FLOATS;
   static constexpr int LDS_BYTES = 2 * BUF * 4;
 };
 
-template <int NW, int MT, int NT, int KB, bool AK, bool BK, int PF>
+template <int NW, int MT, int NT, int KB, bool AK, bool BK, int PF, int ABL = 0, bool AV = true,
+          bool BV = true>
 __global__ __launch_bounds__(64 * NW) void k_gemm_f32(
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
     float* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int64_t kslice,
-    bool avec, bool bvec, float* __restrict__ part) {
+    float* __restrict__ part) {
   using Cfg = GemmCfg<NW, MT, NT, KB, AK, BK, PF>;
   using TA = typename Cfg::TA;
   using TB = typename Cfg::TB;
-  constexpr int SA = Cfg::SA, SB = Cfg::SB, BUF = Cfg::BUF, T = Cfg::THREADS;
+  constexpr int AOFF = Cfg::AOFF, BUF = Cfg::BUF;
   __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -130,31 +169,32 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_f32(
   const int li = lane & 15, lk = lane >> 4;
   auto compute = [&](const float* sa, const float* sb) {
 #pragma unroll
-    for (int ks = 0; ks < KB / 4; ++ks) {
-      const int k = 4 * ks + lk;
-      float af[MT];
+    for (int kc = 0; kc < KB / 16; ++kc) {
+      floatx4 af[MT], bf[NT];
 #pragma unroll
-      for (int a = 0; a < MT; ++a) af[a] = sa[k * SA + wave * 16 * MT + 16 * a + li];
+      for (int a = 0; a < MT; ++a) af[a] = TA::frag(sa, wave * 16 * MT + 16 * a, kc, li, lk);
 #pragma unroll
-      for (int b = 0; b < NT; ++b) {
-        const float bf = sb[k * SB + 16 * b + li];
+      for (int b = 0; b < NT; ++b) bf[b] = TB::frag(sb, 16 * b, kc, li, lk);
 #pragma unroll
-        for (int a = 0; a < MT; ++a)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a], bf, acc[a][b], 0, 0, 0);
-      }
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int b = 0; b < NT; ++b)
+#pragma unroll
+          for (int a = 0; a < MT; ++a)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a][c], bf[b][c], acc[a][b], 0, 0, 0);
     }
   };
 
   TA ra0, ra1;
   TB rb0, rb1;
   if (nk > 0) {
-    ra0.load(A, lda, m0, M, kb, ke, avec, t);
-    rb0.load(B, ldb, n0, N, kb, ke, bvec, t);
+    ra0.template load<AV>(A, lda, m0, M, kb, ke, t);
+    rb0.template load<BV>(B, ldb, n0, N, kb, ke, t);
     ra0.store(lds, t);
-    rb0.store(lds + KB * SA, t);
+    rb0.store(lds + AOFF, t);
     if (PF == 2 && nk > 1) {
-      ra1.load(A, lda, m0, M, kb + KB, ke, avec, t);
-      rb1.load(B, ldb, n0, N, kb + KB, ke, bvec, t);
+      ra1.template load<AV>(A, lda, m0, M, kb + KB, ke, t);
+      rb1.template load<BV>(B, ldb, n0, N, kb + KB, ke, t);
     }
   }
   __syncthreads();
@@ -163,17 +203,23 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_f32(
     int cur = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const bool more = kt + 1 < nk;
-      if (more) {
+      if (more && !(ABL & 1)) {
         const int64_t k0 = kb + (int64_t)(kt + 1) * KB;
-        ra0.load(A, lda, m0, M, k0, ke, avec, t);
-        rb0.load(B, ldb, n0, N, k0, ke, bvec, t);
+        ra0.template load<AV>(A, lda, m0, M, k0, ke, t);
+        rb0.template load<BV>(B, ldb, n0, N, k0, ke, t);
       }
       const float* sa = lds + cur * BUF;
-      compute(sa, sa + KB * SA);
-      if (more) {
+      compute(sa, sa + AOFF);
+      if (more && !(ABL & 2)) {
         float* nxt = lds + (cur ^ 1) * BUF;
         ra0.store(nxt, t);
-        rb0.store(nxt + KB * SA, t);
+        rb0.store(nxt + AOFF, t);
+      }
+      if (ABL & 2) {
+#pragma unroll
+        for (int q = 0; q < TA::PER; ++q) asm volatile("" ::"v"(ra0.v[q].x), "v"(ra0.v[q].w));
+#pragma unroll
+        for (int q = 0; q < TB::PER; ++q) asm volatile("" ::"v"(rb0.v[q].x), "v"(rb0.v[q].w));
       }
       __syncthreads();
       cur ^= 1;
@@ -184,26 +230,26 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_f32(
       {  // even step: compute buf 0, refill set 0 with tile kt+2, store set 1 -> buf 1
         if (kt + 2 < nk) {
           const int64_t k0 = kb + (int64_t)(kt + 2) * KB;
-          ra0.load(A, lda, m0, M, k0, ke, avec, t);
-          rb0.load(B, ldb, n0, N, k0, ke, bvec, t);
+          ra0.template load<AV>(A, lda, m0, M, k0, ke, t);
+          rb0.template load<BV>(B, ldb, n0, N, k0, ke, t);
         }
-        compute(lds, lds + KB * SA);
+        compute(lds, lds + AOFF);
         if (kt + 1 < nk) {
           ra1.store(lds + BUF, t);
-          rb1.store(lds + BUF + KB * SA, t);
+          rb1.store(lds + BUF + AOFF, t);
         }
         __syncthreads();
       }
       if (kt + 1 < nk) {  // odd step: compute buf 1, refill set 1 with tile kt+3, store set 0 -> buf 0
         if (kt + 3 < nk) {
           const int64_t k0 = kb + (int64_t)(kt + 3) * KB;
-          ra1.load(A, lda, m0, M, k0, ke, avec, t);
-          rb1.load(B, ldb, n0, N, k0, ke, bvec, t);
+          ra1.template load<AV>(A, lda, m0, M, k0, ke, t);
+          rb1.template load<BV>(B, ldb, n0, N, k0, ke, t);
         }
-        compute(lds + BUF, lds + BUF + KB * SA);
+        compute(lds + BUF, lds + BUF + AOFF);
         if (kt + 2 < nk) {
           ra0.store(lds, t);
-          rb0.store(lds + KB * SA, t);
+          rb0.store(lds + AOFF, t);
         }
         __syncthreads();
       }
@@ -242,15 +288,24 @@ __global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int6
   C[m * ldc + n] = s0 + s1;
 }
 
-template <int NW, int MT, int NT, int KB, bool AK, bool BK, int PF>
+template <int NW, int MT, int NT, int KB, bool AK, bool BK, int PF, int ABL = 0>
 inline void launch_gemm_cfg(int splitk, int64_t kslice, hipStream_t st, const float* A,
                             int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                             int64_t M, int64_t N, int64_t K, bool avec, bool bvec, float* part) {
   using Cfg = GemmCfg<NW, MT, NT, KB, AK, BK, PF>;
   dim3 grid((unsigned)((M + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN),
             (unsigned)splitk);
-  hipLaunchKernelGGL((k_gemm_f32<NW, MT, NT, KB, AK, BK, PF>), grid, dim3(Cfg::THREADS), 0, st, A,
-                     lda, B, ldb, C, ldc, M, N, K, kslice, avec, bvec, splitk > 1 ? part : nullptr);
+  // the vector path needs the 4-wide extent (k for k-major operands, rows
+  // otherwise) to be a multiple of 4 as well
+  const bool av = avec && ((AK ? K : M) % 4 == 0);
+  const bool bv = bvec && ((BK ? K : N) % 4 == 0);
+  float* pp = splitk > 1 ? part : nullptr;
+  if (av && bv)
+    hipLaunchKernelGGL((k_gemm_f32<NW, MT, NT, KB, AK, BK, PF, ABL, true, true>), grid,
+                       dim3(Cfg::THREADS), 0, st, A, lda, B, ldb, C, ldc, M, N, K, kslice, pp);
+  else
+    hipLaunchKernelGGL((k_gemm_f32<NW, MT, NT, KB, AK, BK, PF, ABL, false, false>), grid,
+                       dim3(Cfg::THREADS), 0, st, A, lda, B, ldb, C, ldc, M, N, K, kslice, pp);
   if (splitk > 1) {
     const int64_t tot = M * N;
     hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, part,
