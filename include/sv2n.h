@@ -21,6 +21,7 @@
  *                          backward products, on f32-input MFMA
  *   sv2n_gat_prep_*        per-step weight folding (a_src/a_dst rows, W̃_edge)
  *                          and its backward straight into the parameter grads
+ *   sv2n_head_*            GATModel's final Linear (a4) fwd/bwd
  *   sv2n_adam_f32          the reference's Adam step over flat buffers (a13)
  *   sv2n_block_rowmask     edge_index -> per-target source bitmask for graph
  *                          batches whose edges are not in canonical order
@@ -177,6 +178,19 @@ int sv2n_gat_prep_bwd_edge(const float* dwfold, int hl_pad, int col0,
 int sv2n_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                   int64_t n, const float* step, float lr, float beta1, float beta2,
                   float eps, float weight_decay, hipStream_t stream);
+
+/* Output head (GATModel.linear, reference utils/models.py:120/:150):
+ *   out[i][o] = Σ_c x[i][c]·weight[o][c] + bias[o]      x [rows][in], weight [out][in]
+ * in_features <= 128, out_features <= 16.  The backward writes dx and
+ * ACCUMULATES into g_weight / g_bias (either may be NULL);
+ * workspace: sv2n_head_bwd_workspace(rows, in, out) floats. */
+int sv2n_head_fwd(const float* x, int64_t num_rows, int in_features, const float* weight,
+                  const float* bias, int out_features, float* out, hipStream_t stream);
+int64_t sv2n_head_bwd_workspace(int64_t num_rows, int in_features, int out_features);
+int sv2n_head_bwd(const float* x, int64_t num_rows, int in_features, const float* weight,
+                  int out_features, const float* dout, float* dx, float* g_weight,
+                  float* g_bias, float* workspace, int64_t workspace_floats,
+                  hipStream_t stream);
 
 /* rowmask[t] |= 1<<(s - g*n) for every non-self edge s->t (rowmask must be
  * zeroed by the caller).  Edges must stay inside their n-node block. */

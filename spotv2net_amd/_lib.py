@@ -44,6 +44,9 @@ _SIGNATURES = {
                                       _p, _p, _p, _p, _i64, _p]),
     "sv2n_gat_prep_bwd_edge": (_i32, [_p, _i32, _i32, _p, _p, _i32, _i32, _i32, _p, _p, _p]),
     "sv2n_adam_f32": (_i32, [_p, _p, _p, _p, _i64, _p, _f32, _f32, _f32, _f32, _f32, _p]),
+    "sv2n_head_fwd": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p]),
+    "sv2n_head_bwd_workspace": (_i64, [_i64, _i32, _i32]),
+    "sv2n_head_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _p, _p, _i64, _p]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

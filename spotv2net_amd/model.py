@@ -12,7 +12,8 @@ The GAT layers run as ONE fused autograd node (``stack.gat_stack``):
   (edge_attr is the same tensor for all layers, utils/models.py:145-146);
 * per layer: projection GEMM (f32 MFMA) -> fused attention kernel with the
   model's activation in its epilogue, then the inter-layer dropout
-  (utils/models.py:147-148); the final ``nn.Linear`` (:150) stays a PyTorch op.
+  (utils/models.py:147-148); the final ``nn.Linear`` (:150) keeps its module
+  and parameters but runs on the sv2n head kernels.
 Documented deviation: an unknown activation raises ValueError instead of
 printing and calling ``sys.exit()`` (utils/models.py:131-133).
 """
@@ -27,7 +28,7 @@ from torch import nn
 from . import ops
 from .conv import GATConv
 from .layout import GraphLayout, analyze_edge_index
-from .stack import gat_stack
+from .stack import gat_stack, linear_head
 
 
 def _layout_of(data, x: torch.Tensor, edge_index: torch.Tensor) -> GraphLayout:
@@ -82,5 +83,5 @@ class GATModel(nn.Module):
         layout = _layout_of(data, x, edge_index)
         x = gat_stack(x, edge_attr, tuple(self.gat_layers), layout, self._act_code,
                       float(self.dropout or 0.0), self.training)
-        x = self.linear(x)
+        x = linear_head(x, self.linear)
         return x.view(-1)

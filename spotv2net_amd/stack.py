@@ -252,3 +252,49 @@ def gat_stack(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs: Sequenc
             raise RuntimeError("parameters and data must be on the same device")
     return _GATStack.apply(x, edge_attr, tuple(convs), layout, int(act), float(post_dropout),
                            bool(training), *params)
+
+
+class _Head(torch.autograd.Function):
+    """GATModel.linear (reference utils/models.py:120, :150) on sv2n_head_*;
+    parameter gradients are accumulated into ``.grad`` like the GAT stack."""
+
+    @staticmethod
+    def forward(ctx, x, linear, weight, bias):
+        lib = _lib.load()
+        x = _aligned(x)
+        N, C = x.shape
+        O = weight.shape[0]
+        out = torch.empty(N, O, device=x.device, dtype=torch.float32)
+        _lib.check(lib.sv2n_head_fwd(x.data_ptr(), N, C, weight.data_ptr(), _lib.ptr(bias), O,
+                                     out.data_ptr(), _lib.stream_handle(x.device)), "sv2n_head_fwd")
+        ctx.linear = linear
+        ctx.save_for_backward(x)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = _lib.load()
+        (x,) = ctx.saved_tensors
+        lin = ctx.linear
+        N, C = x.shape
+        O = lin.weight.shape[0]
+        dout = dout.contiguous()
+        dx = torch.empty_like(x)
+        ws_n = lib.sv2n_head_bwd_workspace(N, C, O)
+        ws = torch.empty(ws_n, device=x.device, dtype=torch.float32)
+        gw = _grad_buf(lin.weight)
+        gb = _grad_buf(lin.bias)
+        _lib.check(lib.sv2n_head_bwd(x.data_ptr(), N, C, lin.weight.data_ptr(), O,
+                                     dout.data_ptr(), dx.data_ptr(), _lib.ptr(gw), _lib.ptr(gb),
+                                     ws.data_ptr(), ws_n, _lib.stream_handle(x.device)),
+                   "sv2n_head_bwd")
+        return dx if ctx.needs_input_grad[0] else None, None, None, None
+
+
+def linear_head(x: torch.Tensor, linear: torch.nn.Linear) -> torch.Tensor:
+    """``linear(x)`` for GATModel's output layer on the sv2n head kernels
+    (in_features <= 128, out_features <= 16; otherwise the nn.Linear itself)."""
+    _require_device(x)
+    if linear.in_features > 128 or linear.out_features > 16:
+        return linear(x)
+    return _Head.apply(x, linear, linear.weight, linear.bias)
