@@ -21,25 +21,88 @@ constexpr int EDGE_THREADS = 256;
 struct LayerPtrs { float* p[SV2N_MAX_LAYERS]; };
 struct LayerCPtrs { const float* p[SV2N_MAX_LAYERS]; };
 
+// Both kernels are persistent (grid-stride over 64-edge chunks) and
+// software-pipelined: the next chunk's edge rows (and, backward, its gathered
+// dAE values) are loaded into registers while the current chunk is computed
+// from LDS, so each workgroup keeps one chunk (32 KB at D = 126) in flight.
+// RF = float4 registers per thread for a chunk: D <= 16*RF.
+constexpr int EDGE_RF_MAX = 24;
+
+__device__ __forceinline__ int rf_needed(int D) { return (EDGE_CHUNK * D / 4 + EDGE_THREADS - 1) / EDGE_THREADS; }
+
+// native vector type: HIP's float4 struct copies lower to memcpy through a
+// stack slot, which keeps the prefetch array in scratch
+typedef float vf4 __attribute__((ext_vector_type(4)));
+
+template <int RF>
+struct ChunkRegs {
+  vf4 v[RF];
+  __device__ __forceinline__ void load(const float* __restrict__ ea, int64_t e0, int ne, int D,
+                                       int t) {
+    const vf4* s4 = reinterpret_cast<const vf4*>(ea + e0 * D);  // 16-B aligned (e0 % 64 == 0)
+    const int last = max(((ne * D) >> 2) - 1, 0);
+    // unconditional loads from clamped slots (the store side skips k >= nf4),
+    // so the register array is always fully defined (no scratch, no branches)
+#pragma unroll
+    for (int s = 0; s < RF; ++s) v[s] = s4[min(t + s * EDGE_THREADS, last)];
+  }
+  // flat copy into an unpadded [64][D] image plus the (ne*D)%4 scalar tail.
+  // The image holds RF*256 float4 slots, so every slot is stored without a
+  // branch (surplus slots land in rows >= ne, which are never read).
+  __device__ __forceinline__ void store_flat(float* __restrict__ s_ea, const float* __restrict__ ea,
+                                             int64_t e0, int ne, int D, int t) const {
+    const int nf = ne * D, nf4 = nf >> 2;
+    vf4* d4 = reinterpret_cast<vf4*>(s_ea);
+#pragma unroll
+    for (int s = 0; s < RF; ++s) d4[t + s * EDGE_THREADS] = v[s];
+    for (int k = (nf4 << 2) + t; k < nf; k += EDGE_THREADS) s_ea[k] = ea[e0 * D + k];
+  }
+  // scatter into a [64][DP] image with padded rows (DP = D rounded up to 4)
+  __device__ __forceinline__ void store_padded(float* __restrict__ s_ea,
+                                               const float* __restrict__ ea, int64_t e0, int ne,
+                                               int D, int DP, int t) const {
+    const int nf = ne * D, nf4 = nf >> 2;
+#pragma unroll
+    for (int s = 0; s < RF; ++s) {
+      const int k = t + s * EDGE_THREADS;
+      if (k < nf4) {
+        const vf4 x = v[s];
+        const int f = k << 2;
+        int r = f / D, d = f - r * D;
+        s_ea[r * DP + d] = x.x; if (++d == D) { d = 0; ++r; }
+        s_ea[r * DP + d] = x.y; if (++d == D) { d = 0; ++r; }
+        s_ea[r * DP + d] = x.z; if (++d == D) { d = 0; ++r; }
+        s_ea[r * DP + d] = x.w;
+      }
+    }
+    for (int f = (nf4 << 2) + t; f < nf; f += EDGE_THREADS) {
+      const int r = f / D;
+      s_ea[r * DP + (f - r * D)] = ea[e0 * D + f];
+    }
+    for (int k = t; k < ne * (DP - D); k += EDGE_THREADS) {
+      const int r = k / (DP - D);
+      s_ea[r * DP + D + (k - r * (DP - D))] = 0.f;
+    }
+  }
+};
+
 // ---------------------------------------------------------------------------
 // forward: ae[l][g][i][j][h] = edge_attr[e] · wfold[:, l*H+h]
-// one block = one chunk of 64 edges; thread (el = t/4, q = t%4) sums d ≡ q (mod 4)
-// for all hl_pad columns, quad-reduced through DPP, then written per layer.
+// per chunk, thread (el = t/4, q = t%4) sums d ≡ q (mod 4) for all hl_pad
+// columns, quad-reduced through DPP, then written per layer.
 // ---------------------------------------------------------------------------
-template <int HLP>
+template <int HLP, int RF>
 __global__ __launch_bounds__(EDGE_THREADS) void k_edge_fwd(
     const float* __restrict__ ea, int64_t E, int D, const int64_t* __restrict__ ei,
     const uint16_t* __restrict__ canon, int E0, const float* __restrict__ wf, LayerPtrs ae,
     int L, int H, int64_t B, int n) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_wf = smem;                            // [D][HLP]
-  float* s_ea = smem + D * HLP;                  // [64][D]
-  float* s_out = s_ea + EDGE_CHUNK * D;          // [64][HLP]
+  float* s_ea = smem + D * HLP;                  // [64][D] (RF*1024 floats)
+  float* s_out = s_ea + RF * EDGE_THREADS * 4;   // [64][HLP]
   __shared__ float* s_ptr[SV2N_MAX_LAYERS];
 
   const int t = threadIdx.x;
-  const int64_t e0 = (int64_t)blockIdx.x * EDGE_CHUNK;
-  const int ne = (int)min((int64_t)EDGE_CHUNK, E - e0);
   if (t < SV2N_MAX_LAYERS) {
 #pragma unroll
     for (int l = 0; l < SV2N_MAX_LAYERS; ++l)
@@ -49,72 +112,100 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_fwd(
     const float4* w4 = reinterpret_cast<const float4*>(wf);
     float4* sw4 = reinterpret_cast<float4*>(s_wf);
     for (int k = t; k < D * HLP / 4; k += EDGE_THREADS) sw4[k] = w4[k];
-    const float* src = ea + e0 * D;  // 64*D*4 bytes per chunk -> 16-B aligned
-    const int nf = ne * D, nf4 = nf >> 2;
-    const float4* s4 = reinterpret_cast<const float4*>(src);
-    float4* d4 = reinterpret_cast<float4*>(s_ea);
-#pragma unroll 4
-    for (int k = t; k < nf4; k += EDGE_THREADS) d4[k] = s4[k];
-    for (int k = (nf4 << 2) + t; k < nf; k += EDGE_THREADS) s_ea[k] = src[k];
   }
-  __syncthreads();
-
+  const int64_t nchunks = (E + EDGE_CHUNK - 1) / EDGE_CHUNK;
   const int el = t >> 2, q = t & 3;
-  float acc[HLP];
+  const int HL = L * H;
+  ChunkRegs<RF> R;
+  int64_t c = blockIdx.x;
+  if (c < nchunks) R.load(ea, c * EDGE_CHUNK, (int)min((int64_t)EDGE_CHUNK, E - c * EDGE_CHUNK), D, t);
+  for (; c < nchunks; c += gridDim.x) {
+    const int64_t e0 = c * EDGE_CHUNK;
+    const int ne = (int)min((int64_t)EDGE_CHUNK, E - e0);
+    __syncthreads();  // previous chunk's LDS fully consumed
+    R.store_flat(s_ea, ea, e0, ne, D, t);
+    __syncthreads();
+    const int64_t cn = c + gridDim.x;
+    if (cn < nchunks)
+      R.load(ea, cn * EDGE_CHUNK, (int)min((int64_t)EDGE_CHUNK, E - cn * EDGE_CHUNK), D, t);
+
+    float acc[HLP];
 #pragma unroll
-  for (int k = 0; k < HLP; ++k) acc[k] = 0.f;
-  if (el < ne) {
-    const float* row = s_ea + el * D;
-    for (int d = q; d < D; d += 4) {
-      const float v = row[d];
-      const float4* w4 = reinterpret_cast<const float4*>(s_wf + d * HLP);
+    for (int k = 0; k < HLP; ++k) acc[k] = 0.f;
+    if (el < ne) {
+      const float* row = s_ea + el * D;
+      for (int d = q; d < D; d += 4) {
+        const float v = row[d];
+        const float4* w4 = reinterpret_cast<const float4*>(s_wf + d * HLP);
 #pragma unroll
-      for (int k4 = 0; k4 < HLP / 4; ++k4) {
-        const float4 w = w4[k4];
-        acc[4 * k4 + 0] = fmaf(v, w.x, acc[4 * k4 + 0]);
-        acc[4 * k4 + 1] = fmaf(v, w.y, acc[4 * k4 + 1]);
-        acc[4 * k4 + 2] = fmaf(v, w.z, acc[4 * k4 + 2]);
-        acc[4 * k4 + 3] = fmaf(v, w.w, acc[4 * k4 + 3]);
+        for (int k4 = 0; k4 < HLP / 4; ++k4) {
+          const float4 w = w4[k4];
+          acc[4 * k4 + 0] = fmaf(v, w.x, acc[4 * k4 + 0]);
+          acc[4 * k4 + 1] = fmaf(v, w.y, acc[4 * k4 + 1]);
+          acc[4 * k4 + 2] = fmaf(v, w.z, acc[4 * k4 + 2]);
+          acc[4 * k4 + 3] = fmaf(v, w.w, acc[4 * k4 + 3]);
+        }
       }
     }
-  }
 #pragma unroll
-  for (int k = 0; k < HLP; ++k) {
-    acc[k] += dpp_xor1(acc[k]);
-    acc[k] += dpp_xor2(acc[k]);
-  }
-  // lane q of the quad parks columns k ≡ q (mod 4) in LDS (compile-time index)
+    for (int k = 0; k < HLP; ++k) {
+      acc[k] += dpp_xor1(acc[k]);
+      acc[k] += dpp_xor2(acc[k]);
+    }
+    // lane q of the quad parks columns k ≡ q (mod 4) in LDS (compile-time index)
 #pragma unroll
-  for (int k = 0; k < HLP; ++k)
-    if ((k & 3) == q) s_out[el * HLP + k] = acc[k];
-  __syncthreads();
-
-  const int HL = L * H;
-  for (int idx = t; idx < ne * HL; idx += EDGE_THREADS) {
-    const int le = idx / HL, k = idx - le * HL;
-    int64_t g;
-    int i, j;
-    if (!decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) continue;
-    const int l = k / H, h = k - l * H;
-    s_ptr[l][((g * n + i) * n + j) * H + h] = s_out[le * HLP + k];
+    for (int k = 0; k < HLP; ++k)
+      if ((k & 3) == q) s_out[el * HLP + k] = acc[k];
+    __syncthreads();
+    for (int idx = t; idx < ne * HL; idx += EDGE_THREADS) {
+      const int le = idx / HL, k = idx - le * HL;
+      int64_t g;
+      int i, j;
+      if (!decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) continue;
+      const int l = k / H, h = k - l * H;
+      s_ptr[l][((g * n + i) * n + j) * H + h] = s_out[le * HLP + k];
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
 // backward: partial[b][d][k] = Σ_{e in block b's chunks} edge_attr[e][d] * dae_e[k]
-// thread tile = 4 d x 4 k outer products, ES edge-groups per tile; grid-stride
-// over chunks, block-level reduction at the end, then k_reduce_partials sums
-// the per-block partials in a fixed order (deterministic).
+// thread tile = 4 d x 4 k outer products, ES edge-groups per tile; block-level
+// reduction at the end, then k_reduce_partials sums the per-block partials in
+// a fixed order (deterministic).
 // ---------------------------------------------------------------------------
 template <int HLP>
+__device__ __forceinline__ void gather_dae(float (&gd)[(EDGE_CHUNK * HLP + EDGE_THREADS - 1) / EDGE_THREADS],
+                                           const float* const* s_ptr, const int64_t* __restrict__ ei,
+                                           int64_t E, const uint16_t* __restrict__ canon, int E0,
+                                           int n, int64_t B, int HL, int H, int64_t e0, int ne,
+                                           int t) {
+  constexpr int GN = (EDGE_CHUNK * HLP + EDGE_THREADS - 1) / EDGE_THREADS;
+#pragma unroll
+  for (int s = 0; s < GN; ++s) {
+    const int idx = t + s * EDGE_THREADS;
+    const int le = idx / HLP, k = idx - le * HLP;
+    float v = 0.f;
+    int64_t g;
+    int i, j;
+    if (le < ne && k < HL && decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) {
+      const int l = k / H, h = k - l * H;
+      v = s_ptr[l][((g * n + i) * n + j) * H + h];
+    }
+    gd[s] = v;
+  }
+}
+
+template <int HLP, int RF>
 __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
     const float* __restrict__ ea, int64_t E, int D, int DP, const int64_t* __restrict__ ei,
     const uint16_t* __restrict__ canon, int E0, LayerCPtrs dae, int L, int H, int64_t B, int n,
     float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_ea = smem;                        // [64][DP]
-  float* s_dae = smem + EDGE_CHUNK * DP;     // [64][HLP]
+  float* s_dae = smem + max(EDGE_CHUNK * DP, RF * EDGE_THREADS * 4);  // [64][HLP]
   __shared__ const float* s_ptr[SV2N_MAX_LAYERS];
+  constexpr int GN = (EDGE_CHUNK * HLP + EDGE_THREADS - 1) / EDGE_THREADS;
 
   const int t = threadIdx.x;
   if (t < SV2N_MAX_LAYERS) {
@@ -122,6 +213,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
     for (int l = 0; l < SV2N_MAX_LAYERS; ++l)
       if (l == t) s_ptr[l] = dae.p[l];
   }
+  __syncthreads();
   const int KG = HLP / 4;
   const int T = (DP / 4) * KG;  // thread tiles
   const int ES = EDGE_THREADS / T;
@@ -135,54 +227,34 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
   for (int k = 0; k < 16; ++k) acc[k] = 0.f;
 
   const int64_t nchunks = (E + EDGE_CHUNK - 1) / EDGE_CHUNK;
-  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+  ChunkRegs<RF> R;
+  float gd[GN];
+  int64_t c = blockIdx.x;
+  if (c < nchunks) {
+    const int64_t e0 = c * EDGE_CHUNK;
+    const int ne = (int)min((int64_t)EDGE_CHUNK, E - e0);
+    R.load(ea, e0, ne, D, t);
+    gather_dae<HLP>(gd, s_ptr, ei, E, canon, E0, n, B, HL, H, e0, ne, t);
+  }
+  for (; c < nchunks; c += gridDim.x) {
     const int64_t e0 = c * EDGE_CHUNK;
     const int ne = (int)min((int64_t)EDGE_CHUNK, E - e0);
     __syncthreads();  // previous chunk fully consumed
-    const float* src = ea + e0 * D;
-    const int nf = ne * D;
-    if (DP == D) {
-      const int nf4 = nf >> 2;
-      const float4* s4 = reinterpret_cast<const float4*>(src);
-      float4* d4 = reinterpret_cast<float4*>(s_ea);
-#pragma unroll 4
-      for (int k = t; k < nf4; k += EDGE_THREADS) d4[k] = s4[k];
-      for (int k = (nf4 << 2) + t; k < nf; k += EDGE_THREADS) s_ea[k] = src[k];
-    } else {
-      const int nf4 = nf >> 2;
-      const float4* s4 = reinterpret_cast<const float4*>(src);
-#pragma unroll 2
-      for (int k = t; k < nf4; k += EDGE_THREADS) {
-        const float4 v = s4[k];
-        const int f = k << 2;
-        int r = f / D, d = f - r * D;
-        s_ea[r * DP + d] = v.x; if (++d == D) { d = 0; ++r; }
-        s_ea[r * DP + d] = v.y; if (++d == D) { d = 0; ++r; }
-        s_ea[r * DP + d] = v.z; if (++d == D) { d = 0; ++r; }
-        s_ea[r * DP + d] = v.w;
-      }
-      for (int f = (nf4 << 2) + t; f < nf; f += EDGE_THREADS) {
-        const int r = f / D;
-        s_ea[r * DP + (f - r * D)] = src[f];
-      }
-      // zero the row padding so the 4-wide tiles read finite values
-      for (int k = t; k < ne * (DP - D); k += EDGE_THREADS) {
-        const int r = k / (DP - D);
-        s_ea[r * DP + D + (k - r * (DP - D))] = 0.f;
-      }
-    }
-    for (int idx = t; idx < ne * HLP; idx += EDGE_THREADS) {
-      const int le = idx / HLP, k = idx - le * HLP;
-      float v = 0.f;
-      int64_t g;
-      int i, j;
-      if (k < HL && decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) {
-        const int l = k / H, h = k - l * H;
-        v = s_ptr[l][((g * n + i) * n + j) * H + h];
-      }
-      s_dae[idx] = v;
+    if (DP == D) R.store_flat(s_ea, ea, e0, ne, D, t);
+    else R.store_padded(s_ea, ea, e0, ne, D, DP, t);
+#pragma unroll
+    for (int s = 0; s < GN; ++s) {
+      const int idx = t + s * EDGE_THREADS;
+      if (idx < EDGE_CHUNK * HLP) s_dae[idx] = gd[s];
     }
     __syncthreads();
+    const int64_t cn = c + gridDim.x;
+    if (cn < nchunks) {
+      const int64_t e1 = cn * EDGE_CHUNK;
+      const int ne1 = (int)min((int64_t)EDGE_CHUNK, E - e1);
+      R.load(ea, e1, ne1, D, t);
+      gather_dae<HLP>(gd, s_ptr, ei, E, canon, E0, n, B, HL, H, e1, ne1, t);
+    }
     if (active) {
       for (int le = es; le < ne; le += ES) {
         const float4 a = *reinterpret_cast<const float4*>(s_ea + le * DP + 4 * dg);
@@ -258,6 +330,7 @@ __global__ void k_block_rowmask(const int64_t* __restrict__ ei, int64_t E, int64
 using namespace sv2n;
 
 static constexpr int EDGE_BWD_GRID = 512;
+static constexpr int EDGE_FWD_GRID = 1024;
 
 template <typename K>
 static void raise_lds_limit(K kernel, size_t bytes) {
@@ -286,25 +359,37 @@ extern "C" int sv2n_edge_logits_fwd(const float* edge_attr, int64_t num_edges, i
     lp.p[l] = ae_layers[l];
   }
   const int E0 = n * (n - 1);
-  const int64_t nblk = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
-  const size_t lds = sizeof(float) * ((size_t)edge_dim * hl_pad + (size_t)EDGE_CHUNK * edge_dim +
+  const int64_t nchunks = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
+  const unsigned grid = (unsigned)std::min<int64_t>(nchunks, EDGE_FWD_GRID);
+  const int rf = (EDGE_CHUNK * edge_dim / 4 + EDGE_THREADS - 1) / EDGE_THREADS;
+  if (rf > EDGE_RF_MAX) return SV2N_ERR_SHAPE;
+  const int rfi = rf <= 2 ? 2 : rf <= 8 ? 8 : rf <= 16 ? 16 : 24;  // instantiated RF
+  const size_t lds = sizeof(float) * ((size_t)edge_dim * hl_pad + (size_t)rfi * EDGE_THREADS * 4 +
                                       (size_t)EDGE_CHUNK * hl_pad);
   if (lds > 160 * 1024) return SV2N_ERR_SHAPE;
-#define SV2N_LAUNCH_EF(HLP)                                                                         \
-  case HLP:                                                                                       \
-    raise_lds_limit(k_edge_fwd<HLP>, lds);                                                        \
-    hipLaunchKernelGGL(k_edge_fwd<HLP>, dim3((unsigned)nblk), dim3(EDGE_THREADS), lds, stream,    \
+#define SV2N_LAUNCH_EF(HLP, RF)                                                                   \
+  {                                                                                               \
+    raise_lds_limit(k_edge_fwd<HLP, RF>, lds);                                                    \
+    hipLaunchKernelGGL((k_edge_fwd<HLP, RF>), dim3(grid), dim3(EDGE_THREADS), lds, stream,        \
                        edge_attr, num_edges, edge_dim, edge_index, canon, E0, wfold, lp,          \
                        num_layers, heads, num_graphs, n);                                         \
+  }
+#define SV2N_LAUNCH_EF_RF(HLP)                                   \
+  case HLP:                                                      \
+    if (rf <= 2) SV2N_LAUNCH_EF(HLP, 2)                          \
+    else if (rf <= 8) SV2N_LAUNCH_EF(HLP, 8)                     \
+    else if (rf <= 16) SV2N_LAUNCH_EF(HLP, 16)                   \
+    else SV2N_LAUNCH_EF(HLP, 24)                                 \
     break;
   switch (hl_pad) {
-    SV2N_LAUNCH_EF(4)
-    SV2N_LAUNCH_EF(8)
-    SV2N_LAUNCH_EF(16)
-    SV2N_LAUNCH_EF(32)
+    SV2N_LAUNCH_EF_RF(4)
+    SV2N_LAUNCH_EF_RF(8)
+    SV2N_LAUNCH_EF_RF(16)
+    SV2N_LAUNCH_EF_RF(32)
     default:
       return SV2N_ERR_SHAPE;
   }
+#undef SV2N_LAUNCH_EF_RF
 #undef SV2N_LAUNCH_EF
   return (int)hipGetLastError();
 }
@@ -339,25 +424,37 @@ extern "C" int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, i
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(EDGE_BWD_GRID, nchunks));
   if (workspace_floats < (int64_t)grid * O) return SV2N_ERR_WORKSPACE;
   const int E0 = n * (n - 1);
-  size_t lds = sizeof(float) * ((size_t)EDGE_CHUNK * DP + (size_t)EDGE_CHUNK * hl_pad);
+  const int rf = (EDGE_CHUNK * edge_dim / 4 + EDGE_THREADS - 1) / EDGE_THREADS;
+  if (rf > EDGE_RF_MAX) return SV2N_ERR_SHAPE;
+  const int rfi = rf <= 2 ? 2 : rf <= 8 ? 8 : rf <= 16 ? 16 : 24;  // instantiated RF
+  const size_t ea_floats = std::max((size_t)EDGE_CHUNK * DP, (size_t)rfi * EDGE_THREADS * 4);
+  size_t lds = sizeof(float) * (ea_floats + (size_t)EDGE_CHUNK * hl_pad);
   lds = std::max(lds, sizeof(float) * (size_t)EDGE_THREADS * 16);
   if (lds > 160 * 1024) return SV2N_ERR_SHAPE;
   if (num_edges == 0) return (int)hipMemsetAsync(dwfold, 0, sizeof(float) * O, stream);
-#define SV2N_LAUNCH_EB(HLP)                                                                       \
-  case HLP:                                                                                     \
-    raise_lds_limit(k_edge_bwd<HLP>, lds);                                                      \
-    hipLaunchKernelGGL(k_edge_bwd<HLP>, dim3(grid), dim3(EDGE_THREADS), lds, stream, edge_attr, \
-                       num_edges, edge_dim, DP, edge_index, canon, E0, lp, num_layers, heads,   \
-                       num_graphs, n, workspace);                                               \
+#define SV2N_LAUNCH_EB(HLP, RF)                                                                   \
+  {                                                                                               \
+    raise_lds_limit(k_edge_bwd<HLP, RF>, lds);                                                    \
+    hipLaunchKernelGGL((k_edge_bwd<HLP, RF>), dim3(grid), dim3(EDGE_THREADS), lds, stream,        \
+                       edge_attr, num_edges, edge_dim, DP, edge_index, canon, E0, lp, num_layers, \
+                       heads, num_graphs, n, workspace);                                          \
+  }
+#define SV2N_LAUNCH_EB_RF(HLP)                                   \
+  case HLP:                                                      \
+    if (rf <= 2) SV2N_LAUNCH_EB(HLP, 2)                          \
+    else if (rf <= 8) SV2N_LAUNCH_EB(HLP, 8)                     \
+    else if (rf <= 16) SV2N_LAUNCH_EB(HLP, 16)                   \
+    else SV2N_LAUNCH_EB(HLP, 24)                                 \
     break;
   switch (hl_pad) {
-    SV2N_LAUNCH_EB(4)
-    SV2N_LAUNCH_EB(8)
-    SV2N_LAUNCH_EB(16)
-    SV2N_LAUNCH_EB(32)
+    SV2N_LAUNCH_EB_RF(4)
+    SV2N_LAUNCH_EB_RF(8)
+    SV2N_LAUNCH_EB_RF(16)
+    SV2N_LAUNCH_EB_RF(32)
     default:
       return SV2N_ERR_SHAPE;
   }
+#undef SV2N_LAUNCH_EB_RF
 #undef SV2N_LAUNCH_EB
   hipLaunchKernelGGL(k_reduce_partials, dim3((O + 63) / 64), dim3(256), 0, stream, workspace,
                      grid, O, dwfold);
