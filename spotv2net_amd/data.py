@@ -197,9 +197,26 @@ class WindowDataset:
                             self.S)
 
     def loader(self, batch_size: int, shuffle: bool, generator: Optional[torch.Generator] = None,
-               subset: Optional[torch.Tensor] = None):
+               subset: Optional[torch.Tensor] = None, rank: int = 0, world_size: int = 1):
+        """Batches of windows; with ``world_size > 1`` each rank walks its own
+        shard (``shard_indices``), so every rank sees batch_size graphs per
+        step (weak scaling).  Pass the same ``generator`` seed on every rank."""
         idx = subset if subset is not None else torch.arange(len(self))
         if shuffle:
             idx = idx[torch.randperm(idx.numel(), generator=generator)]
+        if world_size > 1:
+            idx = shard_indices(idx, rank, world_size)
         for k in range(0, idx.numel(), batch_size):
             yield self.batch(idx[k:k + batch_size])
+
+
+def shard_indices(idx: torch.Tensor, rank: int, world_size: int) -> torch.Tensor:
+    """torch.utils.data.DistributedSampler's partition (drop_last=False) of an
+    already ordered index list: pad by wrapping to a multiple of world_size,
+    then rank r takes positions r, r + world_size, ..."""
+    n = idx.numel()
+    total = -(-n // world_size) * world_size
+    if total > n:
+        reps = -(-(total - n) // max(n, 1))
+        idx = torch.cat([idx, idx.repeat(reps)[:total - n]])
+    return idx[rank:total:world_size]

@@ -93,6 +93,8 @@ def make_adam(params, lr: float):
     """Adam(lr) as in 5_train_SpotV2Net.py:127, with the device-side step
     counter needed for graph capture (fused kernel when available)."""
     params = list(params)
+    if not params[0].is_cuda:  # host-side replicas (gloo tests): plain Adam
+        return torch.optim.Adam(params, lr=lr)
     try:
         return torch.optim.Adam(params, lr=lr, fused=True, capturable=True)
     except (RuntimeError, TypeError):

@@ -1,0 +1,83 @@
+"""HBM traffic per launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+Usage:
+    python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> \
+        [--out profiles/pmc_traffic.json]
+
+Counter values are in KiB (rocprofv3 derived metrics).  Corrections from
+/opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE reports
+exactly half the bytes of a wide coalesced streaming read on gfx950, so it is
+doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.  The edge
+kernel (a pure 16-B/lane stream of a known 224.5 MB edge_attr) is the
+calibration point and its ratio is printed.
+
+The JSON maps bench.py's kernel_table names to per-launch bytes; bench.py
+reads it into roofline.traffic.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+from collections import defaultdict
+
+# bench.py kernel_table name -> rocprof kernel name prefix (the C2 instantiation)
+KERNELS = {
+    "gemm_l0_fwd": "sv2n::k_gemm_f32<8, 1, 13, 16, true, true, 2, 0, true, true>",
+    "gemm_l0_dwT": "sv2n::k_gemm_f32<8, 1, 13, 16, false, false, 2, 0, true, true>",
+    "edge_logits_fwd": "sv2n::k_edge_fwd<8, 8>",
+    "edge_logits_bwd": "sv2n::k_edge_bwd<8, 8>",
+    "gat_attn_fwd_l0": "sv2n::k_attn_fwd<1, true>",
+    "gat_attn_bwd_l0": "sv2n::k_attn_bwd<1, true>",
+}
+
+
+def per_kernel(path, counter):
+    """mean over dispatches of the dispatch's counter sum (KiB), keyed by kernel name."""
+    disp = defaultdict(float)
+    name = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        d = int(r["Dispatch_Id"])
+        disp[d] += float(r["Counter_Value"])
+        name[d] = r["Kernel_Name"]
+    acc = defaultdict(list)
+    for d, v in disp.items():
+        acc[name[d]].append(v)
+    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
+
+
+def find(table, prefix):
+    for k, v in table.items():
+        if prefix + "(" in k:
+            return v
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    a = ap.parse_args()
+    fetch = per_kernel(a.fetch, "FETCH_SIZE")
+    write = per_kernel(a.write, "WRITE_SIZE")
+    out = {"_note": "hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), "
+                    "gfx950 FETCH_SIZE halving corrected per MI355X_MICROARCH.md; "
+                    "mean over the dispatches of the profiled C2 train/forward steps"}
+    for key, prefix in KERNELS.items():
+        f, w = find(fetch, prefix), find(write, prefix)
+        if f is None or w is None:
+            continue
+        fb, wb = 2.0 * f[0] * 1024.0, w[0] * 1024.0
+        out[key] = {"kernel": prefix, "fetch_bytes": round(fb), "write_bytes": round(wb),
+                    "hbm_bytes_per_launch": round(fb + wb), "dispatches": f[1]}
+        print(f"{key:18s} read {fb / 1e6:9.2f} MB  write {wb / 1e6:8.2f} MB  ({f[1]} dispatches)")
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print("wrote", a.out)
+
+
+if __name__ == "__main__":
+    main()
