@@ -23,6 +23,8 @@
  *                          and its backward straight into the parameter grads
  *   sv2n_head_*            GATModel's final Linear (a4) fwd/bwd
  *   sv2n_adam_f32          the reference's Adam step over flat buffers (a13)
+ *   sv2n_gat_attn_tiled_*  the same attention fwd/bwd for 32 < n <= 256 (C5
+ *                          stress shapes), target-row-tiled
  *   sv2n_block_rowmask     edge_index -> per-target source bitmask for graph
  *                          batches whose edges are not in canonical order
  *
@@ -59,9 +61,12 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 1
+#define SV2N_ABI_VERSION 2
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
-#define SV2N_MAX_N 32       /* nodes per graph on the dense-block path     */
+#define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
+                               attention path (sv2n_gat_attn_fwd/bwd)      */
+#define SV2N_MAX_N_TILED 256 /* nodes per graph on the tiled attention path
+                               (sv2n_gat_attn_tiled_*) and the edge pass   */
 #define SV2N_MAX_HEADS 8    /* attention heads per layer                   */
 
 /* argument errors (negative return codes) */
@@ -192,8 +197,34 @@ int sv2n_head_bwd(const float* x, int64_t num_rows, int in_features, const float
                   float* g_bias, float* workspace, int64_t workspace_floats,
                   hipStream_t stream);
 
-/* rowmask[t] |= 1<<(s - g*n) for every non-self edge s->t (rowmask must be
- * zeroed by the caller).  Edges must stay inside their n-node block. */
+/* Fused attention for dense-block graphs of 32 < n <= 256 nodes (any n <= 256
+ * works; n <= 32 is faster on sv2n_gat_attn_fwd/bwd).  Same semantics and
+ * arguments as sv2n_gat_attn_fwd/bwd except:
+ *   rowmask  [N][ceil(n/32)] uint32 words (bit j%32 of word j/32 of row g*n+i:
+ *            edge j->i present) or NULL for complete graphs;
+ *   keep     [num_graphs][H][n][n] uint8 or NULL;
+ *   channels <= 64;
+ *   nothing is saved for the backward: it recomputes the attention from xs
+ *   and ae (pass the forward's ae again);
+ *   concat = 0 needs a workspace of sv2n_gat_attn_tiled_workspace(...)
+ *   floats (per-head aggregates before the mean). */
+int64_t sv2n_gat_attn_tiled_workspace(int64_t num_graphs, int n, int heads, int channels,
+                                      int concat);
+int sv2n_gat_attn_tiled_fwd(const float* xs, int ldx, const float* ae, const uint32_t* rowmask,
+                            const float* bias, const uint8_t* keep, float keep_scale,
+                            float* y, float* workspace, int64_t workspace_floats,
+                            int64_t num_graphs, int n, int heads, int channels, int concat,
+                            int act, float negative_slope, hipStream_t stream);
+int sv2n_gat_attn_tiled_bwd(const float* dy, const float* y, const float* xs, int ldx,
+                            const float* ae, const uint8_t* keep, float keep_scale,
+                            const uint32_t* rowmask, float* dxs, float* dae,
+                            float* dbias_partial, int64_t num_graphs, int n, int heads,
+                            int channels, int concat, int act, float negative_slope,
+                            hipStream_t stream);
+
+/* rowmask[t*W + j/32] |= 1<<(j%32), W = ceil(n/32), j = s - g*n, for every
+ * non-self edge s->t (rowmask [num_nodes][W] must be zeroed by the caller).
+ * Edges must stay inside their n-node block; n <= SV2N_MAX_N_TILED. */
 int sv2n_block_rowmask(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
                        int n, uint32_t* rowmask, hipStream_t stream);
 

@@ -1,0 +1,551 @@
+// Fused GAT attention for dense-block graphs of 32 < n <= 256 nodes (the
+// SURVEY.md §8d C5 stress shapes and any larger block batch) — the same PyG
+// 2.3.0 GATConv semantics as sv2n_attn.hip (reference utils/models.py:146 ->
+// GATConv.forward), re-tiled for rows that no
+// longer fit one 32-lane half:
+//
+// * one workgroup (4 waves) per (graph g, head h); blockIdx is remapped so the
+//   H head-workgroups of a graph run on the same XCD and share its L2 for the
+//   head-interleaved AE rows ([g][i][j][h]) they all read;
+// * targets are walked in blocks of TB = 16 rows; a wave owns a row at a time
+//   and its lanes cover sources j = lane + 64q, so the self-loop mean, the
+//   softmax max / sum are 64-lane wave reductions;
+// * the products run on v_mfma_f32_16x16x4_f32 (exact f32) from LDS:
+//     forward   out_h[i]  = Σ_j P[i][j] · xs_h[j]        (TB x C, K = n)
+//     backward  dP[i][j]  = Σ_c dOut[i][c] · xs_h[j][c]  (TB x n, K = C)
+//               dxs_h[j] += Σ_i P[i][j] · dOut[i]        (n x C, K = TB per block,
+//                                                         accumulated in VGPRs)
+// * nothing is saved between forward and backward except the layer output:
+//   the backward recomputes P from xs and AE (its HBM cost equals reading a
+//   saved P, and the forward skips writing one);
+// * concat = False (mean over heads) needs a cross-head sum: the forward then
+//   writes per-head aggregates to a workspace and k_head_mean finishes
+//   mean + bias + activation.
+//
+// LDS images (floats):
+//   sX [NP][XS]  xs_h rows (zero-padded to NP = round_up(n, 16) rows and
+//                16*CT columns)
+//   sP [TB][PS]  P rows
+// ds_read_b32 banks are (addr/4) % 32 per 32-lane half (cdna_hip_programming.md
+// §2).  A fragment read "row = lane&15, col = lane>>4" is conflict-free for a
+// stride ≡ 2 (mod 32) or odd; "row = lane>>4, col = lane&15" for ≡ 16 (mod 32)
+// (odd: one 2-way pair).  Strides below follow the role each image plays.
+#include "sv2n_common.h"
+
+namespace sv2n {
+
+constexpr int TT = 256;        // threads per workgroup
+constexpr int TB = 16;         // target rows per block
+constexpr int TILED_MAX_N = 256;
+constexpr int TILED_MAX_C = 64;
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+  return v;
+}
+
+// blockIdx -> (graph, head) so that consecutive heads of a graph land on the
+// same XCD (hardware round-robins blockIdx over the 8 XCDs); identity when the
+// grid is not a multiple of 8.
+__device__ __forceinline__ void block_gh(int H, int64_t& g, int& h) {
+  const int64_t nb = (int64_t)gridDim.x;
+  int64_t b = blockIdx.x;
+  if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);
+  g = b / H;
+  h = (int)(b - g * H);
+}
+
+__host__ __device__ constexpr int round_up(int a, int m) { return (a + m - 1) / m * m; }
+__host__ __device__ constexpr int pad32(int a, int mod) {  // smallest s >= a, s % 32 == mod
+  return a + ((mod - a % 32) + 32) % 32;
+}
+
+// One target row of the recomputed attention: scores, self loop (mean fill),
+// leaky_relu, softmax.  Lane owns j = lane + 64q (q < 4).  Returns per-slot
+// probabilities p (0 for absent), the leaky-negative flags and the row's
+// present-edge count.
+struct RowSoftmax {
+  float p[4];
+  bool neg[4];
+  bool present[4];  // j != i edge present
+  int cnt;
+};
+
+__device__ __forceinline__ void row_softmax(RowSoftmax& R, const float* __restrict__ sA,
+                                            float ad, const float* __restrict__ ae,
+                                            const uint32_t* __restrict__ rowmask, int64_t row,
+                                            int64_t aerow, int n, int i, int H, int h,
+                                            float slope, int lane) {
+  const int W = (n + 31) >> 5;
+  float e[4], s[4];
+  float esum = 0.f;
+  int cnt = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = lane + 64 * q;
+    bool pr = false;
+    if (j < n && j != i) {
+      pr = rowmask ? ((rowmask[row * W + (j >> 5)] >> (j & 31)) & 1u) : true;
+    }
+    R.present[q] = pr;
+    e[q] = (pr && ae) ? ae[(aerow + j) * H + h] : 0.f;
+    esum += e[q];
+    cnt += pr ? 1 : 0;
+  }
+  esum = wave_sum(esum);
+  cnt = (int)wave_sum((float)cnt);
+  R.cnt = cnt;
+  const float loopv = (ae && cnt > 0) ? esum / (float)cnt : 0.f;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = lane + 64 * q;
+    const bool valid = R.present[q] || j == i;
+    float v = (j < n ? sA[j] : 0.f) + ad;
+    v += (j == i) ? loopv : e[q];
+    R.neg[q] = !(v > 0.f);
+    const float lr = R.neg[q] ? v * slope : v;
+    s[q] = valid ? lr : -INFINITY;
+    mx = fmaxf(mx, s[q]);
+  }
+  mx = wave_max(mx);
+  float den = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    s[q] = (s[q] == -INFINITY) ? 0.f : expf(s[q] - mx);
+    den += s[q];
+  }
+  den = wave_sum(den) + 1e-16f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) R.p[q] = s[q] / den;
+}
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+template <int ACT, bool CONCAT, int CT>
+__global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
+    const float* __restrict__ xs, int ldx, const float* __restrict__ ae,
+    const uint32_t* __restrict__ rowmask, const float* __restrict__ bias,
+    const uint8_t* __restrict__ keep, float keep_scale, float* __restrict__ out, int n, int H,
+    int C, float slope) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int CW = 16 * CT;
+  constexpr int XS = pad32(CW, 16);  // B operand: row = lane>>4
+  const int NP = round_up(n, 16);
+  const int PS = pad32(NP, 2);       // A operand: row = lane&15
+  float* sX = smem;               // [NP][XS]
+  float* sP = sX + NP * XS;       // [TB][PS]
+  float* sA = sP + TB * PS;       // [NP]
+
+  int64_t g;
+  int h;
+  block_gh(H, g, h);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t row0 = g * n;
+  const int HC = H * C;
+
+  for (int idx = t; idx < NP * CW; idx += TT) {
+    const int j = idx / CW, c = idx - j * CW;
+    sX[j * XS + c] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
+  }
+  for (int j = t; j < NP; j += TT) sA[j] = j < n ? xs[(row0 + j) * ldx + HC + h] : 0.f;
+  __syncthreads();
+
+  const int li = lane & 15, lk = lane >> 4;
+  for (int i0 = 0; i0 < n; i0 += TB) {
+    // ---- P rows of this block ----
+    for (int r = wave; r < TB; r += 4) {
+      const int i = i0 + r;
+      float* prow = sP + r * PS;
+      if (i >= n) {
+        for (int j = lane; j < NP; j += 64) prow[j] = 0.f;
+        continue;
+      }
+      const int64_t row = row0 + i;
+      const float ad = xs[row * ldx + HC + H + h];
+      RowSoftmax R;
+      row_softmax(R, sA, ad, ae, rowmask, row, row * n, n, i, H, h, slope, lane);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = lane + 64 * q;
+        if (j < NP) {
+          float pd = (R.present[q] || j == i) ? R.p[q] : 0.f;
+          if (keep && j < n) pd = keep[((g * H + h) * n + i) * n + j] ? pd * keep_scale : 0.f;
+          prow[j] = pd;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- out[i][c] = Σ_j P[i][j] xs_h[j][c]: wave w owns column tile w (CT <= 4) ----
+    if (wave < CT) {
+      f4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* pa = sP + li * PS + lk;
+      const float* xb = sX + lk * XS + 16 * wave + li;
+      for (int k = 0; k < NP; k += 4)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[k], xb[k * XS], acc, 0, 0, 0);
+      const int c = 16 * wave + li;
+      if (c < C) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + 4 * lk + r;
+          if (i < n) {
+            if (CONCAT) {
+              const float b = bias ? bias[h * C + c] : 0.f;
+              out[(row0 + i) * HC + h * C + c] = act_fwd<ACT>(acc[r] + b);
+            } else {
+              out[(row0 + i) * HC + h * C + c] = acc[r];  // workspace, per head
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// mean over heads + bias + activation (concat = False)
+template <int ACT>
+__global__ __launch_bounds__(256) void k_head_mean(const float* __restrict__ ws,
+                                                   const float* __restrict__ bias,
+                                                   float* __restrict__ y, int64_t N, int H,
+                                                   int C) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= N * C) return;
+  const int64_t row = idx / C;
+  const int c = (int)(idx - row * C);
+  const float* w = ws + row * H * C + c;
+  float s = 0.f;
+  for (int h = 0; h < H; ++h) s += w[h * C];
+  y[idx] = act_fwd<ACT>(s * (1.f / (float)H) + (bias ? bias[c] : 0.f));
+}
+
+// ---------------------------------------------------------------------------
+// backward
+//   dz = act'(y)·dy; dOut_h = dz (concat slice h) or dz / H (mean);
+//   P recomputed; dPd = dOut·xs_hᵀ; dP = dropout-bwd(dPd);
+//   dS = P ⊙ (dP − Σ_j P dP); dL = dS · leaky'(s);
+//   dae[i][j] = dL[i][j] + dL[i][i] / cnt  (present j),  a_d[i] += Σ_j dL,
+//   a_s[j] += Σ_i dL[i][j],  dxs_h[j] += Σ_i Pd[i][j] dOut[i]
+// LDS: sX [NP][XS] | sP [TB][PS] (Pd) | sL [TB][PS] (dP then dL) |
+//      sO [TB][OS] (dOut) | sAs [NP] | sDa [NP] (Σ_i dL[i][j])
+// ---------------------------------------------------------------------------
+template <int ACT, bool CONCAT, int CT>
+__global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
+    const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ xs,
+    int ldx, const float* __restrict__ ae, const uint8_t* __restrict__ keep, float keep_scale,
+    const uint32_t* __restrict__ rowmask, float* __restrict__ dxs, float* __restrict__ dae,
+    float* __restrict__ dbias, int n, int H, int C, float slope) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int CW = 16 * CT;
+  constexpr int XS = CW + 1;         // dP's B operand: row = lane&15
+  constexpr int OS = CW + 1;         // read both ways (dP's A, dxs's B)
+  const int NP = round_up(n, 16);
+  const int PS = pad32(NP, 16);      // Pᵀ operand: row = lane>>4
+  float* sX = smem;               // [NP][XS]
+  float* sP = sX + NP * XS;       // [TB][PS]
+  float* sL = sP + TB * PS;       // [TB][PS]
+  float* sO = sL + TB * PS;       // [TB][OS]
+  float* sA = sO + TB * OS;       // [NP]
+  float* sDa = sA + NP;           // [NP]
+
+  int64_t g;
+  int h;
+  block_gh(H, g, h);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t row0 = g * n;
+  const int HC = H * C;
+  const int OC = CONCAT ? HC : C;
+  const int oc0 = CONCAT ? h * C : 0;
+  const float oscale = CONCAT ? 1.f : 1.f / (float)H;
+
+  for (int idx = t; idx < NP * CW; idx += TT) {
+    const int j = idx / CW, c = idx - j * CW;
+    sX[j * XS + c] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
+  }
+  for (int j = t; j < NP; j += TT) {
+    sA[j] = j < n ? xs[(row0 + j) * ldx + HC + h] : 0.f;
+    sDa[j] = 0.f;
+  }
+  // dxs accumulators: wave w owns row tiles jt = w, w+4, ... (NP/16 <= 16) x CT column tiles
+  constexpr int MAXJT = TILED_MAX_N / 16 / 4;  // 4 row tiles per wave
+  f4 dacc[MAXJT][CT];
+#pragma unroll
+  for (int a = 0; a < MAXJT; ++a)
+#pragma unroll
+    for (int b = 0; b < CT; ++b) dacc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+  float dbias_acc = 0.f;  // thread t < C owns bias column t of this head's slice
+  const int li = lane & 15, lk = lane >> 4;
+  const int njt = NP / 16;
+  __syncthreads();
+
+  for (int i0 = 0; i0 < n; i0 += TB) {
+    // ---- dOut rows ----
+    for (int idx = t; idx < TB * CW; idx += TT) {
+      const int r = idx / CW, c = idx - r * CW;
+      const int i = i0 + r;
+      float v = 0.f;
+      if (i < n && c < C) {
+        const int64_t o = (row0 + i) * OC + oc0 + c;
+        v = act_bwd<ACT>(dy[o], y[o]);
+      }
+      sO[r * OS + c] = v * oscale;
+    }
+    __syncthreads();
+    if (t < C && (CONCAT || h == 0)) {
+      float s = 0.f;
+      for (int r = 0; r < TB; ++r) s += sO[r * OS + t];
+      dbias_acc += s / oscale;  // = Σ dz
+    }
+    // ---- dPd[i][j] = Σ_c dOut[i][c] xs_h[j][c]: tiles over j, waves stride ----
+    for (int jt = wave; jt < njt; jt += 4) {
+      f4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* oa = sO + li * OS + lk;
+      const float* xb = sX + (16 * jt + li) * XS + lk;
+#pragma unroll
+      for (int k = 0; k < CW; k += 4)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(oa[k], xb[k], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sL[(4 * lk + r) * PS + 16 * jt + li] = acc[r];
+    }
+    __syncthreads();
+    // ---- per row: recompute P, softmax / leaky / dropout backward ----
+    for (int r = wave; r < TB; r += 4) {
+      const int i = i0 + r;
+      float* prow = sP + r * PS;
+      float* lrow = sL + r * PS;
+      if (i >= n) {
+        for (int j = lane; j < NP; j += 64) { prow[j] = 0.f; lrow[j] = 0.f; }
+        continue;
+      }
+      const int64_t row = row0 + i;
+      const float ad = xs[row * ldx + HC + H + h];
+      RowSoftmax R;
+      row_softmax(R, sA, ad, ae, rowmask, row, row * n, n, i, H, h, slope, lane);
+      float dp[4], pd[4];
+      float dot = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = lane + 64 * q;
+        const bool valid = R.present[q] || j == i;
+        const float p = valid ? R.p[q] : 0.f;
+        float d = (j < NP) ? lrow[j] : 0.f;
+        pd[q] = p;
+        if (keep && valid) {
+          const bool kp = keep[((g * H + h) * n + i) * n + j] != 0;
+          d = kp ? d * keep_scale : 0.f;
+          pd[q] = kp ? p * keep_scale : 0.f;
+        }
+        dp[q] = valid ? d : 0.f;
+        dot += p * dp[q];
+      }
+      dot = wave_sum(dot);
+      float dl[4], rsum = 0.f, dloop = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = lane + 64 * q;
+        const bool valid = R.present[q] || j == i;
+        const float ds = valid ? R.p[q] * (dp[q] - dot) : 0.f;
+        dl[q] = R.neg[q] ? ds * slope : ds;
+        rsum += dl[q];
+        if (j == i) dloop = dl[q];
+      }
+      rsum = wave_sum(rsum);
+      dloop = wave_sum(dloop);  // only lane of j == i contributes
+      if (lane == 0) dxs[row * ldx + HC + H + h] = rsum;  // d a_dst
+      const float dshare = (ae && R.cnt > 0) ? dloop / (float)R.cnt : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = lane + 64 * q;
+        if (j < NP) {
+          prow[j] = pd[q];
+          lrow[j] = dl[q];
+        }
+        if (dae && j < n) dae[(row * n + j) * H + h] = R.present[q] ? dl[q] + dshare : 0.f;
+      }
+    }
+    __syncthreads();
+    // ---- column sums of dL (d a_src) and dxs_h += Pdᵀ · dOut ----
+    for (int j = t; j < NP; j += TT) {
+      float s = 0.f;
+#pragma unroll
+      for (int r = 0; r < TB; ++r) s += sL[r * PS + j];
+      sDa[j] += s;
+    }
+#pragma unroll
+    for (int a = 0; a < MAXJT; ++a) {
+      const int jt = wave + 4 * a;
+      if (jt < njt) {
+        const float* pa = sP + lk * PS + 16 * jt + li;  // Pᵀ[j][i] = P[i][j]
+#pragma unroll
+        for (int b = 0; b < CT; ++b) {
+          const float* ob = sO + lk * OS + 16 * b + li;
+#pragma unroll
+          for (int k = 0; k < TB; k += 4)
+            dacc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[k * PS], ob[k * OS], dacc[a][b],
+                                                              0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- write dxs_h, d a_src, padding columns, bias partial ----
+#pragma unroll
+  for (int a = 0; a < MAXJT; ++a) {
+    const int jt = wave + 4 * a;
+    if (jt < njt) {
+#pragma unroll
+      for (int b = 0; b < CT; ++b) {
+        const int c = 16 * b + li;
+        if (c < C) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = 16 * jt + 4 * lk + r;
+            if (j < n) dxs[(row0 + j) * ldx + h * C + c] = dacc[a][b][r];
+          }
+        }
+      }
+    }
+  }
+  for (int j = t; j < n; j += TT) dxs[(row0 + j) * ldx + HC + h] = sDa[j];
+  if (h == 0) {
+    const int padc = ldx - HC - 2 * H;
+    for (int idx = t; idx < n * padc; idx += TT) {
+      const int j = idx / padc;
+      dxs[(row0 + j) * ldx + HC + 2 * H + (idx - j * padc)] = 0.f;
+    }
+  }
+  if (t < C && (CONCAT || h == 0)) dbias[g * OC + oc0 + t] = dbias_acc;
+}
+
+}  // namespace sv2n
+
+// ============================ C-ABI ========================================
+using namespace sv2n;
+
+static int ct_of(int C) { return (C + 15) / 16; }
+
+static size_t tiled_fwd_lds(int n, int C) {
+  const int CW = 16 * ct_of(C), NP = round_up(n, 16);
+  return sizeof(float) * ((size_t)NP * pad32(CW, 16) + (size_t)TB * pad32(NP, 2) + NP);
+}
+static size_t tiled_bwd_lds(int n, int C) {
+  const int CW = 16 * ct_of(C), NP = round_up(n, 16);
+  return sizeof(float) * ((size_t)NP * (CW + 1) + 2 * (size_t)TB * pad32(NP, 16) +
+                          (size_t)TB * (CW + 1) + 2 * (size_t)NP);
+}
+
+template <typename K>
+static void raise_lds_tiled(K kernel, size_t bytes) {
+  if (bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+}
+
+static int check_tiled(int64_t B, int n, int H, int C, int ldx, int act) {
+  if (B <= 0 || C <= 0 || n <= 0) return SV2N_ERR_ARG;
+  if (n > TILED_MAX_N || H < 1 || H > SV2N_MAX_HEADS || C > TILED_MAX_C || act < 0 || act > 3)
+    return SV2N_ERR_SHAPE;
+  if (ldx < H * C + 2 * H) return SV2N_ERR_SHAPE;
+  if (B * H > 0x7fffffff) return SV2N_ERR_SHAPE;
+  return 0;
+}
+
+template <int ACT, bool CONCAT, int CT>
+static void tiled_fwd_launch(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
+                             const uint32_t* rowmask, const float* bias, const uint8_t* keep,
+                             float ks, float* out, int n, int H, int C, float slope) {
+  const size_t lds = tiled_fwd_lds(n, C);
+  raise_lds_tiled(k_attn_tiled_fwd<ACT, CONCAT, CT>, lds);
+  hipLaunchKernelGGL((k_attn_tiled_fwd<ACT, CONCAT, CT>), dim3((unsigned)(B * H)), dim3(TT), lds,
+                     st, xs, ldx, ae, rowmask, bias, keep, ks, out, n, H, C, slope);
+}
+
+template <int ACT, bool CONCAT, int CT>
+static void tiled_bwd_launch(int64_t B, hipStream_t st, const float* dy, const float* y,
+                             const float* xs, int ldx, const float* ae, const uint8_t* keep,
+                             float ks, const uint32_t* rowmask, float* dxs, float* dae,
+                             float* dbias, int n, int H, int C, float slope) {
+  const size_t lds = tiled_bwd_lds(n, C);
+  raise_lds_tiled(k_attn_tiled_bwd<ACT, CONCAT, CT>, lds);
+  hipLaunchKernelGGL((k_attn_tiled_bwd<ACT, CONCAT, CT>), dim3((unsigned)(B * H)), dim3(TT), lds,
+                     st, dy, y, xs, ldx, ae, keep, ks, rowmask, dxs, dae, dbias, n, H, C, slope);
+}
+
+#define SV2N_TILED_CT(FN, ACT, CONCAT, ...)                 \
+  switch (ct_of(C)) {                                       \
+    case 1: FN<ACT, CONCAT, 1>(__VA_ARGS__); break;         \
+    case 2: FN<ACT, CONCAT, 2>(__VA_ARGS__); break;         \
+    case 3: FN<ACT, CONCAT, 3>(__VA_ARGS__); break;         \
+    default: FN<ACT, CONCAT, 4>(__VA_ARGS__); break;        \
+  }
+#define SV2N_TILED_ACT(FN, CONCAT, ...)                     \
+  switch (act) {                                            \
+    case 0: SV2N_TILED_CT(FN, 0, CONCAT, __VA_ARGS__) break; \
+    case 1: SV2N_TILED_CT(FN, 1, CONCAT, __VA_ARGS__) break; \
+    case 2: SV2N_TILED_CT(FN, 2, CONCAT, __VA_ARGS__) break; \
+    default: SV2N_TILED_CT(FN, 3, CONCAT, __VA_ARGS__) break; \
+  }
+
+extern "C" int64_t sv2n_gat_attn_tiled_workspace(int64_t num_graphs, int n, int heads,
+                                                 int channels, int concat) {
+  return concat ? 0 : num_graphs * n * (int64_t)heads * channels;
+}
+
+extern "C" int sv2n_gat_attn_tiled_fwd(const float* xs, int ldx, const float* ae,
+                                       const uint32_t* rowmask, const float* bias,
+                                       const uint8_t* keep, float keep_scale, float* y,
+                                       float* workspace, int64_t workspace_floats,
+                                       int64_t num_graphs, int n, int heads, int channels,
+                                       int concat, int act, float negative_slope,
+                                       hipStream_t stream) {
+  if (!xs || !y) return SV2N_ERR_ARG;
+  const int C = channels;
+  if (int rc = check_tiled(num_graphs, n, heads, C, ldx, act)) return rc;
+  if (concat) {
+    SV2N_TILED_ACT(tiled_fwd_launch, true, num_graphs, stream, xs, ldx, ae, rowmask, bias, keep,
+                   keep_scale, y, n, heads, C, negative_slope)
+  } else {
+    const int64_t need = sv2n_gat_attn_tiled_workspace(num_graphs, n, heads, C, 0);
+    if (!workspace || workspace_floats < need) return SV2N_ERR_WORKSPACE;
+    SV2N_TILED_CT(tiled_fwd_launch, 0, false, num_graphs, stream, xs, ldx, ae, rowmask, nullptr,
+                  keep, keep_scale, workspace, n, heads, C, negative_slope)
+    const int64_t tot = num_graphs * n * (int64_t)C;
+    const unsigned grid = (unsigned)((tot + 255) / 256);
+    const int64_t N = num_graphs * n;
+    switch (act) {
+      case 0: hipLaunchKernelGGL(k_head_mean<0>, dim3(grid), dim3(256), 0, stream, workspace, bias, y, N, heads, C); break;
+      case 1: hipLaunchKernelGGL(k_head_mean<1>, dim3(grid), dim3(256), 0, stream, workspace, bias, y, N, heads, C); break;
+      case 2: hipLaunchKernelGGL(k_head_mean<2>, dim3(grid), dim3(256), 0, stream, workspace, bias, y, N, heads, C); break;
+      default: hipLaunchKernelGGL(k_head_mean<3>, dim3(grid), dim3(256), 0, stream, workspace, bias, y, N, heads, C); break;
+    }
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_gat_attn_tiled_bwd(const float* dy, const float* y, const float* xs, int ldx,
+                                       const float* ae, const uint8_t* keep, float keep_scale,
+                                       const uint32_t* rowmask, float* dxs, float* dae,
+                                       float* dbias_partial, int64_t num_graphs, int n,
+                                       int heads, int channels, int concat, int act,
+                                       float negative_slope, hipStream_t stream) {
+  if (!dy || !y || !xs || !dxs || !dbias_partial) return SV2N_ERR_ARG;
+  const int C = channels;
+  if (int rc = check_tiled(num_graphs, n, heads, C, ldx, act)) return rc;
+  if (concat) {
+    SV2N_TILED_ACT(tiled_bwd_launch, true, num_graphs, stream, dy, y, xs, ldx, ae, keep,
+                   keep_scale, rowmask, dxs, dae, dbias_partial, n, heads, C, negative_slope)
+  } else {
+    SV2N_TILED_ACT(tiled_bwd_launch, false, num_graphs, stream, dy, y, xs, ldx, ae, keep,
+                   keep_scale, rowmask, dxs, dae, dbias_partial, n, heads, C, negative_slope)
+  }
+  return (int)hipGetLastError();
+}

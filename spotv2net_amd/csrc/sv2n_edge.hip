@@ -321,7 +321,8 @@ __global__ void k_block_rowmask(const int64_t* __restrict__ ei, int64_t E, int64
   const int64_t g = t / n;
   const int64_t j = s - g * n;
   if (j < 0 || j >= n) return;
-  atomicOr(&rowmask[t], 1u << (int)j);
+  const int W = (n + 31) >> 5;
+  atomicOr(&rowmask[t * W + (j >> 5)], 1u << (int)(j & 31));
 }
 
 }  // namespace sv2n
@@ -348,7 +349,7 @@ extern "C" int sv2n_edge_logits_fwd(const float* edge_attr, int64_t num_edges, i
     return SV2N_ERR_ARG;
   if (num_edges == 0) return 0;  // nothing to project (e.g. single-node graphs)
   if (!edge_index && !canon) return SV2N_ERR_ARG;
-  if (n < 1 || n > SV2N_MAX_N || heads < 1 || heads > SV2N_MAX_HEADS || num_layers < 1 ||
+  if (n < 1 || n > SV2N_MAX_N_TILED || heads < 1 || heads > SV2N_MAX_HEADS || num_layers < 1 ||
       num_layers > SV2N_MAX_LAYERS || num_layers * heads > hl_pad)
     return SV2N_ERR_SHAPE;
   if (((uintptr_t)edge_attr & 15) || ((uintptr_t)wfold & 15)) return SV2N_ERR_ALIGN;
@@ -408,7 +409,7 @@ extern "C" int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, i
       num_graphs <= 0)
     return SV2N_ERR_ARG;
   if (!edge_index && !canon) return SV2N_ERR_ARG;
-  if (n < 1 || n > SV2N_MAX_N || heads < 1 || heads > SV2N_MAX_HEADS || num_layers < 1 ||
+  if (n < 1 || n > SV2N_MAX_N_TILED || heads < 1 || heads > SV2N_MAX_HEADS || num_layers < 1 ||
       num_layers > SV2N_MAX_LAYERS || num_layers * heads > hl_pad)
     return SV2N_ERR_SHAPE;
   if ((uintptr_t)edge_attr & 15) return SV2N_ERR_ALIGN;
@@ -464,7 +465,7 @@ extern "C" int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, i
 extern "C" int sv2n_block_rowmask(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
                                   int n, uint32_t* rowmask, hipStream_t stream) {
   if (!edge_index || !rowmask || num_edges < 0 || num_nodes <= 0) return SV2N_ERR_ARG;
-  if (n < 1 || n > SV2N_MAX_N) return SV2N_ERR_SHAPE;
+  if (n < 1 || n > SV2N_MAX_N_TILED) return SV2N_ERR_SHAPE;
   if (num_edges == 0) return 0;
   hipLaunchKernelGGL(k_block_rowmask, dim3((unsigned)((num_edges + 255) / 256)), dim3(256), 0,
                      stream, edge_index, num_edges, num_nodes, n, rowmask);

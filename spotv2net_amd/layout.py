@@ -16,10 +16,11 @@ on the tensor object (keyed by its version counter):
   with no duplicate (source, target) pair; kernels read edge_index, and a
   per-target source bitmask covers absent edges.
 
-Anything else (ragged graph sizes, duplicate edges, n > 32) raises
-``UnsupportedLayout``: the CSR path for those is a later build step
-(SURVEY.md §8f-f4).  Analysis runs on the device with torch ops and costs one
-host synchronisation per new edge_index tensor.
+Blocks of n <= 32 nodes run on the one-workgroup-per-graph attention
+kernels; 32 < n <= 256 (the C5 stress shapes) on the target-row-tiled ones.
+Anything else (ragged graph sizes, duplicate edges, n > 256) raises
+``UnsupportedLayout``.  Analysis runs on the device with torch ops and costs
+one host synchronisation per new edge_index tensor.
 """
 from __future__ import annotations
 
@@ -30,7 +31,8 @@ import torch
 
 from . import _lib
 
-MAX_N = 32
+MAX_N = 256          # largest block (include/sv2n.h SV2N_MAX_N_TILED)
+SMALL_N = 32         # blocks up to this size use the per-graph kernels
 
 
 class UnsupportedLayout(NotImplementedError):
@@ -45,8 +47,13 @@ class GraphLayout:
     num_nodes: int
     num_edges: int
     edge_index: Optional[torch.Tensor]  # read by kernels on the 'block' path
-    rowmask: Optional[torch.Tensor]     # int32 [N] source bitmask; None = complete graphs
+    rowmask: Optional[torch.Tensor]     # int32 [N][ceil(n/32)] source bitmask; None = complete
     canon: Optional[torch.Tensor]       # int16 [n(n-1)] (target<<8 | source) table
+
+    @property
+    def tiled(self) -> bool:
+        """True when the blocks need the target-row-tiled attention kernels."""
+        return self.n > SMALL_N
 
     @property
     def device(self) -> torch.device:
@@ -92,6 +99,10 @@ def canonical_edge_index(n: int, num_graphs: int = 1, device=None) -> torch.Tens
             return ei  # do not pin very large batches in the cache
         _canon_cache[key] = ei
     return _canon_cache[key]
+
+
+def _words(n: int) -> int:
+    return (n + 31) // 32
 
 
 def _attach(edge_index: torch.Tensor, key, layout: GraphLayout) -> GraphLayout:
@@ -147,15 +158,15 @@ def analyze_edge_index(edge_index: torch.Tensor, num_nodes: int,
                 break
     if nb is None:
         raise UnsupportedLayout(
-            "graph batch is not a union of equal-size blocks of <= 32 nodes; the general "
-            "CSR path is not built yet (SURVEY.md §8f-f4)")
+            f"graph batch is not a union of equal-size blocks of <= {MAX_N} nodes")
     B = N // nb
 
     # 2) canonical?
     E0 = nb * (nb - 1)
     canon = canonical_table(nb, device)
     if E == 0:  # isolated nodes only: every target keeps just its self loop
-        rowmask = None if nb == 1 else torch.zeros(N, dtype=torch.int32, device=device)
+        rowmask = None if nb == 1 else torch.zeros(N * _words(nb), dtype=torch.int32,
+                                                    device=device)
         lay = GraphLayout("canonical" if nb == 1 else "block", nb, B, N, 0, None, rowmask, canon)
         return _attach(edge_index, key, lay)
     if E == B * E0 and bool(torch.equal(edge_index, canonical_edge_index(nb, B, device))):
@@ -170,7 +181,7 @@ def analyze_edge_index(edge_index: torch.Tensor, num_nodes: int,
         raise UnsupportedLayout("duplicate edges: the dense-block kernels need unique pairs")
     rowmask = None
     if nk != B * E0:
-        rowmask = torch.zeros(N, dtype=torch.int32, device=device)
+        rowmask = torch.zeros(N * _words(nb), dtype=torch.int32, device=device)
         if device.type != "cuda":
             raise UnsupportedLayout("the sv2n kernels need a ROCm device")
         _lib.check(_lib.load().sv2n_block_rowmask(edge_index.data_ptr(), E, N, nb,

@@ -239,6 +239,10 @@ def gat_attention(xs: torch.Tensor, ae: Optional[torch.Tensor], bias: Optional[t
                   training: bool = False) -> torch.Tensor:
     """Fused GAT attention for one layer; ``xs`` = [lin_src(x) | a_src | a_dst]."""
     _require_device(xs, ae, bias)
+    if layout.tiled:
+        from .layout import UnsupportedLayout
+        raise UnsupportedLayout("the per-op attention covers n <= 32; larger blocks run through "
+                                "the fused stack (GATConv.forward / gat_stack)")
     if xs.stride(1) != 1 or xs.stride(0) % 4 or xs.data_ptr() % 16:
         xs = _aligned(xs)
     keep, scale = None, 1.0

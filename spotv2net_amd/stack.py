@@ -64,6 +64,7 @@ class _GATStack(torch.autograd.Function):
         B, n, N = layout.num_graphs, layout.n, layout.num_nodes
         use_edge = edge_attr is not None and all(c.lin_edge is not None for c in convs)
         H = convs[0].heads
+        tiled = layout.tiled
         if use_edge and any(c.heads != H for c in convs):
             raise NotImplementedError("fused edge pass needs equal head counts across layers")
 
@@ -114,20 +115,32 @@ class _GATStack(torch.autograd.Function):
                 raise ValueError(f"layer {l}: expected {F} input features, got {xin.size(1)}")
             xs = gemm_f32(xin, True, waugs[l], True, N, waugs[l].size(0), F)
             keep, kscale = None, 1.0
+            kn = n if tiled else 32  # keep-mask tile: [B][H][n][n] tiled, [B][H][32][32] per-graph
             if training and c.dropout > 0.0:
                 if c.dropout >= 1.0:
-                    keep = torch.zeros(B, Hc, 32, 32, device=dev, dtype=torch.uint8)
+                    keep = torch.zeros(B, Hc, kn, kn, device=dev, dtype=torch.uint8)
                     kscale = 0.0
                 else:
-                    keep = (torch.rand(B, Hc, 32, 32, device=dev) >= c.dropout).to(torch.uint8)
+                    keep = (torch.rand(B, Hc, kn, kn, device=dev) >= c.dropout).to(torch.uint8)
                     kscale = 1.0 / (1.0 - c.dropout)
             OC = Hc * C if c.concat else C
             y = torch.empty(N, OC, device=dev, dtype=torch.float32)
-            ps = torch.empty(B, Hc, 32, 32, device=dev, dtype=torch.float32)
-            _lib.check(lib.sv2n_gat_attn_fwd(
-                xs.data_ptr(), xs.stride(0), _lib.ptr(aes[l]), _lib.ptr(layout.rowmask),
-                _lib.ptr(c.bias), _lib.ptr(keep), kscale, y.data_ptr(), ps.data_ptr(), B, n, Hc, C,
-                int(c.concat), act, float(c.negative_slope), st), "sv2n_gat_attn_fwd")
+            if tiled:
+                # nothing saved: the backward recomputes the attention from xs and ae
+                ps = None
+                ws_n = lib.sv2n_gat_attn_tiled_workspace(B, n, Hc, C, int(c.concat))
+                ws = torch.empty(max(ws_n, 1), device=dev, dtype=torch.float32)
+                _lib.check(lib.sv2n_gat_attn_tiled_fwd(
+                    xs.data_ptr(), xs.stride(0), _lib.ptr(aes[l]), _lib.ptr(layout.rowmask),
+                    _lib.ptr(c.bias), _lib.ptr(keep), kscale, y.data_ptr(), ws.data_ptr(), ws_n,
+                    B, n, Hc, C, int(c.concat), act, float(c.negative_slope), st),
+                    "sv2n_gat_attn_tiled_fwd")
+            else:
+                ps = torch.empty(B, Hc, 32, 32, device=dev, dtype=torch.float32)
+                _lib.check(lib.sv2n_gat_attn_fwd(
+                    xs.data_ptr(), xs.stride(0), _lib.ptr(aes[l]), _lib.ptr(layout.rowmask),
+                    _lib.ptr(c.bias), _lib.ptr(keep), kscale, y.data_ptr(), ps.data_ptr(), B, n,
+                    Hc, C, int(c.concat), act, float(c.negative_slope), st), "sv2n_gat_attn_fwd")
             out = y
             dmask = None
             if training and post_dropout > 0.0:
@@ -140,7 +153,7 @@ class _GATStack(torch.autograd.Function):
             saved_x.append(xin)
             saved_xs.append(xs)
             saved_y.append(y)
-            saved_p.append(ps)
+            saved_p.append(aes[l] if tiled else ps)
             saved_keep.append(keep)
             saved_drop.append(dmask)
             xin = out
@@ -188,11 +201,20 @@ class _GATStack(torch.autograd.Function):
             dxs = torch.empty_like(xs)
             dae = torch.empty(B, n, n, Hc, device=dev, dtype=torch.float32) if use_edge else None
             dbp = torch.empty(B, OC, device=dev, dtype=torch.float32)
-            _lib.check(lib.sv2n_gat_attn_bwd(
-                dy.data_ptr(), ys[l].data_ptr(), xs.data_ptr(), xs.stride(0), pss[l].data_ptr(),
-                _lib.ptr(keeps[l]), ctx.kscales[l], _lib.ptr(layout.rowmask), dxs.data_ptr(),
-                _lib.ptr(dae), dbp.data_ptr(), B, n, Hc, C, int(c.concat), act,
-                float(c.negative_slope), st), "sv2n_gat_attn_bwd")
+            if layout.tiled:  # pss[l] holds the layer's ae (or None without edges)
+                _lib.check(lib.sv2n_gat_attn_tiled_bwd(
+                    dy.data_ptr(), ys[l].data_ptr(), xs.data_ptr(), xs.stride(0),
+                    _lib.ptr(pss[l]), _lib.ptr(keeps[l]), ctx.kscales[l],
+                    _lib.ptr(layout.rowmask), dxs.data_ptr(), _lib.ptr(dae), dbp.data_ptr(), B,
+                    n, Hc, C, int(c.concat), act, float(c.negative_slope), st),
+                    "sv2n_gat_attn_tiled_bwd")
+            else:
+                _lib.check(lib.sv2n_gat_attn_bwd(
+                    dy.data_ptr(), ys[l].data_ptr(), xs.data_ptr(), xs.stride(0),
+                    pss[l].data_ptr(), _lib.ptr(keeps[l]), ctx.kscales[l],
+                    _lib.ptr(layout.rowmask), dxs.data_ptr(), _lib.ptr(dae), dbp.data_ptr(), B,
+                    n, Hc, C, int(c.concat), act, float(c.negative_slope), st),
+                    "sv2n_gat_attn_bwd")
             daes[l] = dae
             gW = _grad_buf(c.lin_src.weight)
             gas = _grad_buf(c.att_src)
