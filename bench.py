@@ -35,11 +35,31 @@ F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32, de
 
 S, N_NODES, HEADS, HIDDEN, BATCH = 42, 30, 4, [100, 50], 512
 
+# BASELINE.json configs.  c2 is the headline workload (the
+# driver's default run); the others are measured with --config.
+CONFIGS = {
+    "c1": dict(S=42, n=30, heads=1, hidden=[500], concat=False, batch=32, dropout_att=0.0,
+               desc="C1: 1 GAT layer, 1 head, hidden [500], 30-node dense graphs, S=42"),
+    "c2": dict(S=42, n=30, heads=4, hidden=[100, 50], concat=True, batch=512, dropout_att=0.0,
+               desc="C2 train step (fwd+MSE+bwd+Adam): 30-node dense GAT graphs, "
+                    "870 edges + self loops, seq_length 42 (F=1260, D=126), "
+                    "GAT [100,50] x 4 heads concat, relu"),
+    "c3": dict(S=42, n=30, heads=6, hidden=[500], concat=True, batch=128, dropout_att=0.1,
+               desc="C3: config/GNN_param.yaml model (S=42, hidden [500], 6 heads, "
+                    "dropout_att 0.1, batch 128), fp32"),
+    "c5": dict(S=4, n=256, heads=8, hidden=[16, 16, 16], concat=True, batch=1024,
+               dropout_att=0.0,
+               desc="C5 stress: 256-node dense graphs (65,280 edges), S=4 (F=1024, D=12), "
+                    "3 GAT layers [16,16,16] x 8 heads concat"),
+}
 
-def build_model(dev):
+
+def build_model(dev, cfg=None):
     from spotv2net_amd import GATModel
+    cfg = cfg or CONFIGS["c2"]
     torch.manual_seed(5154)  # config/GNN_param.yaml:23
-    return GATModel(N_NODES * S, 3 * S, HEADS, 1, HIDDEN, concat_heads=True,
+    return GATModel(cfg["n"] * cfg["S"], 3 * cfg["S"], cfg["heads"], 1, cfg["hidden"],
+                    dropout_att=cfg["dropout_att"], concat_heads=cfg["concat"],
                     activation="relu", negative_slope=0.2).to(dev)
 
 
@@ -185,14 +205,16 @@ def load_traffic(kernel):
 # --------------------------------------------------------------------------
 # CPU baseline: PyG-semantics oracle, same model/config, host cores
 # --------------------------------------------------------------------------
-def cpu_baseline(model, budget_s: float, batch: int):
+def cpu_baseline(model, budget_s: float, batch: int, cfg=None):
     from oracle.pyg_gatconv import OracleGATModel
     from spotv2net_amd import Data, synthetic_batch
+    cfg = cfg or CONFIGS["c2"]
     cores = min(os.cpu_count() or 1, int(os.environ.get("SV2N_CPU_THREADS", "16")))
     torch.set_num_threads(cores)
-    ref = OracleGATModel(N_NODES * S, 3 * S, HEADS, 1, HIDDEN, concat_heads=True)
+    ref = OracleGATModel(cfg["n"] * cfg["S"], 3 * cfg["S"], cfg["heads"], 1, cfg["hidden"],
+                         dropout_att=cfg["dropout_att"], concat_heads=cfg["concat"])
     ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
-    data = synthetic_batch(batch, S, seed=4321)
+    data = synthetic_batch(batch, cfg["S"], n=cfg["n"], seed=4321)
     d = Data(x=data.x, edge_index=data.edge_index, edge_attr=data.edge_attr)
     opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
 
@@ -223,7 +245,7 @@ def cpu_baseline(model, budget_s: float, batch: int):
         pass
     return {"value": round(gps, 2), "unit": "graphs/s", "cores": cores, "kind": "port",
             "sample": f"oracle PyG-2.3.0-semantics GATModel (unfolded lin_edge, scatter softmax), "
-                      f"same C2 model, {steps} train steps (fwd+bwd+Adam) x {batch} graphs, "
+                      f"same model, {steps} train steps (fwd+bwd+Adam) x {batch} graphs, "
                       f"{el:.1f}s, torch {torch.__version__} CPU, {cpu_name}"}
 
 
@@ -232,7 +254,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=BATCH, help="graphs per GPU")
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="graphs per GPU (config default)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (no hipGraph)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -250,11 +273,14 @@ def main():
     from spotv2net_amd import synthetic_batch
     from spotv2net_amd.train import ForwardStep, TrainStep
 
-    model = build_model(dev)
+    cfg = CONFIGS[args.config]
+    if args.batch is None:
+        args.batch = cfg["batch"]
+    model = build_model(dev, cfg)
     if world > 1:  # identical replicas: broadcast rank 0's weights
         for p in model.parameters():
             dist.broadcast(p.data, 0)
-    data = synthetic_batch(args.batch, S, n=N_NODES, seed=1234 + rank, device=dev)
+    data = synthetic_batch(args.batch, cfg["S"], n=cfg["n"], seed=1234 + rank, device=dev)
 
     step = TrainStep(model, data, lr=1e-3, use_graph=not args.no_graph)
     for _ in range(args.warmup):
@@ -276,13 +302,15 @@ def main():
     if rank == 0:
         table = {}
         roof = None
-        if not args.no_kernel_table:
+        if not args.no_kernel_table and args.config == "c2":
             table = kernel_table(model, data)
             kname, roof = roofline_entry(table)
             roof["traffic"] = load_traffic(kname)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(model, args.cpu_seconds, args.batch)
+            # bounded sample: about as many edges as 512 C2 graphs
+            cpu_batch = max(1, min(args.batch, 445440 // (cfg["n"] * (cfg["n"] - 1))))
+            cpu = cpu_baseline(model, args.cpu_seconds, cpu_batch, cfg)
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -297,9 +325,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic (standardized symmetric vol / vol-of-vol matrices, "
                     "CovarianceLaggedDataset layout), device-resident, random-init weights",
-            "config": {"workload": "C2 train step (fwd+MSE+bwd+Adam): 30-node dense GAT graphs, "
-                                   "870 edges + self loops, seq_length 42 (F=1260, D=126), "
-                                   "GAT [100,50] x 4 heads concat, relu",
+            "config": {"workload": cfg["desc"], "name": args.config,
                        "graphs_per_gpu": args.batch, "global_batch": args.batch * world,
                        "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
             "fwd_graphs_per_s": round(fwd_value, 1),

@@ -200,27 +200,53 @@ int sv2n_head_bwd(const float* x, int64_t num_rows, int in_features, const float
 /* Fused attention for dense-block graphs of 32 < n <= 256 nodes (any n <= 256
  * works; n <= 32 is faster on sv2n_gat_attn_fwd/bwd).  Same semantics and
  * arguments as sv2n_gat_attn_fwd/bwd except:
+ *   ae       the layer's edge logits as head planes [H][num_edges] in edge
+ *            order (sv2n_edge_logits_fwd_planes), or NULL (no edge term);
+ *   eid      [N][n] int32 edge id of (target row, source j), -1 if absent
+ *            (sv2n_block_eid), or NULL for the canonical edge order;
  *   rowmask  [N][ceil(n/32)] uint32 words (bit j%32 of word j/32 of row g*n+i:
  *            edge j->i present) or NULL for complete graphs;
  *   keep     [num_graphs][H][n][n] uint8 or NULL;
  *   channels <= 64;
+ *   dae      (backward) head planes [H][num_edges]: every present edge's
+ *            entry is written, input self loops are left untouched;
  *   nothing is saved for the backward: it recomputes the attention from xs
  *   and ae (pass the forward's ae again);
  *   concat = 0 needs a workspace of sv2n_gat_attn_tiled_workspace(...)
  *   floats (per-head aggregates before the mean). */
 int64_t sv2n_gat_attn_tiled_workspace(int64_t num_graphs, int n, int heads, int channels,
                                       int concat);
-int sv2n_gat_attn_tiled_fwd(const float* xs, int ldx, const float* ae, const uint32_t* rowmask,
-                            const float* bias, const uint8_t* keep, float keep_scale,
-                            float* y, float* workspace, int64_t workspace_floats,
-                            int64_t num_graphs, int n, int heads, int channels, int concat,
-                            int act, float negative_slope, hipStream_t stream);
-int sv2n_gat_attn_tiled_bwd(const float* dy, const float* y, const float* xs, int ldx,
-                            const float* ae, const uint8_t* keep, float keep_scale,
-                            const uint32_t* rowmask, float* dxs, float* dae,
-                            float* dbias_partial, int64_t num_graphs, int n, int heads,
+int sv2n_gat_attn_tiled_fwd(const float* xs, int ldx, const float* ae, int64_t num_edges,
+                            const int32_t* eid, const uint32_t* rowmask, const float* bias,
+                            const uint8_t* keep, float keep_scale, float* y, float* workspace,
+                            int64_t workspace_floats, int64_t num_graphs, int n, int heads,
                             int channels, int concat, int act, float negative_slope,
                             hipStream_t stream);
+int sv2n_gat_attn_tiled_bwd(const float* dy, const float* y, const float* xs, int ldx,
+                            const float* ae, int64_t num_edges, const int32_t* eid,
+                            const uint8_t* keep, float keep_scale, const uint32_t* rowmask,
+                            float* dxs, float* dae, float* dbias_partial, int64_t num_graphs,
+                            int n, int heads, int channels, int concat, int act,
+                            float negative_slope, hipStream_t stream);
+
+/* Edge logits / their weight gradient with the per-layer output in head
+ * planes [H][num_edges] (edge order), the layout of the tiled attention:
+ * ae_layers[l][h*E + e] = edge_attr[e] · wfold[:, l*H + h] for every edge
+ * (input self loops included; their values are never read).  The backward
+ * skips input self loops when edge_index is given (NULL: none present). */
+int sv2n_edge_logits_fwd_planes(const float* edge_attr, int64_t num_edges, int edge_dim,
+                                const float* wfold, int hl_pad, float* const* ae_layers,
+                                int num_layers, int heads, hipStream_t stream);
+int sv2n_edge_logits_bwd_planes(const float* edge_attr, int64_t num_edges, int edge_dim,
+                                const int64_t* edge_index, const float* const* dae_layers,
+                                int num_layers, int heads, float* workspace,
+                                int64_t workspace_floats, float* dwfold, int hl_pad,
+                                hipStream_t stream);
+
+/* eid[t*n + j] = e for every non-self edge e: s->t, j = s - g*n (eid
+ * [num_nodes][n] int32 must be filled with -1 by the caller). */
+int sv2n_block_eid(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, int n,
+                   int32_t* eid, hipStream_t stream);
 
 /* rowmask[t*W + j/32] |= 1<<(j%32), W = ceil(n/32), j = s - g*n, for every
  * non-self edge s->t (rowmask [num_nodes][W] must be zeroed by the caller).

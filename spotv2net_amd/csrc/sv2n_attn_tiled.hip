@@ -5,8 +5,14 @@
 // longer fit one 32-lane half:
 //
 // * one workgroup (4 waves) per (graph g, head h); blockIdx is remapped so the
-//   H head-workgroups of a graph run on the same XCD and share its L2 for the
-//   head-interleaved AE rows ([g][i][j][h]) they all read;
+//   H head-workgroups of a graph run on the same XCD (shared L2 for the xs
+//   rows they all read);
+// * edge logits come in per-layer head planes AE[h][e] in edge order (what
+//   sv2n_edge_logits_fwd_planes writes with fully coalesced stores); edge e of
+//   (target i, source j) is computed from the canonical order or read from an
+//   eid map [g][i][j] (block layouts).  A target block's first-half edges
+//   (sources j < i) are 16 consecutive edge ids per j, so the gathers stay
+//   sector-coalesced across the block's rows;
 // * targets are walked in blocks of TB = 16 rows; a wave owns a row at a time
 //   and its lanes cover sources j = lane + 64q, so the self-loop mean, the
 //   softmax max / sum are 64-lane wave reductions;
@@ -31,6 +37,8 @@
 // stride ≡ 2 (mod 32) or odd; "row = lane>>4, col = lane&15" for ≡ 16 (mod 32)
 // (odd: one 2-way pair).  Strides below follow the role each image plays.
 #include "sv2n_common.h"
+
+#include <algorithm>
 
 namespace sv2n {
 
@@ -68,75 +76,144 @@ __host__ __device__ constexpr int pad32(int a, int mod) {  // smallest s >= a, s
   return a + ((mod - a % 32) + 32) % 32;
 }
 
-// One target row of the recomputed attention: scores, self loop (mean fill),
-// leaky_relu, softmax.  Lane owns j = lane + 64q (q < 4).  Returns per-slot
-// probabilities p (0 for absent), the leaky-negative flags and the row's
-// present-edge count.
-struct RowSoftmax {
-  float p[4];
-  bool neg[4];
-  bool present[4];  // j != i edge present
-  int cnt;
+// In-graph edge index of (target i <- source j) in the CovarianceLaggedDataset
+// order (reference utils/dataset.py:216-226: the row-major upper pairs (u < v)
+// as u -> v, then the same pairs swapped).  32-bit: n(n-1) < 2^31.
+__device__ __forceinline__ int canon_eid(int n, int i, int j) {
+  const int u = j > i ? i : j, v = j > i ? j : i;
+  return (j > i ? (n * (n - 1)) / 2 : 0) + u * (2 * n - u - 1) / 2 + (v - u - 1);
+}
+
+constexpr int RPW = TB / 4;  // rows per wave per target block
+constexpr int SRS = TB + 4;  // K-split partial row stride (16-B aligned, fewer conflicts)
+
+// One thread per source column j = t: the TB rows' edge logits of a target
+// block (-inf where edge j->i is absent or j == i), every load independent so
+// a block's gathers are all in flight together; issued one block ahead of
+// the block being computed.
+__device__ __forceinline__ void load_block(float (&pv)[TB], int i0, int t,
+                                           const float* __restrict__ ae,
+                                           const int32_t* __restrict__ eid,
+                                           const uint32_t* __restrict__ rowmask, int64_t g, int n) {
+  const int j = t;
+  const int W = (n + 31) >> 5;
+  const int64_t E0 = (int64_t)n * (n - 1);
+#pragma unroll
+  for (int r = 0; r < TB; ++r) {
+    const int i = i0 + r;
+    float v = -INFINITY;
+    if (i < n && j < n && j != i) {
+      const int64_t row = g * n + i;
+      if (eid) {
+        const int e = eid[row * n + j];
+        if (e >= 0) v = ae ? ae[e] : 0.f;
+      } else if (!rowmask || ((rowmask[row * W + (j >> 5)] >> (j & 31)) & 1u)) {
+        v = ae ? ae[g * E0 + canon_eid(n, i, j)] : 0.f;
+      }
+    }
+    pv[r] = v;
+  }
+}
+
+__device__ __forceinline__ int64_t edge_index_of(const int32_t* __restrict__ eid, int64_t g,
+                                                 int n, int i, int j) {
+  return eid ? (int64_t)eid[(g * n + i) * n + j]
+             : g * ((int64_t)n * (n - 1)) + canon_eid(n, i, j);
+}
+
+// Softmax of RPW target rows at once (independent rows share every reduction
+// round).  Lane owns sources j = lane + 64q.  On return p[rr][q] is the
+// probability (0 where invalid), neg[rr][q] the leaky-negative flag,
+// present[rr][q] whether edge j->i exists, cnt[rr] the in-degree.
+struct Rows {
+  float p[RPW][4];
+  bool neg[RPW][4];
+  bool present[RPW][4];
+  float cnt[RPW];
 };
 
-__device__ __forceinline__ void row_softmax(RowSoftmax& R, const float* __restrict__ sA,
-                                            float ad, const float* __restrict__ ae,
-                                            const uint32_t* __restrict__ rowmask, int64_t row,
-                                            int64_t aerow, int n, int i, int H, int h,
-                                            float slope, int lane) {
-  const int W = (n + 31) >> 5;
-  float e[4], s[4];
-  float esum = 0.f;
-  int cnt = 0;
+__device__ __forceinline__ void rows_softmax(Rows& R, const float* __restrict__ sE, int SE,
+                                             const float* __restrict__ sA,
+                                             const float* __restrict__ sD, int rb, int i0, int n,
+                                             int NP, bool has_ae, float slope, int lane) {
+  float e[RPW][4], red[2 * RPW];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int j = lane + 64 * q;
-    bool pr = false;
-    if (j < n && j != i) {
-      pr = rowmask ? ((rowmask[row * W + (j >> 5)] >> (j & 31)) & 1u) : true;
+  for (int rr = 0; rr < RPW; ++rr) {
+    float es = 0.f, c = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = lane + 64 * q;
+      const float ev = j < NP ? sE[(rb + rr) * SE + j] : -INFINITY;
+      const bool pr = ev != -INFINITY;
+      R.present[rr][q] = pr;
+      e[rr][q] = pr ? ev : 0.f;
+      es += e[rr][q];
+      c += pr ? 1.f : 0.f;
     }
-    R.present[q] = pr;
-    e[q] = (pr && ae) ? ae[(aerow + j) * H + h] : 0.f;
-    esum += e[q];
-    cnt += pr ? 1 : 0;
+    red[rr] = es;
+    red[RPW + rr] = c;
   }
-  esum = wave_sum(esum);
-  cnt = (int)wave_sum((float)cnt);
-  R.cnt = cnt;
-  const float loopv = (ae && cnt > 0) ? esum / (float)cnt : 0.f;
-  float mx = -INFINITY;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int j = lane + 64 * q;
-    const bool valid = R.present[q] || j == i;
-    float v = (j < n ? sA[j] : 0.f) + ad;
-    v += (j == i) ? loopv : e[q];
-    R.neg[q] = !(v > 0.f);
-    const float lr = R.neg[q] ? v * slope : v;
-    s[q] = valid ? lr : -INFINITY;
-    mx = fmaxf(mx, s[q]);
+  for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+    for (int k = 0; k < 2 * RPW; ++k) red[k] += __shfl_xor(red[k], m, 64);
+  float mx[RPW], s[RPW][4];
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int i = i0 + rb + rr;
+    R.cnt[rr] = red[RPW + rr];
+    const float loopv = (has_ae && R.cnt[rr] > 0.f) ? red[rr] / R.cnt[rr] : 0.f;
+    const float ad = i < n ? sD[i] : 0.f;
+    mx[rr] = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = lane + 64 * q;
+      const bool valid = i < n && (R.present[rr][q] || j == i);
+      float v = (j < NP ? sA[j] : 0.f) + ad;
+      v += (j == i) ? loopv : e[rr][q];
+      R.neg[rr][q] = !(v > 0.f);
+      const float lr = R.neg[rr][q] ? v * slope : v;
+      s[rr][q] = valid ? lr : -INFINITY;
+      mx[rr] = fmaxf(mx[rr], s[rr][q]);
+    }
   }
-  mx = wave_max(mx);
-  float den = 0.f;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    s[q] = (s[q] == -INFINITY) ? 0.f : expf(s[q] - mx);
-    den += s[q];
+  for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) mx[rr] = fmaxf(mx[rr], __shfl_xor(mx[rr], m, 64));
+  float den[RPW];
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    den[rr] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s[rr][q] = (s[rr][q] == -INFINITY) ? 0.f : expf(s[rr][q] - mx[rr]);
+      den[rr] += s[rr][q];
+    }
   }
-  den = wave_sum(den) + 1e-16f;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) R.p[q] = s[q] / den;
+  for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) den[rr] += __shfl_xor(den[rr], m, 64);
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const float inv = den[rr] + 1e-16f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) R.p[rr][q] = s[rr][q] / inv;
+  }
 }
 
 // ---------------------------------------------------------------------------
 // forward
+// LDS: sX [NP][XS] | sP [TB][PS] | sA [NP] | sD [NP] | sE [TB][NP] (aliased by
+//      the K-split partials sR [4][TB][CW] after the rows phase)
 // ---------------------------------------------------------------------------
 template <int ACT, bool CONCAT, int CT>
 __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
-    const float* __restrict__ xs, int ldx, const float* __restrict__ ae,
-    const uint32_t* __restrict__ rowmask, const float* __restrict__ bias,
-    const uint8_t* __restrict__ keep, float keep_scale, float* __restrict__ out, int n, int H,
-    int C, float slope) {
+    const float* __restrict__ xs, int ldx, const float* __restrict__ ae_planes, int64_t E,
+    const int32_t* __restrict__ eid, const uint32_t* __restrict__ rowmask,
+    const float* __restrict__ bias, const uint8_t* __restrict__ keep, float keep_scale,
+    float* __restrict__ out, int n, int H, int C, float slope) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int CW = 16 * CT;
   constexpr int XS = pad32(CW, 16);  // B operand: row = lane>>4
@@ -145,6 +222,9 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
   float* sX = smem;               // [NP][XS]
   float* sP = sX + NP * XS;       // [TB][PS]
   float* sA = sP + TB * PS;       // [NP]
+  float* sD = sA + NP;            // [NP]
+  float* sE = sD + NP;            // [TB][NP], max(TB*NP, 4*CW*SRS) floats
+  float* sR = sE;                 // [4][CW][SRS], after the rows phase
 
   int64_t g;
   int h;
@@ -152,59 +232,81 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t row0 = g * n;
   const int HC = H * C;
+  const float* ae = ae_planes ? ae_planes + (int64_t)h * E : nullptr;
 
+  float pv[TB];
+  load_block(pv, 0, t, ae, eid, rowmask, g, n);
   for (int idx = t; idx < NP * CW; idx += TT) {
     const int j = idx / CW, c = idx - j * CW;
     sX[j * XS + c] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
   }
-  for (int j = t; j < NP; j += TT) sA[j] = j < n ? xs[(row0 + j) * ldx + HC + h] : 0.f;
-  __syncthreads();
+  for (int j = t; j < NP; j += TT) {
+    sA[j] = j < n ? xs[(row0 + j) * ldx + HC + h] : 0.f;
+    sD[j] = j < n ? xs[(row0 + j) * ldx + HC + H + h] : 0.f;
+  }
 
   const int li = lane & 15, lk = lane >> 4;
+  const int kq = NP / 4;  // K-split: wave w sums sources [w*kq, (w+1)*kq)
   for (int i0 = 0; i0 < n; i0 += TB) {
-    // ---- P rows of this block ----
-    for (int r = wave; r < TB; r += 4) {
-      const int i = i0 + r;
-      float* prow = sP + r * PS;
-      if (i >= n) {
-        for (int j = lane; j < NP; j += 64) prow[j] = 0.f;
-        continue;
-      }
-      const int64_t row = row0 + i;
-      const float ad = xs[row * ldx + HC + H + h];
-      RowSoftmax R;
-      row_softmax(R, sA, ad, ae, rowmask, row, row * n, n, i, H, h, slope, lane);
+    if (t < NP) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = lane + 64 * q;
-        if (j < NP) {
-          float pd = (R.present[q] || j == i) ? R.p[q] : 0.f;
-          if (keep && j < n) pd = keep[((g * H + h) * n + i) * n + j] ? pd * keep_scale : 0.f;
-          prow[j] = pd;
+      for (int r = 0; r < TB; ++r) sE[r * NP + t] = pv[r];
+    }
+    __syncthreads();
+    if (i0 + TB < n) load_block(pv, i0 + TB, t, ae, eid, rowmask, g, n);
+    // ---- P rows: wave w owns rows [4w, 4w+4) of the block ----
+    {
+      const int rb = wave * RPW;
+      Rows R;
+      rows_softmax(R, sE, NP, sA, sD, rb, i0, n, NP, ae != nullptr, slope, lane);
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) {
+        const int i = i0 + rb + rr;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = lane + 64 * q;
+          if (j < NP) {
+            float pd = R.p[rr][q];
+            if (keep && i < n && j < n)
+              pd = keep[((g * H + h) * n + i) * n + j] ? pd * keep_scale : 0.f;
+            sP[(rb + rr) * PS + j] = pd;
+          }
         }
       }
     }
     __syncthreads();
-    // ---- out[i][c] = Σ_j P[i][j] xs_h[j][c]: wave w owns column tile w (CT <= 4) ----
-    if (wave < CT) {
-      f4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* pa = sP + li * PS + lk;
-      const float* xb = sX + lk * XS + 16 * wave + li;
-      for (int k = 0; k < NP; k += 4)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[k], xb[k * XS], acc, 0, 0, 0);
-      const int c = 16 * wave + li;
-      if (c < C) {
+    // ---- out[i][c] = Σ_j P[i][j] xs_h[j][c], K split over the 4 waves ----
+    {
+      f4 acc[CT];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = i0 + 4 * lk + r;
-          if (i < n) {
-            if (CONCAT) {
-              const float b = bias ? bias[h * C + c] : 0.f;
-              out[(row0 + i) * HC + h * C + c] = act_fwd<ACT>(acc[r] + b);
-            } else {
-              out[(row0 + i) * HC + h * C + c] = acc[r];  // workspace, per head
-            }
-          }
+      for (int b = 0; b < CT; ++b) acc[b] = f4{0.f, 0.f, 0.f, 0.f};
+      const float* pa = sP + li * PS + lk;
+      for (int k = wave * kq; k < (wave + 1) * kq; k += 4) {
+        const float a = pa[k];
+#pragma unroll
+        for (int b = 0; b < CT; ++b)
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, sX[(k + lk) * XS + 16 * b + li],
+                                                        acc[b], 0, 0, 0);
+      }
+      // partials column-major [wave][c][row]: one 16-B store per tile (the
+      // row-major scalar form was miscompiled into ds_write2 with wrong
+      // offsets by this toolchain at CT = 4)
+#pragma unroll
+      for (int b = 0; b < CT; ++b)
+        *reinterpret_cast<f4*>(sR + (wave * CW + 16 * b + li) * SRS + 4 * lk) = acc[b];
+    }
+    __syncthreads();
+    for (int idx = t; idx < TB * CW; idx += TT) {
+      const int r = idx / CW, c = idx - r * CW;
+      const int i = i0 + r;
+      if (i < n && c < C) {
+        const float* q = sR + c * SRS + r;
+        const float v = (q[0] + q[CW * SRS]) + (q[2 * CW * SRS] + q[3 * CW * SRS]);
+        if (CONCAT) {
+          const float b = bias ? bias[h * C + c] : 0.f;
+          out[(row0 + i) * HC + h * C + c] = act_fwd<ACT>(v + b);
+        } else {
+          out[(row0 + i) * HC + h * C + c] = v;  // workspace, per head
         }
       }
     }
@@ -236,14 +338,15 @@ __global__ __launch_bounds__(256) void k_head_mean(const float* __restrict__ ws,
 //   dae[i][j] = dL[i][j] + dL[i][i] / cnt  (present j),  a_d[i] += Σ_j dL,
 //   a_s[j] += Σ_i dL[i][j],  dxs_h[j] += Σ_i Pd[i][j] dOut[i]
 // LDS: sX [NP][XS] | sP [TB][PS] (Pd) | sL [TB][PS] (dP then dL) |
-//      sO [TB][OS] (dOut) | sAs [NP] | sDa [NP] (Σ_i dL[i][j])
+//      sO [TB][OS] (dOut) | sA [NP] | sD [NP] | sDa [NP] | sE [TB][NP]
 // ---------------------------------------------------------------------------
 template <int ACT, bool CONCAT, int CT>
 __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ xs,
-    int ldx, const float* __restrict__ ae, const uint8_t* __restrict__ keep, float keep_scale,
-    const uint32_t* __restrict__ rowmask, float* __restrict__ dxs, float* __restrict__ dae,
-    float* __restrict__ dbias, int n, int H, int C, float slope) {
+    int ldx, const float* __restrict__ ae_planes, int64_t E, const int32_t* __restrict__ eid,
+    const uint8_t* __restrict__ keep, float keep_scale, const uint32_t* __restrict__ rowmask,
+    float* __restrict__ dxs, float* __restrict__ dae_planes, float* __restrict__ dbias, int n,
+    int H, int C, float slope) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int CW = 16 * CT;
   constexpr int XS = CW + 1;         // dP's B operand: row = lane&15
@@ -255,7 +358,9 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
   float* sL = sP + TB * PS;       // [TB][PS]
   float* sO = sL + TB * PS;       // [TB][OS]
   float* sA = sO + TB * OS;       // [NP]
-  float* sDa = sA + NP;           // [NP]
+  float* sD = sA + NP;            // [NP]
+  float* sDa = sD + NP;           // [NP]
+  float* sE = sDa + NP;           // [TB][NP]
 
   int64_t g;
   int h;
@@ -266,13 +371,18 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
   const int OC = CONCAT ? HC : C;
   const int oc0 = CONCAT ? h * C : 0;
   const float oscale = CONCAT ? 1.f : 1.f / (float)H;
+  const float* ae = ae_planes ? ae_planes + (int64_t)h * E : nullptr;
+  float* dae = dae_planes ? dae_planes + (int64_t)h * E : nullptr;
 
+  float pv[TB];
+  load_block(pv, 0, t, ae, eid, rowmask, g, n);
   for (int idx = t; idx < NP * CW; idx += TT) {
     const int j = idx / CW, c = idx - j * CW;
     sX[j * XS + c] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
   }
   for (int j = t; j < NP; j += TT) {
     sA[j] = j < n ? xs[(row0 + j) * ldx + HC + h] : 0.f;
+    sD[j] = j < n ? xs[(row0 + j) * ldx + HC + H + h] : 0.f;
     sDa[j] = 0.f;
   }
   // dxs accumulators: wave w owns row tiles jt = w, w+4, ... (NP/16 <= 16) x CT column tiles
@@ -285,10 +395,13 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
   float dbias_acc = 0.f;  // thread t < C owns bias column t of this head's slice
   const int li = lane & 15, lk = lane >> 4;
   const int njt = NP / 16;
-  __syncthreads();
 
   for (int i0 = 0; i0 < n; i0 += TB) {
-    // ---- dOut rows ----
+    // ---- stage: edge logits of this block (prefetched), dOut rows ----
+    if (t < NP) {
+#pragma unroll
+      for (int r = 0; r < TB; ++r) sE[r * NP + t] = pv[r];
+    }
     for (int idx = t; idx < TB * CW; idx += TT) {
       const int r = idx / CW, c = idx - r * CW;
       const int i = i0 + r;
@@ -300,6 +413,7 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
       sO[r * OS + c] = v * oscale;
     }
     __syncthreads();
+    if (i0 + TB < n) load_block(pv, i0 + TB, t, ae, eid, rowmask, g, n);
     if (t < C && (CONCAT || h == 0)) {
       float s = 0.f;
       for (int r = 0; r < TB; ++r) s += sO[r * OS + t];
@@ -317,59 +431,72 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
       for (int r = 0; r < 4; ++r) sL[(4 * lk + r) * PS + 16 * jt + li] = acc[r];
     }
     __syncthreads();
-    // ---- per row: recompute P, softmax / leaky / dropout backward ----
-    for (int r = wave; r < TB; r += 4) {
-      const int i = i0 + r;
-      float* prow = sP + r * PS;
-      float* lrow = sL + r * PS;
-      if (i >= n) {
-        for (int j = lane; j < NP; j += 64) { prow[j] = 0.f; lrow[j] = 0.f; }
-        continue;
-      }
-      const int64_t row = row0 + i;
-      const float ad = xs[row * ldx + HC + H + h];
-      RowSoftmax R;
-      row_softmax(R, sA, ad, ae, rowmask, row, row * n, n, i, H, h, slope, lane);
-      float dp[4], pd[4];
-      float dot = 0.f;
+    // ---- rows: recompute P, softmax / leaky / dropout backward ----
+    {
+      const int rb = wave * RPW;
+      Rows R;
+      rows_softmax(R, sE, NP, sA, sD, rb, i0, n, NP, ae != nullptr, slope, lane);
+      float dp[RPW][4], pd[RPW][4], red[3 * RPW];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = lane + 64 * q;
-        const bool valid = R.present[q] || j == i;
-        const float p = valid ? R.p[q] : 0.f;
-        float d = (j < NP) ? lrow[j] : 0.f;
-        pd[q] = p;
-        if (keep && valid) {
-          const bool kp = keep[((g * H + h) * n + i) * n + j] != 0;
-          d = kp ? d * keep_scale : 0.f;
-          pd[q] = kp ? p * keep_scale : 0.f;
+      for (int rr = 0; rr < RPW; ++rr) {
+        const int i = i0 + rb + rr;
+        float dot = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = lane + 64 * q;
+          const float p = R.p[rr][q];
+          float d = (j < NP) ? sL[(rb + rr) * PS + j] : 0.f;
+          pd[rr][q] = p;
+          if (keep && i < n && j < n && (R.present[rr][q] || j == i)) {
+            const bool kp = keep[((g * H + h) * n + i) * n + j] != 0;
+            d = kp ? d * keep_scale : 0.f;
+            pd[rr][q] = kp ? p * keep_scale : 0.f;
+          }
+          dp[rr][q] = p != 0.f ? d : 0.f;
+          dot += p * dp[rr][q];
         }
-        dp[q] = valid ? d : 0.f;
-        dot += p * dp[q];
+        red[rr] = dot;
       }
-      dot = wave_sum(dot);
-      float dl[4], rsum = 0.f, dloop = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = lane + 64 * q;
-        const bool valid = R.present[q] || j == i;
-        const float ds = valid ? R.p[q] * (dp[q] - dot) : 0.f;
-        dl[q] = R.neg[q] ? ds * slope : ds;
-        rsum += dl[q];
-        if (j == i) dloop = dl[q];
-      }
-      rsum = wave_sum(rsum);
-      dloop = wave_sum(dloop);  // only lane of j == i contributes
-      if (lane == 0) dxs[row * ldx + HC + H + h] = rsum;  // d a_dst
-      const float dshare = (ae && R.cnt > 0) ? dloop / (float)R.cnt : 0.f;
+      for (int m = 32; m >= 1; m >>= 1)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = lane + 64 * q;
-        if (j < NP) {
-          prow[j] = pd[q];
-          lrow[j] = dl[q];
+        for (int k = 0; k < RPW; ++k) red[k] += __shfl_xor(red[k], m, 64);
+      float dl[RPW][4];
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) {
+        const int i = i0 + rb + rr;
+        float rsum = 0.f, dloop = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = lane + 64 * q;
+          const float ds = R.p[rr][q] * (dp[rr][q] - red[rr]);
+          dl[rr][q] = R.neg[rr][q] ? ds * slope : ds;
+          rsum += dl[rr][q];
+          if (j == i) dloop = dl[rr][q];
         }
-        if (dae && j < n) dae[(row * n + j) * H + h] = R.present[q] ? dl[q] + dshare : 0.f;
+        red[RPW + rr] = rsum;
+        red[2 * RPW + rr] = dloop;
+      }
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+        for (int k = RPW; k < 3 * RPW; ++k) red[k] += __shfl_xor(red[k], m, 64);
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) {
+        const int r = rb + rr, i = i0 + r;
+        if (i < n && lane == 0) dxs[(row0 + i) * ldx + HC + H + h] = red[RPW + rr];  // d a_dst
+        const float dshare =
+            (ae && R.cnt[rr] > 0.f) ? red[2 * RPW + rr] / R.cnt[rr] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = lane + 64 * q;
+          if (j < NP) {
+            sP[r * PS + j] = pd[rr][q];
+            sL[r * PS + j] = dl[rr][q];
+          }
+          if (dae && R.present[rr][q])
+            dae[edge_index_of(eid, g, n, i, j)] = dl[rr][q] + dshare;
+        }
       }
     }
     __syncthreads();
@@ -435,12 +562,13 @@ static int ct_of(int C) { return (C + 15) / 16; }
 
 static size_t tiled_fwd_lds(int n, int C) {
   const int CW = 16 * ct_of(C), NP = round_up(n, 16);
-  return sizeof(float) * ((size_t)NP * pad32(CW, 16) + (size_t)TB * pad32(NP, 2) + NP);
+  return sizeof(float) * ((size_t)NP * pad32(CW, 16) + (size_t)TB * pad32(NP, 2) + 2 * NP +
+                          std::max((size_t)TB * NP, (size_t)4 * CW * SRS));
 }
 static size_t tiled_bwd_lds(int n, int C) {
   const int CW = 16 * ct_of(C), NP = round_up(n, 16);
   return sizeof(float) * ((size_t)NP * (CW + 1) + 2 * (size_t)TB * pad32(NP, 16) +
-                          (size_t)TB * (CW + 1) + 2 * (size_t)NP);
+                          (size_t)TB * (CW + 1) + 3 * (size_t)NP + (size_t)TB * NP);
 }
 
 template <typename K>
@@ -461,23 +589,26 @@ static int check_tiled(int64_t B, int n, int H, int C, int ldx, int act) {
 
 template <int ACT, bool CONCAT, int CT>
 static void tiled_fwd_launch(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
-                             const uint32_t* rowmask, const float* bias, const uint8_t* keep,
-                             float ks, float* out, int n, int H, int C, float slope) {
+                             int64_t E, const int32_t* eid, const uint32_t* rowmask,
+                             const float* bias, const uint8_t* keep, float ks, float* out, int n,
+                             int H, int C, float slope) {
   const size_t lds = tiled_fwd_lds(n, C);
   raise_lds_tiled(k_attn_tiled_fwd<ACT, CONCAT, CT>, lds);
   hipLaunchKernelGGL((k_attn_tiled_fwd<ACT, CONCAT, CT>), dim3((unsigned)(B * H)), dim3(TT), lds,
-                     st, xs, ldx, ae, rowmask, bias, keep, ks, out, n, H, C, slope);
+                     st, xs, ldx, ae, E, eid, rowmask, bias, keep, ks, out, n, H, C, slope);
 }
 
 template <int ACT, bool CONCAT, int CT>
 static void tiled_bwd_launch(int64_t B, hipStream_t st, const float* dy, const float* y,
-                             const float* xs, int ldx, const float* ae, const uint8_t* keep,
-                             float ks, const uint32_t* rowmask, float* dxs, float* dae,
-                             float* dbias, int n, int H, int C, float slope) {
+                             const float* xs, int ldx, const float* ae, int64_t E,
+                             const int32_t* eid, const uint8_t* keep, float ks,
+                             const uint32_t* rowmask, float* dxs, float* dae, float* dbias, int n,
+                             int H, int C, float slope) {
   const size_t lds = tiled_bwd_lds(n, C);
   raise_lds_tiled(k_attn_tiled_bwd<ACT, CONCAT, CT>, lds);
   hipLaunchKernelGGL((k_attn_tiled_bwd<ACT, CONCAT, CT>), dim3((unsigned)(B * H)), dim3(TT), lds,
-                     st, dy, y, xs, ldx, ae, keep, ks, rowmask, dxs, dae, dbias, n, H, C, slope);
+                     st, dy, y, xs, ldx, ae, E, eid, keep, ks, rowmask, dxs, dae, dbias, n, H, C,
+                     slope);
 }
 
 #define SV2N_TILED_CT(FN, ACT, CONCAT, ...)                 \
@@ -501,6 +632,7 @@ extern "C" int64_t sv2n_gat_attn_tiled_workspace(int64_t num_graphs, int n, int 
 }
 
 extern "C" int sv2n_gat_attn_tiled_fwd(const float* xs, int ldx, const float* ae,
+                                       int64_t num_edges, const int32_t* eid,
                                        const uint32_t* rowmask, const float* bias,
                                        const uint8_t* keep, float keep_scale, float* y,
                                        float* workspace, int64_t workspace_floats,
@@ -510,14 +642,15 @@ extern "C" int sv2n_gat_attn_tiled_fwd(const float* xs, int ldx, const float* ae
   if (!xs || !y) return SV2N_ERR_ARG;
   const int C = channels;
   if (int rc = check_tiled(num_graphs, n, heads, C, ldx, act)) return rc;
+  if (ae && !eid && num_edges != num_graphs * (int64_t)n * (n - 1)) return SV2N_ERR_SHAPE;
   if (concat) {
-    SV2N_TILED_ACT(tiled_fwd_launch, true, num_graphs, stream, xs, ldx, ae, rowmask, bias, keep,
-                   keep_scale, y, n, heads, C, negative_slope)
+    SV2N_TILED_ACT(tiled_fwd_launch, true, num_graphs, stream, xs, ldx, ae, num_edges, eid,
+                   rowmask, bias, keep, keep_scale, y, n, heads, C, negative_slope)
   } else {
     const int64_t need = sv2n_gat_attn_tiled_workspace(num_graphs, n, heads, C, 0);
     if (!workspace || workspace_floats < need) return SV2N_ERR_WORKSPACE;
-    SV2N_TILED_CT(tiled_fwd_launch, 0, false, num_graphs, stream, xs, ldx, ae, rowmask, nullptr,
-                  keep, keep_scale, workspace, n, heads, C, negative_slope)
+    SV2N_TILED_CT(tiled_fwd_launch, 0, false, num_graphs, stream, xs, ldx, ae, num_edges, eid,
+                  rowmask, nullptr, keep, keep_scale, workspace, n, heads, C, negative_slope)
     const int64_t tot = num_graphs * n * (int64_t)C;
     const unsigned grid = (unsigned)((tot + 255) / 256);
     const int64_t N = num_graphs * n;
@@ -532,7 +665,8 @@ extern "C" int sv2n_gat_attn_tiled_fwd(const float* xs, int ldx, const float* ae
 }
 
 extern "C" int sv2n_gat_attn_tiled_bwd(const float* dy, const float* y, const float* xs, int ldx,
-                                       const float* ae, const uint8_t* keep, float keep_scale,
+                                       const float* ae, int64_t num_edges, const int32_t* eid,
+                                       const uint8_t* keep, float keep_scale,
                                        const uint32_t* rowmask, float* dxs, float* dae,
                                        float* dbias_partial, int64_t num_graphs, int n,
                                        int heads, int channels, int concat, int act,
@@ -540,12 +674,15 @@ extern "C" int sv2n_gat_attn_tiled_bwd(const float* dy, const float* y, const fl
   if (!dy || !y || !xs || !dxs || !dbias_partial) return SV2N_ERR_ARG;
   const int C = channels;
   if (int rc = check_tiled(num_graphs, n, heads, C, ldx, act)) return rc;
+  if (ae && !eid && num_edges != num_graphs * (int64_t)n * (n - 1)) return SV2N_ERR_SHAPE;
   if (concat) {
-    SV2N_TILED_ACT(tiled_bwd_launch, true, num_graphs, stream, dy, y, xs, ldx, ae, keep,
-                   keep_scale, rowmask, dxs, dae, dbias_partial, n, heads, C, negative_slope)
+    SV2N_TILED_ACT(tiled_bwd_launch, true, num_graphs, stream, dy, y, xs, ldx, ae, num_edges,
+                   eid, keep, keep_scale, rowmask, dxs, dae, dbias_partial, n, heads, C,
+                   negative_slope)
   } else {
-    SV2N_TILED_ACT(tiled_bwd_launch, false, num_graphs, stream, dy, y, xs, ldx, ae, keep,
-                   keep_scale, rowmask, dxs, dae, dbias_partial, n, heads, C, negative_slope)
+    SV2N_TILED_ACT(tiled_bwd_launch, false, num_graphs, stream, dy, y, xs, ldx, ae, num_edges,
+                   eid, keep, keep_scale, rowmask, dxs, dae, dbias_partial, n, heads, C,
+                   negative_slope)
   }
   return (int)hipGetLastError();
 }

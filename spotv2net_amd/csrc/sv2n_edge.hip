@@ -91,7 +91,7 @@ struct ChunkRegs {
 // per chunk, thread (el = t/4, q = t%4) sums d ≡ q (mod 4) for all hl_pad
 // columns, quad-reduced through DPP, then written per layer.
 // ---------------------------------------------------------------------------
-template <int HLP, int RF>
+template <int HLP, int RF, bool PLANES>
 __global__ __launch_bounds__(EDGE_THREADS) void k_edge_fwd(
     const float* __restrict__ ea, int64_t E, int D, const int64_t* __restrict__ ei,
     const uint16_t* __restrict__ canon, int E0, const float* __restrict__ wf, LayerPtrs ae,
@@ -157,13 +157,21 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_fwd(
     for (int k = 0; k < HLP; ++k)
       if ((k & 3) == q) s_out[el * HLP + k] = acc[k];
     __syncthreads();
-    for (int idx = t; idx < ne * HL; idx += EDGE_THREADS) {
-      const int le = idx / HL, k = idx - le * HL;
-      int64_t g;
-      int i, j;
-      if (!decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) continue;
-      const int l = k / H, h = k - l * H;
-      s_ptr[l][((g * n + i) * n + j) * H + h] = s_out[le * HLP + k];
+    if constexpr (PLANES) {  // [H][E] per layer: 64 consecutive edges per (layer, head)
+      for (int idx = t; idx < ne * HL; idx += EDGE_THREADS) {
+        const int k = idx / ne, le = idx - k * ne;
+        const int l = k / H, h = k - l * H;
+        s_ptr[l][(int64_t)h * E + e0 + le] = s_out[le * HLP + k];
+      }
+    } else {
+      for (int idx = t; idx < ne * HL; idx += EDGE_THREADS) {
+        const int le = idx / HL, k = idx - le * HL;
+        int64_t g;
+        int i, j;
+        if (!decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) continue;
+        const int l = k / H, h = k - l * H;
+        s_ptr[l][((g * n + i) * n + j) * H + h] = s_out[le * HLP + k];
+      }
     }
   }
 }
@@ -174,7 +182,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_fwd(
 // reduction at the end, then k_reduce_partials sums the per-block partials in
 // a fixed order (deterministic).
 // ---------------------------------------------------------------------------
-template <int HLP>
+template <int HLP, bool PLANES>
 __device__ __forceinline__ void gather_dae(float (&gd)[(EDGE_CHUNK * HLP + EDGE_THREADS - 1) / EDGE_THREADS],
                                            const float* const* s_ptr, const int64_t* __restrict__ ei,
                                            int64_t E, const uint16_t* __restrict__ canon, int E0,
@@ -184,19 +192,28 @@ __device__ __forceinline__ void gather_dae(float (&gd)[(EDGE_CHUNK * HLP + EDGE_
 #pragma unroll
   for (int s = 0; s < GN; ++s) {
     const int idx = t + s * EDGE_THREADS;
-    const int le = idx / HLP, k = idx - le * HLP;
     float v = 0.f;
-    int64_t g;
-    int i, j;
-    if (le < ne && k < HL && decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) {
-      const int l = k / H, h = k - l * H;
-      v = s_ptr[l][((g * n + i) * n + j) * H + h];
+    if constexpr (PLANES) {  // edge fastest: coalesced reads of the [H][E] planes
+      const int le = idx & (EDGE_CHUNK - 1), k = idx / EDGE_CHUNK;
+      const int64_t e = e0 + le;
+      if (le < ne && k < HL && !(ei && ei[e] == ei[E + e])) {
+        const int l = k / H, h = k - l * H;
+        v = s_ptr[l][(int64_t)h * E + e];
+      }
+    } else {
+      const int le = idx / HLP, k = idx - le * HLP;
+      int64_t g;
+      int i, j;
+      if (le < ne && k < HL && decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) {
+        const int l = k / H, h = k - l * H;
+        v = s_ptr[l][((g * n + i) * n + j) * H + h];
+      }
     }
     gd[s] = v;
   }
 }
 
-template <int HLP, int RF>
+template <int HLP, int RF, bool PLANES>
 __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
     const float* __restrict__ ea, int64_t E, int D, int DP, const int64_t* __restrict__ ei,
     const uint16_t* __restrict__ canon, int E0, LayerCPtrs dae, int L, int H, int64_t B, int n,
@@ -234,7 +251,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
     const int64_t e0 = c * EDGE_CHUNK;
     const int ne = (int)min((int64_t)EDGE_CHUNK, E - e0);
     R.load(ea, e0, ne, D, t);
-    gather_dae<HLP>(gd, s_ptr, ei, E, canon, E0, n, B, HL, H, e0, ne, t);
+    gather_dae<HLP, PLANES>(gd, s_ptr, ei, E, canon, E0, n, B, HL, H, e0, ne, t);
   }
   for (; c < nchunks; c += gridDim.x) {
     const int64_t e0 = c * EDGE_CHUNK;
@@ -245,7 +262,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
 #pragma unroll
     for (int s = 0; s < GN; ++s) {
       const int idx = t + s * EDGE_THREADS;
-      if (idx < EDGE_CHUNK * HLP) s_dae[idx] = gd[s];
+      if (idx < EDGE_CHUNK * HLP)
+        s_dae[PLANES ? (idx & (EDGE_CHUNK - 1)) * HLP + idx / EDGE_CHUNK : idx] = gd[s];
     }
     __syncthreads();
     const int64_t cn = c + gridDim.x;
@@ -253,7 +271,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
       const int64_t e1 = cn * EDGE_CHUNK;
       const int ne1 = (int)min((int64_t)EDGE_CHUNK, E - e1);
       R.load(ea, e1, ne1, D, t);
-      gather_dae<HLP>(gd, s_ptr, ei, E, canon, E0, n, B, HL, H, e1, ne1, t);
+      gather_dae<HLP, PLANES>(gd, s_ptr, ei, E, canon, E0, n, B, HL, H, e1, ne1, t);
     }
     if (active) {
       for (int le = es; le < ne; le += ES) {
@@ -325,6 +343,194 @@ __global__ void k_block_rowmask(const int64_t* __restrict__ ei, int64_t E, int64
   atomicOr(&rowmask[t * W + (j >> 5)], 1u << (int)(j & 31));
 }
 
+// ---------------------------------------------------------------------------
+// narrow edge features (D <= 16, e.g. the C5 stress shapes, D = 12): a 64-edge
+// chunk is only 3 KB there, too little in flight per workgroup, so one thread
+// owns one edge row instead.
+//   forward:  acc[k] = Σ_d ea[e][d] · W̃[d][k] (W̃ broadcast from LDS), stored
+//             per (layer, head) — coalesced across the wave in the plane layout
+//   backward: wave w owns columns k in [w*HLP/4, (w+1)*HLP/4) and accumulates
+//             ea[e][d] · dAE[e][k] for its lanes' edges in registers over a
+//             grid-stride loop; one wave reduction per (d, k) at the end, then
+//             k_reduce_partials (fixed order, deterministic).
+// ---------------------------------------------------------------------------
+constexpr int EDGE_SMALL_D = 16;
+
+// per-column output bases, built on the host: column k = l*H + h of layer l's
+// AE lives at col[k][e] (planes) or col[k][((g*n+i)*n+j)*H] (dense block)
+struct ColPtrs { float* p[32]; };
+struct ColCPtrs { const float* p[32]; };
+
+template <int DS>
+__device__ __forceinline__ void load_row_small(float (&x)[DS], const float* __restrict__ ea,
+                                               int64_t e, int D) {
+#pragma unroll
+  for (int d = 0; d < DS; ++d) x[d] = d < D ? ea[e * D + d] : 0.f;
+}
+
+template <int DS, int HLP, bool PLANES>
+__global__ __launch_bounds__(256) void k_edge_fwd_small(
+    const float* __restrict__ ea, int64_t E, int D, const int64_t* __restrict__ ei,
+    const uint16_t* __restrict__ canon, int E0, const float* __restrict__ wf, ColPtrs col,
+    int L, int H, int64_t B, int n) {
+  __shared__ __attribute__((aligned(16))) float s_wf[DS * HLP];
+  const int t = threadIdx.x;
+  for (int k = t; k < DS * HLP; k += 256) s_wf[k] = k < D * HLP ? wf[k] : 0.f;
+  __syncthreads();
+  const int HL = L * H;
+  const float4* w4 = reinterpret_cast<const float4*>(s_wf);
+  for (int64_t e = (int64_t)blockIdx.x * 256 + t; e < E; e += (int64_t)gridDim.x * 256) {
+    float x[DS];
+    load_row_small<DS>(x, ea, e, D);
+    int64_t off = e;
+    if constexpr (!PLANES) {
+      int64_t g;
+      int i, j;
+      if (!decode_edge(e, ei, E, canon, E0, n, B, g, i, j)) continue;
+      off = ((g * n + i) * n + j) * H;
+    }
+    // 4 output columns at a time (not unrolled: W̃ stays in LDS as broadcast
+    // reads instead of D*HLP live VGPRs)
+#pragma unroll 1
+    for (int k0 = 0; k0 < HL; k0 += 4) {
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+      for (int d = 0; d < DS; ++d) {
+        const float4 w = w4[d * (HLP / 4) + (k0 >> 2)];
+        a0 = fmaf(x[d], w.x, a0);
+        a1 = fmaf(x[d], w.y, a1);
+        a2 = fmaf(x[d], w.z, a2);
+        a3 = fmaf(x[d], w.w, a3);
+      }
+      col.p[k0][off] = a0;
+      if (k0 + 1 < HL) col.p[k0 + 1][off] = a1;
+      if (k0 + 2 < HL) col.p[k0 + 2][off] = a2;
+      if (k0 + 3 < HL) col.p[k0 + 3][off] = a3;
+    }
+  }
+}
+
+template <int DS, int HLP, bool PLANES>
+__global__ __launch_bounds__(256) void k_edge_bwd_small(
+    const float* __restrict__ ea, int64_t E, int D, const int64_t* __restrict__ ei,
+    const uint16_t* __restrict__ canon, int E0, ColCPtrs col, int L, int H, int64_t B, int n,
+    float* __restrict__ partial) {
+  constexpr int KQ = HLP / 4;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int HL = L * H;
+  float acc[DS][KQ];
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) acc[d][q] = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * 64 + lane; e < E; e += (int64_t)gridDim.x * 64) {
+    int64_t off = e;
+    bool ok;
+    if constexpr (PLANES) {
+      ok = !(ei && ei[e] == ei[E + e]);
+    } else {
+      int64_t g;
+      int i, j;
+      ok = decode_edge(e, ei, E, canon, E0, n, B, g, i, j);
+      off = ((g * n + i) * n + j) * H;
+    }
+    if (!ok) continue;
+    float x[DS];
+    load_row_small<DS>(x, ea, e, D);
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      const int k = wave * KQ + q;  // wave-uniform
+      const float v = k < HL ? col.p[k][off] : 0.f;
+#pragma unroll
+      for (int d = 0; d < DS; ++d) acc[d][q] = fmaf(x[d], v, acc[d][q]);
+    }
+  }
+  // wave reduction, lane 0 writes this block's [D][HLP] slab entries of its columns
+  float* pb = partial + (int64_t)blockIdx.x * D * HLP;
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      float v = acc[d][q];
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+      if (lane == 0 && d < D) pb[d * HLP + wave * KQ + q] = v;
+    }
+}
+
+// Head-plane backward on MFMA (D <= 16, E % 4 == 0, no input self loops):
+//   partial[d][k] = Σ_e ea[e][d] · dAE_k[e]  =  (eaᵀ · dAE)[d][k]
+// is a 16 x HLP output with K = E: each wave accumulates it in HLP/16
+// v_mfma_f32_16x16x4_f32 tiles over its own grid-stride stream of 64-edge
+// chunks.  Within a chunk lane group lk (= lane>>4) owns edges
+// e0 + 16*lk + s, s = 0..15 (MFMA step s), so its dAE operand for four steps
+// is one 16-B load from the plane and A (= ea[e][d], d = lane&15) is a
+// column read of 16 consecutive rows.  The four waves' tiles are summed
+// through LDS into one slab per block (k_reduce_partials finishes).
+template <int HLP>
+__global__ __launch_bounds__(256) void k_edge_bwd_mfma(const float* __restrict__ ea, int64_t E,
+                                                       int D, ColCPtrs col, int HL,
+                                                       float* __restrict__ partial) {
+  constexpr int NT = HLP >= 16 ? HLP / 16 : 1;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ float s_red[4][16 * NT * 16];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  f4 acc[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) acc[q] = f4{0.f, 0.f, 0.f, 0.f};
+  const float* bp[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) bp[q] = (16 * q + li < HL) ? col.p[16 * q + li] : nullptr;
+  const int64_t nchunks = (E + 63) / 64;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  for (int64_t c = (int64_t)blockIdx.x * 4 + wave; c < nchunks; c += stride) {
+    const int64_t eb = c * 64 + 16 * lk;  // this lane group's 16 edges
+    float a[16];
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2)
+      a[s2] = (li < D && eb + s2 < E) ? ea[(eb + s2) * D + li] : 0.f;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      f4 b[4];
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const int64_t e = eb + 4 * c4;
+        b[c4] = (bp[q] && e < E) ? *reinterpret_cast<const f4*>(bp[q] + e) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2)
+        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], b[s2 >> 2][s2 & 3], acc[q], 0, 0, 0);
+    }
+  }
+  // D layout: acc[q][r] = out[d = 4*lk + r][k = 16q + li]
+#pragma unroll
+  for (int q = 0; q < NT; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s_red[wave][(4 * lk + r) * (16 * NT) + 16 * q + li] = acc[q][r];
+  __syncthreads();
+  float* pb = partial + (int64_t)blockIdx.x * D * HLP;
+  for (int o = t; o < D * HLP; o += 256) {
+    const int d = o / HLP, k = o - d * HLP;
+    float v = 0.f;
+    if (k < 16 * NT) v = (s_red[0][d * 16 * NT + k] + s_red[1][d * 16 * NT + k]) +
+                         (s_red[2][d * 16 * NT + k] + s_red[3][d * 16 * NT + k]);
+    pb[o] = v;
+  }
+}
+
+// eid[t*n + j] = e for every non-self edge s->t, j = s - g*n (caller fills -1)
+__global__ void k_block_eid(const int64_t* __restrict__ ei, int64_t E, int64_t N, int n,
+                            int32_t* __restrict__ eid) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int64_t s = ei[e], t = ei[E + e];
+  if (s == t || t < 0 || t >= N) return;
+  const int64_t j = s - (t / n) * n;
+  if (j < 0 || j >= n) return;
+  eid[t * n + j] = (int32_t)e;
+}
+
 }  // namespace sv2n
 
 // ============================ C-ABI ========================================
@@ -332,6 +538,86 @@ using namespace sv2n;
 
 static constexpr int EDGE_BWD_GRID = 512;
 static constexpr int EDGE_FWD_GRID = 1024;
+static constexpr int EDGE_SMALL_FWD_GRID = 4096;
+static constexpr int EDGE_SMALL_BWD_GRID = 1024;
+
+#define SV2N_SMALL_DISPATCH(KERNEL, GRID, ...)                                              \
+  {                                                                                         \
+    const int ds = (edge_dim + 3) & ~3;                                                     \
+    switch (ds * 100 + hl_pad) {                                                            \
+      case 404: hipLaunchKernelGGL((KERNEL<4, 4, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;   \
+      case 408: hipLaunchKernelGGL((KERNEL<4, 8, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;   \
+      case 416: hipLaunchKernelGGL((KERNEL<4, 16, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;  \
+      case 432: hipLaunchKernelGGL((KERNEL<4, 32, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;  \
+      case 804: hipLaunchKernelGGL((KERNEL<8, 4, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;   \
+      case 808: hipLaunchKernelGGL((KERNEL<8, 8, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;   \
+      case 816: hipLaunchKernelGGL((KERNEL<8, 16, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;  \
+      case 832: hipLaunchKernelGGL((KERNEL<8, 32, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;  \
+      case 1204: hipLaunchKernelGGL((KERNEL<12, 4, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break; \
+      case 1208: hipLaunchKernelGGL((KERNEL<12, 8, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break; \
+      case 1216: hipLaunchKernelGGL((KERNEL<12, 16, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;\
+      case 1232: hipLaunchKernelGGL((KERNEL<12, 32, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;\
+      case 1604: hipLaunchKernelGGL((KERNEL<16, 4, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break; \
+      case 1608: hipLaunchKernelGGL((KERNEL<16, 8, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break; \
+      case 1616: hipLaunchKernelGGL((KERNEL<16, 16, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;\
+      case 1632: hipLaunchKernelGGL((KERNEL<16, 32, PL>), GRID, dim3(256), 0, stream, __VA_ARGS__); break;\
+      default: return SV2N_ERR_SHAPE;                                                       \
+    }                                                                                       \
+  }
+
+template <bool PL>
+static int edge_fwd_small(const float* edge_attr, int64_t num_edges, int edge_dim,
+                          const int64_t* edge_index, const uint16_t* canon, int E0,
+                          const float* wfold, int hl_pad, const LayerPtrs& lp, int num_layers,
+                          int heads, int64_t num_graphs, int n, hipStream_t stream) {
+  const int64_t blocks = (num_edges + 255) / 256;
+  const dim3 grid((unsigned)std::min<int64_t>(blocks, EDGE_SMALL_FWD_GRID));
+  ColPtrs col{};
+  for (int k = 0; k < num_layers * heads; ++k)
+    col.p[k] = lp.p[k / heads] + (PL ? (int64_t)(k % heads) * num_edges : (int64_t)(k % heads));
+  SV2N_SMALL_DISPATCH(k_edge_fwd_small, grid, edge_attr, num_edges, edge_dim, edge_index, canon,
+                      E0, wfold, col, num_layers, heads, num_graphs, n)
+  return (int)hipGetLastError();
+}
+
+template <bool PL>
+static int edge_bwd_small(const float* edge_attr, int64_t num_edges, int edge_dim,
+                          const int64_t* edge_index, const uint16_t* canon, int E0,
+                          const LayerCPtrs& lp, int num_layers, int heads, int64_t num_graphs,
+                          int n, float* workspace, int64_t workspace_floats, float* dwfold,
+                          int hl_pad, hipStream_t stream) {
+  const int O = edge_dim * hl_pad;
+  if (PL && !edge_index && (num_edges & 3) == 0) {  // MFMA path (planes 16-B aligned)
+    const int64_t blocks = (num_edges + 255) / 256;
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, EDGE_SMALL_BWD_GRID));
+    if (workspace_floats < (int64_t)nb * O) return SV2N_ERR_WORKSPACE;
+    ColCPtrs col{};
+    for (int k = 0; k < num_layers * heads; ++k)
+      col.p[k] = lp.p[k / heads] + (int64_t)(k % heads) * num_edges;
+    const int HL = num_layers * heads;
+    switch (hl_pad) {
+      case 4: hipLaunchKernelGGL(k_edge_bwd_mfma<4>, dim3(nb), dim3(256), 0, stream, edge_attr, num_edges, edge_dim, col, HL, workspace); break;
+      case 8: hipLaunchKernelGGL(k_edge_bwd_mfma<8>, dim3(nb), dim3(256), 0, stream, edge_attr, num_edges, edge_dim, col, HL, workspace); break;
+      case 16: hipLaunchKernelGGL(k_edge_bwd_mfma<16>, dim3(nb), dim3(256), 0, stream, edge_attr, num_edges, edge_dim, col, HL, workspace); break;
+      case 32: hipLaunchKernelGGL(k_edge_bwd_mfma<32>, dim3(nb), dim3(256), 0, stream, edge_attr, num_edges, edge_dim, col, HL, workspace); break;
+      default: return SV2N_ERR_SHAPE;
+    }
+    hipLaunchKernelGGL(k_reduce_partials, dim3((O + 63) / 64), dim3(256), 0, stream, workspace,
+                       nb, O, dwfold);
+    return (int)hipGetLastError();
+  }
+  const int64_t blocks = (num_edges + 63) / 64;
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, EDGE_SMALL_BWD_GRID));
+  if (workspace_floats < (int64_t)nb * O) return SV2N_ERR_WORKSPACE;
+  ColCPtrs col{};
+  for (int k = 0; k < num_layers * heads; ++k)
+    col.p[k] = lp.p[k / heads] + (PL ? (int64_t)(k % heads) * num_edges : (int64_t)(k % heads));
+  SV2N_SMALL_DISPATCH(k_edge_bwd_small, dim3(nb), edge_attr, num_edges, edge_dim, edge_index,
+                      canon, E0, col, num_layers, heads, num_graphs, n, workspace)
+  hipLaunchKernelGGL(k_reduce_partials, dim3((O + 63) / 64), dim3(256), 0, stream, workspace,
+                     nb, O, dwfold);
+  return (int)hipGetLastError();
+}
 
 template <typename K>
 static void raise_lds_limit(K kernel, size_t bytes) {
@@ -340,15 +626,14 @@ static void raise_lds_limit(K kernel, size_t bytes) {
                               160 * 1024);
 }
 
-extern "C" int sv2n_edge_logits_fwd(const float* edge_attr, int64_t num_edges, int edge_dim,
-                                    const int64_t* edge_index, const uint16_t* canon,
-                                    const float* wfold, int hl_pad, float* const* ae_layers,
-                                    int num_layers, int heads, int64_t num_graphs, int n,
-                                    hipStream_t stream) {
+static int edge_fwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim,
+                         const int64_t* edge_index, const uint16_t* canon, const float* wfold,
+                         int hl_pad, float* const* ae_layers, int num_layers, int heads,
+                         int64_t num_graphs, int n, bool planes, hipStream_t stream) {
   if (!edge_attr || !wfold || !ae_layers || num_edges < 0 || edge_dim <= 0 || num_graphs <= 0)
     return SV2N_ERR_ARG;
   if (num_edges == 0) return 0;  // nothing to project (e.g. single-node graphs)
-  if (!edge_index && !canon) return SV2N_ERR_ARG;
+  if (!planes && !edge_index && !canon) return SV2N_ERR_ARG;
   if (n < 1 || n > SV2N_MAX_N_TILED || heads < 1 || heads > SV2N_MAX_HEADS || num_layers < 1 ||
       num_layers > SV2N_MAX_LAYERS || num_layers * heads > hl_pad)
     return SV2N_ERR_SHAPE;
@@ -360,6 +645,13 @@ extern "C" int sv2n_edge_logits_fwd(const float* edge_attr, int64_t num_edges, i
     lp.p[l] = ae_layers[l];
   }
   const int E0 = n * (n - 1);
+  if (edge_dim <= EDGE_SMALL_D)
+    return planes ? edge_fwd_small<true>(edge_attr, num_edges, edge_dim, edge_index, canon, E0,
+                                         wfold, hl_pad, lp, num_layers, heads, num_graphs, n,
+                                         stream)
+                  : edge_fwd_small<false>(edge_attr, num_edges, edge_dim, edge_index, canon, E0,
+                                          wfold, hl_pad, lp, num_layers, heads, num_graphs, n,
+                                          stream);
   const int64_t nchunks = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
   const unsigned grid = (unsigned)std::min<int64_t>(nchunks, EDGE_FWD_GRID);
   const int rf = (EDGE_CHUNK * edge_dim / 4 + EDGE_THREADS - 1) / EDGE_THREADS;
@@ -368,12 +660,17 @@ extern "C" int sv2n_edge_logits_fwd(const float* edge_attr, int64_t num_edges, i
   const size_t lds = sizeof(float) * ((size_t)edge_dim * hl_pad + (size_t)rfi * EDGE_THREADS * 4 +
                                       (size_t)EDGE_CHUNK * hl_pad);
   if (lds > 160 * 1024) return SV2N_ERR_SHAPE;
-#define SV2N_LAUNCH_EF(HLP, RF)                                                                   \
+#define SV2N_LAUNCH_EF2(HLP, RF, PL)                                                              \
   {                                                                                               \
-    raise_lds_limit(k_edge_fwd<HLP, RF>, lds);                                                    \
-    hipLaunchKernelGGL((k_edge_fwd<HLP, RF>), dim3(grid), dim3(EDGE_THREADS), lds, stream,        \
+    raise_lds_limit(k_edge_fwd<HLP, RF, PL>, lds);                                                \
+    hipLaunchKernelGGL((k_edge_fwd<HLP, RF, PL>), dim3(grid), dim3(EDGE_THREADS), lds, stream,    \
                        edge_attr, num_edges, edge_dim, edge_index, canon, E0, wfold, lp,          \
                        num_layers, heads, num_graphs, n);                                         \
+  }
+#define SV2N_LAUNCH_EF(HLP, RF)                                  \
+  {                                                              \
+    if (planes) SV2N_LAUNCH_EF2(HLP, RF, true)                   \
+    else SV2N_LAUNCH_EF2(HLP, RF, false)                         \
   }
 #define SV2N_LAUNCH_EF_RF(HLP)                                   \
   case HLP:                                                      \
@@ -392,23 +689,24 @@ extern "C" int sv2n_edge_logits_fwd(const float* edge_attr, int64_t num_edges, i
   }
 #undef SV2N_LAUNCH_EF_RF
 #undef SV2N_LAUNCH_EF
+#undef SV2N_LAUNCH_EF2
   return (int)hipGetLastError();
 }
 
 extern "C" int64_t sv2n_edge_logits_bwd_workspace(int edge_dim, int hl_pad) {
-  return (int64_t)EDGE_BWD_GRID * edge_dim * hl_pad;
+  return (int64_t)(edge_dim <= EDGE_SMALL_D ? EDGE_SMALL_BWD_GRID : EDGE_BWD_GRID) * edge_dim *
+         hl_pad;
 }
 
-extern "C" int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, int edge_dim,
-                                    const int64_t* edge_index, const uint16_t* canon,
-                                    const float* const* dae_layers, int num_layers, int heads,
-                                    int64_t num_graphs, int n, float* workspace,
-                                    int64_t workspace_floats, float* dwfold, int hl_pad,
-                                    hipStream_t stream) {
+static int edge_bwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim,
+                         const int64_t* edge_index, const uint16_t* canon,
+                         const float* const* dae_layers, int num_layers, int heads,
+                         int64_t num_graphs, int n, float* workspace, int64_t workspace_floats,
+                         float* dwfold, int hl_pad, bool planes, hipStream_t stream) {
   if (!edge_attr || !dae_layers || !dwfold || !workspace || num_edges < 0 || edge_dim <= 0 ||
       num_graphs <= 0)
     return SV2N_ERR_ARG;
-  if (!edge_index && !canon) return SV2N_ERR_ARG;
+  if (!planes && !edge_index && !canon) return SV2N_ERR_ARG;
   if (n < 1 || n > SV2N_MAX_N_TILED || heads < 1 || heads > SV2N_MAX_HEADS || num_layers < 1 ||
       num_layers > SV2N_MAX_LAYERS || num_layers * heads > hl_pad)
     return SV2N_ERR_SHAPE;
@@ -421,10 +719,17 @@ extern "C" int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, i
     lp.p[l] = dae_layers[l];
   }
   const int O = edge_dim * hl_pad;
+  const int E0 = n * (n - 1);
+  if (num_edges > 0 && edge_dim <= EDGE_SMALL_D)
+    return planes ? edge_bwd_small<true>(edge_attr, num_edges, edge_dim, edge_index, canon, E0,
+                                         lp, num_layers, heads, num_graphs, n, workspace,
+                                         workspace_floats, dwfold, hl_pad, stream)
+                  : edge_bwd_small<false>(edge_attr, num_edges, edge_dim, edge_index, canon, E0,
+                                          lp, num_layers, heads, num_graphs, n, workspace,
+                                          workspace_floats, dwfold, hl_pad, stream);
   const int64_t nchunks = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(EDGE_BWD_GRID, nchunks));
   if (workspace_floats < (int64_t)grid * O) return SV2N_ERR_WORKSPACE;
-  const int E0 = n * (n - 1);
   const int rf = (EDGE_CHUNK * edge_dim / 4 + EDGE_THREADS - 1) / EDGE_THREADS;
   if (rf > EDGE_RF_MAX) return SV2N_ERR_SHAPE;
   const int rfi = rf <= 2 ? 2 : rf <= 8 ? 8 : rf <= 16 ? 16 : 24;  // instantiated RF
@@ -433,12 +738,17 @@ extern "C" int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, i
   lds = std::max(lds, sizeof(float) * (size_t)EDGE_THREADS * 16);
   if (lds > 160 * 1024) return SV2N_ERR_SHAPE;
   if (num_edges == 0) return (int)hipMemsetAsync(dwfold, 0, sizeof(float) * O, stream);
-#define SV2N_LAUNCH_EB(HLP, RF)                                                                   \
+#define SV2N_LAUNCH_EB2(HLP, RF, PL)                                                              \
   {                                                                                               \
-    raise_lds_limit(k_edge_bwd<HLP, RF>, lds);                                                    \
-    hipLaunchKernelGGL((k_edge_bwd<HLP, RF>), dim3(grid), dim3(EDGE_THREADS), lds, stream,        \
+    raise_lds_limit(k_edge_bwd<HLP, RF, PL>, lds);                                                \
+    hipLaunchKernelGGL((k_edge_bwd<HLP, RF, PL>), dim3(grid), dim3(EDGE_THREADS), lds, stream,    \
                        edge_attr, num_edges, edge_dim, DP, edge_index, canon, E0, lp, num_layers, \
                        heads, num_graphs, n, workspace);                                          \
+  }
+#define SV2N_LAUNCH_EB(HLP, RF)                                  \
+  {                                                              \
+    if (planes) SV2N_LAUNCH_EB2(HLP, RF, true)                   \
+    else SV2N_LAUNCH_EB2(HLP, RF, false)                         \
   }
 #define SV2N_LAUNCH_EB_RF(HLP)                                   \
   case HLP:                                                      \
@@ -457,8 +767,58 @@ extern "C" int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, i
   }
 #undef SV2N_LAUNCH_EB_RF
 #undef SV2N_LAUNCH_EB
+#undef SV2N_LAUNCH_EB2
   hipLaunchKernelGGL(k_reduce_partials, dim3((O + 63) / 64), dim3(256), 0, stream, workspace,
                      grid, O, dwfold);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_edge_logits_fwd(const float* edge_attr, int64_t num_edges, int edge_dim,
+                                    const int64_t* edge_index, const uint16_t* canon,
+                                    const float* wfold, int hl_pad, float* const* ae_layers,
+                                    int num_layers, int heads, int64_t num_graphs, int n,
+                                    hipStream_t stream) {
+  return edge_fwd_impl(edge_attr, num_edges, edge_dim, edge_index, canon, wfold, hl_pad,
+                       ae_layers, num_layers, heads, num_graphs, n, false, stream);
+}
+
+extern "C" int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, int edge_dim,
+                                    const int64_t* edge_index, const uint16_t* canon,
+                                    const float* const* dae_layers, int num_layers, int heads,
+                                    int64_t num_graphs, int n, float* workspace,
+                                    int64_t workspace_floats, float* dwfold, int hl_pad,
+                                    hipStream_t stream) {
+  return edge_bwd_impl(edge_attr, num_edges, edge_dim, edge_index, canon, dae_layers,
+                       num_layers, heads, num_graphs, n, workspace, workspace_floats, dwfold,
+                       hl_pad, false, stream);
+}
+
+extern "C" int sv2n_edge_logits_fwd_planes(const float* edge_attr, int64_t num_edges,
+                                           int edge_dim, const float* wfold, int hl_pad,
+                                           float* const* ae_layers, int num_layers, int heads,
+                                           hipStream_t stream) {
+  return edge_fwd_impl(edge_attr, num_edges, edge_dim, nullptr, nullptr, wfold, hl_pad,
+                       ae_layers, num_layers, heads, 1, 1, true, stream);
+}
+
+extern "C" int sv2n_edge_logits_bwd_planes(const float* edge_attr, int64_t num_edges,
+                                           int edge_dim, const int64_t* edge_index,
+                                           const float* const* dae_layers, int num_layers,
+                                           int heads, float* workspace,
+                                           int64_t workspace_floats, float* dwfold, int hl_pad,
+                                           hipStream_t stream) {
+  return edge_bwd_impl(edge_attr, num_edges, edge_dim, edge_index, nullptr, dae_layers,
+                       num_layers, heads, 1, 1, workspace, workspace_floats, dwfold, hl_pad, true,
+                       stream);
+}
+
+extern "C" int sv2n_block_eid(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
+                              int n, int32_t* eid, hipStream_t stream) {
+  if (!edge_index || !eid || num_edges < 0 || num_nodes <= 0) return SV2N_ERR_ARG;
+  if (n < 1 || n > SV2N_MAX_N_TILED || num_edges > 0x7fffffff) return SV2N_ERR_SHAPE;
+  if (num_edges == 0) return 0;
+  hipLaunchKernelGGL(k_block_eid, dim3((unsigned)((num_edges + 255) / 256)), dim3(256), 0,
+                     stream, edge_index, num_edges, num_nodes, n, eid);
   return (int)hipGetLastError();
 }
 

@@ -49,6 +49,7 @@ class GraphLayout:
     edge_index: Optional[torch.Tensor]  # read by kernels on the 'block' path
     rowmask: Optional[torch.Tensor]     # int32 [N][ceil(n/32)] source bitmask; None = complete
     canon: Optional[torch.Tensor]       # int16 [n(n-1)] (target<<8 | source) table
+    eid: Optional[torch.Tensor] = None  # int32 [N][n] edge ids (tiled 'block' layouts only)
 
     @property
     def tiled(self) -> bool:
@@ -188,5 +189,14 @@ def analyze_edge_index(edge_index: torch.Tensor, num_nodes: int,
                                                   rowmask.data_ptr(),
                                                   _lib.stream_handle(device)),
                    "sv2n_block_rowmask")
-    lay = GraphLayout("block", nb, B, N, E, edge_index, rowmask, canon)
+    eid = None
+    if nb > SMALL_N:  # the tiled kernels address edge logits by edge id
+        if device.type != "cuda":
+            raise UnsupportedLayout("the sv2n kernels need a ROCm device")
+        if E > 0x7FFFFFFF:
+            raise UnsupportedLayout("more than 2^31 edges in one batch")
+        eid = torch.full((N * nb,), -1, dtype=torch.int32, device=device)
+        _lib.check(_lib.load().sv2n_block_eid(edge_index.data_ptr(), E, N, nb, eid.data_ptr(),
+                                              _lib.stream_handle(device)), "sv2n_block_eid")
+    lay = GraphLayout("block", nb, B, N, E, edge_index, rowmask, canon, eid)
     return _attach(edge_index, key, lay)

@@ -96,14 +96,24 @@ class _GATStack(torch.autograd.Function):
         # 2) edge logits of every layer in one pass over edge_attr
         aes = [None] * L
         if use_edge:
-            aes = [torch.empty(B, n, n, H, device=dev, dtype=torch.float32) for _ in range(L)]
             E = ea.size(0)
-            if E > 0:
-                ptrs = _lib.ptr_array([a.data_ptr() for a in aes])
-                ei = layout.edge_index if layout.kind == "block" else None
-                _lib.check(lib.sv2n_edge_logits_fwd(ea.data_ptr(), E, ea.size(1), _lib.ptr(ei),
-                                                    layout.canon.data_ptr(), wf.data_ptr(), hp,
-                                                    ptrs, L, H, B, n, st), "sv2n_edge_logits_fwd")
+            if tiled:  # head planes [H][E] in edge order
+                aes = [torch.empty(H, E, device=dev, dtype=torch.float32) if E > 0 else None
+                       for _ in range(L)]
+                if E > 0:
+                    ptrs = _lib.ptr_array([a.data_ptr() for a in aes])
+                    _lib.check(lib.sv2n_edge_logits_fwd_planes(ea.data_ptr(), E, ea.size(1),
+                                                               wf.data_ptr(), hp, ptrs, L, H, st),
+                               "sv2n_edge_logits_fwd_planes")
+            else:
+                aes = [torch.empty(B, n, n, H, device=dev, dtype=torch.float32) for _ in range(L)]
+                if E > 0:
+                    ptrs = _lib.ptr_array([a.data_ptr() for a in aes])
+                    ei = layout.edge_index if layout.kind == "block" else None
+                    _lib.check(lib.sv2n_edge_logits_fwd(ea.data_ptr(), E, ea.size(1),
+                                                        _lib.ptr(ei), layout.canon.data_ptr(),
+                                                        wf.data_ptr(), hp, ptrs, L, H, B, n, st),
+                               "sv2n_edge_logits_fwd")
 
         # 3) layers
         xin = _aligned(x)
@@ -131,7 +141,8 @@ class _GATStack(torch.autograd.Function):
                 ws_n = lib.sv2n_gat_attn_tiled_workspace(B, n, Hc, C, int(c.concat))
                 ws = torch.empty(max(ws_n, 1), device=dev, dtype=torch.float32)
                 _lib.check(lib.sv2n_gat_attn_tiled_fwd(
-                    xs.data_ptr(), xs.stride(0), _lib.ptr(aes[l]), _lib.ptr(layout.rowmask),
+                    xs.data_ptr(), xs.stride(0), _lib.ptr(aes[l]), layout.num_edges,
+                    _lib.ptr(layout.eid), _lib.ptr(layout.rowmask),
                     _lib.ptr(c.bias), _lib.ptr(keep), kscale, y.data_ptr(), ws.data_ptr(), ws_n,
                     B, n, Hc, C, int(c.concat), act, float(c.negative_slope), st),
                     "sv2n_gat_attn_tiled_fwd")
@@ -199,12 +210,18 @@ class _GATStack(torch.autograd.Function):
                 dy = dy * drops[l]
             xs = xss[l]
             dxs = torch.empty_like(xs)
-            dae = torch.empty(B, n, n, Hc, device=dev, dtype=torch.float32) if use_edge else None
+            dae = None
+            if use_edge and layout.tiled:
+                dae = torch.empty(Hc, ea.size(0), device=dev, dtype=torch.float32) \
+                    if ea.size(0) > 0 else None
+            elif use_edge:
+                dae = torch.empty(B, n, n, Hc, device=dev, dtype=torch.float32)
             dbp = torch.empty(B, OC, device=dev, dtype=torch.float32)
             if layout.tiled:  # pss[l] holds the layer's ae (or None without edges)
                 _lib.check(lib.sv2n_gat_attn_tiled_bwd(
                     dy.data_ptr(), ys[l].data_ptr(), xs.data_ptr(), xs.stride(0),
-                    _lib.ptr(pss[l]), _lib.ptr(keeps[l]), ctx.kscales[l],
+                    _lib.ptr(pss[l]), layout.num_edges, _lib.ptr(layout.eid),
+                    _lib.ptr(keeps[l]), ctx.kscales[l],
                     _lib.ptr(layout.rowmask), dxs.data_ptr(), _lib.ptr(dae), dbp.data_ptr(), B,
                     n, Hc, C, int(c.concat), act, float(c.negative_slope), st),
                     "sv2n_gat_attn_tiled_bwd")
@@ -244,10 +261,15 @@ class _GATStack(torch.autograd.Function):
                 ws = torch.empty(ws_n, device=dev, dtype=torch.float32)
                 dwf = torch.empty(D, hp, device=dev, dtype=torch.float32)
                 ei = layout.edge_index if layout.kind == "block" else None
-                _lib.check(lib.sv2n_edge_logits_bwd(ea.data_ptr(), E, D, _lib.ptr(ei),
-                                                    layout.canon.data_ptr(), ptrs, L, H, B, n,
-                                                    ws.data_ptr(), ws_n, dwf.data_ptr(), hp, st),
-                           "sv2n_edge_logits_bwd")
+                if layout.tiled:
+                    _lib.check(lib.sv2n_edge_logits_bwd_planes(
+                        ea.data_ptr(), E, D, _lib.ptr(ei), ptrs, L, H, ws.data_ptr(), ws_n,
+                        dwf.data_ptr(), hp, st), "sv2n_edge_logits_bwd_planes")
+                else:
+                    _lib.check(lib.sv2n_edge_logits_bwd(ea.data_ptr(), E, D, _lib.ptr(ei),
+                                                        layout.canon.data_ptr(), ptrs, L, H, B,
+                                                        n, ws.data_ptr(), ws_n, dwf.data_ptr(),
+                                                        hp, st), "sv2n_edge_logits_bwd")
                 for l, c in enumerate(convs):
                     gWe, gae = need_e[l]
                     _lib.check(lib.sv2n_gat_prep_bwd_edge(
