@@ -184,11 +184,22 @@ int sv2n_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_av
                   int64_t n, const float* step, float lr, float beta1, float beta2,
                   float eps, float weight_decay, hipStream_t stream);
 
+/* Adam step that also advances the device step counter (t = *step + 1 is used
+ * and stored) and zeroes grad after reading it (the next backward accumulates
+ * into zeros).  counter: one uint32 ticket, zero before the first call (left
+ * zero by every call). */
+int sv2n_adam_f32_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                       float* step, uint32_t* counter, float lr, float beta1, float beta2,
+                       float eps, float weight_decay, hipStream_t stream);
+
 /* Output head (GATModel.linear, reference utils/models.py:120/:150):
  *   out[i][o] = Σ_c x[i][c]·weight[o][c] + bias[o]      x [rows][in], weight [out][in]
  * in_features <= 128, out_features <= 16.  The backward writes dx and
- * ACCUMULATES into g_weight / g_bias (either may be NULL);
- * workspace: sv2n_head_bwd_workspace(rows, in, out) floats. */
+ * ACCUMULATES into g_weight / g_bias (either may be NULL).
+ * workspace: sv2n_head_bwd_workspace(rows, in, out) floats, 16-B aligned; its
+ * first 16 floats are a ticket counter that must be zero before the first
+ * call (every call leaves it zero), the rest per-workgroup partial slabs
+ * reduced in a fixed order inside the launch (deterministic). */
 int sv2n_head_fwd(const float* x, int64_t num_rows, int in_features, const float* weight,
                   const float* bias, int out_features, float* out, hipStream_t stream);
 int64_t sv2n_head_bwd_workspace(int64_t num_rows, int in_features, int out_features);
@@ -196,6 +207,22 @@ int sv2n_head_bwd(const float* x, int64_t num_rows, int in_features, const float
                   int out_features, const float* dout, float* dx, float* g_weight,
                   float* g_bias, float* workspace, int64_t workspace_floats,
                   hipStream_t stream);
+
+/* Head fused with the training loss (5_train_SpotV2Net.py:154, nn.MSELoss
+ * mean): forward writes diff = out - target (kept for the backward), the
+ * prediction to yhat when non-NULL, and loss[0] = mean(diff²); backward
+ * scales diff by 2/(rows·out)·grad_loss[0] (grad_loss: device scalar, the
+ * upstream gradient of the loss) and is otherwise sv2n_head_bwd.
+ * workspace: sv2n_head_mse_workspace(...) floats, same counter rule. */
+int64_t sv2n_head_mse_workspace(int64_t num_rows, int in_features, int out_features);
+int sv2n_head_mse_fwd(const float* x, int64_t num_rows, int in_features, const float* weight,
+                      const float* bias, int out_features, const float* target, float* yhat,
+                      float* diff, float* loss, float* workspace, int64_t workspace_floats,
+                      hipStream_t stream);
+int sv2n_head_mse_bwd(const float* x, int64_t num_rows, int in_features, const float* weight,
+                      int out_features, const float* diff, const float* grad_loss, float* dx,
+                      float* g_weight, float* g_bias, float* workspace,
+                      int64_t workspace_floats, hipStream_t stream);
 
 /* Fused attention for dense-block graphs of 32 < n <= 256 nodes (any n <= 256
  * works; n <= 32 is faster on sv2n_gat_attn_fwd/bwd).  Same semantics and

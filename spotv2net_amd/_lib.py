@@ -53,6 +53,11 @@ _SIGNATURES = {
                                       _p, _p, _p, _p, _i64, _p]),
     "sv2n_gat_prep_bwd_edge": (_i32, [_p, _i32, _i32, _p, _p, _i32, _i32, _i32, _p, _p, _p]),
     "sv2n_adam_f32": (_i32, [_p, _p, _p, _p, _i64, _p, _f32, _f32, _f32, _f32, _f32, _p]),
+    "sv2n_adam_f32_step": (_i32, [_p, _p, _p, _p, _i64, _p, _p, _f32, _f32, _f32, _f32, _f32,
+                                  _p]),
+    "sv2n_head_mse_workspace": (_i64, [_i64, _i32, _i32]),
+    "sv2n_head_mse_fwd": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _i64, _p]),
+    "sv2n_head_mse_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "sv2n_head_fwd": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p]),
     "sv2n_head_bwd_workspace": (_i64, [_i64, _i32, _i32]),
     "sv2n_head_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _p, _p, _i64, _p]),
@@ -107,3 +112,22 @@ def ptr_array(ptrs) -> ctypes.Array:
     for k, p in enumerate(ptrs):
         arr[k] = p
     return arr
+
+
+_persistent: dict = {}
+
+
+def persistent_zeros(tag: str, numel: int, device: torch.device,
+                     dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    """A zero-initialised device buffer reused across calls (workspaces whose
+    ticket counters must start at zero; the kernels leave them zero).  Keyed
+    by device and size, so a hipGraph capture (which runs on its own stream)
+    reuses the buffer made during warm-up instead of recording a fill.  Ops
+    sharing a key must not run concurrently on different streams."""
+    dev = torch.device(device)
+    key = (tag, int(numel), str(dev), dtype)
+    buf = _persistent.get(key)
+    if buf is None:
+        buf = torch.zeros(max(int(numel), 1), device=dev, dtype=dtype)
+        _persistent[key] = buf
+    return buf

@@ -51,6 +51,47 @@ __device__ __forceinline__ float red32_max(float v) {
   return v;
 }
 
+// Last-arriving workgroup of a launch (cdna_hip_programming.md §6 Guideline 16,
+// counter form): every block publishes its plain-stored slab with an
+// agent-scope release and takes a ticket; the block drawing nblocks-1 gets
+// true (in all its threads) after an agent-scope acquire, so its plain loads
+// see every block's slab.  It also resets the counter, which must be zero
+// before the first launch.  s_flag: one int of the kernel's existing LDS.
+__device__ __forceinline__ bool last_block_arrive(unsigned* cnt, unsigned nblocks, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned tk = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = tk == nblocks - 1u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// Last-arriving workgroup WITHOUT publication: for when the last arriver
+// reads nothing the others wrote and only needs "everyone is past this
+// point" (e.g. a value every block read at its start may now be replaced).
+// Relaxed ticket, no fences; the counter is reset by the last arriver.
+__device__ __forceinline__ bool last_block_ticket(unsigned* cnt, unsigned nblocks, int* s_flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned tk = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = tk == nblocks - 1u;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 // rows i of graph g: bit j set <=> edge j->i present (self loop excluded)
 __device__ __forceinline__ uint32_t row_bits(const uint32_t* rowmask, int64_t row, int n, int i) {
   if (rowmask) return rowmask[row] & ~(1u << i);

@@ -1,20 +1,37 @@
 // Output head of GATModel: the final nn.Linear(h_last, out_ch) (reference
-// utils/models.py:120, applied at :150) as two small kernels instead of three
-// library GEMM launches with a skinny N (out_ch is 1 in the reference config,
-// 14 for the multi-output models).
+// utils/models.py:120, applied at :150), and the same head fused with the
+// training loss of 5_train_SpotV2Net.py:154 (nn.MSELoss, mean reduction).
 //   forward   out[i][o] = Σ_c x[i][c] · W[o][c] + b[o]
 //   backward  dx[i][c]  = Σ_o dout[i][o] · W[o][c]
 //             gW[o][c] += Σ_i dout[i][o] · x[i][c],  gb[o] += Σ_i dout[i][o]
-// The weight gradient is reduced per workgroup into partial slabs and summed in
-// a fixed order (deterministic), then ACCUMULATED into the .grad buffers.
+//   MSE       loss = mean((out - y)²),  dout = 2 (out - y) / (rows·out_ch) · dloss
+// Reductions over rows go through per-workgroup partial slabs summed in a
+// fixed order by the last-arriving workgroup of the same launch
+// (last_block_arrive): deterministic, and no separate reduce launch.
+//
+// Workspace layout (floats): [0, 16) ticket counter (zero before the first
+// call; every launch leaves it zero) | [16, ...) partial slabs.
 #include "sv2n_common.h"
 
 namespace sv2n {
 
 constexpr int HEAD_MAX_OUT = 16;
 constexpr int HEAD_ROWS = 256;  // rows per workgroup (one per thread)
+constexpr int HEAD_WS_HDR = 16;
 
 // x rows staged through LDS so the global reads are coalesced
+template <int OUT>
+__device__ __forceinline__ void head_rows(const float* __restrict__ x, int64_t r0, int nr, int C,
+                                          float* __restrict__ sx, const float* __restrict__ W,
+                                          float* __restrict__ sw, int t) {
+  const int CP = C + 1;
+  for (int k = t; k < OUT * C; k += 256) sw[k] = W[k];
+  for (int k = t; k < nr * C; k += 256) {
+    const int r = k / C;
+    sx[r * CP + (k - r * C)] = x[r0 * C + k];
+  }
+}
+
 template <int OUT>
 __global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ x, int64_t N, int C,
                                                   const float* __restrict__ W,
@@ -26,11 +43,7 @@ __global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ x, i
   const int64_t r0 = (int64_t)blockIdx.x * HEAD_ROWS;
   const int nr = (int)min((int64_t)HEAD_ROWS, N - r0);
   const int CP = C + 1;
-  for (int k = t; k < OUT * C; k += 256) sw[k] = W[k];
-  for (int k = t; k < nr * C; k += 256) {
-    const int r = k / C;
-    sx[r * CP + (k - r * C)] = x[r0 * C + k];
-  }
+  head_rows<OUT>(x, r0, nr, C, sx, W, sw, t);
   __syncthreads();
   if (t < nr) {
     float acc[OUT];
@@ -46,41 +59,128 @@ __global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ x, i
   }
 }
 
-// dx rows + per-block partial [OUT][C+1] (last column = bias partial)
+// head + MSE forward: diff = out - y (saved for the backward), optional
+// prediction, loss = Σ diff² · inv_count (last-arriving block)
 template <int OUT>
-__global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ x, int64_t N, int C,
-                                                  const float* __restrict__ W,
-                                                  const float* __restrict__ dout,
-                                                  float* __restrict__ dx,
-                                                  float* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) float sx[];  // [256][C+1] x rows, then dx
+__global__ __launch_bounds__(256) void k_head_mse_fwd(
+    const float* __restrict__ x, int64_t N, int C, const float* __restrict__ W,
+    const float* __restrict__ b, const float* __restrict__ target, float* __restrict__ yhat,
+    float* __restrict__ diff, float* __restrict__ ws, float* __restrict__ loss, float inv_count) {
+  extern __shared__ __attribute__((aligned(16))) float sx[];  // [256][C+1]
   __shared__ float sw[HEAD_MAX_OUT * 128];
-  __shared__ float sd[HEAD_ROWS][HEAD_MAX_OUT];
+  __shared__ float s_red[256];
   const int t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * HEAD_ROWS;
   const int nr = (int)min((int64_t)HEAD_ROWS, N - r0);
   const int CP = C + 1;
-  for (int k = t; k < OUT * C; k += 256) sw[k] = W[k];
-  for (int k = t; k < nr * C; k += 256) {
-    const int r = k / C;
-    sx[r * CP + (k - r * C)] = x[r0 * C + k];
+  head_rows<OUT>(x, r0, nr, C, sx, W, sw, t);
+  __syncthreads();
+  float sq = 0.f;
+  if (t < nr) {
+    float acc[OUT];
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) acc[o] = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float xv = sx[t * CP + c];
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) acc[o] = fmaf(xv, sw[o * C + c], acc[o]);
+    }
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) {
+      const int64_t k = (r0 + t) * OUT + o;
+      const float v = acc[o] + (b ? b[o] : 0.f);
+      if (yhat) yhat[k] = v;
+      const float d = v - target[k];
+      diff[k] = d;
+      sq = fmaf(d, d, sq);
+    }
   }
+  s_red[t] = sq;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s) s_red[t] += s_red[t + s];
+    __syncthreads();
+  }
+  float* part = ws + HEAD_WS_HDR;
+  if (t == 0) part[blockIdx.x] = s_red[0];
+  int* s_flag = reinterpret_cast<int*>(sw);
+  if (last_block_arrive(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
+    float a = 0.f;
+    for (int k = t; k < (int)gridDim.x; k += 256) a += part[k];
+    s_red[t] = a;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (t < s) s_red[t] += s_red[t + s];
+      __syncthreads();
+    }
+    if (t == 0) loss[0] = s_red[0] * inv_count;
+  }
+}
+
+// dx rows + per-block partial [OUT][C+1] (last column = bias partial); the
+// last-arriving block ACCUMULATES Σ partials into gW / gb.  Both the
+// per-block column sums (over 256 rows) and the combine (over the blocks)
+// spread a column over RG = 256 / (OUT·(C+1)) thread groups (>= 1), then add
+// the groups in a fixed order through LDS: deterministic, all threads busy.
+// dout = src · scale (· *dscale when given): plain head backward with
+// src = dout, scale = 1; MSE backward with src = diff, scale = 2/(rows·out),
+// dscale = dloss.
+template <int OUT>
+__global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ x, int64_t N, int C,
+                                                  const float* __restrict__ W,
+                                                  const float* __restrict__ src, float scale,
+                                                  const float* __restrict__ dscale,
+                                                  float* __restrict__ dx, float* __restrict__ ws,
+                                                  float* __restrict__ gW, float* __restrict__ gb) {
+  extern __shared__ __attribute__((aligned(16))) float sx[];  // [256][C+1] x rows
+  __shared__ float sw[HEAD_MAX_OUT * 128];
+  __shared__ float sd[HEAD_ROWS][HEAD_MAX_OUT];
+  __shared__ float s_grp[256];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * HEAD_ROWS;
+  const int nr = (int)min((int64_t)HEAD_ROWS, N - r0);
+  const int CP = C + 1;
+  const int tot = OUT * CP;
+  const int RG = tot <= 256 ? 256 / tot : 1;
+  const float sc = dscale ? scale * dscale[0] : scale;
+  head_rows<OUT>(x, r0, nr, C, sx, W, sw, t);
   for (int k = t; k < HEAD_ROWS * OUT; k += 256) {
     const int r = k / OUT;
-    sd[r][k - r * OUT] = (r < nr) ? dout[(r0 + r) * OUT + (k - r * OUT)] : 0.f;
+    sd[r][k - r * OUT] = (r < nr) ? src[(r0 + r) * OUT + (k - r * OUT)] * sc : 0.f;
   }
   __syncthreads();
-  // weight / bias partials: thread per (o, c) column, sum over the block's rows
-  float* pb = part + (int64_t)blockIdx.x * OUT * CP;
-  for (int oc = t; oc < OUT * CP; oc += 256) {
-    const int o = oc / CP, c = oc - o * CP;
-    float s = 0.f;
-    if (c < C) {
-      for (int r = 0; r < nr; ++r) s = fmaf(sd[r][o], sx[r * CP + c], s);
-    } else {
-      for (int r = 0; r < nr; ++r) s += sd[r][o];
+  float* part = ws + HEAD_WS_HDR;
+  float* pb = part + (int64_t)blockIdx.x * tot;
+  if (RG > 1) {
+    // column oc = t % tot summed over rows r ≡ g (mod RG), g = t / tot
+    if (t < RG * tot) {
+      const int oc = t % tot, g = t / tot;
+      const int o = oc / CP, c = oc - o * CP;
+      float s = 0.f;
+      if (c < C) {
+        for (int r = g; r < nr; r += RG) s = fmaf(sd[r][o], sx[r * CP + c], s);
+      } else {
+        for (int r = g; r < nr; r += RG) s += sd[r][o];
+      }
+      s_grp[t] = s;
     }
-    pb[oc] = s;
+    __syncthreads();
+    if (t < tot) {
+      float s = 0.f;
+      for (int g = 0; g < RG; ++g) s += s_grp[g * tot + t];
+      pb[t] = s;
+    }
+  } else {
+    for (int oc = t; oc < tot; oc += 256) {
+      const int o = oc / CP, c = oc - o * CP;
+      float s = 0.f;
+      if (c < C) {
+        for (int r = 0; r < nr; ++r) s = fmaf(sd[r][o], sx[r * CP + c], s);
+      } else {
+        for (int r = 0; r < nr; ++r) s += sd[r][o];
+      }
+      pb[oc] = s;
+    }
   }
   // dx rows (coalesced store through the row-major global layout)
   for (int k = t; k < nr * C; k += 256) {
@@ -90,27 +190,34 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ x, i
     for (int o = 0; o < OUT; ++o) s = fmaf(sd[r][o], sw[o * C + c], s);
     dx[r0 * C + k] = s;
   }
-}
-
-// gW[o][c] += Σ_b part[b][o][c]; gb[o] += Σ_b part[b][o][C]
-__global__ __launch_bounds__(256) void k_head_reduce(const float* __restrict__ part, int nparts,
-                                                     int OUT, int C, float* __restrict__ gW,
-                                                     float* __restrict__ gb) {
-  const int CP = C + 1;
-  const int oc = blockIdx.x * 256 + threadIdx.x;
-  if (oc >= OUT * CP) return;
-  float s0 = 0.f, s1 = 0.f;
-  int b = 0;
-  for (; b + 1 < nparts; b += 2) {
-    s0 += part[(int64_t)b * OUT * CP + oc];
-    s1 += part[(int64_t)(b + 1) * OUT * CP + oc];
-  }
-  if (b < nparts) s0 += part[(int64_t)b * OUT * CP + oc];
-  const int o = oc / CP, c = oc - o * CP;
-  if (c < C) {
-    if (gW) gW[o * C + c] += s0 + s1;
-  } else if (gb) {
-    gb[o] += s0 + s1;
+  if (!gW && !gb) return;
+  int* s_flag = reinterpret_cast<int*>(&sd[0][0]);
+  __syncthreads();  // sd no longer needed: reuse one word as the flag
+  if (last_block_arrive(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
+    const int nparts = gridDim.x;
+    for (int base = 0; base < tot; base += 256) {
+      const int cols = min(256, tot - base);
+      const int PG = 256 / cols;  // part groups
+      if (t < PG * cols) {
+        const int oc = base + t % cols, g = t / cols;
+        float s = 0.f;
+        for (int bb = g; bb < nparts; bb += PG) s += part[(int64_t)bb * tot + oc];
+        s_grp[t] = s;
+      }
+      __syncthreads();
+      if (t < cols) {
+        float s = 0.f;
+        for (int g = 0; g < PG; ++g) s += s_grp[g * cols + t];
+        const int oc = base + t;
+        const int o = oc / CP, c = oc - o * CP;
+        if (c < C) {
+          if (gW) gW[o * C + c] += s;
+        } else if (gb) {
+          gb[o] += s;
+        }
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -121,7 +228,14 @@ using namespace sv2n;
 static int head_check(int64_t N, int C, int out_ch) {
   if (N <= 0 || C <= 0 || out_ch <= 0) return SV2N_ERR_ARG;
   if (out_ch > HEAD_MAX_OUT || C > 128 || out_ch * C > HEAD_MAX_OUT * 128) return SV2N_ERR_SHAPE;
+  if (N > (int64_t)HEAD_ROWS * 0x7fffffff) return SV2N_ERR_SHAPE;
   return 0;
+}
+
+template <typename K>
+static void raise_head_lds(K kernel) {
+  (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            140 * 1024);
 }
 
 #define SV2N_HEAD_CASE(KERNEL, O, ...) \
@@ -139,12 +253,6 @@ static int head_check(int64_t N, int C, int out_ch) {
     default: return SV2N_ERR_SHAPE;                                                           \
   }
 
-template <typename K>
-static void raise_head_lds(K kernel) {
-  (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            140 * 1024);
-}
-
 extern "C" int sv2n_head_fwd(const float* x, int64_t num_rows, int in_features,
                              const float* weight, const float* bias, int out_features,
                              float* out, hipStream_t stream) {
@@ -158,26 +266,68 @@ extern "C" int sv2n_head_fwd(const float* x, int64_t num_rows, int in_features,
   return (int)hipGetLastError();
 }
 
+static int64_t head_bwd_blocks(int64_t num_rows) {
+  return (num_rows + HEAD_ROWS - 1) / HEAD_ROWS;
+}
+
 extern "C" int64_t sv2n_head_bwd_workspace(int64_t num_rows, int in_features, int out_features) {
-  return ((num_rows + HEAD_ROWS - 1) / HEAD_ROWS) * (int64_t)out_features * (in_features + 1);
+  return HEAD_WS_HDR + head_bwd_blocks(num_rows) * (int64_t)out_features * (in_features + 1);
+}
+
+static int head_bwd_launch(const float* x, int64_t num_rows, int in_features, const float* weight,
+                           int out_ch, const float* src, float scale, const float* dscale,
+                           float* dx, float* g_weight, float* g_bias, float* workspace,
+                           int64_t workspace_floats, hipStream_t stream) {
+  if (!x || !weight || !src || !dx || !workspace) return SV2N_ERR_ARG;
+  if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
+  const int64_t nb = head_bwd_blocks(num_rows);
+  if (workspace_floats < sv2n_head_bwd_workspace(num_rows, in_features, out_ch))
+    return SV2N_ERR_WORKSPACE;
+  if ((uintptr_t)workspace & 15) return SV2N_ERR_ALIGN;
+  const size_t lds = sizeof(float) * HEAD_ROWS * (in_features + 1);
+  SV2N_HEAD_DISPATCH(k_head_bwd, dim3((unsigned)nb), dim3(256), lds, stream, x, num_rows,
+                     in_features, weight, src, scale, dscale, dx, workspace, g_weight, g_bias)
+  return (int)hipGetLastError();
 }
 
 extern "C" int sv2n_head_bwd(const float* x, int64_t num_rows, int in_features,
                              const float* weight, int out_features, const float* dout, float* dx,
                              float* g_weight, float* g_bias, float* workspace,
                              int64_t workspace_floats, hipStream_t stream) {
-  const int out_ch = out_features;
-  if (!x || !weight || !dout || !dx || !workspace) return SV2N_ERR_ARG;
-  if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
+  return head_bwd_launch(x, num_rows, in_features, weight, out_features, dout, 1.f, nullptr, dx,
+                         g_weight, g_bias, workspace, workspace_floats, stream);
+}
+
+extern "C" int64_t sv2n_head_mse_workspace(int64_t num_rows, int in_features, int out_features) {
   const int64_t nb = (num_rows + HEAD_ROWS - 1) / HEAD_ROWS;
-  if (workspace_floats < nb * out_ch * (in_features + 1)) return SV2N_ERR_WORKSPACE;
+  return std::max<int64_t>(sv2n_head_bwd_workspace(num_rows, in_features, out_features),
+                           HEAD_WS_HDR + nb);
+}
+
+extern "C" int sv2n_head_mse_fwd(const float* x, int64_t num_rows, int in_features,
+                                 const float* weight, const float* bias, int out_features,
+                                 const float* target, float* yhat, float* diff, float* loss,
+                                 float* workspace, int64_t workspace_floats, hipStream_t stream) {
+  const int out_ch = out_features;
+  if (!x || !weight || !target || !diff || !loss || !workspace) return SV2N_ERR_ARG;
+  if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
+  if (workspace_floats < sv2n_head_mse_workspace(num_rows, in_features, out_ch))
+    return SV2N_ERR_WORKSPACE;
+  if ((uintptr_t)workspace & 15) return SV2N_ERR_ALIGN;
+  const unsigned grid = (unsigned)((num_rows + HEAD_ROWS - 1) / HEAD_ROWS);
   const size_t lds = sizeof(float) * HEAD_ROWS * (in_features + 1);
-  SV2N_HEAD_DISPATCH(k_head_bwd, dim3((unsigned)nb), dim3(256), lds, stream, x, num_rows,
-                     in_features, weight, dout, dx, workspace)
-  if (g_weight || g_bias) {
-    const int tot = out_ch * (in_features + 1);
-    hipLaunchKernelGGL(k_head_reduce, dim3((tot + 255) / 256), dim3(256), 0, stream, workspace,
-                       (int)nb, out_ch, in_features, g_weight, g_bias);
-  }
+  const float inv_count = 1.f / (float)(num_rows * out_ch);
+  SV2N_HEAD_DISPATCH(k_head_mse_fwd, dim3(grid), dim3(256), lds, stream, x, num_rows,
+                     in_features, weight, bias, target, yhat, diff, workspace, loss, inv_count)
   return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_head_mse_bwd(const float* x, int64_t num_rows, int in_features,
+                                 const float* weight, int out_features, const float* diff,
+                                 const float* grad_loss, float* dx, float* g_weight,
+                                 float* g_bias, float* workspace, int64_t workspace_floats,
+                                 hipStream_t stream) {
+  const float scale = 2.f / (float)(num_rows * (int64_t)out_features);
+  return head_bwd_launch(x, num_rows, in_features, weight, out_features, diff, scale, grad_loss,
+                         dx, g_weight, g_bias, workspace, workspace_floats, stream);
 }

@@ -28,7 +28,7 @@ from torch import nn
 from . import ops
 from .conv import GATConv
 from .layout import GraphLayout, analyze_edge_index
-from .stack import gat_stack, linear_head
+from .stack import gat_stack, head_mse_loss, linear_head
 
 
 def _layout_of(data, x: torch.Tensor, edge_index: torch.Tensor) -> GraphLayout:
@@ -74,14 +74,23 @@ class GATModel(nn.Module):
         self.a = acts[activation]
         self._act_code = ops.ACT_CODES[activation]
 
-    def forward(self, data):
+    def _hidden(self, data) -> torch.Tensor:
         x, edge_index, edge_attr = data.x, data.edge_index, data.edge_attr
         if self.standardize:
             x = self.bnorm_node(x)
             if edge_attr is not None:
                 edge_attr = self.bnorm_edge(edge_attr)
         layout = _layout_of(data, x, edge_index)
-        x = gat_stack(x, edge_attr, tuple(self.gat_layers), layout, self._act_code,
-                      float(self.dropout or 0.0), self.training)
-        x = linear_head(x, self.linear)
-        return x.view(-1)
+        return gat_stack(x, edge_attr, tuple(self.gat_layers), layout, self._act_code,
+                         float(self.dropout or 0.0), self.training)
+
+    def forward(self, data):
+        return linear_head(self._hidden(data), self.linear).view(-1)
+
+    def mse_loss(self, data, target: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``nn.MSELoss()(self(data), target)`` (reference
+        5_train_SpotV2Net.py:125, :150-154; target defaults to ``data.y_x``)
+        with the output head and the loss fused into two kernel launches."""
+        if target is None:
+            target = data.y_x
+        return head_mse_loss(self._hidden(data), self.linear, target)

@@ -325,7 +325,7 @@ class _Head(torch.autograd.Function):
         dout = dout.contiguous()
         dx = torch.empty_like(x)
         ws_n = lib.sv2n_head_bwd_workspace(N, C, O)
-        ws = torch.empty(ws_n, device=x.device, dtype=torch.float32)
+        ws = _lib.persistent_zeros("head", ws_n, x.device)
         gw = _grad_buf(lin.weight)
         gb = _grad_buf(lin.bias)
         _lib.check(lib.sv2n_head_bwd(x.data_ptr(), N, C, lin.weight.data_ptr(), O,
@@ -333,6 +333,61 @@ class _Head(torch.autograd.Function):
                                      ws.data_ptr(), ws_n, _lib.stream_handle(x.device)),
                    "sv2n_head_bwd")
         return dx if ctx.needs_input_grad[0] else None, None, None, None
+
+
+class _HeadMSE(torch.autograd.Function):
+    """``F.mse_loss(linear(x).view(-1), target)`` (reference
+    5_train_SpotV2Net.py:150-154) as two launches: sv2n_head_mse_fwd (head,
+    residual, loss) and sv2n_head_mse_bwd (dx and the head's parameter grads,
+    accumulated into ``.grad``)."""
+
+    @staticmethod
+    def forward(ctx, x, target, linear, weight, bias):
+        lib = _lib.load()
+        x = _aligned(x)
+        N, C = x.shape
+        O = weight.shape[0]
+        target = target.reshape(-1).contiguous()
+        if target.numel() != N * O:
+            raise ValueError(f"target has {target.numel()} elements, expected {N * O}")
+        diff = torch.empty(N * O, device=x.device, dtype=torch.float32)
+        loss = torch.empty((), device=x.device, dtype=torch.float32)
+        ws_n = lib.sv2n_head_mse_workspace(N, C, O)
+        ws = _lib.persistent_zeros("head", ws_n, x.device)
+        _lib.check(lib.sv2n_head_mse_fwd(x.data_ptr(), N, C, weight.data_ptr(), _lib.ptr(bias), O,
+                                         target.data_ptr(), None, diff.data_ptr(),
+                                         loss.data_ptr(), ws.data_ptr(), ws_n,
+                                         _lib.stream_handle(x.device)), "sv2n_head_mse_fwd")
+        ctx.linear = linear
+        ctx.save_for_backward(x, diff)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        lib = _lib.load()
+        x, diff = ctx.saved_tensors
+        lin = ctx.linear
+        N, C = x.shape
+        O = lin.weight.shape[0]
+        gloss = gloss.reshape(()).contiguous().to(torch.float32)
+        dx = torch.empty_like(x)
+        ws_n = lib.sv2n_head_mse_workspace(N, C, O)
+        ws = _lib.persistent_zeros("head", ws_n, x.device)
+        gw = _grad_buf(lin.weight)
+        gb = _grad_buf(lin.bias)
+        _lib.check(lib.sv2n_head_mse_bwd(x.data_ptr(), N, C, lin.weight.data_ptr(), O,
+                                         diff.data_ptr(), gloss.data_ptr(), dx.data_ptr(),
+                                         _lib.ptr(gw), _lib.ptr(gb), ws.data_ptr(), ws_n,
+                                         _lib.stream_handle(x.device)), "sv2n_head_mse_bwd")
+        return dx if ctx.needs_input_grad[0] else None, None, None, None, None
+
+
+def head_mse_loss(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tensor) -> torch.Tensor:
+    """mean((linear(x).view(-1) - target)²) with the head and the loss fused."""
+    _require_device(x, target)
+    if linear.in_features > 128 or linear.out_features > 16:
+        return torch.nn.functional.mse_loss(linear(x).view(-1), target)
+    return _HeadMSE.apply(x, target, linear, linear.weight, linear.bias)
 
 
 def linear_head(x: torch.Tensor, linear: torch.nn.Linear) -> torch.Tensor:

@@ -66,16 +66,19 @@ class FlatAdam:
         self.m = torch.zeros_like(flat_params)
         self.v = torch.zeros_like(flat_params)
         self.step_t = torch.zeros(1, device=flat_params.device, dtype=torch.float32)
+        self.ticket = torch.zeros(4, device=flat_params.device, dtype=torch.int32)
         self.lr, self.betas, self.eps, self.wd = float(lr), betas, float(eps), float(weight_decay)
 
+    # the kernel advances step_t itself and zeroes the consumed gradient
+    zeroes_grads = True
+
     def step(self) -> None:
-        self.step_t += 1
         lib = self._lib.load()
-        self._lib.check(lib.sv2n_adam_f32(
+        self._lib.check(lib.sv2n_adam_f32_step(
             self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
-            self.p.numel(), self.step_t.data_ptr(), self.lr, float(self.betas[0]),
-            float(self.betas[1]), self.eps, self.wd, self._lib.stream_handle(self.p.device)),
-            "sv2n_adam_f32")
+            self.p.numel(), self.step_t.data_ptr(), self.ticket.data_ptr(), self.lr,
+            float(self.betas[0]), float(self.betas[1]), self.eps, self.wd,
+            self._lib.stream_handle(self.p.device)), "sv2n_adam_f32_step")
 
 
 def allreduce_mean_(flat: torch.Tensor, group=None) -> None:
@@ -124,17 +127,23 @@ class TrainStep:
             dist.get_world_size(group) > 1
         self.use_graph = use_graph
         self.loss = torch.zeros((), device=self.flat.device)
+        self._one = torch.ones((), device=self.flat.device)
+        # fused head + MSE (two launches) when the model offers it
+        self._fused_mse = loss_fn is torch.nn.functional.mse_loss and hasattr(model, "mse_loss")
         self._g_fb = self._g_opt = None
         if use_graph:
             self._capture(warmup)
 
     # -- eager pieces -------------------------------------------------------
     def _fwd_bwd(self) -> None:
-        self.flat.zero_()
-        out = self.model(self.data)
-        loss = self.loss_fn(out, self.data.y_x)
-        loss.backward()
-        self.loss.copy_(loss.detach())
+        if not getattr(self.opt, "zeroes_grads", False):
+            self.flat.zero_()
+        if self._fused_mse:
+            loss = self.model.mse_loss(self.data)
+        else:
+            loss = self.loss_fn(self.model(self.data), self.data.y_x)
+        torch.autograd.backward(loss, self._one)
+        self.loss = loss.detach()
 
     def _opt_step(self) -> None:
         self.opt.step()
