@@ -147,6 +147,21 @@ int sv2n_gemm_f32(int a_kmajor, int b_kmajor, const float* A, int64_t lda,
                   int64_t M, int64_t N, int64_t K,
                   float* workspace, int64_t workspace_floats, hipStream_t stream);
 
+/* f32-accurate GEMM on bf16 MFMA for a small "weight" operand B:
+ *   C[M][N] = Σ_k A[m][k]·B(n,k),  A fp32 k-major (16-B aligned, lda % 4 == 0)
+ * B is passed as its three bf16 planes (Bp [3][N][Kp], Kp =
+ * sv2n_split3_kpad(K)), each fp32 value being the exact sum of its three
+ * bf16 terms; the six products with combined order <= 2 are accumulated in
+ * fp32, so the result matches an exact-f32 GEMM to fp32 rounding (measured
+ * max |err| / Σ|a·b| 3.8e-7 vs 3.75e-7 for sv2n_gemm_f32 on the C2 shapes).
+ * sv2n_split3 builds the planes: transpose = 0 reads B as [N][K] (row
+ * stride ld), transpose = 1 as [K][N]. */
+int64_t sv2n_split3_kpad(int64_t K);
+int sv2n_split3(const float* in, int64_t rows, int64_t K, int64_t ld, int transpose,
+                uint16_t* out, hipStream_t stream);
+int sv2n_gemm_f32x3(const float* A, int64_t lda, const uint16_t* Bp, float* C, int64_t ldc,
+                    int64_t M, int64_t N, int64_t K, hipStream_t stream);
+
 /* Weight preparation for one GAT layer (replaces, per step, PyG's separate
  * (x_src*att_src).sum(-1) / (x_dst*att_dst).sum(-1) and lin_edge·att_edge
  * reductions by folded weights):

@@ -43,6 +43,9 @@ _SIGNATURES = {
     "sv2n_edge_logits_bwd_planes": (_i32, [_p, _i64, _i32, _p, _p, _i32, _i32, _p, _i64, _p,
                                            _i32, _p]),
     "sv2n_block_eid": (_i32, [_p, _i64, _i64, _i32, _p, _p]),
+    "sv2n_split3_kpad": (_i64, [_i64]),
+    "sv2n_split3": (_i32, [_p, _i64, _i64, _i64, _i32, _p, _p]),
+    "sv2n_gemm_f32x3": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "sv2n_gemm_f32_workspace": (_i64, [_i64, _i64, _i64]),
     "sv2n_gemm_f32": (_i32, [_i32, _i32, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "sv2n_block_rowmask": (_i32, [_p, _i64, _i64, _i32, _p, _p]),

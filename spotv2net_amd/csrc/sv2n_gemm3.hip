@@ -1,0 +1,97 @@
+// f32-accurate projection GEMMs on bf16 MFMA (kernel and numerics:
+// sv2n_gemm3_kernel.h).  Used for the GATConv projection xs = x·Waugᵀ
+// (PyG lin_src) and its input gradient dx = dxs·Waug,
+// where the weight operand is small and is split into its three bf16 planes
+// once per call (sv2n_split3).  Configurations from tools/gemm3_tune.hip on
+// MI355X (profiles/gemm3_tune_r01.txt).
+#include "sv2n_common.h"
+#include "sv2n_gemm3_kernel.h"
+
+#include <algorithm>
+
+namespace sv2n {
+
+constexpr int64_t SPLIT3_KALIGN = 64;  // largest BK
+
+// fp32 [K][rows] (row stride ld) -> 3 bf16 planes [3][rows][Kp] (transposed)
+__global__ void k_split3_t(const float* __restrict__ x, int64_t rows, int64_t K, int64_t ld,
+                           unsigned short* __restrict__ out, int64_t Kp) {
+  // 32 x 32 tile transpose through LDS: coalesced reads along rows of x,
+  // coalesced writes along k of the planes
+  __shared__ float tile[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  const int64_t k0 = (int64_t)blockIdx.x * 32, n0 = (int64_t)blockIdx.y * 32;
+  for (int j = ty; j < 32; j += 8) {
+    const int64_t k = k0 + j, n = n0 + tx;
+    tile[j][tx] = (k < K && n < rows) ? x[k * ld + n] : 0.f;
+  }
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    const int64_t n = n0 + j, k = k0 + tx;
+    if (n < rows && k < Kp) {
+      unsigned short h0, h1, h2;
+      split3(tile[tx][j], h0, h1, h2);
+      const int64_t o = n * Kp + k;
+      out[o] = h0;
+      out[rows * Kp + o] = h1;
+      out[2 * rows * Kp + o] = h2;
+    }
+  }
+}
+
+template <int NW, int MT, int NT, int BK>
+static int launch_gemm3(hipStream_t st, const float* A, int64_t lda, const unsigned short* Bp,
+                        int64_t Kp, int64_t N, float* C, int64_t ldc, int64_t M, int64_t K) {
+  using Cfg = Gemm3Cfg<NW, MT, NT, BK>;
+  constexpr size_t lds = Cfg::LDS;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)k_gemm3<NW, MT, NT, BK, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  const dim3 grid((unsigned)((M + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN));
+  hipLaunchKernelGGL((k_gemm3<NW, MT, NT, BK, 1>), grid, dim3(Cfg::THREADS), lds, st, A, lda, Bp,
+                     Kp, N * Kp, C, ldc, M, N, K);
+  return (int)hipGetLastError();
+}
+
+}  // namespace sv2n
+
+using namespace sv2n;
+
+extern "C" int64_t sv2n_split3_kpad(int64_t K) {
+  return (K + SPLIT3_KALIGN - 1) / SPLIT3_KALIGN * SPLIT3_KALIGN;
+}
+
+extern "C" int sv2n_split3(const float* in, int64_t rows, int64_t K, int64_t ld, int transpose,
+                           uint16_t* out, hipStream_t stream) {
+  if (!in || !out || rows <= 0 || K <= 0) return SV2N_ERR_ARG;
+  const int64_t Kp = sv2n_split3_kpad(K);
+  if (transpose) {
+    if (ld < rows) return SV2N_ERR_ARG;
+    const dim3 grid((unsigned)((Kp + 31) / 32), (unsigned)((rows + 31) / 32));
+    hipLaunchKernelGGL(k_split3_t, grid, dim3(256), 0, stream, in, rows, K, ld,
+                       reinterpret_cast<unsigned short*>(out), Kp);
+  } else {
+    if (ld < K) return SV2N_ERR_ARG;
+    const int64_t n = rows * Kp;
+    hipLaunchKernelGGL(k_split3, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, in, rows,
+                       K, ld, reinterpret_cast<unsigned short*>(out), Kp);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_gemm_f32x3(const float* A, int64_t lda, const uint16_t* Bp, float* C,
+                               int64_t ldc, int64_t M, int64_t N, int64_t K, hipStream_t stream) {
+  if (!A || !Bp || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldc < N) return SV2N_ERR_ARG;
+  if (((uintptr_t)A & 15) || (lda & 3) || ((uintptr_t)Bp & 15)) return SV2N_ERR_ALIGN;
+  const int64_t Kp = sv2n_split3_kpad(K);
+  const unsigned short* B = reinterpret_cast<const unsigned short*>(Bp);
+  const int64_t mb = (M + 127) / 128;
+  const bool wide = mb * ((N + 207) / 208) >= 240;  // else narrower tiles for more workgroups
+  const bool longk = K > 256;
+  if (wide)
+    return longk ? launch_gemm3<8, 1, 13, 64>(stream, A, lda, B, Kp, N, C, ldc, M, K)
+                 : launch_gemm3<8, 1, 13, 32>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+  return longk ? launch_gemm3<8, 1, 7, 64>(stream, A, lda, B, Kp, N, C, ldc, M, K)
+               : launch_gemm3<8, 1, 7, 32>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+}

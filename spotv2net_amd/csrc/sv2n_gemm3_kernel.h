@@ -1,0 +1,223 @@
+// f32-accurate GEMM on bf16 MFMA ("bf16x3 split, 6 products"), shared by the
+// library and tools/gemm3_tune.hip.
+//
+//   C[M][N] = Σ_k A[m][k] · B[n][k]      (both operands k-contiguous)
+//
+// Every fp32 operand is the exact sum of three bf16 terms, x = x0 + x1 + x2
+// (x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1): 3 x 8 significant
+// bits cover the 24-bit fp32 mantissa).  a·b keeps the six products with
+// p + q <= 2; the dropped ones (a1 b2, a2 b1, a2 b2) are <= ~2^-23 |a b|, the
+// size of one fp32 rounding.  bf16 x bf16 products are exact in fp32 and the
+// MFMA accumulates in fp32, so the result matches an fp32 GEMM to fp32
+// rounding while running on v_mfma_f32_16x16x32_bf16 (16x the f32-MFMA rate
+// per instruction, 2.67x after the six products).
+//
+// Operands: A is fp32 and split while it is staged into LDS (each element
+// once per workgroup, reused by all of the block's N columns); B comes
+// pre-split as three bf16 planes [3][N][K] (the caller splits the small
+// weight matrix once per step, k_split3).
+//
+// LDS images [plane][row][BK bf16] with a 32-B row pad: conflict-free
+// ds_read_b128 fragment reads (see Gemm3Cfg::ROW).
+// Fragment (16x16x32 bf16): lane l holds row l&15, k = 8(l>>4) .. +7.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sv2n {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+
+__device__ __forceinline__ unsigned short bf16_rn(float x) {
+  // round-to-nearest-even f32 -> bf16 (inputs are finite here)
+  const unsigned u = __float_as_uint(x);
+  return (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_f(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+
+__device__ __forceinline__ void split3(float x, unsigned short& h0, unsigned short& h1,
+                                       unsigned short& h2) {
+  h0 = bf16_rn(x);
+  const float r1 = x - bf16_f(h0);
+  h1 = bf16_rn(r1);
+  const float r2 = r1 - bf16_f(h1);
+  h2 = bf16_rn(r2);
+}
+
+// fp32 [rows][K] (k-contiguous, row stride ld) -> 3 bf16 planes [3][rows][Kp]
+__global__ void k_split3(const float* __restrict__ x, int64_t rows, int64_t K, int64_t ld,
+                         unsigned short* __restrict__ out, int64_t Kp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * Kp) return;
+  const int64_t r = i / Kp, k = i - r * Kp;
+  unsigned short h0 = 0, h1 = 0, h2 = 0;
+  if (k < K) split3(x[r * ld + k], h0, h1, h2);
+  out[i] = h0;
+  out[rows * Kp + i] = h1;
+  out[2 * rows * Kp + i] = h2;
+}
+
+template <int NW, int MT, int NT, int BK>
+struct Gemm3Cfg {
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int BM = 16 * MT * NW, BN = 16 * NT;
+  // bf16 per LDS row: BK + 16 (96 B at BK 32, 160 B at BK 64) puts the 16
+  // (row, slot) pairs of each ds_read_b128 lane group ({0-3,12-15,20-27}, ...:
+  // MI355X_MICROARCH.md §LDS) in 16 distinct 16-B bank slots
+  static constexpr int ROW = BK + 16;
+  static constexpr int AV = BM * (BK / 4) / THREADS;         // float4 per thread
+  static constexpr int BV = (3 * BN * (BK / 8) + THREADS - 1) / THREADS;  // uint4 per thread
+  static constexpr size_t LDS = sizeof(unsigned short) * 3 * (BM + BN) * ROW;
+  static_assert(BM * (BK / 4) % THREADS == 0, "A staging must tile the threads");
+};
+
+// Workgroup = NW waves stacked along M (wave tile MT x NT 16x16 tiles), K
+// blocks of BK, PF register sets of staged operands in flight (the loads for
+// block kb+PF are issued while block kb is computed from LDS).
+template <int NW, int MT, int NT, int BK, int PF>
+__global__ __launch_bounds__(64 * NW) void k_gemm3(const float* __restrict__ A, int64_t lda,
+                                                   const unsigned short* __restrict__ Bp,
+                                                   int64_t ldb, int64_t bplane,
+                                                   float* __restrict__ C, int64_t ldc, int64_t M,
+                                                   int64_t N, int64_t K) {
+  using Cfg = Gemm3Cfg<NW, MT, NT, BK>;
+  constexpr int TH = Cfg::THREADS, BM = Cfg::BM, BN = Cfg::BN, ROW = Cfg::ROW;
+  constexpr int AV = Cfg::AV, BV = Cfg::BV;
+  constexpr int AC = BK / 4, BC = BK / 8;  // float4 / uint4 per row
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  unsigned short* sA = lds;                    // [3][BM][ROW]
+  unsigned short* sB = lds + 3 * BM * ROW;     // [3][BN][ROW]
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 ra[PF][AV];
+  uint4 rb[PF][BV];
+  auto load = [&](int set, int64_t k0) {
+#pragma unroll
+    for (int s = 0; s < AV; ++s) {
+      const int idx = t + TH * s;
+      const int r = idx / AC, c4 = idx - r * AC;
+      const int64_t gm = min(m0 + r, M - 1);
+      const int64_t gk = k0 + 4 * c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gk + 3 < K) {
+        v = *reinterpret_cast<const float4*>(A + gm * lda + gk);
+      } else {
+        float* pv = &v.x;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pv[q] = (gk + q < K) ? A[gm * lda + gk + q] : 0.f;
+      }
+      ra[set][s] = v;
+    }
+#pragma unroll
+    for (int s = 0; s < BV; ++s) {
+      const int idx = t + TH * s;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (idx < 3 * BN * BC) {
+        const int p = idx / (BN * BC), rem = idx - p * BN * BC;
+        const int r = rem / BC, c = rem - r * BC;
+        const int64_t gn = min(n0 + r, N - 1);
+        v = *reinterpret_cast<const uint4*>(Bp + p * bplane + gn * ldb + k0 + 8 * c);
+      }
+      rb[set][s] = v;
+    }
+  };
+  auto store = [&](int set) {
+#pragma unroll
+    for (int s = 0; s < AV; ++s) {
+      const int idx = t + TH * s;
+      const int r = idx / AC, c4 = idx - r * AC;
+      const float* pv = &ra[set][s].x;
+      unsigned short h[3][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) split3(pv[q], h[0][q], h[1][q], h[2][q]);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        uint2 w;
+        w.x = (unsigned)h[p][0] | ((unsigned)h[p][1] << 16);
+        w.y = (unsigned)h[p][2] | ((unsigned)h[p][3] << 16);
+        *reinterpret_cast<uint2*>(sA + (p * BM + r) * ROW + 4 * c4) = w;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < BV; ++s) {
+      const int idx = t + TH * s;
+      if (idx < 3 * BN * BC) {
+        const int p = idx / (BN * BC), rem = idx - p * BN * BC;
+        const int r = rem / BC, c = rem - r * BC;
+        *reinterpret_cast<uint4*>(sB + (p * BN + r) * ROW + 8 * c) = rb[set][s];
+      }
+    }
+  };
+  auto compute = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[MT][3];
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          af[a][p] = *reinterpret_cast<const bf16x8*>(
+              sA + (p * BM + wave * 16 * MT + 16 * a + li) * ROW + kk + 8 * lg);
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        bf16x8 bf[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bf[p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + 16 * b + li) * ROW + kk + 8 * lg);
+#pragma unroll
+        for (int a = 0; a < MT; ++a) {
+          // small terms first
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][2], bf[0], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][1], bf[1], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[2], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][1], bf[0], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[1], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[0], acc[a][b], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  const int64_t nk = (K + BK - 1) / BK;
+#pragma unroll
+  for (int s = 0; s < PF; ++s)
+    if (s < nk) load(s, (int64_t)s * BK);
+  for (int64_t kb = 0; kb < nk; kb += PF) {
+#pragma unroll
+    for (int s = 0; s < PF; ++s) {
+      if (kb + s < nk) {
+        __syncthreads();  // previous block's fragments consumed
+        store(s);
+        __syncthreads();
+        if (kb + s + PF < nk) load(s, (kb + s + PF) * BK);
+        compute();
+      }
+    }
+  }
+  // store: acc[a][b][r] = C[row 16a + 4lg + r][col 16b + li] of the wave tile
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int64_t gn = n0 + 16 * b + li;
+      if (gn < N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t gm = m0 + wave * 16 * MT + 16 * a + 4 * lg + r;
+          if (gm < M) C[gm * ldc + gn] = acc[a][b][r];
+        }
+      }
+    }
+}
+
+}  // namespace sv2n

@@ -15,6 +15,8 @@ Operators
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional, Sequence
 
 import torch
@@ -68,6 +70,44 @@ def gemm_f32(a: torch.Tensor, a_kmajor: bool, b: torch.Tensor, b_kmajor: bool,
                                  b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
                                  M, N, K, _lib.ptr(ws), ws_n, _stream(dev)), "sv2n_gemm_f32")
     return out
+
+
+# Projection GEMMs with a small weight operand run on the bf16-split MFMA
+# kernel (sv2n_gemm_f32x3, f32-accurate); SV2N_GEMM=f32 selects the exact-f32
+# MFMA kernel instead.
+_SPLIT_GEMM = os.environ.get("SV2N_GEMM", "split3").lower() != "f32"
+
+
+def weight_planes(w: torch.Tensor, transpose: bool) -> torch.Tensor:
+    """The three bf16 planes [3][rows][Kp] of a weight used as the B operand of
+    sv2n_gemm_f32x3: B(n, k) = w[n][k] (transpose False) or w[k][n] (True)."""
+    lib = _lib.load()
+    rows, K = (w.shape[1], w.shape[0]) if transpose else (w.shape[0], w.shape[1])
+    Kp = lib.sv2n_split3_kpad(K)
+    out = torch.empty(3, rows, Kp, device=w.device, dtype=torch.int16)
+    _lib.check(lib.sv2n_split3(w.data_ptr(), rows, K, w.stride(0), int(transpose), out.data_ptr(),
+                               _stream(w.device)), "sv2n_split3")
+    return out
+
+
+def _split_ok(a: torch.Tensor) -> bool:
+    return _SPLIT_GEMM and a.stride(1) == 1 and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0
+
+
+def project(a: torch.Tensor, w: torch.Tensor, transpose_w: bool) -> torch.Tensor:
+    """C = a · B with B(n,k) = w[n][k] (C = a·wᵀ) or w[k][n] (C = a·w); a is
+    [M][K] k-contiguous.  bf16-split MFMA when a is aligned, else exact f32."""
+    M, K = a.shape
+    N = w.shape[1] if transpose_w else w.shape[0]
+    if _split_ok(a):
+        lib = _lib.load()
+        planes = weight_planes(w, transpose_w)
+        out = torch.empty(M, N, device=a.device, dtype=torch.float32)
+        _lib.check(lib.sv2n_gemm_f32x3(a.data_ptr(), a.stride(0), planes.data_ptr(),
+                                       out.data_ptr(), out.stride(0), M, N, K,
+                                       _stream(a.device)), "sv2n_gemm_f32x3")
+        return out
+    return gemm_f32(a, True, w, not transpose_w, M, N, K)
 
 
 class _Linear(torch.autograd.Function):

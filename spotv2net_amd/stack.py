@@ -27,7 +27,7 @@ import torch
 
 from . import _lib
 from .layout import GraphLayout
-from .ops import _aligned, _require_device, gemm_f32, pad_columns
+from .ops import _aligned, _require_device, gemm_f32, pad_columns, project
 
 
 def _grad_buf(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -123,7 +123,7 @@ class _GATStack(torch.autograd.Function):
             F = c.in_channels
             if xin.size(1) != F:
                 raise ValueError(f"layer {l}: expected {F} input features, got {xin.size(1)}")
-            xs = gemm_f32(xin, True, waugs[l], True, N, waugs[l].size(0), F)
+            xs = project(xin, waugs[l], False)  # x · Waugᵀ
             keep, kscale = None, 1.0
             kn = n if tiled else 32  # keep-mask tile: [B][H][n][n] tiled, [B][H][32][32] per-graph
             if training and c.dropout > 0.0:
@@ -249,7 +249,7 @@ class _GATStack(torch.autograd.Function):
                     _lib.ptr(gas), _lib.ptr(gad), _lib.ptr(gb), ws.data_ptr(), ws_n, st),
                     "sv2n_gat_prep_bwd_node")
             if l > 0 or need_x0:
-                dy = gemm_f32(dxs, True, waugs[l], False, N, F, xs.size(1))
+                dy = project(dxs, waugs[l], True)  # dxs · Waug
 
         if use_edge and ea is not None:
             # grads exist (zeros) even without edges, as in PyG

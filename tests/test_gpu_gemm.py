@@ -39,3 +39,25 @@ def test_linear_autograd(dev):
     assert_close(y, xr @ wr.t(), what="y")
     assert_close(x.grad, xr.grad, what="dx")
     assert_close(w.grad, wr.grad, what="dw")
+
+
+@pytest.mark.parametrize("M,N,K,transpose", [(15360, 408, 1260, False), (300, 17, 5, False),
+                                             (257, 400, 208, True), (64, 1, 70, True),
+                                             (1000, 130, 64, False)])
+def test_split3_gemm_matches_f32_accuracy(dev, M, N, K, transpose):
+    """sv2n_gemm_f32x3 (three bf16 planes, six MFMA products) is as close to
+    the float64 product as the exact-f32 MFMA GEMM: max error relative to
+    Σ|a·b| within 2x of sv2n_gemm_f32's, and below 1e-6."""
+    from spotv2net_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g).to(dev)
+    w = (torch.randn(K, N, generator=g) if transpose else torch.randn(N, K, generator=g)).to(dev)
+    w = w.contiguous()
+    got = ops.project(a, w, transpose)
+    wb = w if transpose else w.t()                      # [K][N]
+    ref = (a.double() @ wb.double())
+    scale = (a.double().abs() @ wb.double().abs())
+    f32 = ops.gemm_f32(a, True, w, not transpose, M, N, K)
+    e3 = ((got.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
+    e32 = ((f32.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
+    assert e3 < 1e-6 and e3 <= 2 * e32 + 1e-9, (e3, e32)

@@ -1,0 +1,158 @@
+// Accuracy + speed harness for the bf16x3-split GEMM (spotv2net_amd/csrc/sv2n_gemm3_kernel.h)
+// against an fp64 reference and the exact-f32 MFMA GEMM (sv2n_gemm_kernel.h), on the
+// C2 forward projection shapes.  Build:
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -Iinclude tools/gemm3_tune.hip -o build/gemm3_tune
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../spotv2net_amd/csrc/sv2n_gemm3_kernel.h"
+#include "../spotv2net_amd/csrc/sv2n_gemm_kernel.h"
+
+using namespace sv2n;
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e = (x);                                                              \
+    if (e != hipSuccess) {                                                           \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+__global__ void k_ref(const float* A, const float* B, double* C, double* S, int64_t M, int64_t N,
+                      int64_t K) {
+  int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * N) return;
+  int64_t m = idx / N, n = idx % N;
+  double s = 0, a = 0;
+  for (int64_t k = 0; k < K; ++k) {
+    s += (double)A[m * K + k] * B[n * K + k];
+    a += fabs((double)A[m * K + k] * B[n * K + k]);
+  }
+  C[idx] = s;
+  S[idx] = a;
+}
+
+__global__ void k_fill(float* p, int64_t n, uint32_t seed, float scale) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+  x ^= x >> 13; x *= 0x5bd1e995; x ^= x >> 15;
+  p[i] = (((x & 0xffffff) / 16777216.0f) * 2.f - 1.f) * scale;
+}
+
+struct Shape { const char* name; int64_t M, N, K; };
+
+template <int NW, int MT, int NT, int BK, int PF>
+void run3(const Shape& sh, hipStream_t st, const float* A, const unsigned short* Bp, int64_t Kp,
+          float* C, const std::vector<double>& ref, const std::vector<double>& absr) {
+  using Cfg = Gemm3Cfg<NW, MT, NT, BK>;
+  const size_t lds = Cfg::LDS;
+  if (lds > 160 * 1024) return;
+  if (lds > 65536)
+    CK(hipFuncSetAttribute((const void*)k_gemm3<NW, MT, NT, BK, PF>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  dim3 grid((unsigned)((sh.M + Cfg::BM - 1) / Cfg::BM), (unsigned)((sh.N + Cfg::BN - 1) / Cfg::BN));
+  auto f = [&]() {
+    hipLaunchKernelGGL((k_gemm3<NW, MT, NT, BK, PF>), grid, dim3(Cfg::THREADS), lds, st, A, sh.K, Bp, Kp,
+                       sh.N * Kp, C, sh.N, sh.M, sh.N, sh.K);
+  };
+  f();
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(st));
+  std::vector<float> out(sh.M * sh.N);
+  CK(hipMemcpy(out.data(), C, sizeof(float) * out.size(), hipMemcpyDeviceToHost));
+  double maxrel = 0, maxabs = 0;
+  for (size_t i = 0; i < out.size(); i += 7) {
+    const double e = fabs(out[i] - ref[i]);
+    maxabs = fmax(maxabs, e);
+    maxrel = fmax(maxrel, e / (absr[i] + 1e-30));
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int reps = 20;
+  CK(hipEventRecord(e0, st));
+  for (int r = 0; r < reps; ++r) f();
+  CK(hipEventRecord(e1, st));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / reps;
+  printf("  gemm3 NW%d MT%d NT%-2d BK%d PF%d %8.1f us %7.1f TF(f32-eq)  max|err| %.2e  max err/S|ab| %.2e\n",
+         NW, MT, NT, BK, PF, us, 2.0 * sh.M * sh.N * sh.K / us / 1e6, maxabs, maxrel);
+  fflush(stdout);
+}
+
+int main() {
+  std::vector<Shape> shapes = {{"fwd L0", 15360, 408, 1260}, {"fwd L1", 15360, 208, 400}};
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  for (auto& sh : shapes) {
+    const int64_t M = sh.M, N = sh.N, K = sh.K;
+    const int64_t Kp = (K + 63) / 64 * 64;
+    float *A, *B, *C;
+    double *R, *S;
+    unsigned short* Bp;
+    CK(hipMalloc(&A, sizeof(float) * M * K));
+    CK(hipMalloc(&B, sizeof(float) * N * K));
+    CK(hipMalloc(&C, sizeof(float) * M * N));
+    CK(hipMalloc(&R, sizeof(double) * M * N));
+    CK(hipMalloc(&S, sizeof(double) * M * N));
+    CK(hipMalloc(&Bp, sizeof(unsigned short) * 3 * N * Kp));
+    k_fill<<<(M * K + 255) / 256, 256, 0, st>>>(A, M * K, 1, 1.0f);
+    k_fill<<<(N * K + 255) / 256, 256, 0, st>>>(B, N * K, 2, 0.05f);
+    k_split3<<<(N * Kp + 255) / 256, 256, 0, st>>>(B, N, K, K, Bp, Kp);
+    k_ref<<<(M * N + 255) / 256, 256, 0, st>>>(A, B, R, S, M, N, K);
+    CK(hipStreamSynchronize(st));
+    std::vector<double> ref(M * N), absr(M * N);
+    CK(hipMemcpy(ref.data(), R, sizeof(double) * M * N, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(absr.data(), S, sizeof(double) * M * N, hipMemcpyDeviceToHost));
+    printf("== %s M=%ld N=%ld K=%ld\n", sh.name, (long)M, (long)N, (long)K);
+    // exact-f32 MFMA baseline (library config)
+    {
+      auto f = [&]() {
+        launch_gemm_cfg<8, 1, 13, 16, true, true, 2, 0>(1, K, st, A, K, B, K, C, N, M, N, K, true,
+                                                       true, nullptr);
+      };
+      f();
+      CK(hipStreamSynchronize(st));
+      std::vector<float> out(M * N);
+      CK(hipMemcpy(out.data(), C, sizeof(float) * M * N, hipMemcpyDeviceToHost));
+      double maxrel = 0, maxabs = 0;
+      for (size_t i = 0; i < out.size(); i += 7) {
+        const double e = fabs(out[i] - ref[i]);
+        maxabs = fmax(maxabs, e);
+        maxrel = fmax(maxrel, e / (absr[i] + 1e-30));
+      }
+      hipEvent_t e0, e1;
+      CK(hipEventCreate(&e0));
+      CK(hipEventCreate(&e1));
+      CK(hipEventRecord(e0, st));
+      for (int r = 0; r < 20; ++r) f();
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double us = ms * 1e3 / 20;
+      printf("  f32 MFMA NT13     %8.1f us %7.1f TF          max|err| %.2e  max err/Σ|ab| %.2e\n", us,
+             2.0 * M * N * K / us / 1e6, maxabs, maxrel);
+    }
+    run3<4, 1, 13, 32, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3<4, 1, 13, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3<8, 1, 13, 32, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3<8, 1, 13, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3<8, 1, 13, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3<4, 2, 13, 32, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3<8, 2, 13, 32, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3<8, 1, 7, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3<8, 2, 7, 32, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3<4, 2, 7, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+    CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(S)); CK(hipFree(Bp));
+  }
+  return 0;
+}
