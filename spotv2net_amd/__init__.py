@@ -10,6 +10,7 @@ from .data import Batch, Data, WindowDataset, collate, shard_indices, synthetic_
     synthetic_series, window_batch, window_graph
 from .layout import GraphLayout, UnsupportedLayout, analyze_edge_index, canonical_edge_index
 from .model import GATModel
+from . import evaluate, series
 
 __all__ = [
     "GATConv", "GATModel", "Linear", "Data", "Batch", "collate", "window_graph", "window_batch",

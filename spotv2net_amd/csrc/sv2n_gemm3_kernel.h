@@ -220,4 +220,150 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3(const float* __restrict__ A, 
     }
 }
 
+// Both operands k-strided (the weight gradients dWᵀ = xᵀ·dxs):
+//   C[m][n] = Σ_k A[k][m] · B[k][n]   (A row stride lda, B row stride ldb)
+// over the K slice [kz*kslice, min(K, (kz+1)*kslice)) of gridDim.z; with
+// more than one slice every slice writes its own slab C + kz*M*N (summed in
+// a fixed order by the caller's reduce).  Both operands are split while
+// staged: each thread loads 4(k) x 4(row) micro-tiles with 16-B loads along
+// the contiguous row index, transposes them in registers and writes 4
+// consecutive k per plane (ds_write_b64) into the same [plane][row][k] LDS
+// image the k-major kernel reads.
+template <int NW, int MT, int NT, int BK>
+struct Gemm3TCfg {
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int BM = 16 * MT * NW, BN = 16 * NT;
+  static constexpr int ROW = BK + 16;
+  static constexpr int AU = BM * BK / 16, BU = BN * BK / 16;   // 4x4 micro-tiles
+  static constexpr int AV = (AU + THREADS - 1) / THREADS, BV = (BU + THREADS - 1) / THREADS;
+  static constexpr size_t LDS = sizeof(unsigned short) * 3 * (BM + BN) * ROW;
+};
+
+template <int BK, int ROWS, int TH, int V>
+__device__ __forceinline__ void t_load(float4 (&r)[V][4], const float* __restrict__ X,
+                                       int64_t ld, int64_t row0, int64_t rows, int64_t k0,
+                                       int64_t kend, int t) {
+  constexpr int UR = ROWS / 4;  // micro-tiles along the row index
+#pragma unroll
+  for (int s = 0; s < V; ++s) {
+    const int idx = t + TH * s;
+    const int ug = idx % UR, kg = idx / UR;
+    const bool on = idx < UR * (BK / 4);
+    int64_t col = row0 + 4 * ug;
+    col = col + 3 < rows ? col : (rows >= 4 ? rows - 4 : 0);  // clamped (rows >= M are never stored)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t k = k0 + 4 * kg + q;
+      r[s][q] = (on && k < kend) ? *reinterpret_cast<const float4*>(X + k * ld + col)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+template <int BK, int ROWS, int TH, int V, int ROW>
+__device__ __forceinline__ void t_store(const float4 (&r)[V][4], unsigned short* __restrict__ sX,
+                                        int t) {
+  constexpr int UR = ROWS / 4;
+#pragma unroll
+  for (int s = 0; s < V; ++s) {
+    const int idx = t + TH * s;
+    if (idx >= UR * (BK / 4)) continue;
+    const int ug = idx % UR, kg = idx / UR;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {  // row 4ug + c, k = 4kg .. 4kg+3
+      unsigned short h[3][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float* pv = &r[s][q].x;
+        split3(pv[c], h[0][q], h[1][q], h[2][q]);
+      }
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        uint2 w;
+        w.x = (unsigned)h[p][0] | ((unsigned)h[p][1] << 16);
+        w.y = (unsigned)h[p][2] | ((unsigned)h[p][3] << 16);
+        *reinterpret_cast<uint2*>(sX + (p * ROWS + 4 * ug + c) * ROW + 4 * kg) = w;
+      }
+    }
+  }
+}
+
+template <int NW, int MT, int NT, int BK>
+__global__ __launch_bounds__(64 * NW) void k_gemm3_t(const float* __restrict__ A, int64_t lda,
+                                                     const float* __restrict__ B, int64_t ldb,
+                                                     float* __restrict__ C, int64_t ldc,
+                                                     int64_t M, int64_t N, int64_t K,
+                                                     int64_t kslice) {
+  using Cfg = Gemm3TCfg<NW, MT, NT, BK>;
+  constexpr int TH = Cfg::THREADS, BM = Cfg::BM, BN = Cfg::BN, ROW = Cfg::ROW;
+  constexpr int AV = Cfg::AV, BV = Cfg::BV;
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  unsigned short* sA = lds;                    // [3][BM][ROW]
+  unsigned short* sB = lds + 3 * BM * ROW;     // [3][BN][ROW]
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
+  const int64_t kbeg = (int64_t)blockIdx.z * kslice, kend = min(K, kbeg + kslice);
+  if (gridDim.z > 1) C += (int64_t)blockIdx.z * M * ldc;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 ra[AV][4], rb[BV][4];
+  t_load<BK, BM, TH, AV>(ra, A, lda, m0, M, kbeg, kend, t);
+  t_load<BK, BN, TH, BV>(rb, B, ldb, n0, N, kbeg, kend, t);
+  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+    t_store<BK, BM, TH, AV, ROW>(ra, sA, t);
+    t_store<BK, BN, TH, BV, ROW>(rb, sB, t);
+    __syncthreads();
+    if (k0 + BK < kend) {
+      t_load<BK, BM, TH, AV>(ra, A, lda, m0, M, k0 + BK, kend, t);
+      t_load<BK, BN, TH, BV>(rb, B, ldb, n0, N, k0 + BK, kend, t);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[MT][3];
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          af[a][p] = *reinterpret_cast<const bf16x8*>(
+              sA + (p * BM + wave * 16 * MT + 16 * a + li) * ROW + kk + 8 * lg);
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        bf16x8 bf[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bf[p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + 16 * b + li) * ROW + kk + 8 * lg);
+#pragma unroll
+        for (int a = 0; a < MT; ++a) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][2], bf[0], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][1], bf[1], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[2], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][1], bf[0], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[1], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[0], acc[a][b], 0, 0, 0);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int64_t gn = n0 + 16 * b + li;
+      if (gn < N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t gm = m0 + wave * 16 * MT + 16 * a + 4 * lg + r;
+          if (gm < M) C[gm * ldc + gn] = acc[a][b][r];
+        }
+      }
+    }
+}
+
 }  // namespace sv2n

@@ -106,3 +106,44 @@ def test_c2_full_batch_properties(dev):
             one = window_batch(V, W, torch.tensor([g * (S + 1)], device=dev), S)
             o1 = model(one)
             assert_close(o1, out[g * 30:(g + 1) * 30], what=f"graph {g} alone vs batched")
+
+
+def test_evaluate_matches_notebook_metrics(dev):
+    """spotv2net_amd.evaluate reproduces 6_results.ipynb's eval cells (batch-mean
+    MSE of de-standardised predictions, elementwise QLIKE) against the oracle
+    model evaluated the same way on CPU, and checkpoints round-trip through
+    torch.save / load_checkpoint (weights_only)."""
+    import os
+    import tempfile
+
+    from oracle.pyg_gatconv import OracleGATModel
+    from spotv2net_amd import GATModel, WindowDataset, synthetic_series
+    from spotv2net_amd.evaluate import evaluate, load_checkpoint, qlike
+    S, n = 4, 30
+    V, W = synthetic_series(40, n, seed=3)
+    ds_cpu = WindowDataset(V, W, S)
+    ds_gpu = WindowDataset(V.to(dev), W.to(dev), S)
+    torch.manual_seed(2)
+    ref = OracleGATModel(n * S, 3 * S, 4, 1, [8, 4], concat_heads=True)
+    mine = GATModel(n * S, 3 * S, 4, 1, [8, 4], concat_heads=True)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "GAT_weights_seed_5154.pth")
+        torch.save(ref.state_dict(), path)
+        load_checkpoint(mine, path)
+    mine = mine.to(dev)
+    scaler = (10.0, 2.0)
+    got = evaluate(mine, ds_gpu.loader(7, shuffle=False), scaler)
+    ref.eval()
+    tot, nb, ps, ys = 0.0, 0, [], []
+    with torch.no_grad():
+        for b in ds_cpu.loader(7, shuffle=False):
+            yh = ref(b) * scaler[1] + scaler[0]
+            y = b.y_x * scaler[1] + scaler[0]
+            tot += torch.nn.functional.mse_loss(yh, y)
+            nb += 1
+            ps.append(yh)
+            ys.append(y)
+    assert abs(got.mse - float(tot / nb)) <= 1e-5 * max(1.0, float(tot / nb))
+    q = qlike(torch.cat(ys), torch.cat(ps))
+    assert_parity(got.qlike, q, q.double(), what="qlike")
+    assert abs(got.qlike_mean - float(q.mean())) < 1e-5
