@@ -20,6 +20,7 @@
 // (16-B aligned rows); the sign bit of a saved probability records
 // leaky_relu's negative side for the backward.
 #include "sv2n_common.h"
+#include <algorithm>
 
 namespace sv2n {
 
@@ -35,108 +36,350 @@ __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)
 
 // ---------------------------------------------------------------------------
 // forward
-// LDS: sP[H][32][TS] | sA[H][32] | sD[H][32]
+// LDS: sP[H][32][TS] | sA[H][32] | sD[H][32] | sB[XS] (bias of the chunk) |
+//      sU = sE[H][32][TS] (edge logits, one row per (head, target)) during the
+//      softmax, then sX[32][XS] (one xs chunk: rows j, `span` columns)
+// All global loads of a chunk are issued before any store of the launch, so
+// no `s_waitcnt vmcnt` ever waits on an output store: gfx950 counts stores on
+// the same in-order counter, and a wait for a load issued after a store drains
+// the store too (measured: a bias load behind the y stores cost 6 of 33 µs).
+// A chunk is heads [h0, h0+hpc) x columns [c0, c0+cw) of each head; the C2
+// layers (H·C = 400 / 200) are one chunk, so the whole graph's inputs arrive
+// in one memory round trip.
 // ---------------------------------------------------------------------------
+constexpr int XW = 512;                           // max xs columns per chunk
+constexpr int XV = 32 * XW / 4 / ATT_THREADS;     // 16-B register slots per thread
+constexpr int AEV = 32 * 32 * SV2N_MAX_HEADS / 4 / ATT_THREADS;  // covers n·n·H for all n, H
+constexpr int RPT = SV2N_MAX_HEADS * 64 / ATT_THREADS;            // softmax lane-rows per thread
+
+__host__ __device__ inline int ae_floats(int H) { return H * 32 * TS; }  // sE[h][i][TS]
+// chunk row stride: room for a 32-column tile starting at any head slot
+__host__ __device__ inline int x_stride(int span) { return ((span + 32 + 3) & ~3) + 4; }
+
+struct FwdChunking {
+  int hpc, cw;  // heads per chunk, columns per head per chunk
+};
+static inline FwdChunking fwd_chunking(int H, int C, bool concat) {
+  if (H * C <= XW) return {H, C};
+  if (!concat) return {H, (XW / H) & ~31};        // every head, a column window
+  if (C <= XW) return {XW / C, C};                // whole heads
+  return {1, XW};                                 // one head, a column window
+}
+
 template <int ACT, bool CONCAT>
 __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
     const float* __restrict__ xs, int ldx, const float* __restrict__ ae,
     const uint32_t* __restrict__ rowmask, const float* __restrict__ bias,
     const uint8_t* __restrict__ keep, float keep_scale, float* __restrict__ y,
-    float* __restrict__ psave, int n, int H, int C, float slope) {
+    float* __restrict__ psave, int n, int H, int C, float slope, int hpc, int cw) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int XSmax = x_stride(hpc * cw);
   float* sP = smem;
   float* sA = sP + H * 32 * TS;
   float* sD = sA + H * 32;
+  float* sB = sD + H * 32;
+  float* sE = sB + XSmax;  // sE during the softmax, then sX
+  float* sX = sE;
 
   const int g = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int half = lane >> 5, l32 = lane & 31;
   const int64_t row0 = (int64_t)g * n;
   const int HC = H * C;
-
-  for (int idx = t; idx < H * 32; idx += ATT_THREADS) {
-    const int h = idx >> 5, j = idx & 31;
-    float as = 0.f, ad = 0.f;
-    if (j < n) {
-      const float* r = xs + (row0 + j) * ldx + HC;
-      as = r[h];
-      ad = r[H + h];
-    }
-    sA[idx] = as;
-    sD[idx] = ad;
-  }
-  __syncthreads();
-
-  // ---- per-target softmax over all 32 (padded) rows of every head ----
-  const int j = l32;
-  for (int rb = wave * 2; rb < H * 32; rb += 8) {
-    const int r = rb + half;
-    const int h = r >> 5, i = r & 31;
-    const bool rv = i < n;
-    const uint32_t bits = rv ? row_bits(rowmask, row0 + i, n, i) : 0u;
-    const bool off = rv && j < n && j != i && ((bits >> j) & 1u);
-    const bool valid = rv && j < n && (j == i || off);
-    float s = sA[h * 32 + j] + sD[h * 32 + i];
-    if (ae) {
-      const float e = off ? ae[((row0 + i) * n + j) * H + h] : 0.f;
-      const float esum = red32_sum(e);
-      const int cnt = __popc(bits);
-      const float loopv = cnt > 0 ? esum / (float)cnt : 0.f;
-      s += (j == i) ? loopv : e;
-    }
-    const bool neg = !(s > 0.f);
-    const float lr = neg ? s * slope : s;
-    const float mx = red32_max(valid ? lr : -INFINITY);
-    const float ex = valid ? expf(lr - mx) : 0.f;
-    const float den = red32_sum(ex);
-    const float p = ex / (den + 1e-16f);
-    float pd = valid ? p : 0.f;
-    if (rv) {
-      const int64_t pidx = (((int64_t)g * H + h) * 32 + i) * 32 + j;
-      psave[pidx] = valid ? (neg ? -p : p) : 0.f;
-      if (keep && valid) pd = keep[pidx] ? p * keep_scale : 0.f;
-    }
-    sP[(h * 32 + i) * TS + j] = pd;
-  }
-  __syncthreads();
-
-  // ---- aggregation on MFMA: acc[i][c] = Σ_j P[h][i][j] · xs[j][h*C + c] ----
-  const int nck = (C + 31) / 32;
-  const int items = CONCAT ? H * nck : nck;
   const int OC = CONCAT ? HC : C;
-  const float invH = 1.f / (float)H;
-  for (int it = wave; it < items; it += 4) {
-    const int hb = CONCAT ? it / nck : 0;
-    const int c0 = 32 * (CONCAT ? it - hb * nck : it);
-    const int he = CONCAT ? hb + 1 : H;
-    const int c = c0 + l32;
-    const bool cok = c < C;
-    floatx16 acc;
+  const int nhb = (H + hpc - 1) / hpc, ncb = (C + cw - 1) / cw;
+  const int nchunk = CONCAT ? nhb * ncb : ncb;
+  const bool row_vec = ((ldx & 3) == 0) && ((((uintptr_t)xs) & 15) == 0);
+  const bool contig = cw == C;  // a chunk = contiguous columns [h0*C, (h0+nh)*C) of a row
+
+  // ---- chunk geometry and its loads (addresses clamped, never branched
+  //      around: the compiler can then count vmcnt past them) ----
+  struct Chunk { int h0, nh, c0, cwv, span; bool vec; };
+  auto chunk_of = [&](int ch) {
+    Chunk k;
+    const int hb = CONCAT ? ch / ncb : 0, cb = CONCAT ? ch - hb * ncb : ch;
+    k.h0 = hb * hpc;
+    k.nh = min(hpc, H - k.h0);
+    k.c0 = cb * cw;
+    k.cwv = min(cw, C - k.c0);
+    k.span = k.nh * cw;
+    k.vec = row_vec && (contig ? (((k.h0 * C) | k.span) & 3) == 0 : (C & 3) == 0);
+    return k;
+  };
+  float4 xr[XV];
+  float br[XW / ATT_THREADS];
+  const float* xg = xs + row0 * ldx;  // this graph's rows (32-bit offsets below)
+  auto load_chunk = [&](const Chunk& k) {
+    // opaque copy of the thread index: keeps the compiler from hoisting the
+    // per-slot offsets out of the chunk loop (16+ VGPRs held across it)
+    int tt = t;
+    asm volatile("" : "+v"(tt));
+    if (k.vec) {
+      const int nq = k.span >> 2;                         // 16-B slots per row
+      int j = tt / nq, o4 = tt - j * nq;
+      const int dj = ATT_THREADS / nq, do4 = ATT_THREADS - dj * nq;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    for (int h = hb; h < he; ++h) {
-      float bv[16];
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const int jj = 2 * kk + half;
-        bv[kk] = (jj < n && cok) ? xs[(row0 + jj) * ldx + h * C + c] : 0.f;
+      for (int v = 0; v < XV; ++v) {
+        const int o = 4 * o4;
+        int col;
+        bool ok = j < n;
+        if (contig) {
+          col = k.h0 * C + o;
+        } else {
+          const int hh = o / cw, cc = o - hh * cw;
+          ok = ok && cc < k.cwv;
+          col = (k.h0 + hh) * C + k.c0 + cc;
+        }
+        const float4 w = *reinterpret_cast<const float4*>(xg + (ok ? j * ldx + col : 0));
+        xr[v] = ok ? w : make_float4(0.f, 0.f, 0.f, 0.f);
+        o4 += do4;
+        j += dj;
+        if (o4 >= nq) { o4 -= nq; ++j; }
       }
-      const float* prow = sP + (h * 32 + l32) * TS + half;
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(prow[2 * kk], bv[kk], acc, 0, 0, 0);
     }
-    if (cok) {
-      const int oc = CONCAT ? hb * C + c : c;
-      const float b = bias ? bias[oc] : 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = crow(r, half);
-        if (i < n) {
-          const float z = (CONCAT ? acc[r] : acc[r] * invH) + b;
-          y[(row0 + i) * OC + oc] = act_fwd<ACT>(z);
+    for (int v = 0; v < XW / ATT_THREADS; ++v) {
+      const int o = tt + ATT_THREADS * v;
+      const int hh = o / cw, cc = o - hh * cw;
+      const bool ok = bias && o < k.span && cc < k.cwv;
+      const float b = bias[ok ? (CONCAT ? (k.h0 + hh) * C : 0) + k.c0 + cc : 0];
+      br[v] = ok ? b : 0.f;
+    }
+  };
+  // chunk -> sX[j][o] (row stride XS), bias -> sB
+  auto store_chunk = [&](const Chunk& k, int XS) {
+    int tt = t;
+    asm volatile("" : "+v"(tt));
+    if (k.vec) {
+      const int nq = k.span >> 2;
+      int j = tt / nq, o4 = tt - j * nq;
+      const int dj = ATT_THREADS / nq, do4 = ATT_THREADS - dj * nq;
+#pragma unroll
+      for (int v = 0; v < XV; ++v) {
+        if (j < 32) *reinterpret_cast<float4*>(sX + j * XS + 4 * o4) = xr[v];
+        o4 += do4;
+        j += dj;
+        if (o4 >= nq) { o4 -= nq; ++j; }
+      }
+    } else {  // unaligned rows: straight from global (not register-staged)
+      for (int e = t; e < 32 * k.span; e += ATT_THREADS) {
+        const int j = e / k.span, o = e - j * k.span;
+        const int hh = o / cw, cc = o - hh * cw;
+        sX[j * XS + o] = (j < n && cc < k.cwv) ? xs[(row0 + j) * ldx + (k.h0 + hh) * C + k.c0 + cc]
+                                               : 0.f;
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < XW / ATT_THREADS; ++v) {
+      const int o = t + ATT_THREADS * v;
+      if (o < XS) sB[o] = br[v];
+    }
+  };
+
+  // ---- every load of the softmax phase, then chunk 0's ----
+  const int nae = n * n * H;
+  const int nv = nae >> 2;
+  const float* aesrc = ae ? ae + row0 * n * H : xs;
+  const bool ae_vec = (((uintptr_t)aesrc) & 15) == 0;
+  float4 av[AEV];
+  if (ae) {
+#pragma unroll
+    for (int q = 0; q < AEV; ++q) {
+      const int k = t + ATT_THREADS * q;
+      const int kc = k < nv ? k : 0;
+      float4 w;
+      if (ae_vec) {
+        w = reinterpret_cast<const float4*>(aesrc)[kc];
+      } else {
+        w.x = aesrc[4 * kc]; w.y = aesrc[4 * kc + 1]; w.z = aesrc[4 * kc + 2]; w.w = aesrc[4 * kc + 3];
+      }
+      av[q] = w;
+    }
+  }
+  const int ha = t >> 5, ja = t & 31;  // sA/sD slot (t < H*32 <= 256)
+  const bool aok = ha < H && ja < n;
+  const float* arow = xs + (aok ? (row0 + ja) * ldx + HC + ha : 0);
+  const float as_v = arow[0], ad_v = arow[aok ? H : 0];
+  // softmax inputs from global: each lane-row's source bitmask and keep bytes
+  // (clamped, unconditional loads)
+  const int nlr = 64 * H;  // lane-rows: two lanes per (head, target) row
+  uint32_t rbits[RPT], kw[RPT][4];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int rr = t + ATT_THREADS * q;
+    const int r = rr >> 1, i = r & 31, h = r >> 5;
+    const bool ok = rr < nlr && i < n;
+    const uint32_t* rm = rowmask ? rowmask : reinterpret_cast<const uint32_t*>(xs);
+    const uint32_t w = rm[rowmask && ok ? row0 + i : 0];
+    rbits[q] = !ok ? 0u : (rowmask ? w & ~(1u << i) : row_bits(nullptr, row0 + i, n, i));
+    const uint8_t* kp = keep ? keep : reinterpret_cast<const uint8_t*>(xs);
+    const int64_t kb = (keep && ok) ? ((((int64_t)g * H + h) * 32 + i) * 32 + 16 * (rr & 1)) : 0;
+#pragma unroll
+    for (int w4 = 0; w4 < 4; ++w4) kw[q][w4] = *reinterpret_cast<const uint32_t*>(kp + kb + 4 * w4);
+  }
+
+  Chunk cur = chunk_of(0);  // issued last: only the aggregation waits for it
+  load_chunk(cur);
+
+  if (ae) {
+    // element kk = 4k + e of AE [n][n][H] -> (i, j, h), kk = (i*n + j)*H + h
+    const int kb = 4 * t;
+    int h = kb % H, ij = kb / H;
+    int i = ij / n, jj = ij - i * n;
+    const int step = 4 * ATT_THREADS;  // elements per q
+    const int sh = step % H, sij = step / H;
+    const int si = sij / n, sj = sij - si * n;
+#pragma unroll
+    for (int q = 0; q < AEV; ++q) {
+      const float* pa = &av[q].x;
+      int h2 = h, j2 = jj, i2 = i;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (i2 < n) sE[(h2 * 32 + i2) * TS + j2] = pa[e];
+        if (++h2 == H) { h2 = 0; if (++j2 == n) { j2 = 0; ++i2; } }
+      }
+      h += sh;
+      if (h >= H) { h -= H; ++jj; }
+      jj += sj;
+      if (jj >= n) { jj -= n; ++i; }
+      i += si;
+    }
+  }
+  if (ha < H) {
+    sA[t] = aok ? as_v : 0.f;
+    sD[t] = aok ? ad_v : 0.f;
+  }
+  __syncthreads();
+
+  // ---- per-target softmax: two lanes per (head, target) row, 16 columns each;
+  //      the signed probabilities stay in registers until the xs chunk has
+  //      left them (a wait for its loads would otherwise drain these stores) ----
+  float4 psv[RPT][4];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int rr = t + ATT_THREADS * q;
+    if (q * ATT_THREADS >= nlr) break;
+    if (rr >= nlr) continue;  // wave-uniform: nlr is a multiple of 64
+    const int r = rr >> 1, part = rr & 1;
+    const int h = r >> 5, i = r & 31;
+    const int jb = 16 * part;
+    const bool rv = i < n;
+    const uint32_t bits = rbits[q];
+    const uint32_t pb = bits >> jb;  // this lane's 16 columns
+    const float* er = sE + (h * 32 + i) * TS + jb;
+    const float* ar = sA + h * 32 + jb;
+    const float ad = sD[h * 32 + i];
+    float ev[16];
+    float loopv = 0.f;
+    if (ae) {
+      float esum = 0.f;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        ev[c] = ((pb >> c) & 1u) ? er[c] : 0.f;
+        esum += ev[c];
+      }
+      esum += __shfl_xor(esum, 1, 64);
+      const int cnt = __popc(bits);
+      loopv = cnt > 0 ? esum / (float)cnt : 0.f;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) ev[c] = 0.f;
+    }
+    const uint32_t validm = rv ? ((bits | (1u << i)) >> jb) : 0u;
+    float lr[16];
+    uint32_t negm = 0u;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const float sv = ar[c] + ad + ((jb + c == i) ? loopv : ev[c]);
+      const bool neg = !(sv > 0.f);
+      negm |= neg ? (1u << c) : 0u;
+      lr[c] = neg ? sv * slope : sv;
+      if ((validm >> c) & 1u) mx = fmaxf(mx, lr[c]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+    float den = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      lr[c] = ((validm >> c) & 1u) ? expf(lr[c] - mx) : 0.f;
+      den += lr[c];
+    }
+    den += __shfl_xor(den, 1, 64);
+    const float inv = 1.f / (den + 1e-16f);
+    float* prow = sP + (h * 32 + i) * TS + jb;
+#pragma unroll
+    for (int c4 = 0; c4 < 16; c4 += 4) {
+      float sq[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = c4 + e;
+        const float p = lr[c] * inv;
+        const bool valid = (validm >> c) & 1u;
+        sq[e] = valid ? (((negm >> c) & 1u) ? -p : p) : 0.f;
+        float pd = valid ? p : 0.f;
+        if (keep) pd = ((kw[q][c >> 2] >> (8 * (c & 3))) & 0xffu) ? pd * keep_scale : 0.f;
+        prow[c] = pd;
+      }
+      psv[q][c4 >> 2] = make_float4(sq[0], sq[1], sq[2], sq[3]);
+    }
+  }
+  __syncthreads();  // sE dead, sP complete
+  store_chunk(cur, x_stride(cur.span));
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int rr = t + ATT_THREADS * q;
+    const int r = rr >> 1, h = r >> 5, i = r & 31;
+    if (rr < nlr && i < n) {
+      float4* dst = reinterpret_cast<float4*>(psave + (((int64_t)g * H + h) * 32 + i) * 32 + 16 * (rr & 1));
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) dst[c4] = psv[q][c4];
+    }
+  }
+
+  // ---- aggregation per chunk: out[i][c] = Σ_j P[h][i][j] · xs[j][h*C + c] ----
+  const float invH = 1.f / (float)H;
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const Chunk k = cur;
+    const int XS = x_stride(k.span);
+    __syncthreads();
+    if (ch + 1 < nchunk) {
+      cur = chunk_of(ch + 1);
+      load_chunk(cur);
+    }
+    const int ntc = (k.cwv + 31) >> 5;  // 32-column tiles per head
+    const int ntile = CONCAT ? k.nh * ntc : ntc;
+    for (int tl = wave; tl < ntile; tl += ATT_THREADS / 64) {
+      const int hh0 = CONCAT ? tl / ntc : 0;
+      const int tc = CONCAT ? tl - hh0 * ntc : tl;
+      floatx16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const int hh_end = CONCAT ? hh0 + 1 : k.nh;
+#pragma unroll 1
+      for (int hh = hh0; hh < hh_end; ++hh) {
+        const float* prow = sP + ((k.h0 + hh) * 32 + l32) * TS + half;
+        const float* xcol = sX + half * XS + hh * cw + 32 * tc + l32;
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(prow[2 * kk], xcol[2 * kk * XS], acc, 0, 0, 0);
+      }
+      const int cc = 32 * tc + l32;
+      if (cc < k.cwv) {
+        const int oc = (CONCAT ? (k.h0 + hh0) * C : 0) + k.c0 + cc;
+        const float b = sB[(CONCAT ? hh0 * cw : 0) + cc];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = crow(r, half);
+          if (i < n) {
+            const float z = (CONCAT ? acc[r] : acc[r] * invH) + b;
+            y[(row0 + i) * OC + oc] = act_fwd<ACT>(z);
+          }
         }
       }
+    }
+    if (ch + 1 < nchunk) {
+      __syncthreads();  // chunk consumed before the next one overwrites sX / sB
+      store_chunk(cur, x_stride(cur.span));
     }
   }
 }
@@ -165,14 +408,27 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
   float* tO = sP + H * 32 * TS + wave * 2 * 32 * TS;
   float* tX = tO + 32 * TS;
 
-  for (int idx = t; idx < H * 1024; idx += ATT_THREADS) {
-    const int h = idx >> 10, i = (idx >> 5) & 31, jj = idx & 31;
-    float pd = 0.f;
-    if (i < n) {
-      pd = fabsf(psave[pbase + idx]);
-      if (keep) pd = keep[pbase + idx] ? pd * keep_scale : 0.f;
+  // psave -> LDS: loads issued 8 at a time (independent), then stored
+  for (int k0 = 0; k0 < H * 1024; k0 += 8 * ATT_THREADS) {
+    float pv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = k0 + t + ATT_THREADS * k;
+      const int i = (idx >> 5) & 31;
+      pv[k] = 0.f;
+      if (idx < H * 1024 && i < n) {
+        pv[k] = fabsf(psave[pbase + idx]);
+        if (keep) pv[k] = keep[pbase + idx] ? pv[k] * keep_scale : 0.f;
+      }
     }
-    sP[(h * 32 + i) * TS + jj] = pd;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = k0 + t + ATT_THREADS * k;
+      if (idx < H * 1024) {
+        const int h = idx >> 10, i = (idx >> 5) & 31, jj = idx & 31;
+        sP[(h * 32 + i) * TS + jj] = pv[k];
+      }
+    }
   }
   __syncthreads();
 
@@ -309,7 +565,11 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
 // ============================ C-ABI ========================================
 using namespace sv2n;
 
-static size_t fwd_lds(int H) { return sizeof(float) * ((size_t)H * 32 * TS + 2 * (size_t)H * 32); }
+static size_t fwd_lds(int H, FwdChunking ck) {
+  const size_t xs = (size_t)x_stride(ck.hpc * ck.cw);
+  return sizeof(float) * ((size_t)H * 32 * TS + 2 * (size_t)H * 32 + xs +
+                          std::max((size_t)ae_floats(H), 32 * xs));
+}
 static size_t bwd_lds(int H) { return sizeof(float) * ((size_t)H * 32 * TS + 4 * 2 * 32 * TS); }
 
 template <typename K>
@@ -323,10 +583,12 @@ template <int ACT, bool CONCAT>
 static void launch_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
                        const uint32_t* rowmask, const float* bias, const uint8_t* keep,
                        float keep_scale, float* y, float* psave, int n, int H, int C, float slope) {
-  const size_t lds = fwd_lds(H);
+  const FwdChunking ck = fwd_chunking(H, C, CONCAT);
+  const size_t lds = fwd_lds(H, ck);
   raise_lds(k_attn_fwd<ACT, CONCAT>, lds);
   hipLaunchKernelGGL((k_attn_fwd<ACT, CONCAT>), dim3((unsigned)B), dim3(ATT_THREADS), lds, st, xs,
-                     ldx, ae, rowmask, bias, keep, keep_scale, y, psave, n, H, C, slope);
+                     ldx, ae, rowmask, bias, keep, keep_scale, y, psave, n, H, C, slope, ck.hpc,
+                     ck.cw);
 }
 
 template <int ACT, bool CONCAT>
