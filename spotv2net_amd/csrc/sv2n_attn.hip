@@ -386,15 +386,47 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
 
 // ---------------------------------------------------------------------------
 // backward
-// LDS: sP[H][32][TS] (post-dropout P) | per wave: tO[32][TS] (dOut chunk, [i][c]),
-//      tX[32][TS] (xs chunk [j][c], later dLᵀ [j][i])
+// Per graph: dz = act'(dy, y) (· 1/H for the head mean), then per head h
+//   G_h   = X_h · dZ_hᵀ          (dPᵀ, [j][i])            wave h mod 4
+//   dxs_h = P_dᵀ · dZ_h           (message/gather bwd)    same wave
+// and the softmax / leaky_relu backward of G_h gives dl -> d a_src, d a_dst,
+// d ae.  Same memory discipline as the forward: every access is a buffer
+// load/store (out-of-range offsets read 0 / drop the store, so nothing is
+// branched around and vmcnt is counted), the prologue issues all loads of
+// the graph's first chunk at once, and the next chunk's loads are in flight
+// while the current chunk's MFMAs run.
+// LDS: sP[H][32][TS] (signed saved P) | sKB[H][32] keep bits | sRB[32] row
+//      bits | sSh[H][32] (self-loop share) | sDad[H][32] (d a_dst) |
+//      area: sX[32][XS] + sZ[32][ZS] per chunk (odd strides: conflict-free
+//      column reads), after the chunks sDL[H][32][TS] (dl)
+// A chunk is heads [h0, h0+hpc) x columns [c0, c0+cw) of each head.
 // ---------------------------------------------------------------------------
+constexpr int XB = 224;                                   // max xs columns per chunk
+constexpr int BV = 32 * XB / 4 / ATT_THREADS;             // 16-B slots per thread per array
+constexpr int PV = SV2N_MAX_HEADS * 1024 / 4 / ATT_THREADS;
+
+struct BwdChunking {
+  int hpc, cw;
+};
+static inline BwdChunking bwd_chunking(int H, int C, bool concat) {
+  if (H * C <= XB) return {H, C};
+  if ((C & 3) == 0 || !concat) {  // every head, balanced column windows
+    const int cwmax = (C & 3) == 0 ? ((XB / H) & ~3) : XB / H;
+    const int nch = (C + cwmax - 1) / cwmax;
+    int cw = (C + nch - 1) / nch;
+    if ((C & 3) == 0) cw = (cw + 3) & ~3;
+    return {H, cw};
+  }
+  if (C <= XB) return {XB / C, C};  // whole heads
+  return {1, XB};
+}
+
 template <int ACT, bool CONCAT>
 __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ xs,
     int ldx, const float* __restrict__ psave, const uint8_t* __restrict__ keep, float keep_scale,
     const uint32_t* __restrict__ rowmask, float* __restrict__ dxs, float* __restrict__ dae,
-    float* __restrict__ dbias_part, int n, int H, int C, float slope) {
+    float* __restrict__ dbias_part, int n, int H, int C, float slope, int hpc, int cw) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int g = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -403,109 +435,299 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
   const int HC = H * C;
   const int OC = CONCAT ? HC : C;
   const float invH = 1.f / (float)H;
-  const int64_t pbase = (int64_t)g * H * 1024;
   float* sP = smem;
-  float* tO = sP + H * 32 * TS + wave * 2 * 32 * TS;
-  float* tX = tO + 32 * TS;
+  uint32_t* sKB = reinterpret_cast<uint32_t*>(sP + H * 32 * TS);
+  uint32_t* sRB = sKB + H * 32;
+  float* sSh = reinterpret_cast<float*>(sRB + 32);
+  float* sDad = sSh + H * 32;
+  float* sArea = sDad + H * 32;
+  float* sDL = sArea;
 
-  // psave -> LDS: loads issued 8 at a time (independent), then stored
-  for (int k0 = 0; k0 < H * 1024; k0 += 8 * ATT_THREADS) {
-    float pv[8];
+  const rsrc_t rx = make_rsrc(xs + row0 * ldx, (uint32_t)(n * ldx) * 4u);
+  const rsrc_t rdy = make_rsrc(dy + row0 * OC, (uint32_t)(n * OC) * 4u);
+  const rsrc_t ry = make_rsrc(y + row0 * OC, (uint32_t)(n * OC) * 4u);
+  const rsrc_t rps = make_rsrc(psave + (int64_t)g * H * 1024, (uint32_t)H * 4096u);
+  const rsrc_t rkp = make_rsrc(keep ? keep + (int64_t)g * H * 1024 : nullptr,
+                               keep ? (uint32_t)H * 1024u : 0u);
+  const rsrc_t rrm = make_rsrc(rowmask ? rowmask + row0 : nullptr, rowmask ? (uint32_t)n * 4u : 0u);
+  const rsrc_t rdx = make_rsrc(dxs + row0 * ldx, (uint32_t)(n * ldx) * 4u);
+  const rsrc_t rdb = make_rsrc(dbias_part + (int64_t)g * OC, (uint32_t)OC * 4u);
+
+  // ---- chunk geometry ----
+  const int nhb = (H + hpc - 1) / hpc, ncb = (C + cw - 1) / cw;
+  const int nchunk = nhb * ncb;
+  const bool contig = cw == C;
+  struct Chunk { int h0, nh, c0, cwv, span, zw; bool vec; };
+  auto chunk_of = [&](int ch) {
+    Chunk k;
+    const int hb = ch / ncb, cb = ch - hb * ncb;
+    k.h0 = hb * hpc;
+    k.nh = min(hpc, H - k.h0);
+    k.c0 = cb * cw;
+    k.cwv = min(cw, C - k.c0);
+    k.span = k.nh * cw;
+    k.zw = CONCAT ? k.span : cw;
+    k.vec = ((ldx | OC) & 3) == 0 &&
+            (contig ? (((k.h0 * C) | k.span) & 3) == 0 && (CONCAT || (C & 3) == 0) : (C & 3) == 0);
+    return k;
+  };
+  // xs (+ dy, y) chunk -> registers.  vec: 16-B slots over row spans; else
+  // one element per slot component.
+  f32x4 xr[BV], dyr[BV], yr[BV];
+  auto load_chunk = [&](const Chunk& k) {
+    int tt = t;
+    asm volatile("" : "+v"(tt));  // keep per-slot offsets out of the chunk loop
+    if (k.vec) {
+      const int nq = k.span >> 2;
+      int j = tt / nq, q = tt - j * nq;
+      const int dj = ATT_THREADS / nq, dq = ATT_THREADS - dj * nq;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int idx = k0 + t + ATT_THREADS * k;
-      const int i = (idx >> 5) & 31;
-      pv[k] = 0.f;
-      if (idx < H * 1024 && i < n) {
-        pv[k] = fabsf(psave[pbase + idx]);
-        if (keep) pv[k] = keep[pbase + idx] ? pv[k] * keep_scale : 0.f;
+      for (int v = 0; v < BV; ++v) {
+        const int L = 4 * q;
+        int col;
+        bool ok = j < n;
+        if (contig) {
+          col = k.h0 * C + L;
+        } else {
+          const int seg = L / cw, cc = L - seg * cw;
+          ok = ok && cc < k.cwv;
+          col = (k.h0 + seg) * C + k.c0 + cc;
+        }
+        xr[v] = bld4(rx, ok ? (j * ldx + col) * 4 : OOB);
+        if (CONCAT) {
+          const int off = ok ? (j * OC + col) * 4 : OOB;
+          dyr[v] = bld4(rdy, off);
+          yr[v] = bld4(ry, off);
+        }
+        q += dq;
+        j += dj;
+        if (q >= nq) { q -= nq; ++j; }
+      }
+      if (!CONCAT) {
+        const int nz = cw >> 2;
+        int j2 = tt / nz, q2 = tt - j2 * nz;
+        const int dj2 = ATT_THREADS / nz, dq2 = ATT_THREADS - dj2 * nz;
+#pragma unroll
+        for (int v = 0; v < BV; ++v) {
+          const int L = 4 * q2;
+          const int off = (j2 < n && L < k.cwv) ? (j2 * OC + k.c0 + L) * 4 : OOB;
+          dyr[v] = bld4(rdy, off);
+          yr[v] = bld4(ry, off);
+          q2 += dq2;
+          j2 += dj2;
+          if (q2 >= nz) { q2 -= nz; ++j2; }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < BV; ++v) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int sl = tt + ATT_THREADS * (4 * v + e);
+          const int j = sl / k.span, L = sl - j * k.span;
+          const int seg = L / cw, cc = L - seg * cw;
+          const bool ok = j < n && cc < k.cwv;
+          const int col = (k.h0 + seg) * C + k.c0 + cc;
+          xr[v][e] = bld(rx, ok ? (j * ldx + col) * 4 : OOB);
+          if (CONCAT) {
+            const int off = ok ? (j * OC + col) * 4 : OOB;
+            dyr[v][e] = bld(rdy, off);
+            yr[v][e] = bld(ry, off);
+          } else {
+            const int j2 = sl / cw, L2 = sl - j2 * cw;
+            const int off = (j2 < n && L2 < k.cwv) ? (j2 * OC + k.c0 + L2) * 4 : OOB;
+            dyr[v][e] = bld(rdy, off);
+            yr[v][e] = bld(ry, off);
+          }
+        }
       }
     }
+  };
+  // registers -> sX[j][L], sZ[j][L] = act'(dy, y)
+  auto stage_chunk = [&](const Chunk& k, float* sX, int XS, float* sZ, int ZS) {
+    int tt = t;
+    asm volatile("" : "+v"(tt));
+    if (k.vec) {
+      const int nq = k.span >> 2;
+      int j = tt / nq, q = tt - j * nq;
+      const int dj = ATT_THREADS / nq, dq = ATT_THREADS - dj * nq;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int idx = k0 + t + ATT_THREADS * k;
-      if (idx < H * 1024) {
-        const int h = idx >> 10, i = (idx >> 5) & 31, jj = idx & 31;
-        sP[(h * 32 + i) * TS + jj] = pv[k];
+      for (int v = 0; v < BV; ++v) {
+        if (j < 32) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sX[j * XS + 4 * q + e] = xr[v][e];
+            if (CONCAT) sZ[j * ZS + 4 * q + e] = act_bwd<ACT>(dyr[v][e], yr[v][e]);
+          }
+        }
+        q += dq;
+        j += dj;
+        if (q >= nq) { q -= nq; ++j; }
       }
+      if (!CONCAT) {
+        const int nz = cw >> 2;
+        int j2 = tt / nz, q2 = tt - j2 * nz;
+        const int dj2 = ATT_THREADS / nz, dq2 = ATT_THREADS - dj2 * nz;
+#pragma unroll
+        for (int v = 0; v < BV; ++v) {
+          if (j2 < 32) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sZ[j2 * ZS + 4 * q2 + e] = act_bwd<ACT>(dyr[v][e], yr[v][e]);
+          }
+          q2 += dq2;
+          j2 += dj2;
+          if (q2 >= nz) { q2 -= nz; ++j2; }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < BV; ++v) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int sl = tt + ATT_THREADS * (4 * v + e);
+          const int j = sl / k.span, L = sl - j * k.span;
+          if (j < 32) {
+            sX[j * XS + L] = xr[v][e];
+            if (CONCAT) sZ[j * ZS + L] = act_bwd<ACT>(dyr[v][e], yr[v][e]);
+          }
+          if (!CONCAT) {
+            const int j2 = sl / cw, L2 = sl - j2 * cw;
+            if (j2 < 32) sZ[j2 * ZS + L2] = act_bwd<ACT>(dyr[v][e], yr[v][e]);
+          }
+        }
+      }
+    }
+  };
+
+  // ---- prologue: saved P, keep bits, row bits, then chunk 0 ----
+  f32x4 pr[PV];
+#pragma unroll
+  for (int v = 0; v < PV; ++v) {
+    const int idx4 = t + ATT_THREADS * v;  // 16-B slot of [h][i][32]
+    pr[v] = bld4(rps, (idx4 >> 8) < H ? idx4 * 16 : OOB);
+  }
+  const bool krow = t < H * 32;  // (h, i) = (t >> 5, t & 31)
+  const u32x4 kw0 = bld4_u32(rkp, krow ? t * 32 : OOB);
+  const u32x4 kw1 = bld4_u32(rkp, krow ? t * 32 + 16 : OOB);
+  const uint32_t rmw = bld_u32(rrm, t < n ? t * 4 : OOB);
+  Chunk cur = chunk_of(0);
+  load_chunk(cur);
+
+#pragma unroll
+  for (int v = 0; v < PV; ++v) {
+    const int idx4 = t + ATT_THREADS * v;
+    const int h = idx4 >> 8, i = (idx4 >> 3) & 31, j0 = (idx4 & 7) * 4;
+    if (h < H) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sP[(h * 32 + i) * TS + j0 + e] = i < n ? pr[v][e] : 0.f;
     }
   }
-  __syncthreads();
+  if (krow) {
+    uint32_t kb = 0u;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const uint32_t word = w < 4 ? kw0[w] : kw1[w - 4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) kb |= ((word >> (8 * b)) & 0xffu) ? (1u << (4 * w + b)) : 0u;
+    }
+    sKB[t] = kb;
+  }
+  if (t < 32) {
+    const uint32_t all = (n >= 32) ? 0xffffffffu : ((1u << n) - 1u);
+    sRB[t] = t < n ? ((rowmask ? rmw : all) & ~(1u << t)) : 0u;
+  }
 
-  for (int h = wave; h < H; h += 4) {
-    floatx16 G;  // dPᵀ: G[j][i] = Σ_c xs[j][c] · dOut[i][c]
+  // ---- chunks ----
+  floatx16 G0, G1;  // G_h for heads wave and wave + 4
 #pragma unroll
-    for (int r = 0; r < 16; ++r) G[r] = 0.f;
-    for (int c0 = 0; c0 < C; c0 += 32) {
-      const int c = c0 + l32;
-      const bool cok = c < C;
-      const int ycol = CONCAT ? h * C + c : c;
-      float bsum = 0.f;
-#pragma unroll 4
-      for (int s = 0; s < 16; ++s) {
-        const int rr = half + 2 * s;
-        const bool ok = rr < n && cok;
-        const float dz = ok ? act_bwd<ACT>(dy[(row0 + rr) * OC + ycol], y[(row0 + rr) * OC + ycol])
-                            : 0.f;
-        bsum += dz;
-        tO[rr * TS + l32] = CONCAT ? dz : dz * invH;
-        tX[rr * TS + l32] = ok ? xs[(row0 + rr) * ldx + h * C + c] : 0.f;
+  for (int r = 0; r < 16; ++r) { G0[r] = 0.f; G1[r] = 0.f; }
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const Chunk k = cur;
+    const int XS = k.span | 1, ZS = k.zw | 1;
+    float* sX = sArea;
+    float* sZ = sArea + 32 * XS;
+    __syncthreads();  // previous chunk consumed (first pass: prologue LDS writes ordered)
+    stage_chunk(k, sX, XS, sZ, ZS);
+    __syncthreads();
+    if (ch + 1 < nchunk) {
+      cur = chunk_of(ch + 1);
+      load_chunk(cur);
+    }
+    // bias gradient partials: column sums of dz
+    for (int L = t; L < k.zw; L += ATT_THREADS) {
+      float sb = 0.f;
+#pragma unroll 8
+      for (int j = 0; j < 32; ++j) sb += sZ[j * ZS + L];
+      const int seg = L / cw, cc = L - seg * cw;
+      const int oc = (CONCAT ? (k.h0 + seg) * C : 0) + k.c0 + cc;
+      bst(rdb, cc < k.cwv ? oc * 4 : OOB, sb);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int h = wave + 4 * s2;
+      const int hh = h - k.h0;
+      if (hh < 0 || hh >= k.nh) continue;  // wave-uniform
+      floatx16 G = s2 ? G1 : G0;
+      const int zoff = CONCAT ? hh * cw : 0;
+      const float* xa = sX + l32 * XS + hh * cw + half;
+      const float* zb = sZ + l32 * ZS + zoff + half;
+      const int nk = (k.cwv + 1) >> 1;
+      for (int kk = 0; kk < nk; ++kk) {
+        const bool cv = 2 * kk + half < k.cwv;
+        const float a = cv ? xa[2 * kk] : 0.f;
+        const float b = cv ? (CONCAT ? zb[2 * kk] : zb[2 * kk] * invH) : 0.f;
+        G = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, G, 0, 0, 0);
       }
-      bsum += __shfl_xor(bsum, 32, 64);
-      if (half == 0 && cok && (CONCAT || h == 0)) dbias_part[(int64_t)g * OC + ycol] = bsum;
-      lds_fence();
-      // G += X · Oᵀ   (A[j][c] = tX[j][c], B[c][i] = tO[i][c])
-      const float* xr = tX + l32 * TS + half;
-      const float* orow = tO + l32 * TS + half;
+      if (s2) G1 = G; else G0 = G;
+      // dxs tiles: D[j][c] = Σ_i P_d[i][j] · dZ[i][c]
+      const uint32_t* kbh = sKB + h * 32;
+      const float* ph = sP + h * 32 * TS + l32;
+      const int ntc = (k.cwv + 31) >> 5;
+      for (int tc = 0; tc < ntc; ++tc) {
+        floatx16 D;
 #pragma unroll
-      for (int kk = 0; kk < 16; ++kk)
-        G = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[2 * kk], orow[2 * kk], G, 0, 0, 0);
-      // dxs chunk = Pdᵀ · O   (A[j][i] = sP[h][i][j], B[i][c] = tO[i][c])
-      floatx16 D2;
+        for (int r = 0; r < 16; ++r) D[r] = 0.f;
+        const float* zc = sZ + half * ZS + zoff + 32 * tc + l32;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) D2[r] = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const int ii = 2 * kk + half;
-        D2 = __builtin_amdgcn_mfma_f32_32x32x2f32(sP[(h * 32 + ii) * TS + l32], tO[ii * TS + l32],
-                                                  D2, 0, 0, 0);
-      }
-      if (cok) {
+        for (int kk = 0; kk < 16; ++kk) {
+          const int ii = 2 * kk + half;
+          float a = fabsf(ph[ii * TS]);
+          if (keep) a = ((kbh[ii] >> l32) & 1u) ? a * keep_scale : 0.f;
+          const float b = CONCAT ? zc[2 * kk * ZS] : zc[2 * kk * ZS] * invH;
+          D = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, D, 0, 0, 0);
+        }
+        const int cl = 32 * tc + l32;
+        const int gcol = h * C + k.c0 + cl;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int jr = crow(r, half);
-          if (jr < n) dxs[(row0 + jr) * ldx + h * C + c] = D2[r];
+          bst(rdx, (cl < k.cwv && jr < n) ? (jr * ldx + gcol) * 4 : OOB, D[r]);
         }
       }
-      lds_fence();  // tile reads retired before the next chunk overwrites them
     }
+  }
+  __syncthreads();  // chunk area dead: sDL
 
-    // ---- softmax + leaky_relu backward on G: lane column i, rows j = crow(r, half) ----
+  // ---- softmax + leaky_relu backward of G_h: lane column i, rows j = crow(r, half) ----
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int h = wave + 4 * s2;
+    if (h >= H) continue;  // wave-uniform
+    const floatx16 G = s2 ? G1 : G0;
     const int i = l32;
     const bool iv = i < n;
-    const uint32_t bits = iv ? row_bits(rowmask, row0 + i, n, i) : 0u;
-    const int64_t prow = pbase + ((int64_t)h * 32 + i) * 32;
-    float ps[16];
-    uint32_t kp[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int jb = 8 * q + 4 * half;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (iv) v = *reinterpret_cast<const float4*>(psave + prow + jb);
-      ps[4 * q + 0] = v.x;
-      ps[4 * q + 1] = v.y;
-      ps[4 * q + 2] = v.z;
-      ps[4 * q + 3] = v.w;
-      kp[q] = (keep && iv) ? *reinterpret_cast<const uint32_t*>(keep + prow + jb) : 0u;
-    }
-    float dp[16];
+    const uint32_t bits = sRB[i];
+    const uint32_t kb = keep ? sKB[h * 32 + i] : 0xffffffffu;
+    const float* prw = sP + (h * 32 + i) * TS;
+    float ps[16], dp[16];
     float tl = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int jr = crow(r, half);
+      ps[r] = prw[jr];
       const bool valid = iv && jr < n && (jr == i || ((bits >> jr) & 1u));
       float d = valid ? G[r] : 0.f;
-      if (keep) d = ((kp[r >> 2] >> (8 * (r & 3))) & 0xffu) ? d * keep_scale : 0.f;
+      if (keep) d = ((kb >> jr) & 1u) ? d * keep_scale : 0.f;
       dp[r] = d;
       tl += fabsf(ps[r]) * d;
     }
@@ -516,13 +738,11 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
     for (int r = 0; r < 16; ++r) {
       const int jr = crow(r, half);
       const bool valid = iv && jr < n && (jr == i || ((bits >> jr) & 1u));
-      const float p = fabsf(ps[r]);
-      const float ds = p * (dp[r] - tl);
+      const float ds = fabsf(ps[r]) * (dp[r] - tl);
       dl[r] = valid ? (signbit(ps[r]) ? ds * slope : ds) : 0.f;
       dad += dl[r];
     }
     dad += __shfl_xor(dad, 32, 64);
-    if (half == 0 && iv) dxs[(row0 + i) * ldx + HC + H + h] = dad;
     // dl[i][i] sits in half (i>>2)&1, register (i&3) + 4*(i>>3)
     const int hi = (i >> 2) & 1, ri = (i & 3) + 4 * (i >> 3);
     float mine = 0.f;
@@ -530,33 +750,67 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
     for (int r = 0; r < 16; ++r) mine = (r == ri) ? dl[r] : mine;
     const float other = __shfl_xor(mine, 32, 64);
     const float dlii = (half == hi) ? mine : other;
-    if (dae && iv) {
+    if (half == 0) {
       const int cnt = __popc(bits);
-      const float share = cnt > 0 ? dlii / (float)cnt : 0.f;
+      sDad[h * 32 + i] = dad;
+      sSh[h * 32 + i] = cnt > 0 ? dlii / (float)cnt : 0.f;
+    }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int jr = crow(r, half);
-        if (jr < n)
-          dae[((row0 + i) * n + jr) * H + h] =
-              (jr != i && ((bits >> jr) & 1u)) ? dl[r] + share : 0.f;
+    for (int r = 0; r < 16; ++r) sDL[(h * 32 + i) * TS + crow(r, half)] = dl[r];
+  }
+  __syncthreads();
+
+  // ---- d ae: the graph's [n][n][H] block, four elements per slot ----
+  if (dae) {
+    const int nae = n * n * H;
+    const rsrc_t rdae = make_rsrc(dae + row0 * n * H, (uint32_t)nae * 4u);
+    auto dae_val = [&](int i, int j, int h) {
+      const bool e = j != i && ((sRB[i] >> j) & 1u);
+      return e ? sDL[(h * 32 + i) * TS + j] + sSh[h * 32 + i] : 0.f;
+    };
+    if ((nae & 3) == 0 && ((((uintptr_t)dae) & 15) == 0)) {
+      const int kb = 4 * t;
+      int h = kb % H, ij = kb / H;
+      int i = ij / n, j = ij - i * n;
+      const int step = 4 * ATT_THREADS;
+      const int sh = step % H, sij = step / H;
+      const int si = sij / n, sj = sij - si * n;
+      for (int k4 = kb; k4 < nae; k4 += step) {
+        f32x4 v;
+        int h2 = h, j2 = j, i2 = i;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = dae_val(i2, j2, h2);
+          if (++h2 == H) { h2 = 0; if (++j2 == n) { j2 = 0; ++i2; } }
+        }
+        bst4(rdae, k4 * 4, v);
+        h += sh;
+        if (h >= H) { h -= H; ++j; }
+        j += sj;
+        if (j >= n) { j -= n; ++i; }
+        i += si;
+      }
+    } else {
+      for (int kk = t; kk < nae; kk += ATT_THREADS) {
+        const int h = kk % H, ij = kk / H;
+        const int i = ij / n, j = ij - i * n;
+        bst(rdae, kk * 4, dae_val(i, j, h));
       }
     }
-    // d a_src[j] = Σ_i dL[i][j]: transpose through LDS (tX as [j][i])
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tX[crow(r, half) * TS + i] = dl[r];
-    lds_fence();
-    if (lane < 32 && lane < n) {
-      float s = 0.f;
-      for (int ii = 0; ii < 32; ++ii) s += tX[lane * TS + ii];
-      dxs[(row0 + lane) * ldx + HC + h] = s;
-    }
-    lds_fence();
   }
-
-  const int npad = ldx - (HC + 2 * H);
-  for (int idx = t; idx < n * npad; idx += ATT_THREADS) {
-    const int rr = idx / npad;
-    dxs[(row0 + rr) * ldx + HC + 2 * H + (idx - rr * npad)] = 0.f;
+  // ---- dxs columns [HC, ldx): d a_src (Σ_i dl[i][j]), d a_dst, zero padding ----
+  const int ntail = ldx - HC;
+  for (int e = t; e < n * ntail; e += ATT_THREADS) {
+    const int j = e / ntail, c2 = e - j * ntail;
+    float v = 0.f;
+    if (c2 < H) {
+      const float* col = sDL + c2 * 32 * TS + j;
+#pragma unroll 8
+      for (int ii = 0; ii < 32; ++ii) v += col[ii * TS];
+    } else if (c2 < 2 * H) {
+      v = sDad[(c2 - H) * 32 + j];
+    }
+    bst(rdx, (j * ldx + HC + c2) * 4, v);
   }
 }
 
@@ -570,7 +824,12 @@ static size_t fwd_lds(int H, FwdChunking ck) {
   return sizeof(float) * ((size_t)H * 32 * TS + 2 * (size_t)H * 32 + xs +
                           std::max((size_t)ae_floats(H), 32 * xs));
 }
-static size_t bwd_lds(int H) { return sizeof(float) * ((size_t)H * 32 * TS + 4 * 2 * 32 * TS); }
+static size_t bwd_lds(int H, BwdChunking ck, bool concat) {
+  const size_t span = (size_t)ck.hpc * ck.cw;
+  const size_t area = 32 * ((span | 1) + ((concat ? span : (size_t)ck.cw) | 1)) + 32;
+  return sizeof(float) * ((size_t)H * 32 * TS + 4 * (size_t)H * 32 + 32 +
+                          std::max(area, (size_t)H * 32 * TS));
+}
 
 template <typename K>
 static void raise_lds(K kernel, size_t bytes) {
@@ -596,10 +855,12 @@ static void launch_bwd(int64_t B, hipStream_t st, const float* dy, const float* 
                        const float* xs, int ldx, const float* psave, const uint8_t* keep,
                        float keep_scale, const uint32_t* rowmask, float* dxs, float* dae,
                        float* dbias, int n, int H, int C, float slope) {
-  const size_t lds = bwd_lds(H);
+  const BwdChunking ck = bwd_chunking(H, C, CONCAT);
+  const size_t lds = bwd_lds(H, ck, CONCAT);
   raise_lds(k_attn_bwd<ACT, CONCAT>, lds);
   hipLaunchKernelGGL((k_attn_bwd<ACT, CONCAT>), dim3((unsigned)B), dim3(ATT_THREADS), lds, st, dy,
-                     y, xs, ldx, psave, keep, keep_scale, rowmask, dxs, dae, dbias, n, H, C, slope);
+                     y, xs, ldx, psave, keep, keep_scale, rowmask, dxs, dae, dbias, n, H, C, slope,
+                     ck.hpc, ck.cw);
 }
 
 static int check_attn_args(int64_t B, int n, int H, int C, int ldx, int act) {

@@ -120,4 +120,37 @@ __device__ __forceinline__ bool decode_edge(int64_t e, const int64_t* __restrict
   return g < B;
 }
 
+// ---- buffer descriptors (cdna_hip_programming.md T8/T20) -------------------
+// A raw buffer over [base, base + bytes): loads at an offset past `bytes`
+// return 0 and stores there are dropped by the hardware, so predicated
+// accesses need no branch and the compiler can count vmcnt across them.
+// Build descriptors only from wave-uniform values (kernel args, blockIdx);
+// `bytes` = 0 makes every access through the descriptor a no-op.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int OOB = 0x7ffffff0;  // byte offset past any buffer (< 2^31)
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+// (the b32/b128 builtins move raw bits: unsigned int / uint x4)
+__device__ __forceinline__ uint32_t bld_u32(rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+__device__ __forceinline__ float bld(rsrc_t r, int off) { return __uint_as_float(bld_u32(r, off)); }
+__device__ __forceinline__ f32x4 bld4(rsrc_t r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ u32x4 bld4_u32(rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ void bst(rsrc_t r, int off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bst4(rsrc_t r, int off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+
 }  // namespace sv2n
