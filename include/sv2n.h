@@ -186,6 +186,24 @@ int sv2n_gat_prep_bwd_node(const float* dwaug_t, int ldx, const float* W,
                            float* g_att_dst, float* g_bias, float* workspace,
                            int64_t workspace_floats, hipStream_t stream);
 
+/* Weight gradients of one GAT layer in two launches: the split-K GEMM
+ *   T = dWaugᵀ[f][o] = Σ_k x[k][f] · dxs[k][o]        (x [num_nodes][ld_x], dxs [num_nodes][ldx])
+ * and one fused epilogue that reduces its K slabs in a fixed order and
+ * ACCUMULATES gW (+ the att_src / att_dst fold terms), g_att_src, g_att_dst and
+ * g_bias (Σ of dbias_partial [num_parts][bias_len]) — what
+ * sv2n_gemm_f32 + sv2n_gat_prep_bwd_node compute, without materialising T.
+ * Replaces lin_src / att_src / att_dst / bias autograd of PyG GATConv
+ * (torch_geometric/nn/conv/gat_conv.py, reference utils/models.py:146).
+ * workspace: sv2n_gat_wgrad_node_workspace floats (no state between calls). */
+int64_t sv2n_gat_wgrad_node_workspace(int64_t num_nodes, int in_features, int ldx, int heads,
+                                      int channels);
+int sv2n_gat_wgrad_node(const float* x, int64_t ld_x, const float* dxs, int ldx,
+                        int64_t num_nodes, int in_features, const float* W,
+                        const float* att_src, const float* att_dst, int heads, int channels,
+                        const float* dbias_partial, int num_parts, int bias_len, float* gW,
+                        float* g_att_src, float* g_att_dst, float* g_bias, float* workspace,
+                        int64_t workspace_floats, hipStream_t stream);
+
 /* Backward of the edge fold: ACCUMULATE gW_edge[h*C+c][d] += dwfold[d][col0+h]·att_edge[h*C+c]
  * and g_att_edge[h*C+c] += Σ_d W_edge[h*C+c][d]·dwfold[d][col0+h]. */
 int sv2n_gat_prep_bwd_edge(const float* dwfold, int hl_pad, int col0,

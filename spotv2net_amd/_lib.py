@@ -52,6 +52,9 @@ _SIGNATURES = {
     "sv2n_gat_prep_fwd": (_i32, [_p, _p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _i32, _p, _i32,
                                  _i32, _p]),
     "sv2n_gat_prep_bwd_workspace": (_i64, [_i32, _i32]),
+    "sv2n_gat_wgrad_node_workspace": (_i64, [_i64, _i32, _i32, _i32, _i32]),
+    "sv2n_gat_wgrad_node": (_i32, [_p, _i64, _p, _i32, _i64, _i32, _p, _p, _p, _i32, _i32, _p,
+                                   _i32, _i32, _p, _p, _p, _p, _p, _i64, _p]),
     "sv2n_gat_prep_bwd_node": (_i32, [_p, _i32, _p, _p, _p, _i32, _i32, _i32, _p, _i32, _i32, _p,
                                       _p, _p, _p, _p, _i64, _p]),
     "sv2n_gat_prep_bwd_edge": (_i32, [_p, _i32, _i32, _p, _p, _i32, _i32, _i32, _p, _p, _p]),

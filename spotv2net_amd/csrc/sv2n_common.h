@@ -76,6 +76,32 @@ __device__ __forceinline__ bool last_block_arrive(unsigned* cnt, unsigned nblock
   return *s_flag != 0;
 }
 
+// Write-through hand-off (cdna_hip_programming.md §6 G16, the split-K recipe's
+// "sc1 slab stores"): data handed to another workgroup of the launch is
+// stored with st_sc1 (agent-scope relaxed atomic store = global_store sc1),
+// every storing wave drains it (s_waitcnt vmcnt(0)) before the block's
+// barrier, one lane takes a relaxed ticket, and the last arriver reads the
+// data ONLY with ld_sc1.  No release / acquire fence: a fence in every block
+// cost 3-4x the whole reduction here.
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool last_block_sc1(unsigned* cnt, unsigned nblocks, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned tk = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = tk == nblocks - 1u;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 // Last-arriving workgroup WITHOUT publication: for when the last arriver
 // reads nothing the others wrote and only needs "everyone is past this
 // point" (e.g. a value every block read at its start may now be replaced).

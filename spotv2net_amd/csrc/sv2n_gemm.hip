@@ -45,6 +45,139 @@ static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t K) {
   return p;
 }
 
+
+// ---------------------------------------------------------------------------
+// Fused weight-gradient epilogue of one GAT layer (the
+// backward of lin_src and of the att_src / att_dst folds, plus the bias).
+// The split-K GEMM's slabs are summed in a fixed order by one contiguous
+// streaming pass (k_splitk_reduce) into T = dWaugᵀ [F][ldt] (ldt = the
+// projection width; columns HC.. hold the fold rows).  One launch of
+// independent blocks then does
+//   tile blocks   gW[o][f]   += T[f][o] + T[f][HC+h]·att_s[o] + T[f][HC+H+h]·att_d[o]
+//                 (16 f x 64 o, transposed through LDS, gW written along f)
+//   att blocks    g_att_s[o] += Σ_f T[f][HC+h] · W[o][f]   (one wave per o,
+//                 same for dst; o = h*C+c)
+//   bias blocks   g_bias[o]  += Σ_b dbias_partial[b][o]
+// with every sum in a fixed order and no hand-off between blocks (tiles
+// summing their att partials through a shared ticket serialised on the
+// counter: 25 us).  Every load is a buffer load (out-of-range offsets read
+// 0): nothing sits behind a branch, each batch is one memory round trip.
+// ---------------------------------------------------------------------------
+constexpr int WG_FT = 16, WG_OT = 64;
+constexpr int WG_FPL = 24;  // f per lane in an att block (F <= 64 * 24 per pass)
+
+__global__ __launch_bounds__(256) void k_wgrad_epi(
+    const float* __restrict__ T, int ldt, const float* __restrict__ W,
+    const float* __restrict__ att_s, const float* __restrict__ att_d, int H, int C, int F,
+    float* __restrict__ gW, float* __restrict__ g_as, float* __restrict__ g_ad, int ntile,
+    int nft, int natt, const float* __restrict__ dbp, int nparts, int OC,
+    float* __restrict__ g_bias) {
+  __shared__ float tile[WG_FT][WG_OT + 1];
+  __shared__ float sfold[WG_FT][2 * SV2N_MAX_HEADS];
+  __shared__ float s_red[16][17];
+  const int HC = H * C;
+  const int t = threadIdx.x;
+  const int b = blockIdx.x;
+  const rsrc_t rt = make_rsrc(T, (uint32_t)F * (uint32_t)ldt * 4u);
+  if (b >= ntile + natt) {  // ---- bias column sums: 16 columns x 16 row groups ----
+    const rsrc_t rb = make_rsrc(dbp, (uint32_t)nparts * (uint32_t)OC * 4u);
+    const int lo = t & 15, grp = t >> 4;
+    const int o = (b - ntile - natt) * 16 + lo;
+    float a = 0.f;
+    for (int q0 = 0; q0 < nparts; q0 += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = q0 + grp + 16 * u;
+        v[u] = bld(rb, (o < OC && q < nparts) ? (q * OC + o) * 4 : OOB);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a += v[u];
+    }
+    s_red[grp][lo] = a;
+    __syncthreads();
+    if (grp == 0 && o < OC) {
+      float sb = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) sb += s_red[k][lo];
+      g_bias[o] += sb;
+    }
+    return;
+  }
+  if (b >= ntile) {  // ---- att grads: one wave per row o ----
+    const int lane = t & 63;
+    const int o = (b - ntile) * 4 + (t >> 6);
+    if (o >= HC) return;
+    const int h = o / C;
+    const rsrc_t rw = make_rsrc(W + (int64_t)o * F, (uint32_t)F * 4u);
+    float as = 0.f, ad = 0.f;
+    for (int f0 = 0; f0 < F; f0 += 64 * WG_FPL) {
+      float w[WG_FPL], gs[WG_FPL], gd[WG_FPL];
+#pragma unroll
+      for (int u = 0; u < WG_FPL; ++u) {
+        const int f = f0 + lane + 64 * u;
+        const bool ok = f < F;
+        w[u] = bld(rw, ok ? f * 4 : OOB);
+        gs[u] = bld(rt, ok ? (f * ldt + HC + h) * 4 : OOB);
+        gd[u] = bld(rt, ok ? (f * ldt + HC + H + h) * 4 : OOB);
+      }
+#pragma unroll
+      for (int u = 0; u < WG_FPL; ++u) {
+        as = fmaf(gs[u], w[u], as);
+        ad = fmaf(gd[u], w[u], ad);
+      }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      as += __shfl_xor(as, m, 64);
+      ad += __shfl_xor(ad, m, 64);
+    }
+    if (lane == 0) {
+      if (g_as) g_as[o] += as;
+      if (g_ad) g_ad[o] += ad;
+    }
+    return;
+  }
+  // ---- gW tile: 16 f x 64 o ----
+  const int ft = b % nft, ot = b / nft;
+  const int f0 = ft * WG_FT, o0 = ot * WG_OT;
+  {
+    const int ol = t & 63, fr = t >> 6;
+    const int o = o0 + ol;
+    constexpr int R = WG_FT / 4;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int f = f0 + fr + 4 * r;
+      tile[fr + 4 * r][ol] = bld(rt, (o < HC && f < F) ? (f * ldt + o) * 4 : OOB);
+    }
+    if (t < WG_FT * 2 * H) {  // 16 x 2H <= 256
+      const int fl = t / (2 * H), k = t - fl * 2 * H;
+      const int f = f0 + fl;
+      sfold[fl][k] = bld(rt, f < F ? (f * ldt + HC + k) * 4 : OOB);
+    }
+  }
+  __syncthreads();
+  const int fl = t & (WG_FT - 1), og = t / WG_FT;  // 256 / WG_FT o-rows per pass
+  const int f = f0 + fl;
+  constexpr int OPP = 256 / WG_FT, Q = WG_OT / OPP;
+  const rsrc_t rg = make_rsrc(gW, (uint32_t)HC * (uint32_t)F * 4u);
+  const rsrc_t ras = make_rsrc(att_s, (uint32_t)HC * 4u), rad = make_rsrc(att_d, (uint32_t)HC * 4u);
+  float gv[Q], av[Q], dv[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {  // all loads first
+    const int o = o0 + og + OPP * q;
+    gv[q] = bld(rg, (o < HC && f < F) ? (o * F + f) * 4 : OOB);
+    av[q] = bld(ras, o < HC ? o * 4 : OOB);
+    dv[q] = bld(rad, o < HC ? o * 4 : OOB);
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int orow = og + OPP * q, o = o0 + orow;
+    const int h = min(o, HC - 1) / C;
+    const float v = gv[q] + (tile[fl][orow] + sfold[fl][h] * av[q] + sfold[fl][H + h] * dv[q]);
+    bst(rg, (o < HC && f < F) ? (o * F + f) * 4 : OOB, v);
+  }
+}
 }  // namespace sv2n
 
 using namespace sv2n;
@@ -103,5 +236,67 @@ extern "C" int sv2n_gemm_f32(int a_kmajor, int b_kmajor, const float* A, int64_t
       dispatch_layout<8, 1>(a_kmajor, b_kmajor, p, stream, A, lda, B, ldb, C, ldc, M, N, K, avec,
                             bvec, part);
   }
+  return (int)hipGetLastError();
+}
+
+// ---- weight gradients of one layer: split-K GEMM + fused epilogue ----------
+static int64_t wgrad_slab_floats(int64_t n_nodes, int F, int ldt) {
+  const GemmPlan p = plan_gemm(F, ldt, n_nodes);
+  return p.splitk > 1 ? (int64_t)p.splitk * F * ldt : 0;
+}
+
+extern "C" int64_t sv2n_gat_wgrad_node_workspace(int64_t num_nodes, int in_features, int ldx,
+                                                 int heads, int channels) {
+  if (num_nodes <= 0 || in_features <= 0 || ldx <= 0 || heads <= 0 || channels <= 0) return 0;
+  return (int64_t)in_features * ldx + wgrad_slab_floats(num_nodes, in_features, ldx);
+}
+
+extern "C" int sv2n_gat_wgrad_node(const float* x, int64_t ld_x, const float* dxs, int ldx,
+                                   int64_t num_nodes, int in_features, const float* W,
+                                   const float* att_src, const float* att_dst, int heads,
+                                   int channels, const float* dbias_partial, int num_parts,
+                                   int bias_len, float* gW, float* g_att_src, float* g_att_dst,
+                                   float* g_bias, float* workspace, int64_t workspace_floats,
+                                   hipStream_t stream) {
+  const bool weights = gW || g_att_src || g_att_dst;
+  const int F = in_features, H = heads, C = channels, HC = heads * channels;
+  if (H < 1 || C < 1 || F < 1 || num_nodes < 1) return SV2N_ERR_ARG;
+  if (H > SV2N_MAX_HEADS || ldx < HC + 2 * H) return SV2N_ERR_SHAPE;
+  if (weights && (!x || !dxs || !W || !att_src || !att_dst)) return SV2N_ERR_ARG;
+  if (weights && ld_x < F) return SV2N_ERR_SHAPE;
+  if ((int64_t)F * ldx >= (int64_t)1 << 29 || (int64_t)HC * F >= (int64_t)1 << 29)
+    return SV2N_ERR_SHAPE;  // 32-bit buffer offsets
+  const bool bias = g_bias && dbias_partial && bias_len > 0 && num_parts > 0;
+  if (!weights && !bias) return 0;
+  if ((int64_t)num_parts * bias_len >= (int64_t)1 << 29) return SV2N_ERR_SHAPE;
+  if (!workspace || workspace_floats < sv2n_gat_wgrad_node_workspace(num_nodes, F, ldx, H, C))
+    return SV2N_ERR_WORKSPACE;
+  float* T = workspace;  // reduced dWaugᵀ [F][ldx]
+  float* slabs = T + (int64_t)F * ldx;
+  if (weights) {
+    // T[f][o] = Σ_k x[k][f] · dxs[k][o]   (both operands k-strided)
+    const GemmPlan p = plan_gemm(F, ldx, num_nodes);
+    const bool avec = ((uintptr_t)x % 16 == 0) && (ld_x % 4 == 0);
+    const bool bvec = ((uintptr_t)dxs % 16 == 0) && (ldx % 4 == 0);
+    float* out = p.splitk > 1 ? slabs : T;
+    if (p.nt == 13)
+      launch_gemm_slabs<8, 1, 13, 16, false, false, 2>(p.splitk, p.kslice, stream, x, ld_x, dxs,
+                                                       ldx, F, ldx, num_nodes, avec, bvec, out);
+    else
+      launch_gemm_slabs<8, 1, 8, 16, false, false, 2>(p.splitk, p.kslice, stream, x, ld_x, dxs,
+                                                      ldx, F, ldx, num_nodes, avec, bvec, out);
+    if (p.splitk > 1) {
+      const int64_t tot = (int64_t)F * ldx;
+      hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                         stream, slabs, p.splitk, (int64_t)F, (int64_t)ldx, T, (int64_t)ldx);
+    }
+  }
+  const int nft = (F + WG_FT - 1) / WG_FT, not_ = (HC + WG_OT - 1) / WG_OT;
+  const int ntile = gW ? nft * not_ : 0;
+  const int natt = (g_att_src || g_att_dst) ? (HC + 3) / 4 : 0;
+  const int nbias = bias ? (bias_len + 15) / 16 : 0;
+  hipLaunchKernelGGL(k_wgrad_epi, dim3((unsigned)(ntile + natt + nbias)), dim3(256), 0, stream, T,
+                     ldx, W, att_src, att_dst, H, C, F, gW, g_att_src, g_att_dst, ntile, nft, natt,
+                     dbias_partial, num_parts, bias_len, g_bias);
   return (int)hipGetLastError();
 }

@@ -313,4 +313,24 @@ inline void launch_gemm_cfg(int splitk, int64_t kslice, hipStream_t st, const fl
   }
 }
 
+// As launch_gemm_cfg, but the K slices stay as slabs part[z][M][N] for a
+// consumer that reduces them itself (splitk == 1 writes slab 0).
+template <int NW, int MT, int NT, int KB, bool AK, bool BK, int PF, int ABL = 0>
+inline void launch_gemm_slabs(int splitk, int64_t kslice, hipStream_t st, const float* A,
+                              int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N,
+                              int64_t K, bool avec, bool bvec, float* part) {
+  using Cfg = GemmCfg<NW, MT, NT, KB, AK, BK, PF>;
+  dim3 grid((unsigned)((M + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN),
+            (unsigned)splitk);
+  const bool av = avec && ((AK ? K : M) % 4 == 0);
+  const bool bv = bvec && ((BK ? K : N) % 4 == 0);
+  float* pp = splitk > 1 ? part : nullptr;
+  if (av && bv)
+    hipLaunchKernelGGL((k_gemm_f32<NW, MT, NT, KB, AK, BK, PF, ABL, true, true>), grid,
+                       dim3(Cfg::THREADS), 0, st, A, lda, B, ldb, part, N, M, N, K, kslice, pp);
+  else
+    hipLaunchKernelGGL((k_gemm_f32<NW, MT, NT, KB, AK, BK, PF, ABL, false, false>), grid,
+                       dim3(Cfg::THREADS), 0, st, A, lda, B, ldb, part, N, M, N, K, kslice, pp);
+}
+
 }  // namespace sv2n

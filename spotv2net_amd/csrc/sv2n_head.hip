@@ -7,7 +7,7 @@
 //   MSE       loss = mean((out - y)²),  dout = 2 (out - y) / (rows·out_ch) · dloss
 // Reductions over rows go through per-workgroup partial slabs summed in a
 // fixed order by the last-arriving workgroup of the same launch
-// (last_block_arrive): deterministic, and no separate reduce launch.
+// (last_block_sc1): deterministic, and no separate reduce launch.
 //
 // Workspace layout (floats): [0, 16) ticket counter (zero before the first
 // call; every launch leaves it zero) | [16, ...) partial slabs.
@@ -102,11 +102,11 @@ __global__ __launch_bounds__(256) void k_head_mse_fwd(
     __syncthreads();
   }
   float* part = ws + HEAD_WS_HDR;
-  if (t == 0) part[blockIdx.x] = s_red[0];
+  if (t == 0) st_sc1(part + blockIdx.x, s_red[0]);
   int* s_flag = reinterpret_cast<int*>(sw);
-  if (last_block_arrive(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
+  if (last_block_sc1(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
     float a = 0.f;
-    for (int k = t; k < (int)gridDim.x; k += 256) a += part[k];
+    for (int k = t; k < (int)gridDim.x; k += 256) a += ld_sc1(part + k);
     s_red[t] = a;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ x, i
     if (t < tot) {
       float s = 0.f;
       for (int g = 0; g < RG; ++g) s += s_grp[g * tot + t];
-      pb[t] = s;
+      st_sc1(pb + t, s);
     }
   } else {
     for (int oc = t; oc < tot; oc += 256) {
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ x, i
       } else {
         for (int r = 0; r < nr; ++r) s += sd[r][o];
       }
-      pb[oc] = s;
+      st_sc1(pb + oc, s);
     }
   }
   // dx rows (coalesced store through the row-major global layout)
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ x, i
   if (!gW && !gb) return;
   int* s_flag = reinterpret_cast<int*>(&sd[0][0]);
   __syncthreads();  // sd no longer needed: reuse one word as the flag
-  if (last_block_arrive(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
+  if (last_block_sc1(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
     const int nparts = gridDim.x;
     for (int base = 0; base < tot; base += 256) {
       const int cols = min(256, tot - base);
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ x, i
       if (t < PG * cols) {
         const int oc = base + t % cols, g = t / cols;
         float s = 0.f;
-        for (int bb = g; bb < nparts; bb += PG) s += part[(int64_t)bb * tot + oc];
+        for (int bb = g; bb < nparts; bb += PG) s += ld_sc1(part + (int64_t)bb * tot + oc);
         s_grp[t] = s;
       }
       __syncthreads();

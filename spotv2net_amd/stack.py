@@ -237,17 +237,17 @@ class _GATStack(torch.autograd.Function):
             gas = _grad_buf(c.att_src)
             gad = _grad_buf(c.att_dst)
             gb = _grad_buf(c.bias)
-            T = None
-            if gW is not None or gas is not None or gad is not None:
-                T = gemm_f32(xs_in[l], False, dxs, False, F, xs.size(1), N)  # dWaugᵀ [F][ldx]
-            if T is not None or gb is not None:
-                ws_n = lib.sv2n_gat_prep_bwd_workspace(Hc, F)
-                ws = torch.empty(ws_n, device=dev, dtype=torch.float32)
-                _lib.check(lib.sv2n_gat_prep_bwd_node(
-                    _lib.ptr(T), xs.size(1), c.lin_src.weight.data_ptr(), c.att_src.data_ptr(),
-                    c.att_dst.data_ptr(), Hc, C, F, dbp.data_ptr(), B, OC, _lib.ptr(gW),
-                    _lib.ptr(gas), _lib.ptr(gad), _lib.ptr(gb), ws.data_ptr(), ws_n, st),
-                    "sv2n_gat_prep_bwd_node")
+            if any(g is not None for g in (gW, gas, gad, gb)):
+                # split-K dWaugᵀ GEMM + one fused epilogue (fold, transpose,
+                # att and bias grads), accumulated into .grad
+                x_l = xs_in[l]
+                ws_n = lib.sv2n_gat_wgrad_node_workspace(N, F, xs.size(1), Hc, C)
+                ws = torch.empty(max(ws_n, 1), device=dev, dtype=torch.float32)
+                _lib.check(lib.sv2n_gat_wgrad_node(
+                    x_l.data_ptr(), x_l.stride(0), dxs.data_ptr(), dxs.stride(0), N, F,
+                    c.lin_src.weight.data_ptr(), c.att_src.data_ptr(), c.att_dst.data_ptr(), Hc, C,
+                    dbp.data_ptr(), B, OC, _lib.ptr(gW), _lib.ptr(gas), _lib.ptr(gad),
+                    _lib.ptr(gb), ws.data_ptr(), ws_n, st), "sv2n_gat_wgrad_node")
             if l > 0 or need_x0:
                 dy = project(dxs, waugs[l], True)  # dxs · Waug
 

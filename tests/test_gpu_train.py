@@ -130,3 +130,53 @@ def test_head_backward_repeatable(dev):
     out.backward(g)
     for n, p in m.named_parameters():
         assert torch.equal(p.grad, 2 * first[n]), n
+
+
+@pytest.mark.parametrize("F,H,C,nodes", [(1260, 4, 100, 15360), (70, 3, 21, 300)])
+def test_fused_wgrad_matches_gemm_and_fold(dev, F, H, C, nodes):
+    """sv2n_gat_wgrad_node (split-K GEMM + fused epilogue) against the
+    unfused sv2n_gemm_f32 + sv2n_gat_prep_bwd_node path it replaces; two
+    accumulating calls, then a bias-only call."""
+    from spotv2net_amd import _lib
+    from spotv2net_amd.ops import gemm_f32
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    HC = H * C
+    ldx = (HC + 2 * H + 3) // 4 * 4
+    x = torch.randn(nodes, F, generator=g).to(dev)
+    dxs = torch.randn(nodes, ldx, generator=g).to(dev)
+    W = torch.randn(HC, F, generator=g).to(dev)
+    a_s = torch.randn(H, C, generator=g).to(dev)
+    a_d = torch.randn(H, C, generator=g).to(dev)
+    B = max(1, nodes // 30)
+    dbp = torch.randn(B, HC, generator=g).to(dev)
+    st = _lib.stream_handle(dev)
+
+    def grads():
+        return [torch.zeros(HC, F, device=dev), torch.zeros(H, C, device=dev),
+                torch.zeros(H, C, device=dev), torch.zeros(HC, device=dev)]
+
+    ref = grads()
+    T = gemm_f32(x, False, dxs, False, F, ldx, nodes)
+    ws_n = lib.sv2n_gat_prep_bwd_workspace(H, F)
+    wsr = torch.empty(ws_n, device=dev)
+    _lib.check(lib.sv2n_gat_prep_bwd_node(T.data_ptr(), ldx, W.data_ptr(), a_s.data_ptr(),
+                                          a_d.data_ptr(), H, C, F, dbp.data_ptr(), B, HC,
+                                          *[r.data_ptr() for r in ref], wsr.data_ptr(), ws_n, st),
+               "prep_bwd_node")
+    got = grads()
+    ws_n = lib.sv2n_gat_wgrad_node_workspace(nodes, F, ldx, H, C)
+    ws = torch.zeros(ws_n, device=dev)
+    for _ in range(2):
+        _lib.check(lib.sv2n_gat_wgrad_node(x.data_ptr(), x.stride(0), dxs.data_ptr(), ldx, nodes,
+                                           F, W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), H, C,
+                                           dbp.data_ptr(), B, HC, *[r.data_ptr() for r in got],
+                                           ws.data_ptr(), ws_n, st), "wgrad_node")
+    torch.cuda.synchronize()
+    for r, o, name in zip(ref, got, ("gW", "g_att_src", "g_att_dst", "g_bias")):
+        assert_close(o, 2 * r, tol=2e-5, what=name)
+    gb = torch.zeros(HC, device=dev)
+    _lib.check(lib.sv2n_gat_wgrad_node(None, 0, None, ldx, nodes, F, None, None, None, H, C,
+                                       dbp.data_ptr(), B, HC, None, None, None, gb.data_ptr(),
+                                       ws.data_ptr(), ws_n, st), "wgrad bias only")
+    assert_close(gb, ref[3], tol=1e-6, what="bias only")
