@@ -305,29 +305,35 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
   }
 }
 
-// out[o] = Σ_b partial[b][o] in a fixed order: a block owns 64 outputs, its
-// four waves sum interleaved quarters of the partials (4 loads in flight per
-// lane), then combine through LDS.
+// out[o] = Σ_b partial[b][o] in a fixed order: a block owns 16 outputs, 16
+// row groups each sum every 16th partial with 8 buffer loads in flight per
+// round (out-of-range offsets read 0), then combine through LDS.
 __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ partial,
                                                          int nparts, int O,
                                                          float* __restrict__ out) {
-  __shared__ float s_red[4][64];
-  const int lo = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int o = blockIdx.x * 64 + lo;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  if (o < O) {
-    int b = grp;
-    for (; b + 12 < nparts; b += 16) {
-      a0 += partial[(int64_t)b * O + o];
-      a1 += partial[(int64_t)(b + 4) * O + o];
-      a2 += partial[(int64_t)(b + 8) * O + o];
-      a3 += partial[(int64_t)(b + 12) * O + o];
+  __shared__ float s_red[16][17];
+  const int lo = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int o = blockIdx.x * 16 + lo;
+  const rsrc_t rp = make_rsrc(partial, (uint32_t)nparts * (uint32_t)O * 4u);
+  float a = 0.f;
+  for (int b0 = 0; b0 < nparts; b0 += 16 * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = b0 + grp + 16 * u;
+      v[u] = bld(rp, (o < O && b < nparts) ? (b * O + o) * 4 : OOB);
     }
-    for (; b < nparts; b += 4) a0 += partial[(int64_t)b * O + o];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a += v[u];
   }
-  s_red[grp][lo] = (a0 + a1) + (a2 + a3);
+  s_red[grp][lo] = a;
   __syncthreads();
-  if (grp == 0 && o < O) out[o] = (s_red[0][lo] + s_red[1][lo]) + (s_red[2][lo] + s_red[3][lo]);
+  if (grp == 0 && o < O) {
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sm += s_red[k][lo];
+    out[o] = sm;
+  }
 }
 
 __global__ void k_block_rowmask(const int64_t* __restrict__ ei, int64_t E, int64_t N, int n,
@@ -602,7 +608,7 @@ static int edge_bwd_small(const float* edge_attr, int64_t num_edges, int edge_di
       case 32: hipLaunchKernelGGL(k_edge_bwd_mfma<32>, dim3(nb), dim3(256), 0, stream, edge_attr, num_edges, edge_dim, col, HL, workspace); break;
       default: return SV2N_ERR_SHAPE;
     }
-    hipLaunchKernelGGL(k_reduce_partials, dim3((O + 63) / 64), dim3(256), 0, stream, workspace,
+    hipLaunchKernelGGL(k_reduce_partials, dim3((O + 15) / 16), dim3(256), 0, stream, workspace,
                        nb, O, dwfold);
     return (int)hipGetLastError();
   }
@@ -614,7 +620,7 @@ static int edge_bwd_small(const float* edge_attr, int64_t num_edges, int edge_di
     col.p[k] = lp.p[k / heads] + (PL ? (int64_t)(k % heads) * num_edges : (int64_t)(k % heads));
   SV2N_SMALL_DISPATCH(k_edge_bwd_small, dim3(nb), edge_attr, num_edges, edge_dim, edge_index,
                       canon, E0, col, num_layers, heads, num_graphs, n, workspace)
-  hipLaunchKernelGGL(k_reduce_partials, dim3((O + 63) / 64), dim3(256), 0, stream, workspace,
+  hipLaunchKernelGGL(k_reduce_partials, dim3((O + 15) / 16), dim3(256), 0, stream, workspace,
                      nb, O, dwfold);
   return (int)hipGetLastError();
 }
@@ -768,7 +774,7 @@ static int edge_bwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
 #undef SV2N_LAUNCH_EB_RF
 #undef SV2N_LAUNCH_EB
 #undef SV2N_LAUNCH_EB2
-  hipLaunchKernelGGL(k_reduce_partials, dim3((O + 63) / 64), dim3(256), 0, stream, workspace,
+  hipLaunchKernelGGL(k_reduce_partials, dim3((O + 15) / 16), dim3(256), 0, stream, workspace,
                      grid, O, dwfold);
   return (int)hipGetLastError();
 }

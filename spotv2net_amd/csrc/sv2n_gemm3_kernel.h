@@ -23,6 +23,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "sv2n_common.h"
 
 namespace sv2n {
 
@@ -44,6 +45,26 @@ __device__ __forceinline__ void split3(float x, unsigned short& h0, unsigned sho
   h1 = bf16_rn(r1);
   const float r2 = r1 - bf16_f(h1);
   h2 = bf16_rn(r2);
+}
+
+// Two elements at once on v_cvt_pk_bf16_f32 (round-to-nearest-even, as
+// bf16_rn): ~5.5 VALU per element instead of ~16 for the integer rounding —
+// the split shares the SIMD's issue slots with the MFMAs (an MFMA 16x16x32
+// leaves 8 of its 16 cycles), so its cost sets the GEMM's rate.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned bf16_pk(float x, float y) {
+  const f32x2_t v = {x, y};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_t));
+}
+// (x, y) -> packed planes p0, p1, p2 (low half = x), x == x0 + x1 + x2 exactly
+__device__ __forceinline__ void split3_pk(float x, float y, unsigned& p0, unsigned& p1,
+                                          unsigned& p2) {
+  p0 = bf16_pk(x, y);
+  const float rx = x - __uint_as_float(p0 << 16), ry = y - __uint_as_float(p0 & 0xffff0000u);
+  p1 = bf16_pk(rx, ry);
+  const float sx = rx - __uint_as_float(p1 << 16), sy = ry - __uint_as_float(p1 & 0xffff0000u);
+  p2 = bf16_pk(sx, sy);
 }
 
 // fp32 [rows][K] (k-contiguous, row stride ld) -> 3 bf16 planes [3][rows][Kp]
@@ -136,17 +157,13 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3(const float* __restrict__ A, 
     for (int s = 0; s < AV; ++s) {
       const int idx = t + TH * s;
       const int r = idx / AC, c4 = idx - r * AC;
-      const float* pv = &ra[set][s].x;
-      unsigned short h[3][4];
+      const float4 v = ra[set][s];
+      uint2 w[3];
+      split3_pk(v.x, v.y, w[0].x, w[1].x, w[2].x);
+      split3_pk(v.z, v.w, w[0].y, w[1].y, w[2].y);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) split3(pv[q], h[0][q], h[1][q], h[2][q]);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        uint2 w;
-        w.x = (unsigned)h[p][0] | ((unsigned)h[p][1] << 16);
-        w.y = (unsigned)h[p][2] | ((unsigned)h[p][3] << 16);
-        *reinterpret_cast<uint2*>(sA + (p * BM + r) * ROW + 4 * c4) = w;
-      }
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<uint2*>(sA + (p * BM + r) * ROW + 4 * c4) = w[p];
     }
 #pragma unroll
     for (int s = 0; s < BV; ++s) {
@@ -360,6 +377,167 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3_t(const float* __restrict__ A
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t gm = m0 + wave * 16 * MT + 16 * a + 4 * lg + r;
+          if (gm < M) C[gm * ldc + gn] = acc[a][b][r];
+        }
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// A-direct variant.  Each wave owns 16*MT rows of A, so A needs no LDS: its
+// fragments (lane: row l&15, k = 8(l>>4) .. +7, two 16-B loads) go from
+// global straight to registers AP k-steps ahead and are split there.  Only
+// the shared B planes are staged through LDS, double-buffered: one barrier
+// per K-step, and the next step's B is written while this step's MFMAs run.
+// Blocks are ordered so the NN column tiles of one row block are dispatched
+// together onto one XCD (id % 8 picks the XCD): they share A through L2.
+// Requires K % 4 == 0, lda % 4 == 0, 16-B aligned A (checked by the caller).
+// ---------------------------------------------------------------------------
+template <int NW, int MT, int NT, int BK>
+struct Gemm3bCfg {
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int BM = 16 * MT * NW, BN = 16 * NT;
+  static constexpr int ROW = BK + 16;  // conflict-free ds_read_b128 (see Gemm3Cfg)
+  static constexpr int BV = (3 * BN * (BK / 8) + THREADS - 1) / THREADS;  // uint4 per thread
+  static constexpr int STAGE = 3 * BN * ROW;                              // bf16 per stage
+  static constexpr size_t LDS = sizeof(unsigned short) * 2 * STAGE;
+};
+
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+// eight elements (two float4) -> the three plane fragments
+__device__ __forceinline__ void split3_frag(const f32x4& lo, const f32x4& hi, bf16x8 (&h)[3]) {
+  u32x4_t w0, w1, w2;
+  unsigned a, b, c;
+  split3_pk(lo[0], lo[1], a, b, c); w0[0] = a; w1[0] = b; w2[0] = c;
+  split3_pk(lo[2], lo[3], a, b, c); w0[1] = a; w1[1] = b; w2[1] = c;
+  split3_pk(hi[0], hi[1], a, b, c); w0[2] = a; w1[2] = b; w2[2] = c;
+  split3_pk(hi[2], hi[3], a, b, c); w0[3] = a; w1[3] = b; w2[3] = c;
+  h[0] = __builtin_bit_cast(bf16x8, w0);
+  h[1] = __builtin_bit_cast(bf16x8, w1);
+  h[2] = __builtin_bit_cast(bf16x8, w2);
+}
+
+template <int NW, int MT, int NT, int BK, int AP>
+__global__ __launch_bounds__(64 * NW) void k_gemm3b(const float* __restrict__ A, int64_t lda,
+                                                    const unsigned short* __restrict__ Bp,
+                                                    int64_t ldb, int64_t bplane,
+                                                    float* __restrict__ C, int64_t ldc, int64_t M,
+                                                    int64_t N, int64_t K, int nm, int nn) {
+  using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
+  constexpr int TH = Cfg::THREADS, BM = Cfg::BM, BN = Cfg::BN, ROW = Cfg::ROW, BV = Cfg::BV;
+  constexpr int STAGE = Cfg::STAGE, BC = BK / 8, KS = BK / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  // XCD-grouped block order: id = q*8*nn + n*8 + r  ->  row block q*8 + r, column block n
+  const int id = blockIdx.x;
+  const int q = id / (8 * nn), rem = id - q * 8 * nn;
+  const int nb = rem >> 3, mb = q * 8 + (rem & 7);
+  if (mb >= nm) return;
+  const int64_t m0 = (int64_t)mb * BM, n0 = (int64_t)nb * BN;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // A: rows of this wave through a buffer descriptor (rows >= M read 0)
+  const int64_t arow0 = m0 + (int64_t)wave * 16 * MT;
+  const int64_t arows = M - arow0;
+  const rsrc_t ra_src = make_rsrc(A + (arow0 > M ? 0 : arow0 * lda),
+                                  arows > 0 ? (uint32_t)(min(arows, (int64_t)16 * MT) * lda * 4) : 0u);
+  f32x4 ra[AP][MT][KS][2];
+  auto load_a = [&](int set, int64_t k0) {
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int hv = 0; hv < 2; ++hv) {
+          const int64_t k = k0 + 32 * ks + 8 * lg + 4 * hv;
+          const int off = k < K ? (int)(((16 * a + li) * lda + k) * 4) : OOB;
+          ra[set][a][ks][hv] = bld4(ra_src, off);
+        }
+  };
+  // B planes: [3][N][ldb] bf16, rows >= N clamped (never stored)
+  uint4 rb[BV];
+  auto load_b = [&](int64_t k0) {
+#pragma unroll
+    for (int sv = 0; sv < BV; ++sv) {
+      const int idx = t + TH * sv;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (idx < 3 * BN * BC) {
+        const int p = idx / (BN * BC), r2 = idx - p * BN * BC;
+        const int r = r2 / BC, c = r2 - r * BC;
+        const int64_t gn = min(n0 + r, N - 1);
+        v = *reinterpret_cast<const uint4*>(Bp + p * bplane + gn * ldb + k0 + 8 * c);
+      }
+      rb[sv] = v;
+    }
+  };
+  auto store_b = [&](unsigned short* sB) {
+#pragma unroll
+    for (int sv = 0; sv < BV; ++sv) {
+      const int idx = t + TH * sv;
+      if (idx < 3 * BN * BC) {
+        const int p = idx / (BN * BC), r2 = idx - p * BN * BC;
+        const int r = r2 / BC, c = r2 - r * BC;
+        *reinterpret_cast<uint4*>(sB + (p * BN + r) * ROW + 8 * c) = rb[sv];
+      }
+    }
+  };
+
+  const int nk = (int)((K + BK - 1) / BK);
+#pragma unroll
+  for (int s = 0; s < AP; ++s)
+    if (s < nk) load_a(s, (int64_t)s * BK);
+  load_b(0);
+  store_b(lds);
+  if (nk > 1) load_b(BK);
+  __syncthreads();
+  for (int s = 0; s < nk; ++s) {
+    const unsigned short* sB = lds + (s & 1) * STAGE;
+    const int set = s % AP;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 af[MT][3];
+#pragma unroll
+      for (int a = 0; a < MT; ++a) split3_frag(ra[set][a][ks][0], ra[set][a][ks][1], af[a]);
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        bf16x8 bf[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bf[p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + 16 * b + li) * ROW + 32 * ks +
+                                                   8 * lg);
+#pragma unroll
+        for (int a = 0; a < MT; ++a) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][2], bf[0], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][1], bf[1], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[2], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][1], bf[0], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[1], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[0], acc[a][b], 0, 0, 0);
+        }
+      }
+    }
+    if (s + AP < nk) load_a(set, (int64_t)(s + AP) * BK);
+    if (s + 1 < nk) {
+      store_b(lds + ((s + 1) & 1) * STAGE);
+      if (s + 2 < nk) load_b((int64_t)(s + 2) * BK);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int64_t gn = n0 + 16 * b + li;
+      if (gn < N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t gm = arow0 + 16 * a + 4 * lg + r;
           if (gm < M) C[gm * ldc + gn] = acc[a][b][r];
         }
       }

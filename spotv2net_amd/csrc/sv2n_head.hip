@@ -19,16 +19,47 @@ constexpr int HEAD_MAX_OUT = 16;
 constexpr int HEAD_ROWS = 256;  // rows per workgroup (one per thread)
 constexpr int HEAD_WS_HDR = 16;
 
-// x rows staged through LDS so the global reads are coalesced
+// x rows staged through LDS so the global reads are coalesced.  The block's
+// rows are one contiguous span of nr*C floats: it is read as 16-B buffer
+// loads, 8 per thread in flight per round (a plain element loop of
+// load -> LDS store is not pipelined by the compiler: one round trip per
+// element), then scattered into the padded [row][C+1] image.
 template <int OUT>
 __device__ __forceinline__ void head_rows(const float* __restrict__ x, int64_t r0, int nr, int C,
                                           float* __restrict__ sx, const float* __restrict__ W,
                                           float* __restrict__ sw, int t) {
   const int CP = C + 1;
   for (int k = t; k < OUT * C; k += 256) sw[k] = W[k];
-  for (int k = t; k < nr * C; k += 256) {
-    const int r = k / C;
-    sx[r * CP + (k - r * C)] = x[r0 * C + k];
+  const int n = nr * C;
+  const float* base = x + r0 * C;
+  if ((((uintptr_t)base) & 15) == 0) {
+    const rsrc_t rx = make_rsrc(base, (uint32_t)n * 4u);
+    const int nv = (n + 3) >> 2;
+    for (int v0 = 0; v0 < nv; v0 += 8 * 256) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = v0 + t + 256 * u;
+        v[u] = bld4(rx, q < nv ? q * 16 : OOB);  // tail floats past n read 0
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = v0 + t + 256 * u;
+        if (q < nv) {
+          int e = 4 * q, r = e / C, c = e - r * C;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (e + k < n) sx[r * CP + c] = v[u][k];
+            if (++c == C) { c = 0; ++r; }
+          }
+        }
+      }
+    }
+  } else {
+    for (int k = t; k < n; k += 256) {
+      const int r = k / C;
+      sx[r * CP + (k - r * C)] = base[k];
+    }
   }
 }
 

@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "../spotv2net_amd/csrc/sv2n_common.h"
 #include "../spotv2net_amd/csrc/sv2n_gemm3_kernel.h"
 #include "../spotv2net_amd/csrc/sv2n_gemm_kernel.h"
 
@@ -88,8 +89,52 @@ void run3(const Shape& sh, hipStream_t st, const float* A, const unsigned short*
   fflush(stdout);
 }
 
+template <int NW, int MT, int NT, int BK, int AP>
+void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short* Bp, int64_t Kp,
+           float* C, const std::vector<double>& ref, const std::vector<double>& absr) {
+  using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
+  const size_t lds = Cfg::LDS;
+  if (lds > 160 * 1024) return;
+  auto kern = k_gemm3b<NW, MT, NT, BK, AP>;
+  if (lds > 65536)
+    CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  const int nm = (int)((sh.M + Cfg::BM - 1) / Cfg::BM), nn = (int)((sh.N + Cfg::BN - 1) / Cfg::BN);
+  const unsigned grid = (unsigned)(((nm + 7) / 8) * 8 * nn);
+  CK(hipMemset(C, 0, sizeof(float) * sh.M * sh.N));
+  auto f = [&]() {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(Cfg::THREADS), lds, st, A, sh.K, Bp, Kp, sh.N * Kp,
+                       C, sh.N, sh.M, sh.N, sh.K, nm, nn);
+  };
+  f();
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(st));
+  std::vector<float> out(sh.M * sh.N);
+  CK(hipMemcpy(out.data(), C, sizeof(float) * out.size(), hipMemcpyDeviceToHost));
+  double maxrel = 0, maxabs = 0;
+  for (size_t i = 0; i < out.size(); i += 7) {
+    const double e = fabs(out[i] - ref[i]);
+    maxabs = fmax(maxabs, e);
+    maxrel = fmax(maxrel, e / (absr[i] + 1e-30));
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int reps = 20;
+  CK(hipEventRecord(e0, st));
+  for (int r = 0; r < reps; ++r) f();
+  CK(hipEventRecord(e1, st));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / reps;
+  printf("  gemm3b NW%d MT%d NT%-2d BK%d AP%d %8.1f us %7.1f TF(f32-eq)  max|err| %.2e  max err/S|ab| %.2e\n",
+         NW, MT, NT, BK, AP, us, 2.0 * sh.M * sh.N * sh.K / us / 1e6, maxabs, maxrel);
+  fflush(stdout);
+}
+
 int main() {
-  std::vector<Shape> shapes = {{"fwd L0", 15360, 408, 1260}, {"fwd L1", 15360, 208, 400}};
+  std::vector<Shape> shapes = {{"fwd L0", 15360, 408, 1260}, {"fwd L1", 15360, 208, 400},
+                               {"dX L1", 15360, 400, 208}};
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (auto& sh : shapes) {
@@ -142,16 +187,14 @@ int main() {
       printf("  f32 MFMA NT13     %8.1f us %7.1f TF          max|err| %.2e  max err/Σ|ab| %.2e\n", us,
              2.0 * M * N * K / us / 1e6, maxabs, maxrel);
     }
-    run3<4, 1, 13, 32, 1>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3<4, 1, 13, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3<8, 1, 13, 32, 1>(sh, st, A, Bp, Kp, C, ref, absr);
     run3<8, 1, 13, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3<8, 1, 13, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3<4, 2, 13, 32, 1>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3<8, 2, 13, 32, 1>(sh, st, A, Bp, Kp, C, ref, absr);
     run3<8, 1, 7, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3<8, 2, 7, 32, 1>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3<4, 2, 7, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 13, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 13, 32, 3>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<4, 2, 13, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 7, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 2, 7, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<4, 1, 13, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(S)); CK(hipFree(Bp));
   }
   return 0;
