@@ -32,6 +32,9 @@ sys.path.insert(0, ROOT)
 METRIC = "graphs/sec (30-node dense GAT, batch=512) at 1/2/4/8 MI355X vs PyG-CPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32, dense
+# the split GEMM computes each f32 product as 6 bf16 MFMA products: its
+# f32-equivalent ceiling is the dense bf16 MFMA peak (~2.5 PF) / 6
+BF16X3_PEAK_TFLOPS = round(2500.0 / 6, 1)
 
 S, N_NODES, HEADS, HIDDEN, BATCH = 42, 30, 4, [100, 50], 512
 
@@ -143,26 +146,43 @@ def kernel_table(model, data, reps=50):
                                  dwf.data_ptr(), hp, sh)
 
     out0 = torch.empty_like(xs0)
+    # the layer-0 projection as the step runs it: the f32-accurate split GEMM
+    # (sv2n_gemm_f32x3) on the weight's pre-split bf16 planes
+    planes0 = ops.weight_planes(W[0], False)
 
     def gemm_fwd():
-        ops.gemm_f32(x0, True, W[0], True, N0, W[0].shape[0], x0.shape[1], out=out0)
+        lib.sv2n_gemm_f32x3(x0.data_ptr(), x0.stride(0), planes0.data_ptr(), out0.data_ptr(),
+                            out0.stride(0), N0, W[0].shape[0], x0.shape[1], sh)
+
+    # the layer-0 weight-gradient GEMM (split-K f32 MFMA; its slab reduce and
+    # epilogue are separate launches of sv2n_gat_wgrad_node)
+    Fd, Nd = x0.shape[1], W[0].shape[0]
+    nslab = lib.sv2n_gemm_f32_slabs_count(Fd, Nd, N0)
+    slabs = torch.empty(nslab * Fd * Nd, device=dev)
 
     def gemm_dwt():
-        ops.gemm_f32(x0, False, dxs0, False, x0.shape[1], W[0].shape[0], N0)
+        lib.sv2n_gemm_f32_slabs(0, 0, x0.data_ptr(), x0.stride(0), dxs0.data_ptr(),
+                                dxs0.stride(0), Fd, Nd, N0, slabs.data_ptr(), slabs.numel(), sh)
 
     M0, N0c, K0 = N0, W[0].shape[0], x0.shape[1]
+    # (fn, bound, algorithmic flops, algorithmic bytes, peak for the arithmetic used)
     rows = {
-        "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * N0c * K0, 4.0 * (M0 * K0 + N0c * K0 + M0 * N0c)),
-        "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * N0c * K0, 4.0 * (M0 * K0 + M0 * N0c + N0c * K0)),
-        "edge_logits_fwd": (edge_fwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS)),
-        "edge_logits_bwd": (edge_bwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS)),
+        "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * N0c * K0,
+                        4.0 * (M0 * K0 + N0c * K0 + M0 * N0c), BF16X3_PEAK_TFLOPS),
+        "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * N0c * K0,
+                        4.0 * (M0 * K0 + M0 * N0c + N0c * K0), F32_MFMA_PEAK_TFLOPS),
+        "edge_logits_fwd": (edge_fwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS),
+                            None),
+        "edge_logits_bwd": (edge_bwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS),
+                            None),
         "gat_attn_fwd_l0": (attn_fwd, "hbm", 2.0 * B * N_NODES * N_NODES * HEADS * conv0.out_channels,
-                            4.0 * (xs0.numel() + ae[0].numel() + y0.numel() + ps0.numel())),
+                            4.0 * (xs0.numel() + ae[0].numel() + y0.numel() + ps0.numel()), None),
         "gat_attn_bwd_l0": (attn_bwd, "hbm", 4.0 * B * N_NODES * N_NODES * HEADS * conv0.out_channels,
-                            4.0 * (2 * y0.numel() + 2 * xs0.numel() + 2 * ps0.numel() + ae[0].numel())),
+                            4.0 * (2 * y0.numel() + 2 * xs0.numel() + 2 * ps0.numel() + ae[0].numel()),
+                            None),
     }
     res = {}
-    for name, (fn, bound, flops, nbytes) in rows.items():
+    for name, (fn, bound, flops, nbytes, peak) in rows.items():
         for _ in range(3):
             fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -173,7 +193,7 @@ def kernel_table(model, data, reps=50):
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / reps
         res[name] = dict(avg_us=us, bound=bound, flops=flops, bytes=nbytes,
-                         tflops=flops / us / 1e6, gbs=nbytes / us / 1e3)
+                         tflops=flops / us / 1e6, gbs=nbytes / us / 1e3, peak_tflops=peak)
     return res
 
 
@@ -182,7 +202,7 @@ def roofline_entry(table, traffic=None):
     name = max(table, key=lambda k: table[k]["avg_us"])
     r = table[name]
     if r["bound"] == "mfma":
-        ach, peak, unit = r["tflops"], F32_MFMA_PEAK_TFLOPS, "TFLOP/s"
+        ach, peak, unit = r["tflops"], r.get("peak_tflops") or F32_MFMA_PEAK_TFLOPS, "TFLOP/s"
     else:
         ach, peak, unit = r["gbs"], HBM_PEAK_GBS, "GB/s"
     return name, {"kernel": name, "bound": r["bound"], "achieved": round(ach, 2), "peak": peak,
@@ -336,7 +356,8 @@ def main():
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv)
                             for kk, vv in v.items() if kk in ("avg_us", "tflops", "gbs", "bound")}
                         for k, v in table.items()},
-            "peaks_assumed": {"hbm_GBs": HBM_PEAK_GBS, "f32_mfma_TFLOPs": F32_MFMA_PEAK_TFLOPS},
+            "peaks_assumed": {"hbm_GBs": HBM_PEAK_GBS, "f32_mfma_TFLOPs": F32_MFMA_PEAK_TFLOPS,
+                              "bf16x3_f32eq_TFLOPs": BF16X3_PEAK_TFLOPS},
         }
         print(json.dumps(result), flush=True)
     if world > 1:

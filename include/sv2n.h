@@ -68,6 +68,8 @@ extern "C" {
 #define SV2N_MAX_N_TILED 256 /* nodes per graph on the tiled attention path
                                (sv2n_gat_attn_tiled_*) and the edge pass   */
 #define SV2N_MAX_HEADS 8    /* attention heads per layer                   */
+#define SV2N_TICKET_WORDS 288 /* counter words of a two-level in-launch ticket
+                                 (Adam counter, head workspace header)     */
 
 /* argument errors (negative return codes) */
 #define SV2N_ERR_ARG       (-1)  /* null pointer / non-positive size        */
@@ -172,6 +174,28 @@ int sv2n_gat_prep_fwd(const float* W, const float* att_src, const float* att_dst
                       const float* W_edge, const float* att_edge, int edge_dim,
                       float* wfold, int hl_pad, int col0, hipStream_t stream);
 
+/* All layers' weight preparation in ONE launch: per layer what
+ * sv2n_gat_prep_fwd writes (waug, wfold columns), plus the bf16 split planes
+ * the f32-accurate GEMM (sv2n_gemm_f32x3) consumes:
+ *   planes  [3][ldx][kp]  = split3(waug)        (B of xs = x · waugᵀ; kp = sv2n_split3_kpad(F))
+ *   planesT [3][F][kpt]   = split3(waugᵀ)       (B of dx = dxs · waug; kpt = sv2n_split3_kpad(ldx)),
+ *                                               skipped when NULL
+ * i.e. sv2n_gat_prep_fwd + sv2n_split3 (+ transposed) per layer, fused. */
+typedef struct sv2n_prep_layer {
+  const float* W;         /* lin_src.weight [H*C][F] */
+  const float* att_src;   /* [H*C] */
+  const float* att_dst;   /* [H*C] */
+  int heads, channels, in_features, ldx;
+  float* waug;            /* [ldx][F] */
+  uint16_t* planes;       /* [3][ldx][kp] */
+  uint16_t* planes_t;     /* [3][F][kpt] or NULL */
+  const float* W_edge;    /* lin_edge.weight [H*C][edge_dim] or NULL */
+  const float* att_edge;  /* [H*C] */
+  int edge_dim, hl_pad, col0;
+  float* wfold;           /* [edge_dim][hl_pad] */
+} sv2n_prep_layer;
+int sv2n_gat_prep_fwd_all(const sv2n_prep_layer* layers, int num_layers, hipStream_t stream);
+
 /* Backward of the node half of sv2n_gat_prep_fwd plus the bias: from
  * dwaug_t = dWaugᵀ [F][ldx] ACCUMULATE (+=) into gW [H*C][F], g_att_src /
  * g_att_dst [H*C] and g_bias[o] += Σ_b dbias_partial[b][o] (any output NULL
@@ -185,6 +209,15 @@ int sv2n_gat_prep_bwd_node(const float* dwaug_t, int ldx, const float* W,
                            int num_parts, int bias_len, float* gW, float* g_att_src,
                            float* g_att_dst, float* g_bias, float* workspace,
                            int64_t workspace_floats, hipStream_t stream);
+
+/* The split-K f32 GEMM of sv2n_gemm_f32 alone: C's K slices are left as
+ * slabs [count][M][N] (count = sv2n_gemm_f32_slabs_count(M, N, K); a single
+ * slice writes slab 0 = C).  The caller sums them (fixed order, as the
+ * library's reduce does). */
+int sv2n_gemm_f32_slabs_count(int64_t M, int64_t N, int64_t K);
+int sv2n_gemm_f32_slabs(int a_kmajor, int b_kmajor, const float* A, int64_t lda, const float* B,
+                        int64_t ldb, int64_t M, int64_t N, int64_t K, float* slabs,
+                        int64_t slab_floats, hipStream_t stream);
 
 /* Weight gradients of one GAT layer in two launches: the split-K GEMM
  *   T = dWaugᵀ[f][o] = Σ_k x[k][f] · dxs[k][o]        (x [num_nodes][ld_x], dxs [num_nodes][ldx])
@@ -219,8 +252,8 @@ int sv2n_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_av
 
 /* Adam step that also advances the device step counter (t = *step + 1 is used
  * and stored) and zeroes grad after reading it (the next backward accumulates
- * into zeros).  counter: one uint32 ticket, zero before the first call (left
- * zero by every call). */
+ * into zeros).  counter: SV2N_TICKET_WORDS uint32 ticket words (two-level
+ * tickets), zero before the first call (left zero by every call). */
 int sv2n_adam_f32_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                        float* step, uint32_t* counter, float lr, float beta1, float beta2,
                        float eps, float weight_decay, hipStream_t stream);
@@ -230,8 +263,9 @@ int sv2n_adam_f32_step(float* param, float* grad, float* exp_avg, float* exp_avg
  * in_features <= 128, out_features <= 16.  The backward writes dx and
  * ACCUMULATES into g_weight / g_bias (either may be NULL).
  * workspace: sv2n_head_bwd_workspace(rows, in, out) floats, 16-B aligned; its
- * first 16 floats are a ticket counter that must be zero before the first
- * call (every call leaves it zero), the rest per-workgroup partial slabs
+ * first SV2N_TICKET_WORDS (288) floats are ticket counters that must be zero
+ * before the first call (every call leaves them zero), the rest per-workgroup
+ * partial slabs
  * reduced in a fixed order inside the launch (deterministic). */
 int sv2n_head_fwd(const float* x, int64_t num_rows, int in_features, const float* weight,
                   const float* bias, int out_features, float* out, hipStream_t stream);

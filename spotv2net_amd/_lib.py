@@ -22,6 +22,18 @@ _i64 = ctypes.c_int64
 _i32 = ctypes.c_int
 _f32 = ctypes.c_float
 
+class PrepLayer(ctypes.Structure):
+    """sv2n_prep_layer (include/sv2n.h)."""
+    _fields_ = [
+        ("W", _p), ("att_src", _p), ("att_dst", _p),
+        ("heads", _i32), ("channels", _i32), ("in_features", _i32), ("ldx", _i32),
+        ("waug", _p), ("planes", _p), ("planes_t", _p),
+        ("W_edge", _p), ("att_edge", _p),
+        ("edge_dim", _i32), ("hl_pad", _i32), ("col0", _i32),
+        ("wfold", _p),
+    ]
+
+
 # name -> (restype, argtypes); mirrors include/sv2n.h
 _SIGNATURES = {
     "sv2n_abi_version": (_i32, []),
@@ -47,11 +59,14 @@ _SIGNATURES = {
     "sv2n_split3": (_i32, [_p, _i64, _i64, _i64, _i32, _p, _p]),
     "sv2n_gemm_f32x3": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "sv2n_gemm_f32_workspace": (_i64, [_i64, _i64, _i64]),
+    "sv2n_gemm_f32_slabs_count": (_i32, [_i64, _i64, _i64]),
+    "sv2n_gemm_f32_slabs": (_i32, [_i32, _i32, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "sv2n_gemm_f32": (_i32, [_i32, _i32, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "sv2n_block_rowmask": (_i32, [_p, _i64, _i64, _i32, _p, _p]),
     "sv2n_gat_prep_fwd": (_i32, [_p, _p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _i32, _p, _i32,
                                  _i32, _p]),
     "sv2n_gat_prep_bwd_workspace": (_i64, [_i32, _i32]),
+    "sv2n_gat_prep_fwd_all": (_i32, [_p, _i32, _p]),
     "sv2n_gat_wgrad_node_workspace": (_i64, [_i64, _i32, _i32, _i32, _i32]),
     "sv2n_gat_wgrad_node": (_i32, [_p, _i64, _p, _i32, _i64, _i32, _p, _p, _p, _i32, _i32, _p,
                                    _i32, _i32, _p, _p, _p, _p, _p, _i64, _p]),

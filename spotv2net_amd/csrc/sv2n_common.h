@@ -102,6 +102,36 @@ __device__ __forceinline__ bool last_block_sc1(unsigned* cnt, unsigned nblocks, 
   return *s_flag != 0;
 }
 
+// Two-level tickets: same-address atomics serialise at L2 (a launch's blocks
+// all finish together), so block b first takes a ticket on group counter
+// b % 8, and only the last of each group on the top counter — ~nblocks/8 + 8
+// serialised atomics instead of nblocks.  Counter words are SV2N_TICKET_STRIDE
+// apart (their own 128-B lines): cnt[0] top, cnt[(1 + g) * stride] group g.
+// All must be zero before the first launch; the last arrivers reset them.
+#define SV2N_TICKET_STRIDE 32
+static_assert(SV2N_TICKET_WORDS == 9 * SV2N_TICKET_STRIDE, "sv2n.h ticket size");
+__device__ __forceinline__ bool ticket2_lane0(unsigned* cnt, unsigned nblocks) {
+  const unsigned g = blockIdx.x & 7u;
+  const unsigned groups = nblocks < 8u ? nblocks : 8u;
+  const unsigned members = (nblocks - g + 7u) / 8u;
+  unsigned* gc = cnt + (1 + g) * SV2N_TICKET_STRIDE;
+  const unsigned tk = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tk != members - 1u) return false;
+  __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned t2 = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t2 != groups - 1u) return false;
+  __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+// last_block_sc1 with two-level tickets (cnt: SV2N_TICKET_WORDS words)
+__device__ __forceinline__ bool last_block_sc1_2(unsigned* cnt, unsigned nblocks, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) *s_flag = ticket2_lane0(cnt, nblocks);
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 // Last-arriving workgroup WITHOUT publication: for when the last arriver
 // reads nothing the others wrote and only needs "everyone is past this
 // point" (e.g. a value every block read at its start may now be replaced).
@@ -114,6 +144,14 @@ __device__ __forceinline__ bool last_block_ticket(unsigned* cnt, unsigned nblock
     if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *s_flag = last;
   }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// last_block_ticket with two-level tickets (cnt: SV2N_TICKET_WORDS words)
+__device__ __forceinline__ bool last_block_ticket2(unsigned* cnt, unsigned nblocks, int* s_flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) *s_flag = ticket2_lane0(cnt, nblocks);
   __syncthreads();
   return *s_flag != 0;
 }

@@ -239,6 +239,41 @@ extern "C" int sv2n_gemm_f32(int a_kmajor, int b_kmajor, const float* A, int64_t
   return (int)hipGetLastError();
 }
 
+// ---- the split-K GEMM alone: C's K slices left as slabs [nsplit][M][N] ------
+// (what sv2n_gat_wgrad_node runs before its reduce; exposed for consumers that
+// fuse the reduction, and so the kernel can be timed by itself)
+extern "C" int sv2n_gemm_f32_slabs_count(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  return plan_gemm(M, N, K).splitk;
+}
+
+extern "C" int sv2n_gemm_f32_slabs(int a_kmajor, int b_kmajor, const float* A, int64_t lda,
+                                   const float* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                                   float* slabs, int64_t slab_floats, hipStream_t stream) {
+  if (!A || !B || !slabs || M <= 0 || N <= 0 || K <= 0) return SV2N_ERR_ARG;
+  if (lda < (a_kmajor ? K : M) || ldb < (b_kmajor ? K : N)) return SV2N_ERR_SHAPE;
+  const GemmPlan p = plan_gemm(M, N, K);
+  if (slab_floats < (int64_t)p.splitk * M * N) return SV2N_ERR_WORKSPACE;
+  const bool avec = ((uintptr_t)A % 16 == 0) && (lda % 4 == 0);
+  const bool bvec = ((uintptr_t)B % 16 == 0) && (ldb % 4 == 0);
+#define SV2N_SLABS(NT, AK, BK)                                                                    \
+  launch_gemm_slabs<8, 1, NT, 16, AK, BK, 2>(p.splitk, p.kslice, stream, A, lda, B, ldb, M, N, K, \
+                                             avec, bvec, slabs)
+  if (p.nt == 13) {
+    if (a_kmajor && b_kmajor) SV2N_SLABS(13, true, true);
+    else if (a_kmajor) SV2N_SLABS(13, true, false);
+    else if (b_kmajor) SV2N_SLABS(13, false, true);
+    else SV2N_SLABS(13, false, false);
+  } else {
+    if (a_kmajor && b_kmajor) SV2N_SLABS(8, true, true);
+    else if (a_kmajor) SV2N_SLABS(8, true, false);
+    else if (b_kmajor) SV2N_SLABS(8, false, true);
+    else SV2N_SLABS(8, false, false);
+  }
+#undef SV2N_SLABS
+  return (int)hipGetLastError();
+}
+
 // ---- weight gradients of one layer: split-K GEMM + fused epilogue ----------
 static int64_t wgrad_slab_floats(int64_t n_nodes, int F, int ldt) {
   const GemmPlan p = plan_gemm(F, ldt, n_nodes);

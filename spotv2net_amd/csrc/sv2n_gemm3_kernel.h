@@ -68,7 +68,7 @@ __device__ __forceinline__ void split3_pk(float x, float y, unsigned& p0, unsign
 }
 
 // fp32 [rows][K] (k-contiguous, row stride ld) -> 3 bf16 planes [3][rows][Kp]
-__global__ void k_split3(const float* __restrict__ x, int64_t rows, int64_t K, int64_t ld,
+static __global__ __attribute__((unused)) void k_split3(const float* __restrict__ x, int64_t rows, int64_t K, int64_t ld,
                          unsigned short* __restrict__ out, int64_t Kp) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= rows * Kp) return;

@@ -7,9 +7,9 @@
 //   MSE       loss = mean((out - y)²),  dout = 2 (out - y) / (rows·out_ch) · dloss
 // Reductions over rows go through per-workgroup partial slabs summed in a
 // fixed order by the last-arriving workgroup of the same launch
-// (last_block_sc1): deterministic, and no separate reduce launch.
+// (last_block_sc1_2): deterministic, and no separate reduce launch.
 //
-// Workspace layout (floats): [0, 16) ticket counter (zero before the first
+// Workspace layout (floats): [0, 288) ticket counters (zero before the first
 // call; every launch leaves it zero) | [16, ...) partial slabs.
 #include "sv2n_common.h"
 
@@ -17,7 +17,7 @@ namespace sv2n {
 
 constexpr int HEAD_MAX_OUT = 16;
 constexpr int HEAD_ROWS = 256;  // rows per workgroup (one per thread)
-constexpr int HEAD_WS_HDR = 16;
+constexpr int HEAD_WS_HDR = SV2N_TICKET_WORDS;  // two-level ticket counters
 
 // x rows staged through LDS so the global reads are coalesced.  The block's
 // rows are one contiguous span of nr*C floats: it is read as 16-B buffer
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void k_head_mse_fwd(
   float* part = ws + HEAD_WS_HDR;
   if (t == 0) st_sc1(part + blockIdx.x, s_red[0]);
   int* s_flag = reinterpret_cast<int*>(sw);
-  if (last_block_sc1(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
+  if (last_block_sc1_2(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
     float a = 0.f;
     for (int k = t; k < (int)gridDim.x; k += 256) a += ld_sc1(part + k);
     s_red[t] = a;
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ x, i
   if (!gW && !gb) return;
   int* s_flag = reinterpret_cast<int*>(&sd[0][0]);
   __syncthreads();  // sd no longer needed: reuse one word as the flag
-  if (last_block_sc1(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
+  if (last_block_sc1_2(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
     const int nparts = gridDim.x;
     for (int base = 0; base < tot; base += 256) {
       const int cols = min(256, tot - base);

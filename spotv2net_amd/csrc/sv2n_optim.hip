@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __re
   }
   // every block read *step at its start; once all have taken a ticket the
   // last one may advance it (nothing else is handed over: no fences)
-  if (STEP && last_block_ticket(cnt, gridDim.x, &s_flag) && threadIdx.x == 0) *step = t;
+  if (STEP && last_block_ticket2(cnt, gridDim.x, &s_flag) && threadIdx.x == 0) *step = t;
 }
 
 }  // namespace sv2n

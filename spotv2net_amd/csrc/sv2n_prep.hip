@@ -15,6 +15,7 @@
 //   g_att_edge[h,c] += Σ_d W_e[hC+c][d] · dwfold[d][col0+h]
 //   g_bias[o]     += Σ_g dbias_partial[g][o]
 #include "sv2n_common.h"
+#include "sv2n_gemm3_kernel.h"
 
 namespace sv2n {
 
@@ -193,6 +194,167 @@ __global__ __launch_bounds__(256) void k_colsum_accum(const float* __restrict__ 
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// All layers in one launch (sv2n_gat_prep_fwd_all).  Two kinds of blocks,
+// none depending on another:
+//   P blocks (layer, 64 columns f, head or edge head): k_prep_fwd's work,
+//     plus the bf16 planes of every waug row they write (columns up to kp,
+//     zero past F);
+//   T blocks (layer, 32 f x 32 o tile): the transposed planes planesT[f][o]
+//     = split3(waug[o][f]), the fold rows recomputed from W in k_prep_fwd's
+//     summation order (bit-identical to waug), transposed through LDS.
+// ---------------------------------------------------------------------------
+struct PrepAllArgs {
+  sv2n_prep_layer l[SV2N_MAX_LAYERS];
+  int64_t kp[SV2N_MAX_LAYERS], kpt[SV2N_MAX_LAYERS];
+  int px[SV2N_MAX_LAYERS];       // P blocks along columns
+  int pstart[SV2N_MAX_LAYERS];   // first P block of the layer
+  int tf[SV2N_MAX_LAYERS];       // T tiles along f
+  int tstart[SV2N_MAX_LAYERS];   // first T block of the layer
+  int tcount[SV2N_MAX_LAYERS];
+  int pcount[SV2N_MAX_LAYERS];
+  int L;
+};
+
+__device__ __forceinline__ void put3(uint16_t* planes, int64_t plane, int64_t idx, float v) {
+  unsigned short h0, h1, h2;
+  split3(v, h0, h1, h2);
+  planes[idx] = h0;
+  planes[plane + idx] = h1;
+  planes[2 * plane + idx] = h2;
+}
+
+__global__ __launch_bounds__(256) void k_prep_fwd_all(const PrepAllArgs a) {
+  __shared__ float s_red[2][4][64];
+  __shared__ float tile[32][33];
+  const int t = threadIdx.x;
+  const int b = blockIdx.x;
+  int l = 0, local = -1;
+  bool tblock = false;
+  for (int k = 0; k < a.L; ++k) {
+    if (b >= a.pstart[k] && b < a.pstart[k] + a.pcount[k]) { l = k; local = b - a.pstart[k]; }
+    if (b >= a.tstart[k] && b < a.tstart[k] + a.tcount[k]) {
+      l = k; local = b - a.tstart[k]; tblock = true;
+    }
+  }
+  if (local < 0) return;
+  const sv2n_prep_layer& P = a.l[l];
+  const int H = P.heads, C = P.channels, F = P.in_features, ldx = P.ldx, HC = H * C;
+  if (!tblock) {
+    const int64_t kp = a.kp[l], plane = (int64_t)ldx * kp;
+    const int lane = t & 63, grp = t >> 6;
+    const int bx = local % a.px[l], y = local / a.px[l];
+    const int col = bx * 64 + lane;
+    if (y < H) {
+      const int h = y;
+      float ss = 0.f, sd = 0.f;
+      // rows c = grp, grp+4, ...: 8 rows' loads issued before any store (W
+      // is reached through the argument struct, so the compiler cannot move
+      // a load above an earlier store itself)
+      constexpr int RB = 8;
+      for (int c0 = grp; c0 < C; c0 += 4 * RB) {
+        float w[RB], as[RB], ad[RB];
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+          const int c = c0 + 4 * u;
+          const int row = h * C + min(c, C - 1);
+          const bool ok = c < C && col < F;
+          w[u] = ok ? P.W[(int64_t)row * F + min(col, F - 1)] : 0.f;
+          as[u] = P.att_src[row];
+          ad[u] = P.att_dst[row];
+        }
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+          const int c = c0 + 4 * u;
+          if (c < C) {
+            const int row = h * C + c;
+            if (col < F) P.waug[(int64_t)row * F + col] = w[u];
+            if (col < kp) put3(P.planes, plane, (int64_t)row * kp + col, w[u]);
+            ss = fmaf(as[u], w[u], ss);
+            sd = fmaf(ad[u], w[u], sd);
+          }
+        }
+      }
+      s_red[0][grp][lane] = ss;
+      s_red[1][grp][lane] = sd;
+      __syncthreads();
+      if (grp < 2 && col < kp) {
+        const float v = (s_red[grp][0][lane] + s_red[grp][1][lane]) +
+                        (s_red[grp][2][lane] + s_red[grp][3][lane]);
+        const int row = HC + grp * H + h;
+        if (col < F) P.waug[(int64_t)row * F + col] = v;
+        put3(P.planes, plane, (int64_t)row * kp + col, v);
+      }
+      if (h == 0 && col < kp) {  // zero padding rows
+        for (int r = HC + 2 * H + grp; r < ldx; r += 4) {
+          if (col < F) P.waug[(int64_t)r * F + col] = 0.f;
+          put3(P.planes, plane, (int64_t)r * kp + col, 0.f);
+        }
+      }
+    } else {
+      if (!P.W_edge) return;
+      const int h = y - H, D = P.edge_dim;
+      float se = 0.f;
+      if (col < D) {
+        for (int c = grp; c < C; c += 4) {
+          const int row = h * C + c;
+          se = fmaf(P.att_edge[row], P.W_edge[(int64_t)row * D + col], se);
+        }
+      }
+      s_red[0][grp][lane] = se;
+      __syncthreads();
+      if (grp == 0 && col < D)
+        P.wfold[(int64_t)col * P.hl_pad + P.col0 + h] =
+            (s_red[0][0][lane] + s_red[0][1][lane]) + (s_red[0][2][lane] + s_red[0][3][lane]);
+    }
+    return;
+  }
+  // ---- T block: planesT[f][o] for a 32 x 32 tile ----
+  const int64_t kpt = a.kpt[l], plane = (int64_t)F * kpt;
+  const int f0 = (local % a.tf[l]) * 32, o0 = (local / a.tf[l]) * 32;
+  {
+    const int fl = t & 31, og = t >> 5;
+    const int f = f0 + fl;
+    for (int oi = og; oi < 32; oi += 8) {
+      const int o = o0 + oi;
+      float v = 0.f;
+      if (f < F && o < HC) {
+        v = P.W[(int64_t)o * F + f];
+      } else if (f < F && o < HC + 2 * H) {
+        const int q = o - HC, h = q % H;
+        const float* att = q < H ? P.att_src : P.att_dst;
+        float p4[4] = {0.f, 0.f, 0.f, 0.f};
+        // k_prep_fwd's four row groups (row c in group c % 4, in c order),
+        // 8 rows of each group loaded per round
+        for (int c0 = 0; c0 < C; c0 += 32) {
+          float w[32], at[32];
+#pragma unroll
+          for (int u = 0; u < 32; ++u) {
+            const int row = h * C + min(c0 + u, C - 1);
+            w[u] = P.W[(int64_t)row * F + f];
+            at[u] = att[row];
+          }
+#pragma unroll
+          for (int u = 0; u < 32; ++u)
+            if (c0 + u < C) p4[u & 3] = fmaf(at[u], w[u], p4[u & 3]);
+        }
+        v = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+      }
+      tile[oi][fl] = v;
+    }
+  }
+  __syncthreads();
+  {
+    const int ol = t & 31, fg = t >> 5;
+    const int o = o0 + ol;
+    for (int fi = fg; fi < 32; fi += 8) {
+      const int f = f0 + fi;
+      if (f < F && o < kpt) put3(P.planes_t, plane, (int64_t)f * kpt + o, tile[ol][fi]);
+    }
+  }
+}
+
 }  // namespace sv2n
 
 using namespace sv2n;
@@ -259,5 +421,40 @@ extern "C" int sv2n_gat_prep_bwd_edge(const float* dwfold, int hl_pad, int col0,
   const int HC = heads * channels;
   hipLaunchKernelGGL(k_prep_bwd_edge, dim3((HC + 3) / 4), dim3(256), 0, stream, dwfold, hl_pad,
                      col0, W_edge, att_edge, heads, channels, edge_dim, gW_edge, g_att_edge);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_gat_prep_fwd_all(const sv2n_prep_layer* layers, int num_layers,
+                                     hipStream_t stream) {
+  if (!layers || num_layers < 1 || num_layers > SV2N_MAX_LAYERS) return SV2N_ERR_ARG;
+  PrepAllArgs a{};
+  a.L = num_layers;
+  int nb = 0;
+  for (int l = 0; l < num_layers; ++l) {
+    const sv2n_prep_layer& P = layers[l];
+    if (!P.W || !P.att_src || !P.att_dst || !P.waug || !P.planes) return SV2N_ERR_ARG;
+    if (P.heads < 1 || P.channels < 1 || P.in_features < 1) return SV2N_ERR_ARG;
+    if (P.heads > SV2N_MAX_HEADS || P.ldx < P.heads * P.channels + 2 * P.heads)
+      return SV2N_ERR_SHAPE;
+    const bool edge = P.W_edge && P.att_edge && P.wfold;
+    if (edge && (P.edge_dim < 1 || P.col0 + P.heads > P.hl_pad)) return SV2N_ERR_SHAPE;
+    a.l[l] = P;
+    if (!edge) a.l[l].W_edge = nullptr;
+    a.kp[l] = sv2n_split3_kpad(P.in_features);
+    a.kpt[l] = sv2n_split3_kpad(P.ldx);
+    const int64_t cols = std::max<int64_t>(a.kp[l], edge ? P.edge_dim : 0);
+    a.px[l] = (int)((cols + 63) / 64);
+    a.pstart[l] = nb;
+    a.pcount[l] = a.px[l] * (edge ? 2 * P.heads : P.heads);
+    nb += a.pcount[l];
+  }
+  for (int l = 0; l < num_layers; ++l) {
+    const sv2n_prep_layer& P = layers[l];
+    a.tf[l] = (P.in_features + 31) / 32;
+    a.tstart[l] = nb;
+    a.tcount[l] = P.planes_t ? a.tf[l] * (int)((a.kpt[l] + 31) / 32) : 0;
+    nb += a.tcount[l];
+  }
+  hipLaunchKernelGGL(k_prep_fwd_all, dim3((unsigned)nb), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }

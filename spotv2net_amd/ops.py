@@ -110,6 +110,21 @@ def project(a: torch.Tensor, w: torch.Tensor, transpose_w: bool) -> torch.Tensor
     return gemm_f32(a, True, w, not transpose_w, M, N, K)
 
 
+def project_planes(a: torch.Tensor, planes: Optional[torch.Tensor], w: torch.Tensor,
+                   transpose_w: bool) -> torch.Tensor:
+    """project(a, w, transpose_w) with w's bf16 split planes already made
+    (sv2n_gat_prep_fwd_all); exact-f32 fallback on w as in project()."""
+    if planes is None or not _split_ok(a):
+        return project(a, w, transpose_w)
+    lib = _lib.load()
+    M, K = a.shape
+    N = w.shape[1] if transpose_w else w.shape[0]
+    out = torch.empty(M, N, device=a.device, dtype=torch.float32)
+    _lib.check(lib.sv2n_gemm_f32x3(a.data_ptr(), a.stride(0), planes.data_ptr(), out.data_ptr(),
+                                   out.stride(0), M, N, K, _stream(a.device)), "sv2n_gemm_f32x3")
+    return out
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:

@@ -21,13 +21,14 @@ these parameters therefore do not fire for this path (documented deviation).
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Sequence
 
 import torch
 
 from . import _lib
 from .layout import GraphLayout
-from .ops import _aligned, _require_device, gemm_f32, pad_columns, project
+from .ops import _aligned, _require_device, gemm_f32, pad_columns, project, project_planes
 
 
 def _grad_buf(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -80,18 +81,30 @@ class _GATStack(torch.autograd.Function):
             _, hp = pad_columns(torch.empty(0, L * H))
             wf = torch.empty(D, hp, device=dev, dtype=torch.float32)
 
-        # 1) weight preparation
-        waugs = []
+        # 1) weight preparation: every layer's folded Waug, its bf16 split planes
+        #    (and the transposed ones the backward's dx GEMM needs) and the edge
+        #    fold, in one launch
+        waugs, planes, planes_t = [], [], []
+        arr = (_lib.PrepLayer * L)()
         for l, c in enumerate(convs):
             F = c.in_channels
-            waug = torch.empty(_ldx(c), F, device=dev, dtype=torch.float32)
+            ldx = _ldx(c)
+            waug = torch.empty(ldx, F, device=dev, dtype=torch.float32)
+            pl = torch.empty(3, ldx, lib.sv2n_split3_kpad(F), device=dev, dtype=torch.int16)
+            need_t = training and (l > 0 or x.requires_grad)
+            plt = (torch.empty(3, F, lib.sv2n_split3_kpad(ldx), device=dev, dtype=torch.int16)
+                   if need_t else None)
             We = c.lin_edge.weight if use_edge else None
-            _lib.check(lib.sv2n_gat_prep_fwd(
+            arr[l] = _lib.PrepLayer(
                 c.lin_src.weight.data_ptr(), c.att_src.data_ptr(), c.att_dst.data_ptr(), c.heads,
-                c.out_channels, F, waug.data_ptr(), waug.size(0), _lib.ptr(We),
-                _lib.ptr(c.att_edge if use_edge else None), ea.size(1) if use_edge else 0,
-                _lib.ptr(wf), hp, l * H, st), "sv2n_gat_prep_fwd")
+                c.out_channels, F, ldx, waug.data_ptr(), pl.data_ptr(), _lib.ptr(plt),
+                _lib.ptr(We), _lib.ptr(c.att_edge if use_edge else None),
+                ea.size(1) if use_edge else 0, hp, l * H, _lib.ptr(wf))
             waugs.append(waug)
+            planes.append(pl)
+            planes_t.append(plt)
+        _lib.check(lib.sv2n_gat_prep_fwd_all(ctypes.addressof(arr), L, st),
+                   "sv2n_gat_prep_fwd_all")
 
         # 2) edge logits of every layer in one pass over edge_attr
         aes = [None] * L
@@ -123,7 +136,7 @@ class _GATStack(torch.autograd.Function):
             F = c.in_channels
             if xin.size(1) != F:
                 raise ValueError(f"layer {l}: expected {F} input features, got {xin.size(1)}")
-            xs = project(xin, waugs[l], False)  # x · Waugᵀ
+            xs = project_planes(xin, planes[l], waugs[l], False)  # x · Waugᵀ
             keep, kscale = None, 1.0
             kn = n if tiled else 32  # keep-mask tile: [B][H][n][n] tiled, [B][H][32][32] per-graph
             if training and c.dropout > 0.0:
@@ -175,7 +188,7 @@ class _GATStack(torch.autograd.Function):
         ctx.kscales = [(1.0 / (1.0 - c.dropout)) if (training and 0.0 < c.dropout < 1.0) else
                        (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs]
         ctx.save_for_backward(ea, *saved_x, *saved_xs, *saved_y, *saved_p, *saved_keep,
-                              *saved_drop, *waugs)
+                              *saved_drop, *waugs, *planes_t)
         return xin
 
     @staticmethod
@@ -193,7 +206,8 @@ class _GATStack(torch.autograd.Function):
         pss = sv[k:k + L]; k += L
         keeps = sv[k:k + L]; k += L
         drops = sv[k:k + L]; k += L
-        waugs = sv[k:k + L]
+        waugs = sv[k:k + L]; k += L
+        planes_t = sv[k:k + L]
         dev = dout.device
         st = _lib.stream_handle(dev)
         B, n, N = layout.num_graphs, layout.n, layout.num_nodes
@@ -249,7 +263,7 @@ class _GATStack(torch.autograd.Function):
                     dbp.data_ptr(), B, OC, _lib.ptr(gW), _lib.ptr(gas), _lib.ptr(gad),
                     _lib.ptr(gb), ws.data_ptr(), ws_n, st), "sv2n_gat_wgrad_node")
             if l > 0 or need_x0:
-                dy = project(dxs, waugs[l], True)  # dxs · Waug
+                dy = project_planes(dxs, planes_t[l], waugs[l], True)  # dxs · Waug
 
         if use_edge and ea is not None:
             # grads exist (zeros) even without edges, as in PyG

@@ -66,7 +66,7 @@ class FlatAdam:
         self.m = torch.zeros_like(flat_params)
         self.v = torch.zeros_like(flat_params)
         self.step_t = torch.zeros(1, device=flat_params.device, dtype=torch.float32)
-        self.ticket = torch.zeros(4, device=flat_params.device, dtype=torch.int32)
+        self.ticket = torch.zeros(288, device=flat_params.device, dtype=torch.int32)  # SV2N_TICKET_WORDS
         self.lr, self.betas, self.eps, self.wd = float(lr), betas, float(eps), float(weight_decay)
 
     # the kernel advances step_t itself and zeroes the consumed gradient

@@ -61,3 +61,51 @@ def test_split3_gemm_matches_f32_accuracy(dev, M, N, K, transpose):
     e3 = ((got.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
     e32 = ((f32.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
     assert e3 < 1e-6 and e3 <= 2 * e32 + 1e-9, (e3, e32)
+
+
+def test_prep_fwd_all_matches_per_layer(dev):
+    """sv2n_gat_prep_fwd_all (one launch, all layers) equals sv2n_gat_prep_fwd
+    + sv2n_split3 (+ the transposed split) per layer, bit for bit."""
+    import ctypes
+    from spotv2net_amd import _lib
+    lib = _lib.load()
+    st = _lib.stream_handle(dev)
+    g = torch.Generator().manual_seed(3)
+    shapes = [(4, 100, 1260), (4, 50, 400)]  # (H, C, F) of the C2 layers
+    D, H = 126, 4
+    hp = 8
+    arr = (_lib.PrepLayer * len(shapes))()
+    keep = []
+    wf_all = torch.zeros(D, hp, device=dev)
+    wf_ref = torch.zeros(D, hp, device=dev)
+    for l, (Hh, C, F) in enumerate(shapes):
+        HC = Hh * C
+        ldx = (HC + 2 * Hh + 3) // 4 * 4
+        W = torch.randn(HC, F, generator=g).to(dev)
+        a_s, a_d, a_e = (torch.randn(HC, generator=g).to(dev) for _ in range(3))
+        We = torch.randn(HC, D, generator=g).to(dev)
+        kp, kpt = lib.sv2n_split3_kpad(F), lib.sv2n_split3_kpad(ldx)
+        waug = torch.empty(ldx, F, device=dev)
+        pl = torch.empty(3, ldx, kp, device=dev, dtype=torch.int16)
+        plt = torch.empty(3, F, kpt, device=dev, dtype=torch.int16)
+        arr[l] = _lib.PrepLayer(W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), Hh, C, F, ldx,
+                                waug.data_ptr(), pl.data_ptr(), plt.data_ptr(), We.data_ptr(),
+                                a_e.data_ptr(), D, hp, l * H, wf_all.data_ptr())
+        # reference: the per-layer entries
+        waug_r = torch.empty(ldx, F, device=dev)
+        _lib.check(lib.sv2n_gat_prep_fwd(W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), Hh, C, F,
+                                         waug_r.data_ptr(), ldx, We.data_ptr(), a_e.data_ptr(), D,
+                                         wf_ref.data_ptr(), hp, l * H, st), "prep_fwd")
+        pl_r = torch.empty(3, ldx, kp, device=dev, dtype=torch.int16)
+        _lib.check(lib.sv2n_split3(waug_r.data_ptr(), ldx, F, F, 0, pl_r.data_ptr(), st), "split3")
+        plt_r = torch.empty(3, F, kpt, device=dev, dtype=torch.int16)
+        _lib.check(lib.sv2n_split3(waug_r.data_ptr(), F, ldx, F, 1, plt_r.data_ptr(), st),
+                   "split3 transposed")
+        keep.append((W, a_s, a_d, a_e, We, waug, pl, plt, waug_r, pl_r, plt_r))
+    _lib.check(lib.sv2n_gat_prep_fwd_all(ctypes.addressof(arr), len(shapes), st), "prep_fwd_all")
+    torch.cuda.synchronize()
+    for (*_, waug, pl, plt, waug_r, pl_r, plt_r) in keep:
+        assert torch.equal(waug, waug_r)
+        assert torch.equal(pl, pl_r)
+        assert torch.equal(plt, plt_r)
+    assert torch.equal(wf_all, wf_ref)
