@@ -87,31 +87,119 @@ __device__ __forceinline__ int canon_eid(int n, int i, int j) {
 constexpr int RPW = TB / 4;  // rows per wave per target block
 constexpr int SRS = TB + 4;  // K-split partial row stride (16-B aligned, fewer conflicts)
 
-// One thread per source column j = t: the TB rows' edge logits of a target
-// block (-inf where edge j->i is absent or j == i), every load independent so
-// a block's gathers are all in flight together; issued one block ahead of
-// the block being computed.
-__device__ __forceinline__ void load_block(float (&pv)[TB], int i0, int t,
+// Edge logits of one target block [i0, i0+TB) x sources [0, NP), staged into
+// sE[r][j] (row stride SE; -inf where edge j->i is absent or j == i).
+//
+// In the canonical order (utils/dataset.py:216-226) an upper element (j > i)
+// has the in-graph id U + off(i) + (j-i-1), contiguous in j, and a lower one
+// (j < i) the id off(j) + (i-j-1), contiguous in i (U = n(n-1)/2,
+// off(u) = u(2n-u-1)/2).  The block is cut into 16x16 tiles over sources,
+// tile k = t>>4 served by 16 threads (q = t&15), 16 elements each:
+//   k above the block's diagonal tile: element m = (r = m, j = 16k+q)  -> lanes along j
+//   k at or below it:                  element m = (r = q, j = 16k+m)  -> lanes along i
+// so every load instruction reads 16-lane runs of consecutive ids (64 B)
+// instead of 64 scattered words, and each thread holds 16 values with 32-bit
+// buffer offsets.  With an edge-id map (block layouts) every tile uses the
+// first mapping (the eid row reads are then coalesced; the logit gather is
+// arbitrary by nature).
+__device__ __forceinline__ int tri_off(int n, int u) { return u * (2 * n - u - 1) / 2; }
+
+__device__ __forceinline__ bool mask_bit(const uint32_t* __restrict__ rowmask, int64_t row, int W,
+                                         int j) {
+  return !rowmask || ((rowmask[row * W + (j >> 5)] >> (j & 31)) & 1u);
+}
+
+// element m of thread t in block i0 -> (r, j); `along_j` for the first mapping
+__device__ __forceinline__ void tile_elem(int t, int m, bool along_j, int& r, int& j) {
+  const int k = t >> 4, q = t & 15;
+  r = along_j ? m : q;
+  j = 16 * k + (along_j ? q : m);
+}
+__device__ __forceinline__ bool tile_along_j(int t, int i0, bool has_eid) {
+  return has_eid || (t >> 4) > (i0 >> 4);
+}
+
+// canonical in-graph id of (i <- j), or -1 when the pair is not an edge slot
+__device__ __forceinline__ int canon_id(int n, int U, int i, int j) {
+  if (i >= n || j >= n || i == j) return -1;
+  return j > i ? U + tri_off(n, i) + (j - i - 1) : tri_off(n, j) + (i - j - 1);
+}
+
+struct BlockLoad {
+  float v[TB];
+  uint32_t valid;  // bit m: element m is a present edge
+};
+
+__device__ __forceinline__ void load_block(BlockLoad& L, int i0, int t,
                                            const float* __restrict__ ae,
                                            const int32_t* __restrict__ eid,
                                            const uint32_t* __restrict__ rowmask, int64_t g, int n) {
-  const int j = t;
+  const int W = (n + 31) >> 5;
+  const bool aj = tile_along_j(t, i0, eid != nullptr);
+  L.valid = 0u;
+  if (eid) {
+#pragma unroll
+    for (int m = 0; m < TB; ++m) {
+      int r, j;
+      tile_elem(t, m, aj, r, j);
+      const int i = i0 + r;
+      int e = -1;
+      if (i < n && j < n && j != i) e = eid[(g * n + i) * n + j];
+      L.v[m] = (e >= 0 && ae) ? ae[e] : 0.f;
+      L.valid |= (e >= 0 ? 1u : 0u) << m;
+    }
+    return;
+  }
+  const int64_t E0 = (int64_t)n * (n - 1);
+  const int U = (n * (n - 1)) / 2;
+  const rsrc_t rs = make_rsrc(ae ? ae + g * E0 : nullptr, ae ? (uint32_t)(E0 * 4) : 0u);
+#pragma unroll
+  for (int m = 0; m < TB; ++m) {
+    int r, j;
+    tile_elem(t, m, aj, r, j);
+    const int i = i0 + r;
+    const int id = canon_id(n, U, i, j);
+    const bool ok = id >= 0 && mask_bit(rowmask, g * n + i, W, j);
+    L.v[m] = bld(rs, ok ? 4 * id : OOB);
+    L.valid |= (ok ? 1u : 0u) << m;
+  }
+}
+
+__device__ __forceinline__ void stage_block(const BlockLoad& L, float* __restrict__ sE, int SE,
+                                            int i0, int t, bool has_eid, int NP) {
+  const bool aj = tile_along_j(t, i0, has_eid);
+  if ((t >> 4) < NP / 16) {
+#pragma unroll
+    for (int m = 0; m < TB; ++m) {
+      int r, j;
+      tile_elem(t, m, aj, r, j);
+      sE[r * SE + j] = ((L.valid >> m) & 1u) ? L.v[m] : -INFINITY;
+    }
+  }
+}
+
+// d(edge logit) of one target block, staged in sE[r][j] by the rows phase,
+// written to the head plane through the same tile mapping (canonical order,
+// present edges only; other slots go to an out-of-range offset and drop).
+__device__ __forceinline__ void store_block_dae(const float* __restrict__ sE, int SE, int i0,
+                                                int t, float* __restrict__ dae,
+                                                const uint32_t* __restrict__ rowmask, int64_t g,
+                                                int n, int NP) {
   const int W = (n + 31) >> 5;
   const int64_t E0 = (int64_t)n * (n - 1);
+  const int U = (n * (n - 1)) / 2;
+  const bool aj = tile_along_j(t, i0, false);
+  const rsrc_t rs = make_rsrc(dae + g * E0, (uint32_t)(E0 * 4));
+  if ((t >> 4) < NP / 16) {
 #pragma unroll
-  for (int r = 0; r < TB; ++r) {
-    const int i = i0 + r;
-    float v = -INFINITY;
-    if (i < n && j < n && j != i) {
-      const int64_t row = g * n + i;
-      if (eid) {
-        const int e = eid[row * n + j];
-        if (e >= 0) v = ae ? ae[e] : 0.f;
-      } else if (!rowmask || ((rowmask[row * W + (j >> 5)] >> (j & 31)) & 1u)) {
-        v = ae ? ae[g * E0 + canon_eid(n, i, j)] : 0.f;
-      }
+    for (int m = 0; m < TB; ++m) {
+      int r, j;
+      tile_elem(t, m, aj, r, j);
+      const int i = i0 + r;
+      const int id = canon_id(n, U, i, j);
+      const bool ok = id >= 0 && mask_bit(rowmask, g * n + i, W, j);
+      bst(rs, ok ? 4 * id : OOB, sE[r * SE + j]);
     }
-    pv[r] = v;
   }
 }
 
@@ -223,7 +311,8 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
   float* sP = sX + NP * XS;       // [TB][PS]
   float* sA = sP + TB * PS;       // [NP]
   float* sD = sA + NP;            // [NP]
-  float* sE = sD + NP;            // [TB][NP], max(TB*NP, 4*CW*SRS) floats
+  const int SE = NP + 1;          // conflict-free column-wise tile writes
+  float* sE = sD + NP;            // [TB][SE], max(TB*SE, 4*CW*SRS) floats
   float* sR = sE;                 // [4][CW][SRS], after the rows phase
 
   int64_t g;
@@ -234,8 +323,8 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
   const int HC = H * C;
   const float* ae = ae_planes ? ae_planes + (int64_t)h * E : nullptr;
 
-  float pv[TB];
-  load_block(pv, 0, t, ae, eid, rowmask, g, n);
+  BlockLoad L;
+  load_block(L, 0, t, ae, eid, rowmask, g, n);
   for (int idx = t; idx < NP * CW; idx += TT) {
     const int j = idx / CW, c = idx - j * CW;
     sX[j * XS + c] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
@@ -248,17 +337,14 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
   const int li = lane & 15, lk = lane >> 4;
   const int kq = NP / 4;  // K-split: wave w sums sources [w*kq, (w+1)*kq)
   for (int i0 = 0; i0 < n; i0 += TB) {
-    if (t < NP) {
-#pragma unroll
-      for (int r = 0; r < TB; ++r) sE[r * NP + t] = pv[r];
-    }
+    stage_block(L, sE, SE, i0, t, eid != nullptr, NP);
     __syncthreads();
-    if (i0 + TB < n) load_block(pv, i0 + TB, t, ae, eid, rowmask, g, n);
+    if (i0 + TB < n) load_block(L, i0 + TB, t, ae, eid, rowmask, g, n);
     // ---- P rows: wave w owns rows [4w, 4w+4) of the block ----
     {
       const int rb = wave * RPW;
       Rows R;
-      rows_softmax(R, sE, NP, sA, sD, rb, i0, n, NP, ae != nullptr, slope, lane);
+      rows_softmax(R, sE, SE, sA, sD, rb, i0, n, NP, ae != nullptr, slope, lane);
 #pragma unroll
       for (int rr = 0; rr < RPW; ++rr) {
         const int i = i0 + rb + rr;
@@ -360,7 +446,8 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
   float* sA = sO + TB * OS;       // [NP]
   float* sD = sA + NP;            // [NP]
   float* sDa = sD + NP;           // [NP]
-  float* sE = sDa + NP;           // [TB][NP]
+  const int SE = NP + 1;          // conflict-free column-wise tile accesses
+  float* sE = sDa + NP;           // [TB][SE]: edge logits, then d(edge logit)
 
   int64_t g;
   int h;
@@ -374,8 +461,23 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
   const float* ae = ae_planes ? ae_planes + (int64_t)h * E : nullptr;
   float* dae = dae_planes ? dae_planes + (int64_t)h * E : nullptr;
 
-  float pv[TB];
-  load_block(pv, 0, t, ae, eid, rowmask, g, n);
+  // dOut rows of the next block, prefetched in registers with its edge logits
+  // (a load issued after this block's dae stores would wait for all of them)
+  constexpr int OPT = TB * CW / TT;  // = CT
+  float pdy[OPT], py[OPT];
+  auto load_dout = [&](int i0n) {
+#pragma unroll
+    for (int m = 0; m < OPT; ++m) {
+      const int idx = t + TT * m, r = idx / CW, c = idx - r * CW, i = i0n + r;
+      const bool ok = i < n && c < C;
+      const int64_t o = ok ? (row0 + i) * OC + oc0 + c : 0;
+      pdy[m] = ok ? dy[o] : 0.f;
+      py[m] = ok ? y[o] : 0.f;
+    }
+  };
+  BlockLoad L;
+  load_block(L, 0, t, ae, eid, rowmask, g, n);
+  load_dout(0);
   for (int idx = t; idx < NP * CW; idx += TT) {
     const int j = idx / CW, c = idx - j * CW;
     sX[j * XS + c] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
@@ -398,22 +500,17 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
 
   for (int i0 = 0; i0 < n; i0 += TB) {
     // ---- stage: edge logits of this block (prefetched), dOut rows ----
-    if (t < NP) {
+    stage_block(L, sE, SE, i0, t, eid != nullptr, NP);
 #pragma unroll
-      for (int r = 0; r < TB; ++r) sE[r * NP + t] = pv[r];
-    }
-    for (int idx = t; idx < TB * CW; idx += TT) {
-      const int r = idx / CW, c = idx - r * CW;
-      const int i = i0 + r;
-      float v = 0.f;
-      if (i < n && c < C) {
-        const int64_t o = (row0 + i) * OC + oc0 + c;
-        v = act_bwd<ACT>(dy[o], y[o]);
-      }
-      sO[r * OS + c] = v * oscale;
+    for (int m = 0; m < OPT; ++m) {
+      const int idx = t + TT * m, r = idx / CW, c = idx - r * CW;
+      sO[r * OS + c] = act_bwd<ACT>(pdy[m], py[m]) * oscale;
     }
     __syncthreads();
-    if (i0 + TB < n) load_block(pv, i0 + TB, t, ae, eid, rowmask, g, n);
+    if (i0 + TB < n) {
+      load_block(L, i0 + TB, t, ae, eid, rowmask, g, n);
+      load_dout(i0 + TB);
+    }
     if (t < C && (CONCAT || h == 0)) {
       float s = 0.f;
       for (int r = 0; r < TB; ++r) s += sO[r * OS + t];
@@ -435,7 +532,7 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
     {
       const int rb = wave * RPW;
       Rows R;
-      rows_softmax(R, sE, NP, sA, sD, rb, i0, n, NP, ae != nullptr, slope, lane);
+      rows_softmax(R, sE, SE, sA, sD, rb, i0, n, NP, ae != nullptr, slope, lane);
       float dp[RPW][4], pd[RPW][4], red[3 * RPW];
 #pragma unroll
       for (int rr = 0; rr < RPW; ++rr) {
@@ -494,12 +591,16 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
             sP[r * PS + j] = pd[rr][q];
             sL[r * PS + j] = dl[rr][q];
           }
-          if (dae && R.present[rr][q])
-            dae[edge_index_of(eid, g, n, i, j)] = dl[rr][q] + dshare;
+          if (eid) {
+            if (dae && R.present[rr][q]) dae[edge_index_of(eid, g, n, i, j)] = dl[rr][q] + dshare;
+          } else if (j < NP) {
+            sE[r * SE + j] = dl[rr][q] + dshare;  // this wave's own rows of sE
+          }
         }
       }
     }
     __syncthreads();
+    if (dae && !eid) store_block_dae(sE, SE, i0, t, dae, rowmask, g, n, NP);
     // ---- column sums of dL (d a_src) and dxs_h += Pdᵀ · dOut ----
     for (int j = t; j < NP; j += TT) {
       float s = 0.f;
@@ -563,12 +664,12 @@ static int ct_of(int C) { return (C + 15) / 16; }
 static size_t tiled_fwd_lds(int n, int C) {
   const int CW = 16 * ct_of(C), NP = round_up(n, 16);
   return sizeof(float) * ((size_t)NP * pad32(CW, 16) + (size_t)TB * pad32(NP, 2) + 2 * NP +
-                          std::max((size_t)TB * NP, (size_t)4 * CW * SRS));
+                          std::max((size_t)TB * (NP + 1), (size_t)4 * CW * SRS));
 }
 static size_t tiled_bwd_lds(int n, int C) {
   const int CW = 16 * ct_of(C), NP = round_up(n, 16);
   return sizeof(float) * ((size_t)NP * (CW + 1) + 2 * (size_t)TB * pad32(NP, 16) +
-                          (size_t)TB * (CW + 1) + 3 * (size_t)NP + (size_t)TB * NP);
+                          (size_t)TB * (CW + 1) + 3 * (size_t)NP + (size_t)TB * (NP + 1));
 }
 
 template <typename K>

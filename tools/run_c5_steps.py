@@ -1,7 +1,7 @@
 """Runs a few eager C5 training steps (for rocprofv3 counter passes)."""
 import sys
 import torch
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from bench import CONFIGS, build_model  # noqa: E402
 from spotv2net_amd import synthetic_batch  # noqa: E402
 from spotv2net_amd.train import TrainStep  # noqa: E402
