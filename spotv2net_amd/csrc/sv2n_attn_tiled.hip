@@ -2,40 +2,44 @@
 // SURVEY.md §8d C5 stress shapes and any larger block batch) — the same PyG
 // 2.3.0 GATConv semantics as sv2n_attn.hip (reference utils/models.py:146 ->
 // GATConv.forward), re-tiled for rows that no
-// longer fit one 32-lane half:
+// longer fit one 32-lane half.
+//
+// Edge logits come as per-layer head planes [H][E] in edge order (what
+// sv2n_edge_logits_fwd_planes writes with fully coalesced stores).  In the
+// canonical order (reference utils/dataset.py:216-226) the logit of (target
+// i <- source j) sits at
+//     j > i:  U + off(i) + (j-i-1)   — contiguous along the row's sources,
+//     j < i:  off(j) + (i-j-1)       — contiguous along the block's targets,
+// (U = n(n-1)/2, off(u) = u(2n-u-1)/2), so the lanes that own a row load its
+// logits straight into registers with one add per element (off(j)-j-1 is a
+// per-lane constant): row runs for the upper part, 16-B runs shared by the
+// four rows of a wave for the lower part, which the block's other waves
+// complete from the same lines.  No LDS staging of the logits.  Block
+// layouts (any order, missing edges) read an [N][n] edge-id map instead.
 //
 // * one workgroup (4 waves) per (graph g, head h); blockIdx is remapped so the
 //   H head-workgroups of a graph run on the same XCD (shared L2 for the xs
 //   rows they all read);
-// * edge logits come in per-layer head planes AE[h][e] in edge order (what
-//   sv2n_edge_logits_fwd_planes writes with fully coalesced stores); edge e of
-//   (target i, source j) is computed from the canonical order or read from an
-//   eid map [g][i][j] (block layouts).  A target block's first-half edges
-//   (sources j < i) are 16 consecutive edge ids per j, so the gathers stay
-//   sector-coalesced across the block's rows;
-// * targets are walked in blocks of TB = 16 rows; a wave owns a row at a time
-//   and its lanes cover sources j = lane + 64q, so the self-loop mean, the
-//   softmax max / sum are 64-lane wave reductions;
+// * targets are walked in blocks of TB = 16 rows; within a block, 16-lane
+//   group gq of wave w owns target row r = 4w + gq and lane q of the group
+//   sources j = 64c + 4q + s (c, s = 0..3): four b128 loads per row, the
+//   softmax max / sums are 16-lane DPP reductions (row_ror 8, 4, quad xor);
+// * a_src of the lane's 16 sources stays in registers for the whole graph;
 // * the products run on v_mfma_f32_16x16x4_f32 (exact f32) from LDS:
-//     forward   out_h[i]  = Σ_j P[i][j] · xs_h[j]        (TB x C, K = n)
+//     forward   out_h[i]  = Σ_j P[i][j] · xs_h[j]        (TB x C, K = n, split over waves)
 //     backward  dP[i][j]  = Σ_c dOut[i][c] · xs_h[j][c]  (TB x n, K = C)
 //               dxs_h[j] += Σ_i P[i][j] · dOut[i]        (n x C, K = TB per block,
 //                                                         accumulated in VGPRs)
+// * the next block's logit rows (and, backward, its dy / y rows) are loaded
+//   into registers while the current block is computed; the backward's
+//   d-logit rows go out as b128 stores after the next block's loads were
+//   issued (gfx950 retires loads and stores on one in-order vmcnt);
 // * nothing is saved between forward and backward except the layer output:
-//   the backward recomputes P from xs and AE (its HBM cost equals reading a
-//   saved P, and the forward skips writing one);
+//   the backward recomputes P from xs and the logits (its HBM cost equals
+//   reading a saved P, and the forward skips writing one);
 // * concat = False (mean over heads) needs a cross-head sum: the forward then
 //   writes per-head aggregates to a workspace and k_head_mean finishes
 //   mean + bias + activation.
-//
-// LDS images (floats):
-//   sX [NP][XS]  xs_h rows (zero-padded to NP = round_up(n, 16) rows and
-//                16*CT columns)
-//   sP [TB][PS]  P rows
-// ds_read_b32 banks are (addr/4) % 32 per 32-lane half (cdna_hip_programming.md
-// §2).  A fragment read "row = lane&15, col = lane>>4" is conflict-free for a
-// stride ≡ 2 (mod 32) or odd; "row = lane>>4, col = lane&15" for ≡ 16 (mod 32)
-// (odd: one 2-way pair).  Strides below follow the role each image plays.
 #include "sv2n_common.h"
 
 #include <algorithm>
@@ -49,14 +53,26 @@ constexpr int TILED_MAX_C = 64;
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+__host__ __device__ constexpr int round_up(int a, int m) { return (a + m - 1) / m * m; }
+
+// 16-lane row reductions: row_ror 8, row_ror 4, then quad xor 2 and 1.  Every
+// lane of the row ends with the same bits (each step adds two equal pairs).
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dppf<0x128>(v);
+  v += dppf<0x124>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0xB1>(v);
   return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dppf<0x128>(v));
+  v = fmaxf(v, dppf<0x124>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0xB1>(v));
   return v;
 }
 
@@ -71,230 +87,196 @@ __device__ __forceinline__ void block_gh(int H, int64_t& g, int& h) {
   h = (int)(b - g * H);
 }
 
-__host__ __device__ constexpr int round_up(int a, int m) { return (a + m - 1) / m * m; }
-__host__ __device__ constexpr int pad32(int a, int mod) {  // smallest s >= a, s % 32 == mod
-  return a + ((mod - a % 32) + 32) % 32;
-}
+// source of element k (0..15) of lane q
+__device__ __forceinline__ int src_of(int q, int k) { return 64 * (k >> 2) + 4 * q + (k & 3); }
 
-// In-graph edge index of (target i <- source j) in the CovarianceLaggedDataset
-// order (reference utils/dataset.py:216-226: the row-major upper pairs (u < v)
-// as u -> v, then the same pairs swapped).  32-bit: n(n-1) < 2^31.
-__device__ __forceinline__ int canon_eid(int n, int i, int j) {
-  const int u = j > i ? i : j, v = j > i ? j : i;
-  return (j > i ? (n * (n - 1)) / 2 : 0) + u * (2 * n - u - 1) / 2 + (v - u - 1);
-}
-
-constexpr int RPW = TB / 4;  // rows per wave per target block
-constexpr int SRS = TB + 4;  // K-split partial row stride (16-B aligned, fewer conflicts)
-
-// Edge logits of one target block [i0, i0+TB) x sources [0, NP), staged into
-// sE[r][j] (row stride SE; -inf where edge j->i is absent or j == i).
-//
-// In the canonical order (utils/dataset.py:216-226) an upper element (j > i)
-// has the in-graph id U + off(i) + (j-i-1), contiguous in j, and a lower one
-// (j < i) the id off(j) + (i-j-1), contiguous in i (U = n(n-1)/2,
-// off(u) = u(2n-u-1)/2).  The block is cut into 16x16 tiles over sources,
-// tile k = t>>4 served by 16 threads (q = t&15), 16 elements each:
-//   k above the block's diagonal tile: element m = (r = m, j = 16k+q)  -> lanes along j
-//   k at or below it:                  element m = (r = q, j = 16k+m)  -> lanes along i
-// so every load instruction reads 16-lane runs of consecutive ids (64 B)
-// instead of 64 scattered words, and each thread holds 16 values with 32-bit
-// buffer offsets.  With an edge-id map (block layouts) every tile uses the
-// first mapping (the eid row reads are then coalesced; the logit gather is
-// arbitrary by nature).
 __device__ __forceinline__ int tri_off(int n, int u) { return u * (2 * n - u - 1) / 2; }
 
-__device__ __forceinline__ bool mask_bit(const uint32_t* __restrict__ rowmask, int64_t row, int W,
-                                         int j) {
-  return !rowmask || ((rowmask[row * W + (j >> 5)] >> (j & 31)) & 1u);
+// Per-lane constants of the graph: a_src of the lane's sources (0 past n)
+// and kmax, the number of the lane's sources below n (src_of rises with k).
+struct LaneConst {
+  float as[16];
+  int kmax;
+};
+
+__device__ __forceinline__ void init_lane_const(LaneConst& K, rsrc_t rxs, int n, int q, int ldx,
+                                                int asoff) {
+  K.kmax = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int j = src_of(q, k);
+    K.as[k] = bld(rxs, j < n ? 4 * (j * ldx + asoff) : OOB);
+    K.kmax += j < n ? 1 : 0;
+  }
 }
 
-// element m of thread t in block i0 -> (r, j); `along_j` for the first mapping
-__device__ __forceinline__ void tile_elem(int t, int m, bool along_j, int& r, int& j) {
+// in-plane offset (floats) of (target i <- source j) or -1
+__device__ __forceinline__ int logit_id(const int32_t* __restrict__ eid, int64_t erow, int upb,
+                                        int i, int j, int n) {
+  if (i >= n || j >= n || j == i) return -1;
+  if (eid) return eid[erow + j];
+  return j > i ? upb + j : tri_off(n, j) - j - 1 + i;
+}
+
+// One target row's inputs, loaded one block ahead.
+struct RowIn {
+  float e[16];  // logits of the lane's sources
+  float ad;     // a_dst[i]
+};
+
+// rae spans the graph's slice of the head plane (canonical) or the whole
+// plane (edge-id map: erow = (g*n + i)*n).
+__device__ __forceinline__ void load_row(RowIn& R, rsrc_t rae, rsrc_t rxs, const LaneConst& K,
+                                         const int32_t* __restrict__ eid, int64_t erow, int i,
+                                         int n, int U, int q, int adoff, int ldx) {
+  const int upb = U + tri_off(n, i) - i - 1;
+  int id[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) id[k] = logit_id(eid, erow, upb, i, src_of(q, k), n);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) R.e[k] = bld(rae, id[k] >= 0 ? 4 * id[k] : OOB);
+  R.ad = bld(rxs, i < n ? 4 * (i * ldx + adoff) : OOB);
+}
+
+__device__ __forceinline__ void unpack(float (&e)[16], const RowIn& R) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) e[k] = R.e[k];
+}
+
+// What the softmax of one row yields.  e[] is consumed (zeroed where absent);
+// bit k of negm is leaky_relu's negative branch of element k (backward).
+struct RowSoft {
+  float p[16];
+  uint32_t negm;
+  float cnt;
+  int kd;  // this lane's element index of the self loop, -1 if none
+};
+
+// general: a rowmask is given (absent edges are selected away); otherwise
+// every off-diagonal source below n is an edge.
+__device__ __forceinline__ void row_softmax(RowSoft& S, float (&e)[16], const LaneConst& K,
+                                            float ad, int i, int n, int q, bool general,
+                                            const uint32_t* __restrict__ rowmask, int64_t grow,
+                                            bool has_ae, float slope) {
+  const int kd = ((i >> 2) & 15) == q ? 4 * (i >> 6) + (i & 3) : -1;
+  S.kd = kd;
+  float esum = 0.f;
+  uint32_t valid;
+  if (general) {
+    uint32_t pres = 0u;
+    const int W = (n + 31) >> 5;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int j = src_of(q, k);
+      bool pr = i < n && j < n && j != i;
+      if (rowmask && pr) pr = (rowmask[grow * W + (j >> 5)] >> (j & 31)) & 1u;
+      pres |= (pr ? 1u : 0u) << k;
+    }
+    valid = pres | (kd >= 0 ? (1u << kd) : 0u);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      e[k] = ((pres >> k) & 1u) ? e[k] : 0.f;
+      esum += e[k];
+    }
+    S.cnt = row16_sum((float)__popc(pres));
+  } else {
+    // sources past n and the (never stored) self slot load 0
+    valid = (1u << K.kmax) - 1u;
+    esum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) esum += e[k];
+    S.cnt = (float)(n - 1);
+  }
+  esum = row16_sum(esum);
+  const float loopv = (has_ae && S.cnt > 0.f) ? esum / S.cnt : 0.f;
+  float mx = -INFINITY;
+  S.negm = 0u;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    float v = K.as[k] + ad;
+    v += (k == kd) ? loopv : e[k];
+    const bool pos = v > 0.f;
+    S.negm |= pos ? 0u : (1u << k);
+    const float lr = pos ? v : v * slope;
+    const float s = ((valid >> k) & 1u) ? lr : -INFINITY;
+    S.p[k] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = row16_max(mx);
+  float den = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    S.p[k] = expf(S.p[k] - mx);  // exp(-inf) = 0 for masked sources
+    den += S.p[k];
+  }
+  den = row16_sum(den);
+  const float inv = 1.f / (den + 1e-16f);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) S.p[k] *= inv;
+}
+
+// keep[((g*H+h)*n + i)*n + j] of the lane's 16 sources (dropout on attention)
+__device__ __forceinline__ uint32_t keep_bits(const uint8_t* __restrict__ keep, int64_t base,
+                                              int i, int n, int q) {
+  uint32_t kb = 0u;
+  if (i < n) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int j = src_of(q, k);
+      if (j < n && keep[base + (int64_t)i * n + j]) kb |= 1u << k;
+    }
+  }
+  return kb;
+}
+
+// head plane h of a layer: the graph's slice (canonical order) or the whole
+// plane (edge-id map); a null plane reads 0 / drops stores
+__device__ __forceinline__ rsrc_t plane_rsrc(const float* planes, int64_t E,
+                                             const int32_t* eid, int64_t g, int h, int n) {
+  if (!planes) return make_rsrc(nullptr, 0u);
+  const float* p = planes + (int64_t)h * E;
+  if (eid) return make_rsrc(p, (uint32_t)(4 * E));
+  const int64_t E0 = (int64_t)n * (n - 1);
+  return make_rsrc(p + g * E0, (uint32_t)(4 * E0));
+}
+
+// d(edge logit) rows of target block [i0, i0+TB), staged in s[r][j] (row
+// stride PS), to the canonical-order plane slice: the block is cut into 16x16
+// source tiles, tile k = t>>4 served by 16 threads (q = t&15):
+//   above the block's diagonal tile: element m = (r = m, j = 16k+q) -> lanes along j
+//   at or below it:                  element m = (r = q, j = 16k+m) -> lanes along i
+// so every store instruction writes 16-lane runs of consecutive ids (64 B).
+__device__ __forceinline__ void store_block_dae(const float* __restrict__ sl, int PS, int i0,
+                                                int t, rsrc_t rdae, int n, int U, int NP) {
   const int k = t >> 4, q = t & 15;
-  r = along_j ? m : q;
-  j = 16 * k + (along_j ? q : m);
-}
-__device__ __forceinline__ bool tile_along_j(int t, int i0, bool has_eid) {
-  return has_eid || (t >> 4) > (i0 >> 4);
-}
-
-// canonical in-graph id of (i <- j), or -1 when the pair is not an edge slot
-__device__ __forceinline__ int canon_id(int n, int U, int i, int j) {
-  if (i >= n || j >= n || i == j) return -1;
-  return j > i ? U + tri_off(n, i) + (j - i - 1) : tri_off(n, j) + (i - j - 1);
-}
-
-struct BlockLoad {
-  float v[TB];
-  uint32_t valid;  // bit m: element m is a present edge
-};
-
-__device__ __forceinline__ void load_block(BlockLoad& L, int i0, int t,
-                                           const float* __restrict__ ae,
-                                           const int32_t* __restrict__ eid,
-                                           const uint32_t* __restrict__ rowmask, int64_t g, int n) {
-  const int W = (n + 31) >> 5;
-  const bool aj = tile_along_j(t, i0, eid != nullptr);
-  L.valid = 0u;
-  if (eid) {
+  if (16 * k >= NP) return;
+  const bool along_j = k > (i0 >> 4);
 #pragma unroll
-    for (int m = 0; m < TB; ++m) {
-      int r, j;
-      tile_elem(t, m, aj, r, j);
-      const int i = i0 + r;
-      int e = -1;
-      if (i < n && j < n && j != i) e = eid[(g * n + i) * n + j];
-      L.v[m] = (e >= 0 && ae) ? ae[e] : 0.f;
-      L.valid |= (e >= 0 ? 1u : 0u) << m;
-    }
-    return;
-  }
-  const int64_t E0 = (int64_t)n * (n - 1);
-  const int U = (n * (n - 1)) / 2;
-  const rsrc_t rs = make_rsrc(ae ? ae + g * E0 : nullptr, ae ? (uint32_t)(E0 * 4) : 0u);
-#pragma unroll
-  for (int m = 0; m < TB; ++m) {
-    int r, j;
-    tile_elem(t, m, aj, r, j);
+  for (int m = 0; m < 16; ++m) {
+    const int r = along_j ? m : q, j = 16 * k + (along_j ? q : m);
     const int i = i0 + r;
-    const int id = canon_id(n, U, i, j);
-    const bool ok = id >= 0 && mask_bit(rowmask, g * n + i, W, j);
-    L.v[m] = bld(rs, ok ? 4 * id : OOB);
-    L.valid |= (ok ? 1u : 0u) << m;
+    const int id = logit_id(nullptr, 0, U + tri_off(n, i) - i - 1, i, j, n);
+    bst(rdae, id >= 0 ? 4 * id : OOB, sl[r * PS + j]);
   }
 }
 
-__device__ __forceinline__ void stage_block(const BlockLoad& L, float* __restrict__ sE, int SE,
-                                            int i0, int t, bool has_eid, int NP) {
-  const bool aj = tile_along_j(t, i0, has_eid);
-  if ((t >> 4) < NP / 16) {
+__device__ __forceinline__ void store_row4(float* __restrict__ dst, int NP, int q, bool rv,
+                                           const float (&v)[16]) {
 #pragma unroll
-    for (int m = 0; m < TB; ++m) {
-      int r, j;
-      tile_elem(t, m, aj, r, j);
-      sE[r * SE + j] = ((L.valid >> m) & 1u) ? L.v[m] : -INFINITY;
-    }
-  }
-}
-
-// d(edge logit) of one target block, staged in sE[r][j] by the rows phase,
-// written to the head plane through the same tile mapping (canonical order,
-// present edges only; other slots go to an out-of-range offset and drop).
-__device__ __forceinline__ void store_block_dae(const float* __restrict__ sE, int SE, int i0,
-                                                int t, float* __restrict__ dae,
-                                                const uint32_t* __restrict__ rowmask, int64_t g,
-                                                int n, int NP) {
-  const int W = (n + 31) >> 5;
-  const int64_t E0 = (int64_t)n * (n - 1);
-  const int U = (n * (n - 1)) / 2;
-  const bool aj = tile_along_j(t, i0, false);
-  const rsrc_t rs = make_rsrc(dae + g * E0, (uint32_t)(E0 * 4));
-  if ((t >> 4) < NP / 16) {
-#pragma unroll
-    for (int m = 0; m < TB; ++m) {
-      int r, j;
-      tile_elem(t, m, aj, r, j);
-      const int i = i0 + r;
-      const int id = canon_id(n, U, i, j);
-      const bool ok = id >= 0 && mask_bit(rowmask, g * n + i, W, j);
-      bst(rs, ok ? 4 * id : OOB, sE[r * SE + j]);
-    }
-  }
-}
-
-__device__ __forceinline__ int64_t edge_index_of(const int32_t* __restrict__ eid, int64_t g,
-                                                 int n, int i, int j) {
-  return eid ? (int64_t)eid[(g * n + i) * n + j]
-             : g * ((int64_t)n * (n - 1)) + canon_eid(n, i, j);
-}
-
-// Softmax of RPW target rows at once (independent rows share every reduction
-// round).  Lane owns sources j = lane + 64q.  On return p[rr][q] is the
-// probability (0 where invalid), neg[rr][q] the leaky-negative flag,
-// present[rr][q] whether edge j->i exists, cnt[rr] the in-degree.
-struct Rows {
-  float p[RPW][4];
-  bool neg[RPW][4];
-  bool present[RPW][4];
-  float cnt[RPW];
-};
-
-__device__ __forceinline__ void rows_softmax(Rows& R, const float* __restrict__ sE, int SE,
-                                             const float* __restrict__ sA,
-                                             const float* __restrict__ sD, int rb, int i0, int n,
-                                             int NP, bool has_ae, float slope, int lane) {
-  float e[RPW][4], red[2 * RPW];
-#pragma unroll
-  for (int rr = 0; rr < RPW; ++rr) {
-    float es = 0.f, c = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = lane + 64 * q;
-      const float ev = j < NP ? sE[(rb + rr) * SE + j] : -INFINITY;
-      const bool pr = ev != -INFINITY;
-      R.present[rr][q] = pr;
-      e[rr][q] = pr ? ev : 0.f;
-      es += e[rr][q];
-      c += pr ? 1.f : 0.f;
-    }
-    red[rr] = es;
-    red[RPW + rr] = c;
-  }
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1)
-#pragma unroll
-    for (int k = 0; k < 2 * RPW; ++k) red[k] += __shfl_xor(red[k], m, 64);
-  float mx[RPW], s[RPW][4];
-#pragma unroll
-  for (int rr = 0; rr < RPW; ++rr) {
-    const int i = i0 + rb + rr;
-    R.cnt[rr] = red[RPW + rr];
-    const float loopv = (has_ae && R.cnt[rr] > 0.f) ? red[rr] / R.cnt[rr] : 0.f;
-    const float ad = i < n ? sD[i] : 0.f;
-    mx[rr] = -INFINITY;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = lane + 64 * q;
-      const bool valid = i < n && (R.present[rr][q] || j == i);
-      float v = (j < NP ? sA[j] : 0.f) + ad;
-      v += (j == i) ? loopv : e[rr][q];
-      R.neg[rr][q] = !(v > 0.f);
-      const float lr = R.neg[rr][q] ? v * slope : v;
-      s[rr][q] = valid ? lr : -INFINITY;
-      mx[rr] = fmaxf(mx[rr], s[rr][q]);
-    }
-  }
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1)
-#pragma unroll
-    for (int rr = 0; rr < RPW; ++rr) mx[rr] = fmaxf(mx[rr], __shfl_xor(mx[rr], m, 64));
-  float den[RPW];
-#pragma unroll
-  for (int rr = 0; rr < RPW; ++rr) {
-    den[rr] = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      s[rr][q] = (s[rr][q] == -INFINITY) ? 0.f : expf(s[rr][q] - mx[rr]);
-      den[rr] += s[rr][q];
-    }
-  }
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1)
-#pragma unroll
-    for (int rr = 0; rr < RPW; ++rr) den[rr] += __shfl_xor(den[rr], m, 64);
-#pragma unroll
-  for (int rr = 0; rr < RPW; ++rr) {
-    const float inv = den[rr] + 1e-16f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) R.p[rr][q] = s[rr][q] / inv;
+  for (int c = 0; c < 4; ++c) {
+    const int j0 = 64 * c + 4 * q;
+    if (j0 < NP)
+      *reinterpret_cast<f4*>(dst + j0) =
+          rv ? f4{v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]} : f4{0.f, 0.f, 0.f, 0.f};
   }
 }
 
 // ---------------------------------------------------------------------------
 // forward
-// LDS: sX [NP][XS] | sP [TB][PS] | sA [NP] | sD [NP] | sE [TB][NP] (aliased by
-//      the K-split partials sR [4][TB][CW] after the rows phase)
+// LDS: sXT [CW][XT] xs_hᵀ (B operand, b128 along sources) | sP [TB][PS] P rows
+//      (A operand, b128 along sources) | sR [4][CW][SRS] K-split partials,
+//      column-major (one 16-B store per tile: the row-major scalar form was
+//      miscompiled into ds_write2 with wrong offsets by this toolchain at CT = 4)
 // ---------------------------------------------------------------------------
 template <int ACT, bool CONCAT, int CT>
 __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
@@ -304,61 +286,56 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
     float* __restrict__ out, int n, int H, int C, float slope) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int CW = 16 * CT;
-  constexpr int XS = pad32(CW, 16);  // B operand: row = lane>>4
+  constexpr int SRS = TB + 4;
   const int NP = round_up(n, 16);
-  const int PS = pad32(NP, 2);       // A operand: row = lane&15
-  float* sX = smem;               // [NP][XS]
-  float* sP = sX + NP * XS;       // [TB][PS]
-  float* sA = sP + TB * PS;       // [NP]
-  float* sD = sA + NP;            // [NP]
-  const int SE = NP + 1;          // conflict-free column-wise tile writes
-  float* sE = sD + NP;            // [TB][SE], max(TB*SE, 4*CW*SRS) floats
-  float* sR = sE;                 // [4][CW][SRS], after the rows phase
+  const int XT = NP + 4, PS = NP + 4;
+  float* sXT = smem;              // [CW][XT]
+  float* sP = sXT + CW * XT;      // [TB][PS]
+  float* sR = sP + TB * PS;       // [4][CW][SRS]
 
   int64_t g;
   int h;
   block_gh(H, g, h);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int gq = lane >> 4, q = lane & 15;
   const int64_t row0 = g * n;
   const int HC = H * C;
-  const float* ae = ae_planes ? ae_planes + (int64_t)h * E : nullptr;
+  const bool general = rowmask != nullptr;
+  const bool has_ae = ae_planes != nullptr;
+  const rsrc_t rae = plane_rsrc(ae_planes, E, eid, g, h, n);
+  const rsrc_t rxs = make_rsrc(xs + row0 * ldx, (uint32_t)(4 * n * ldx));
+  const int U = (n * (n - 1)) / 2;
 
-  BlockLoad L;
-  load_block(L, 0, t, ae, eid, rowmask, g, n);
+  LaneConst K;
+  init_lane_const(K, rxs, n, q, ldx, HC + h);
+  RowIn R;
+  load_row(R, rae, rxs, K, eid, (row0 + wave * 4 + gq) * n, wave * 4 + gq, n, U, q, HC + H + h,
+           ldx);
   for (int idx = t; idx < NP * CW; idx += TT) {
     const int j = idx / CW, c = idx - j * CW;
-    sX[j * XS + c] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
+    sXT[c * XT + j] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
   }
-  for (int j = t; j < NP; j += TT) {
-    sA[j] = j < n ? xs[(row0 + j) * ldx + HC + h] : 0.f;
-    sD[j] = j < n ? xs[(row0 + j) * ldx + HC + H + h] : 0.f;
-  }
+  const int64_t kbase = (g * H + h) * (int64_t)n * n;
 
   const int li = lane & 15, lk = lane >> 4;
-  const int kq = NP / 4;  // K-split: wave w sums sources [w*kq, (w+1)*kq)
+  const int kq = NP / 4;  // K-split: wave w sums sources [w*kq, (w+1)*kq), kq % 4 == 0
   for (int i0 = 0; i0 < n; i0 += TB) {
-    stage_block(L, sE, SE, i0, t, eid != nullptr, NP);
-    __syncthreads();
-    if (i0 + TB < n) load_block(L, i0 + TB, t, ae, eid, rowmask, g, n);
-    // ---- P rows: wave w owns rows [4w, 4w+4) of the block ----
+    const int r = wave * 4 + gq, i = i0 + r;
+    // ---- softmax of row i (16-lane group), P -> sP ----
     {
-      const int rb = wave * RPW;
-      Rows R;
-      rows_softmax(R, sE, SE, sA, sD, rb, i0, n, NP, ae != nullptr, slope, lane);
+      float e[16];
+      unpack(e, R);
+      const float ad = R.ad;
+      if (i0 + TB < n)
+        load_row(R, rae, rxs, K, eid, (row0 + i + TB) * n, i + TB, n, U, q, HC + H + h, ldx);
+      RowSoft S;
+      row_softmax(S, e, K, ad, i, n, q, general, rowmask, row0 + i, has_ae, slope);
+      if (keep) {
+        const uint32_t kb = keep_bits(keep, kbase, i, n, q);
 #pragma unroll
-      for (int rr = 0; rr < RPW; ++rr) {
-        const int i = i0 + rb + rr;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int j = lane + 64 * q;
-          if (j < NP) {
-            float pd = R.p[rr][q];
-            if (keep && i < n && j < n)
-              pd = keep[((g * H + h) * n + i) * n + j] ? pd * keep_scale : 0.f;
-            sP[(rb + rr) * PS + j] = pd;
-          }
-        }
+        for (int k = 0; k < 16; ++k) S.p[k] = ((kb >> k) & 1u) ? S.p[k] * keep_scale : 0.f;
       }
+      store_row4(sP + r * PS, NP, q, i < n, S.p);
     }
     __syncthreads();
     // ---- out[i][c] = Σ_j P[i][j] xs_h[j][c], K split over the 4 waves ----
@@ -366,37 +343,43 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
       f4 acc[CT];
 #pragma unroll
       for (int b = 0; b < CT; ++b) acc[b] = f4{0.f, 0.f, 0.f, 0.f};
-      const float* pa = sP + li * PS + lk;
-      for (int k = wave * kq; k < (wave + 1) * kq; k += 4) {
-        const float a = pa[k];
+      // lane (li, lk) feeds k = k0 + 4lk + s at MFMA step s of a 16-wide k
+      // chunk (every k of the chunk once: the order of the sum is permuted)
+      for (int k0 = wave * kq; k0 < (wave + 1) * kq; k0 += 16) {
+        const int kk = min(k0 + 4 * lk, NP - 4);
+        const bool kin = k0 + 4 * lk < (wave + 1) * kq;
+        const f4 a = kin ? *reinterpret_cast<const f4*>(sP + li * PS + kk) : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int b = 0; b < CT; ++b)
-          acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, sX[(k + lk) * XS + 16 * b + li],
-                                                        acc[b], 0, 0, 0);
+        for (int b = 0; b < CT; ++b) {
+          const f4 bb = *reinterpret_cast<const f4*>(sXT + (16 * b + li) * XT + kk);
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bb.x, acc[b], 0, 0, 0);
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bb.y, acc[b], 0, 0, 0);
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bb.z, acc[b], 0, 0, 0);
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bb.w, acc[b], 0, 0, 0);
+        }
       }
-      // partials column-major [wave][c][row]: one 16-B store per tile (the
-      // row-major scalar form was miscompiled into ds_write2 with wrong
-      // offsets by this toolchain at CT = 4)
+      // D layout: acc[b][rr] = out[row 4lk + rr][col 16b + li]
 #pragma unroll
       for (int b = 0; b < CT; ++b)
         *reinterpret_cast<f4*>(sR + (wave * CW + 16 * b + li) * SRS + 4 * lk) = acc[b];
     }
     __syncthreads();
     for (int idx = t; idx < TB * CW; idx += TT) {
-      const int r = idx / CW, c = idx - r * CW;
-      const int i = i0 + r;
-      if (i < n && c < C) {
-        const float* q = sR + c * SRS + r;
-        const float v = (q[0] + q[CW * SRS]) + (q[2 * CW * SRS] + q[3 * CW * SRS]);
+      const int rr = idx / CW, c = idx - rr * CW;
+      const int ii = i0 + rr;
+      if (ii < n && c < C) {
+        const float* pr = sR + c * SRS + rr;
+        const float v = (pr[0] + pr[CW * SRS]) + (pr[2 * CW * SRS] + pr[3 * CW * SRS]);
         if (CONCAT) {
           const float b = bias ? bias[h * C + c] : 0.f;
-          out[(row0 + i) * HC + h * C + c] = act_fwd<ACT>(v + b);
+          out[(row0 + ii) * HC + h * C + c] = act_fwd<ACT>(v + b);
         } else {
-          out[(row0 + i) * HC + h * C + c] = v;  // workspace, per head
+          out[(row0 + ii) * HC + h * C + c] = v;  // workspace, per head
         }
       }
     }
-    __syncthreads();
+    // sP is rewritten only after every wave passed this block's second
+    // barrier; sR only after the next block's first
   }
 }
 
@@ -423,11 +406,11 @@ __global__ __launch_bounds__(256) void k_head_mean(const float* __restrict__ ws,
 //   dS = P ⊙ (dP − Σ_j P dP); dL = dS · leaky'(s);
 //   dae[i][j] = dL[i][j] + dL[i][i] / cnt  (present j),  a_d[i] += Σ_j dL,
 //   a_s[j] += Σ_i dL[i][j],  dxs_h[j] += Σ_i Pd[i][j] dOut[i]
-// LDS: sX [NP][XS] | sP [TB][PS] (Pd) | sL [TB][PS] (dP then dL) |
-//      sO [TB][OS] (dOut) | sA [NP] | sD [NP] | sDa [NP] | sE [TB][NP]
+// LDS: sX [NP][XR] xs_h rows (dPd's B, b128 along c) | sP [TB][PS] Pd rows |
+//      sL [TB][PS] dPd rows | sO [2][TB][OS] dOut (double-buffered)
 // ---------------------------------------------------------------------------
 template <int ACT, bool CONCAT, int CT>
-__global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
+__global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ xs,
     int ldx, const float* __restrict__ ae_planes, int64_t E, const int32_t* __restrict__ eid,
     const uint8_t* __restrict__ keep, float keep_scale, const uint32_t* __restrict__ rowmask,
@@ -435,179 +418,182 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
     int H, int C, float slope) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int CW = 16 * CT;
-  constexpr int XS = CW + 1;         // dP's B operand: row = lane&15
-  constexpr int OS = CW + 1;         // read both ways (dP's A, dxs's B)
+  constexpr int XR = CW + 4;
+  constexpr int OS = CW + 4;
   const int NP = round_up(n, 16);
-  const int PS = pad32(NP, 16);      // Pᵀ operand: row = lane>>4
-  float* sX = smem;               // [NP][XS]
-  float* sP = sX + NP * XS;       // [TB][PS]
+  const int PS = NP + 4;
+  float* sX = smem;               // [NP][XR]
+  float* sP = sX + NP * XR;       // [TB][PS]
   float* sL = sP + TB * PS;       // [TB][PS]
-  float* sO = sL + TB * PS;       // [TB][OS]
-  float* sA = sO + TB * OS;       // [NP]
-  float* sD = sA + NP;            // [NP]
-  float* sDa = sD + NP;           // [NP]
-  const int SE = NP + 1;          // conflict-free column-wise tile accesses
-  float* sE = sDa + NP;           // [TB][SE]: edge logits, then d(edge logit)
+  float* sO = sL + TB * PS;       // [2][TB][OS]
 
   int64_t g;
   int h;
   block_gh(H, g, h);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int gq = lane >> 4, q = lane & 15;
   const int64_t row0 = g * n;
   const int HC = H * C;
   const int OC = CONCAT ? HC : C;
   const int oc0 = CONCAT ? h * C : 0;
   const float oscale = CONCAT ? 1.f : 1.f / (float)H;
-  const float* ae = ae_planes ? ae_planes + (int64_t)h * E : nullptr;
-  float* dae = dae_planes ? dae_planes + (int64_t)h * E : nullptr;
+  const bool general = rowmask != nullptr;
+  const bool has_ae = ae_planes != nullptr;
+  const rsrc_t rae = plane_rsrc(ae_planes, E, eid, g, h, n);
+  const rsrc_t rdae = plane_rsrc(dae_planes, E, eid, g, h, n);
+  const int U = (n * (n - 1)) / 2;
+  const rsrc_t rxs = make_rsrc(xs + row0 * ldx, (uint32_t)(4 * n * ldx));
+  const rsrc_t rdy = make_rsrc(dy + row0 * OC, (uint32_t)(4 * n * OC));
+  const rsrc_t ry = make_rsrc(y + row0 * OC, (uint32_t)(4 * n * OC));
 
-  // dOut rows of the next block, prefetched in registers with its edge logits
-  // (a load issued after this block's dae stores would wait for all of them)
-  constexpr int OPT = TB * CW / TT;  // = CT
-  float pdy[OPT], py[OPT];
+  // dOut rows of a block: TB*CW values, CT per thread
+  float pdy[CT], py[CT];
   auto load_dout = [&](int i0n) {
 #pragma unroll
-    for (int m = 0; m < OPT; ++m) {
-      const int idx = t + TT * m, r = idx / CW, c = idx - r * CW, i = i0n + r;
-      const bool ok = i < n && c < C;
-      const int64_t o = ok ? (row0 + i) * OC + oc0 + c : 0;
-      pdy[m] = ok ? dy[o] : 0.f;
-      py[m] = ok ? y[o] : 0.f;
+    for (int m = 0; m < CT; ++m) {
+      const int idx = t + TT * m, rr = idx / CW, c = idx - rr * CW, ii = i0n + rr;
+      const int off = (ii < n && c < C) ? 4 * (ii * OC + oc0 + c) : OOB;
+      pdy[m] = bld(rdy, off);
+      py[m] = bld(ry, off);
     }
   };
-  BlockLoad L;
-  load_block(L, 0, t, ae, eid, rowmask, g, n);
+
+  LaneConst K;
+  init_lane_const(K, rxs, n, q, ldx, HC + h);
+  RowIn R;
+  load_row(R, rae, rxs, K, eid, (row0 + wave * 4 + gq) * n, wave * 4 + gq, n, U, q, HC + H + h,
+           ldx);
   load_dout(0);
   for (int idx = t; idx < NP * CW; idx += TT) {
     const int j = idx / CW, c = idx - j * CW;
-    sX[j * XS + c] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
+    sX[j * XR + c] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
   }
-  for (int j = t; j < NP; j += TT) {
-    sA[j] = j < n ? xs[(row0 + j) * ldx + HC + h] : 0.f;
-    sD[j] = j < n ? xs[(row0 + j) * ldx + HC + H + h] : 0.f;
-    sDa[j] = 0.f;
-  }
+  const int64_t kbase = (g * H + h) * (int64_t)n * n;
+
   // dxs accumulators: wave w owns row tiles jt = w, w+4, ... (NP/16 <= 16) x CT column tiles
-  constexpr int MAXJT = TILED_MAX_N / 16 / 4;  // 4 row tiles per wave
+  constexpr int MAXJT = TILED_MAX_N / 16 / 4;
   f4 dacc[MAXJT][CT];
 #pragma unroll
   for (int a = 0; a < MAXJT; ++a)
 #pragma unroll
     for (int b = 0; b < CT; ++b) dacc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+  float das[16];  // Σ_i dL[i][j] over this lane group's rows, per source of the lane
+#pragma unroll
+  for (int k = 0; k < 16; ++k) das[k] = 0.f;
   float dbias_acc = 0.f;  // thread t < C owns bias column t of this head's slice
   const int li = lane & 15, lk = lane >> 4;
   const int njt = NP / 16;
 
-  for (int i0 = 0; i0 < n; i0 += TB) {
-    // ---- stage: edge logits of this block (prefetched), dOut rows ----
-    stage_block(L, sE, SE, i0, t, eid != nullptr, NP);
+  int buf = 0;
+  for (int i0 = 0; i0 < n; i0 += TB, buf ^= 1) {
+    float* sOb = sO + buf * TB * OS;
+    // ---- stage dOut (prefetched) ----
 #pragma unroll
-    for (int m = 0; m < OPT; ++m) {
-      const int idx = t + TT * m, r = idx / CW, c = idx - r * CW;
-      sO[r * OS + c] = act_bwd<ACT>(pdy[m], py[m]) * oscale;
+    for (int m = 0; m < CT; ++m) {
+      const int idx = t + TT * m, rr = idx / CW, c = idx - rr * CW;
+      sOb[rr * OS + c] = act_bwd<ACT>(pdy[m], py[m]) * oscale;
     }
     __syncthreads();
-    if (i0 + TB < n) {
-      load_block(L, i0 + TB, t, ae, eid, rowmask, g, n);
-      load_dout(i0 + TB);
-    }
     if (t < C && (CONCAT || h == 0)) {
       float s = 0.f;
-      for (int r = 0; r < TB; ++r) s += sO[r * OS + t];
+      for (int rr = 0; rr < TB; ++rr) s += sOb[rr * OS + t];
       dbias_acc += s / oscale;  // = Σ dz
     }
     // ---- dPd[i][j] = Σ_c dOut[i][c] xs_h[j][c]: tiles over j, waves stride ----
     for (int jt = wave; jt < njt; jt += 4) {
       f4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* oa = sO + li * OS + lk;
-      const float* xb = sX + (16 * jt + li) * XS + lk;
 #pragma unroll
-      for (int k = 0; k < CW; k += 4)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(oa[k], xb[k], acc, 0, 0, 0);
+      for (int kb = 0; kb < CW; kb += 16) {
+        const f4 a = *reinterpret_cast<const f4*>(sOb + li * OS + kb + 4 * lk);
+        const f4 bb = *reinterpret_cast<const f4*>(sX + (16 * jt + li) * XR + kb + 4 * lk);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bb.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bb.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bb.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bb.w, acc, 0, 0, 0);
+      }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sL[(4 * lk + r) * PS + 16 * jt + li] = acc[r];
+      for (int rr = 0; rr < 4; ++rr) sL[(4 * lk + rr) * PS + 16 * jt + li] = acc[rr];
     }
     __syncthreads();
     // ---- rows: recompute P, softmax / leaky / dropout backward ----
     {
-      const int rb = wave * RPW;
-      Rows R;
-      rows_softmax(R, sE, SE, sA, sD, rb, i0, n, NP, ae != nullptr, slope, lane);
-      float dp[RPW][4], pd[RPW][4], red[3 * RPW];
-#pragma unroll
-      for (int rr = 0; rr < RPW; ++rr) {
-        const int i = i0 + rb + rr;
-        float dot = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int j = lane + 64 * q;
-          const float p = R.p[rr][q];
-          float d = (j < NP) ? sL[(rb + rr) * PS + j] : 0.f;
-          pd[rr][q] = p;
-          if (keep && i < n && j < n && (R.present[rr][q] || j == i)) {
-            const bool kp = keep[((g * H + h) * n + i) * n + j] != 0;
-            d = kp ? d * keep_scale : 0.f;
-            pd[rr][q] = kp ? p * keep_scale : 0.f;
-          }
-          dp[rr][q] = p != 0.f ? d : 0.f;
-          dot += p * dp[rr][q];
-        }
-        red[rr] = dot;
+      const int r = wave * 4 + gq, i = i0 + r;
+      const bool rv = i < n;
+      float e[16];
+      unpack(e, R);
+      const float ad = R.ad;
+      if (i0 + TB < n) {
+        load_row(R, rae, rxs, K, eid, (row0 + i + TB) * n, i + TB, n, U, q, HC + H + h, ldx);
+        load_dout(i0 + TB);
       }
+      RowSoft S;
+      row_softmax(S, e, K, ad, i, n, q, general, rowmask, row0 + i, has_ae, slope);
+      float d[16];
 #pragma unroll
-      for (int m = 32; m >= 1; m >>= 1)
-#pragma unroll
-        for (int k = 0; k < RPW; ++k) red[k] += __shfl_xor(red[k], m, 64);
-      float dl[RPW][4];
-#pragma unroll
-      for (int rr = 0; rr < RPW; ++rr) {
-        const int i = i0 + rb + rr;
-        float rsum = 0.f, dloop = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int j = lane + 64 * q;
-          const float ds = R.p[rr][q] * (dp[rr][q] - red[rr]);
-          dl[rr][q] = R.neg[rr][q] ? ds * slope : ds;
-          rsum += dl[rr][q];
-          if (j == i) dloop = dl[rr][q];
-        }
-        red[RPW + rr] = rsum;
-        red[2 * RPW + rr] = dloop;
+      for (int c = 0; c < 4; ++c) {
+        const int j0 = 64 * c + 4 * q;
+        const f4 v = j0 < NP ? *reinterpret_cast<const f4*>(sL + r * PS + j0)
+                             : f4{0.f, 0.f, 0.f, 0.f};
+        d[4 * c] = v.x;
+        d[4 * c + 1] = v.y;
+        d[4 * c + 2] = v.z;
+        d[4 * c + 3] = v.w;
       }
+      float pd[16];
+      if (keep) {
+        const uint32_t kb = keep_bits(keep, kbase, i, n, q);
 #pragma unroll
-      for (int m = 32; m >= 1; m >>= 1)
-#pragma unroll
-        for (int k = RPW; k < 3 * RPW; ++k) red[k] += __shfl_xor(red[k], m, 64);
-#pragma unroll
-      for (int rr = 0; rr < RPW; ++rr) {
-        const int r = rb + rr, i = i0 + r;
-        if (i < n && lane == 0) dxs[(row0 + i) * ldx + HC + H + h] = red[RPW + rr];  // d a_dst
-        const float dshare =
-            (ae && R.cnt[rr] > 0.f) ? red[2 * RPW + rr] / R.cnt[rr] : 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int j = lane + 64 * q;
-          if (j < NP) {
-            sP[r * PS + j] = pd[rr][q];
-            sL[r * PS + j] = dl[rr][q];
-          }
-          if (eid) {
-            if (dae && R.present[rr][q]) dae[edge_index_of(eid, g, n, i, j)] = dl[rr][q] + dshare;
-          } else if (j < NP) {
-            sE[r * SE + j] = dl[rr][q] + dshare;  // this wave's own rows of sE
-          }
+        for (int k = 0; k < 16; ++k) {
+          const bool kp = (kb >> k) & 1u;
+          d[k] = kp ? d[k] * keep_scale : 0.f;
+          pd[k] = kp ? S.p[k] * keep_scale : 0.f;
         }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) pd[k] = S.p[k];
       }
+      float dot = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) dot = fmaf(S.p[k], d[k], dot);
+      dot = row16_sum(dot);
+      float rsum = 0.f, dloop = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float ds = S.p[k] * (d[k] - dot);
+        const float dl = ((S.negm >> k) & 1u) ? ds * slope : ds;
+        d[k] = rv ? dl : 0.f;
+        rsum += d[k];
+        dloop = (k == S.kd) ? d[k] : dloop;
+        das[k] += d[k];
+      }
+      rsum = row16_sum(rsum);
+      dloop = row16_sum(dloop);  // one lane holds it, the others add 0
+      if (rv && q == 0) dxs[(row0 + i) * ldx + HC + H + h] = rsum;  // d a_dst
+      const float dshare = (has_ae && S.cnt > 0.f) ? dloop / S.cnt : 0.f;
+      // d(edge logit) of every present edge of the row: with an edge-id map
+      // straight from the lanes; in canonical order staged in this group's own
+      // sL row (its dPd was read above) and written tile-wise below
+      if (dae_planes && eid) {
+        const int W = (n + 31) >> 5;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int j = src_of(q, k);
+          int id = logit_id(eid, (row0 + i) * n, 0, i, j, n);
+          if (rowmask && id >= 0 && !((rowmask[(row0 + i) * W + (j >> 5)] >> (j & 31)) & 1u))
+            id = -1;
+          bst(rdae, id >= 0 ? 4 * id : OOB, d[k] + dshare);
+        }
+      } else if (dae_planes) {
+        float dv[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) dv[k] = d[k] + dshare;
+        store_row4(sL + r * PS, NP, q, rv, dv);
+      }
+      store_row4(sP + r * PS, NP, q, rv, pd);
     }
     __syncthreads();
-    if (dae && !eid) store_block_dae(sE, SE, i0, t, dae, rowmask, g, n, NP);
-    // ---- column sums of dL (d a_src) and dxs_h += Pdᵀ · dOut ----
-    for (int j = t; j < NP; j += TT) {
-      float s = 0.f;
-#pragma unroll
-      for (int r = 0; r < TB; ++r) s += sL[r * PS + j];
-      sDa[j] += s;
-    }
+    if (dae_planes && !eid) store_block_dae(sL, PS, i0, t, rdae, n, U, NP);
+    // ---- dxs_h += Pdᵀ · dOut ----
 #pragma unroll
     for (int a = 0; a < MAXJT; ++a) {
       const int jt = wave + 4 * a;
@@ -615,7 +601,7 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
         const float* pa = sP + lk * PS + 16 * jt + li;  // Pᵀ[j][i] = P[i][j]
 #pragma unroll
         for (int b = 0; b < CT; ++b) {
-          const float* ob = sO + lk * OS + 16 * b + li;
+          const float* ob = sOb + lk * OS + 16 * b + li;
 #pragma unroll
           for (int k = 0; k < TB; k += 4)
             dacc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[k * PS], ob[k * OS], dacc[a][b],
@@ -623,9 +609,28 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
         }
       }
     }
-    __syncthreads();
+    // sP / sL are rewritten only after the next block's first barrier, sO
+    // is double-buffered
   }
-  // ---- write dxs_h, d a_src, padding columns, bias partial ----
+  // ---- d a_src: sum das over the 4 lane groups of each wave, then the waves ----
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    das[k] += __shfl_xor(das[k], 16, 64);
+    das[k] += __shfl_xor(das[k], 32, 64);
+  }
+  __syncthreads();
+  float* sDa = sP;  // [4][NP] <= 2 * TB * PS floats (sP, sL are free now)
+  if (gq == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int j = src_of(q, k);
+      if (j < NP) sDa[wave * NP + j] = das[k];
+    }
+  }
+  __syncthreads();
+  for (int j = t; j < n; j += TT)
+    dxs[(row0 + j) * ldx + HC + h] = (sDa[j] + sDa[NP + j]) + (sDa[2 * NP + j] + sDa[3 * NP + j]);
+  // ---- write dxs_h, padding columns, bias partial ----
 #pragma unroll
   for (int a = 0; a < MAXJT; ++a) {
     const int jt = wave + 4 * a;
@@ -635,15 +640,14 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_bwd(
         const int c = 16 * b + li;
         if (c < C) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int j = 16 * jt + 4 * lk + r;
-            if (j < n) dxs[(row0 + j) * ldx + h * C + c] = dacc[a][b][r];
+          for (int rr = 0; rr < 4; ++rr) {
+            const int j = 16 * jt + 4 * lk + rr;
+            if (j < n) dxs[(row0 + j) * ldx + h * C + c] = dacc[a][b][rr];
           }
         }
       }
     }
   }
-  for (int j = t; j < n; j += TT) dxs[(row0 + j) * ldx + HC + h] = sDa[j];
   if (h == 0) {
     const int padc = ldx - HC - 2 * H;
     for (int idx = t; idx < n * padc; idx += TT) {
@@ -663,13 +667,13 @@ static int ct_of(int C) { return (C + 15) / 16; }
 
 static size_t tiled_fwd_lds(int n, int C) {
   const int CW = 16 * ct_of(C), NP = round_up(n, 16);
-  return sizeof(float) * ((size_t)NP * pad32(CW, 16) + (size_t)TB * pad32(NP, 2) + 2 * NP +
-                          std::max((size_t)TB * (NP + 1), (size_t)4 * CW * SRS));
+  return sizeof(float) *
+         ((size_t)CW * (NP + 4) + (size_t)TB * (NP + 4) + (size_t)4 * CW * (TB + 4));
 }
 static size_t tiled_bwd_lds(int n, int C) {
   const int CW = 16 * ct_of(C), NP = round_up(n, 16);
-  return sizeof(float) * ((size_t)NP * (CW + 1) + 2 * (size_t)TB * pad32(NP, 16) +
-                          (size_t)TB * (CW + 1) + 3 * (size_t)NP + (size_t)TB * (NP + 1));
+  return sizeof(float) * ((size_t)NP * (CW + 4) + 2 * (size_t)TB * (NP + 4) +
+                          2 * (size_t)TB * (CW + 4));
 }
 
 template <typename K>
@@ -685,6 +689,7 @@ static int check_tiled(int64_t B, int n, int H, int C, int ldx, int act) {
     return SV2N_ERR_SHAPE;
   if (ldx < H * C + 2 * H) return SV2N_ERR_SHAPE;
   if (B * H > 0x7fffffff) return SV2N_ERR_SHAPE;
+  if ((int64_t)n * ldx * 4 > 0x7fffffff) return SV2N_ERR_SHAPE;  // 32-bit buffer offsets
   return 0;
 }
 
@@ -732,6 +737,14 @@ extern "C" int64_t sv2n_gat_attn_tiled_workspace(int64_t num_graphs, int n, int 
   return concat ? 0 : num_graphs * n * (int64_t)heads * channels;
 }
 
+// planes are addressed with 32-bit byte offsets
+static int check_planes(const float* ae, int64_t num_edges, const int32_t* eid, int64_t B, int n) {
+  if (!ae) return 0;
+  if (!eid && num_edges != B * (int64_t)n * (n - 1)) return SV2N_ERR_SHAPE;
+  if (num_edges * 4 > 0x7fffff00LL) return SV2N_ERR_SHAPE;
+  return 0;
+}
+
 extern "C" int sv2n_gat_attn_tiled_fwd(const float* xs, int ldx, const float* ae,
                                        int64_t num_edges, const int32_t* eid,
                                        const uint32_t* rowmask, const float* bias,
@@ -743,7 +756,7 @@ extern "C" int sv2n_gat_attn_tiled_fwd(const float* xs, int ldx, const float* ae
   if (!xs || !y) return SV2N_ERR_ARG;
   const int C = channels;
   if (int rc = check_tiled(num_graphs, n, heads, C, ldx, act)) return rc;
-  if (ae && !eid && num_edges != num_graphs * (int64_t)n * (n - 1)) return SV2N_ERR_SHAPE;
+  if (int rc = check_planes(ae, num_edges, eid, num_graphs, n)) return rc;
   if (concat) {
     SV2N_TILED_ACT(tiled_fwd_launch, true, num_graphs, stream, xs, ldx, ae, num_edges, eid,
                    rowmask, bias, keep, keep_scale, y, n, heads, C, negative_slope)
@@ -775,7 +788,10 @@ extern "C" int sv2n_gat_attn_tiled_bwd(const float* dy, const float* y, const fl
   if (!dy || !y || !xs || !dxs || !dbias_partial) return SV2N_ERR_ARG;
   const int C = channels;
   if (int rc = check_tiled(num_graphs, n, heads, C, ldx, act)) return rc;
-  if (ae && !eid && num_edges != num_graphs * (int64_t)n * (n - 1)) return SV2N_ERR_SHAPE;
+  if (int rc = check_planes(ae, num_edges, eid, num_graphs, n)) return rc;
+  if (int rc = check_planes(dae, num_edges, eid, num_graphs, n)) return rc;
+  const int OC = concat ? heads * C : C;
+  if ((int64_t)n * OC * 4 > 0x7fffffff) return SV2N_ERR_SHAPE;
   if (concat) {
     SV2N_TILED_ACT(tiled_bwd_launch, true, num_graphs, stream, dy, y, xs, ldx, ae, num_edges,
                    eid, keep, keep_scale, rowmask, dxs, dae, dbias_partial, n, heads, C,
