@@ -197,6 +197,81 @@ def kernel_table(model, data, reps=50):
     return res
 
 
+def kernel_table_tiled(model, data, cfg, reps=10):
+    """C5 (32 < n <= 256): the tiled attention of layer 0 and the plane edge
+    passes, HIP events on the launch stream.  Algorithmic bytes: every logit
+    plane, xs row, output row read or written once per launch."""
+    from spotv2net_amd import ops
+    dev = data.x.device
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    n, H = cfg["n"], cfg["heads"]
+    N0 = data.x.shape[0]
+    B = N0 // n
+    L = len(model.gat_layers)
+    lib = ops._lib.load()
+    with torch.no_grad():
+        W0 = model.gat_layers[0].projection_weight().contiguous()
+        wf = torch.cat([c.edge_fold() for c in model.gat_layers], 1)
+    conv0 = model.gat_layers[0]
+    C = conv0.out_channels
+    ldx = (H * C + 2 * H + 3) // 4 * 4
+    xs0 = torch.zeros(N0, ldx, device=dev)
+    xs0[:, :W0.shape[0]] = ops.gemm_f32(data.x, True, W0, True, N0, W0.shape[0], data.x.shape[1])
+    E, D = data.edge_attr.shape
+    wfp, hp = ops.pad_columns(wf)
+    aes = [torch.empty(H, E, device=dev) for _ in range(L)]
+    ptrs = ops._lib.ptr_array([a.data_ptr() for a in aes])
+    y0 = torch.empty(N0, H * C, device=dev)
+    dy0 = torch.randn_like(y0)
+    dxs0 = torch.empty_like(xs0)
+    dae0 = torch.empty(L, H, E, device=dev)
+    dptrs = ops._lib.ptr_array([dae0[l].data_ptr() for l in range(L)])
+    dbp = torch.empty(B, H * C, device=dev)
+    ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hp)
+    ws = torch.empty(ws_n, device=dev)
+    dwf = torch.empty(D, hp, device=dev)
+
+    def edge_fwd():
+        lib.sv2n_edge_logits_fwd_planes(data.edge_attr.data_ptr(), E, D, wfp.data_ptr(), hp, ptrs,
+                                        L, H, sh)
+
+    def edge_bwd():
+        lib.sv2n_edge_logits_bwd_planes(data.edge_attr.data_ptr(), E, D, None, dptrs, L, H,
+                                        ws.data_ptr(), ws_n, dwf.data_ptr(), hp, sh)
+
+    def attn_fwd():
+        lib.sv2n_gat_attn_tiled_fwd(xs0.data_ptr(), ldx, aes[0].data_ptr(), E, None, None,
+                                    conv0.bias.data_ptr(), None, 1.0, y0.data_ptr(), None, 0, B,
+                                    n, H, C, 1, 1, 0.2, sh)
+
+    def attn_bwd():
+        lib.sv2n_gat_attn_tiled_bwd(dy0.data_ptr(), y0.data_ptr(), xs0.data_ptr(), ldx,
+                                    aes[0].data_ptr(), E, None, None, 1.0, None, dxs0.data_ptr(),
+                                    dae0[0].data_ptr(), dbp.data_ptr(), B, n, H, C, 1, 1, 0.2, sh)
+
+    plane, xsb, yb = 4.0 * H * E, 4.0 * N0 * ldx, 4.0 * N0 * H * C
+    rows = {
+        "edge_logits_fwd": (edge_fwd, "hbm", 4.0 * E * D + L * plane),
+        "edge_logits_bwd": (edge_bwd, "hbm", 4.0 * E * D + L * plane),
+        "gat_attn_tiled_fwd_l0": (attn_fwd, "hbm", plane + xsb + yb),
+        "gat_attn_tiled_bwd_l0": (attn_bwd, "hbm", 2 * plane + 2 * xsb + 2 * yb),
+    }
+    res = {}
+    for name, (fn, bound, nbytes) in rows.items():
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        res[name] = dict(avg_us=us, bound=bound, flops=0.0, bytes=nbytes, tflops=0.0,
+                         gbs=nbytes / us / 1e3, peak_tflops=None)
+    return res
+
+
 def roofline_entry(table, traffic=None):
     # dominant = largest time per training step (gemm rows run once per step at L0)
     name = max(table, key=lambda k: table[k]["avg_us"])
@@ -326,6 +401,9 @@ def main():
             table = kernel_table(model, data)
             kname, roof = roofline_entry(table)
             roof["traffic"] = load_traffic(kname)
+        elif not args.no_kernel_table and args.config == "c5":
+            table = kernel_table_tiled(model, data, cfg)
+            kname, roof = roofline_entry(table)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             # bounded sample: about as many edges as 512 C2 graphs

@@ -542,7 +542,7 @@ __global__ void k_block_eid(const int64_t* __restrict__ ei, int64_t E, int64_t N
 // ============================ C-ABI ========================================
 using namespace sv2n;
 
-static constexpr int EDGE_BWD_GRID = 512;
+static constexpr int EDGE_BWD_GRID = 768;
 static constexpr int EDGE_FWD_GRID = 1024;
 static constexpr int EDGE_SMALL_FWD_GRID = 4096;
 static constexpr int EDGE_SMALL_BWD_GRID = 1024;

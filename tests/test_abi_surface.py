@@ -36,7 +36,7 @@ def test_argument_errors_without_gpu():
     assert lib.sv2n_gat_attn_fwd(None, 8, None, None, None, None, 1.0, None, None, 1, 30, 4, 8,
                                  1, 1, 0.2, None) == -1
     assert lib.sv2n_gemm_f32(1, 1, None, 4, None, 4, None, 4, 4, 4, 4, None, 0, None) == -1
-    assert lib.sv2n_edge_logits_bwd_workspace(126, 8) == 512 * 126 * 8
+    assert lib.sv2n_edge_logits_bwd_workspace(126, 8) == 768 * 126 * 8
 
 
 def _ref_layer_dims(F, D, H, hidden, concat_heads):
