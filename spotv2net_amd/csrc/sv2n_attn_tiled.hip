@@ -110,12 +110,19 @@ __device__ __forceinline__ void init_lane_const(LaneConst& K, rsrc_t rxs, int n,
   }
 }
 
-// in-plane offset (floats) of (target i <- source j) or -1
-__device__ __forceinline__ int logit_id(const int32_t* __restrict__ eid, int64_t erow, int upb,
-                                        int i, int j, int n) {
-  if (i >= n || j >= n || j == i) return -1;
-  if (eid) return eid[erow + j];
-  return j > i ? upb + j : tri_off(n, j) - j - 1 + i;
+// in-plane offset (floats) of (target i <- source j) in canonical order, or
+// -1 for the self slot / past n.  Selects only: a divergent early return per
+// element made the compiler emit an exec-masked branch region per element.
+__device__ __forceinline__ int canon_logit_id(int upb, int i, int j, int n) {
+  const int id = j > i ? upb + j : tri_off(n, j) - j - 1 + i;
+  return (i < n && j < n && j != i) ? id : -1;
+}
+// the same through an edge-id map row (erow = (g*n + i)*n)
+__device__ __forceinline__ int eid_logit_id(const int32_t* __restrict__ eid, int64_t erow, int i,
+                                            int j, int n) {
+  const bool ok = i < n && j < n && j != i;
+  const int e = eid[erow + (ok ? j : 0)];
+  return ok ? e : -1;
 }
 
 // One target row's inputs, loaded one block ahead.
@@ -129,10 +136,15 @@ struct RowIn {
 __device__ __forceinline__ void load_row(RowIn& R, rsrc_t rae, rsrc_t rxs, const LaneConst& K,
                                          const int32_t* __restrict__ eid, int64_t erow, int i,
                                          int n, int U, int q, int adoff, int ldx) {
-  const int upb = U + tri_off(n, i) - i - 1;
   int id[16];
+  if (eid) {
 #pragma unroll
-  for (int k = 0; k < 16; ++k) id[k] = logit_id(eid, erow, upb, i, src_of(q, k), n);
+    for (int k = 0; k < 16; ++k) id[k] = eid_logit_id(eid, erow, i, src_of(q, k), n);
+  } else {
+    const int upb = U + tri_off(n, i) - i - 1;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) id[k] = canon_logit_id(upb, i, src_of(q, k), n);
+  }
 #pragma unroll
   for (int k = 0; k < 16; ++k) R.e[k] = bld(rae, id[k] >= 0 ? 4 * id[k] : OOB);
   R.ad = bld(rxs, i < n ? 4 * (i * ldx + adoff) : OOB);
@@ -168,9 +180,9 @@ __device__ __forceinline__ void row_softmax(RowSoft& S, float (&e)[16], const La
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int j = src_of(q, k);
-      bool pr = i < n && j < n && j != i;
-      if (rowmask && pr) pr = (rowmask[grow * W + (j >> 5)] >> (j & 31)) & 1u;
-      pres |= (pr ? 1u : 0u) << k;
+      const bool in = i < n && j < n && j != i;
+      const uint32_t w = rowmask ? rowmask[grow * W + (in ? (j >> 5) : 0)] : ~0u;
+      pres |= ((in && ((w >> (j & 31)) & 1u)) ? 1u : 0u) << k;
     }
     valid = pres | (kd >= 0 ? (1u << kd) : 0u);
 #pragma unroll
@@ -255,7 +267,7 @@ __device__ __forceinline__ void store_block_dae(const float* __restrict__ sl, in
   for (int m = 0; m < 16; ++m) {
     const int r = along_j ? m : q, j = 16 * k + (along_j ? q : m);
     const int i = i0 + r;
-    const int id = logit_id(nullptr, 0, U + tri_off(n, i) - i - 1, i, j, n);
+    const int id = canon_logit_id(U + tri_off(n, i) - i - 1, i, j, n);
     bst(rdae, id >= 0 ? 4 * id : OOB, sl[r * PS + j]);
   }
 }
@@ -574,13 +586,10 @@ __global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
       // straight from the lanes; in canonical order staged in this group's own
       // sL row (its dPd was read above) and written tile-wise below
       if (dae_planes && eid) {
-        const int W = (n + 31) >> 5;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-          const int j = src_of(q, k);
-          int id = logit_id(eid, (row0 + i) * n, 0, i, j, n);
-          if (rowmask && id >= 0 && !((rowmask[(row0 + i) * W + (j >> 5)] >> (j & 31)) & 1u))
-            id = -1;
+          // eid holds -1 for absent edges (rowmask agrees)
+          const int id = eid_logit_id(eid, (row0 + i) * n, i, src_of(q, k), n);
           bst(rdae, id >= 0 ? 4 * id : OOB, d[k] + dshare);
         }
       } else if (dae_planes) {
