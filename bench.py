@@ -35,6 +35,7 @@ F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32, de
 # the split GEMM computes each f32 product as 6 bf16 MFMA products: its
 # f32-equivalent ceiling is the dense bf16 MFMA peak (~2.5 PF) / 6
 BF16X3_PEAK_TFLOPS = round(2500.0 / 6, 1)
+BF16_MFMA_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (no sparsity)
 
 S, N_NODES, HEADS, HIDDEN, BATCH = 42, 30, 4, [100, 50], 512
 
@@ -42,16 +43,20 @@ S, N_NODES, HEADS, HIDDEN, BATCH = 42, 30, 4, [100, 50], 512
 # driver's default run); the others are measured with --config.
 CONFIGS = {
     "c1": dict(S=42, n=30, heads=1, hidden=[500], concat=False, batch=32, dropout_att=0.0,
+               dropout=0.0,
                desc="C1: 1 GAT layer, 1 head, hidden [500], 30-node dense graphs, S=42"),
     "c2": dict(S=42, n=30, heads=4, hidden=[100, 50], concat=True, batch=512, dropout_att=0.0,
+               dropout=0.0,
                desc="C2 train step (fwd+MSE+bwd+Adam): 30-node dense GAT graphs, "
                     "870 edges + self loops, seq_length 42 (F=1260, D=126), "
                     "GAT [100,50] x 4 heads concat, relu"),
-    "c3": dict(S=42, n=30, heads=6, hidden=[500], concat=True, batch=128, dropout_att=0.1,
+    # config/GNN_param.yaml:26-39 as-is: dropout_att 0.0, dropout 0.1
+    "c3": dict(S=42, n=30, heads=6, hidden=[500], concat=True, batch=128, dropout_att=0.0,
+               dropout=0.1,
                desc="C3: config/GNN_param.yaml model (S=42, hidden [500], 6 heads, "
-                    "dropout_att 0.1, batch 128), fp32"),
+                    "dropout_att 0.0, dropout 0.1, batch 128)"),
     "c5": dict(S=4, n=256, heads=8, hidden=[16, 16, 16], concat=True, batch=1024,
-               dropout_att=0.0,
+               dropout_att=0.0, dropout=0.0,
                desc="C5 stress: 256-node dense graphs (65,280 edges), S=4 (F=1024, D=12), "
                     "3 GAT layers [16,16,16] x 8 heads concat"),
 }
@@ -62,8 +67,8 @@ def build_model(dev, cfg=None):
     cfg = cfg or CONFIGS["c2"]
     torch.manual_seed(5154)  # config/GNN_param.yaml:23
     return GATModel(cfg["n"] * cfg["S"], 3 * cfg["S"], cfg["heads"], 1, cfg["hidden"],
-                    dropout_att=cfg["dropout_att"], concat_heads=cfg["concat"],
-                    activation="relu", negative_slope=0.2).to(dev)
+                    dropout_att=cfg["dropout_att"], dropout=cfg["dropout"],
+                    concat_heads=cfg["concat"], activation="relu", negative_slope=0.2).to(dev)
 
 
 def time_replays(fn, k, sync_group=True):
@@ -105,12 +110,20 @@ def kernel_table(model, data, reps=50):
     N0 = x0.shape[0]
     xs0 = ops.gemm_f32(x0, True, W[0], True, N0, W[0].shape[0], x0.shape[1])
     conv0 = model.gat_layers[0]
-    ae = ops._EdgeLogits.apply(data.edge_attr, wf, layout, L, HEADS)
-    y0 = torch.empty(N0, conv0.out_dim, device=dev)
-    ps0 = torch.empty(B, HEADS, 32, 32, device=dev)
     lib = ops._lib.load()
     sh = stream.cuda_stream
     E, D = data.edge_attr.shape
+    wfp, hp = ops.pad_columns(wf)
+    ae = [torch.empty(B, N_NODES, N_NODES, HEADS, device=dev) for _ in range(L)]
+    ptrs = ops._lib.ptr_array([a.data_ptr() for a in ae])
+
+    def edge_fwd():
+        lib.sv2n_edge_logits_fwd(data.edge_attr.data_ptr(), E, D, None, layout.canon.data_ptr(),
+                                 wfp.data_ptr(), hp, ptrs, L, HEADS, B, N_NODES, sh)
+
+    edge_fwd()
+    y0 = torch.empty(N0, conv0.out_dim, device=dev)
+    ps0 = torch.empty(B, HEADS, 32, 32, device=dev)
 
     def attn_fwd():
         lib.sv2n_gat_attn_fwd(xs0.data_ptr(), xs0.stride(0), ae[0].data_ptr(), None,
@@ -127,14 +140,6 @@ def kernel_table(model, data, reps=50):
                               ps0.data_ptr(), None, 1.0, None, dxs0.data_ptr(), dae0.data_ptr(),
                               dbp.data_ptr(), B, N_NODES, HEADS, conv0.out_channels, 1, 1, 0.2,
                               sh)
-
-    wfp, hp = ops.pad_columns(wf)
-    aeb = [torch.empty_like(a) for a in ae]
-    ptrs = ops._lib.ptr_array([a.data_ptr() for a in aeb])
-
-    def edge_fwd():
-        lib.sv2n_edge_logits_fwd(data.edge_attr.data_ptr(), E, D, None, layout.canon.data_ptr(),
-                                 wfp.data_ptr(), hp, ptrs, L, HEADS, B, N_NODES, sh)
 
     ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hp)
     ws = torch.empty(ws_n, device=dev)
@@ -300,48 +305,114 @@ def load_traffic(kernel):
 # --------------------------------------------------------------------------
 # CPU baseline: PyG-semantics oracle, same model/config, host cores
 # --------------------------------------------------------------------------
-def cpu_baseline(model, budget_s: float, batch: int, cfg=None):
-    from oracle.pyg_gatconv import OracleGATModel
-    from spotv2net_amd import Data, synthetic_batch
-    cfg = cfg or CONFIGS["c2"]
-    cores = min(os.cpu_count() or 1, int(os.environ.get("SV2N_CPU_THREADS", "16")))
-    torch.set_num_threads(cores)
-    ref = OracleGATModel(cfg["n"] * cfg["S"], 3 * cfg["S"], cfg["heads"], 1, cfg["hidden"],
-                         dropout_att=cfg["dropout_att"], concat_heads=cfg["concat"])
-    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
-    data = synthetic_batch(batch, cfg["S"], n=cfg["n"], seed=4321)
-    d = Data(x=data.x, edge_index=data.edge_index, edge_attr=data.edge_attr)
-    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+def usable_cores() -> int:
+    """CPUs this process may actually run on: the affinity mask, further
+    capped by a cgroup-v2 CPU quota when one is set (a GPU box's share of a
+    large host; os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, int(n or 1))
 
-    def step():
-        out = ref(d)
-        loss = torch.nn.functional.mse_loss(out, data.y_x)
-        opt.zero_grad()
-        loss.backward()
-        opt.step()
 
-    step()  # warm-up
-    steps, t0 = 0, time.perf_counter()
-    while True:
-        step()
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or steps >= 20:
-            break
-    gps = steps * batch / el
-    cpu_name = platform.processor() or "cpu"
+def _cpu_name() -> str:
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu_name = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": round(gps, 2), "unit": "graphs/s", "cores": cores, "kind": "port",
+    return platform.processor() or "cpu"
+
+
+def _cpu_rate(cfg, state, batch: int, train: bool, warmup: int = 3, steps: int = 20,
+              seed: int = 4321) -> float:
+    """SURVEY §8(d) CPU protocol: the oracle GATModel with PyG 2.3.0's
+    unfolded op sequence (lin_edge materialised, scatter softmax, index_add
+    aggregation), `warmup` + `steps` iterations timed with perf_counter."""
+    from oracle.pyg_gatconv import OracleGATModel
+    from spotv2net_amd import Data, synthetic_batch
+    ref = OracleGATModel(cfg["n"] * cfg["S"], 3 * cfg["S"], cfg["heads"], 1, cfg["hidden"],
+                         dropout_att=cfg["dropout_att"], dropout=cfg["dropout"],
+                         concat_heads=cfg["concat"])
+    if state is not None:
+        ref.load_state_dict(state)
+    data = synthetic_batch(batch, cfg["S"], n=cfg["n"], seed=seed)
+    d = Data(x=data.x, edge_index=data.edge_index, edge_attr=data.edge_attr)
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    ref.train(train)
+
+    def step():
+        if train:
+            loss = torch.nn.functional.mse_loss(ref(d), data.y_x)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+        else:
+            with torch.no_grad():
+                ref(d)
+
+    for _ in range(warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    return steps * batch / (time.perf_counter() - t0)
+
+
+def cpu_baseline(model, cfg, batch: int) -> dict:
+    """The reference's CPU path (PyG-semantics restatement; PyG itself is
+    absent) on this box's host cores, rank 0 at N = 1: the benched config's
+    train step (value) and forward, and the C1 config (B = 32) beside it."""
+    cores = usable_cores()
+    torch.set_num_threads(cores)
+    state = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    t0 = time.perf_counter()
+    train = _cpu_rate(cfg, state, batch, True)
+    fwd = _cpu_rate(cfg, state, batch, False)
+    c1 = CONFIGS["c1"]
+    c1_train = _cpu_rate(c1, None, c1["batch"], True)
+    c1_fwd = _cpu_rate(c1, None, c1["batch"], False)
+    el = time.perf_counter() - t0
+    return {"value": round(train, 2), "unit": "graphs/s", "cores": cores, "kind": "port",
+            "fwd_value": round(fwd, 2), "c1_train_value": round(c1_train, 2),
+            "c1_fwd_value": round(c1_fwd, 2), "host_cpu_count": os.cpu_count(),
             "sample": f"oracle PyG-2.3.0-semantics GATModel (unfolded lin_edge, scatter softmax), "
-                      f"same model, {steps} train steps (fwd+bwd+Adam) x {batch} graphs, "
-                      f"{el:.1f}s, torch {torch.__version__} CPU, {cpu_name}"}
+                      f"{cfg['desc'].split(':')[0]} model at B={batch} and C1 at B=32, train "
+                      f"(fwd+MSE+bwd+Adam) and forward, 3 warm-up + 20 timed steps each, "
+                      f"{cores} threads (usable cores of {os.cpu_count()} on the host), "
+                      f"{el:.1f}s, torch {torch.__version__} CPU, {_cpu_name()}"}
+
+
+def step_roofline(cfg, train_gps: float, fwd_gps: float, dtype: str) -> dict:
+    """SURVEY §8(d) whole-step rule: graphs/s ÷ min(HBM-bound, compute-bound)
+    graphs/s, from the algorithmic bytes and folded flops per graph (fwd);
+    a train step counts 3x the forward flops."""
+    n, S, H = cfg["n"], cfg["S"], cfg["heads"]
+    F0, D, E0 = n * S, 3 * S, n * (n - 1)
+    hidden = cfg["hidden"]
+    L = len(hidden)
+    flops, fin = 0.0, F0
+    for l, C in enumerate(hidden):
+        concat = cfg["concat"] and l < L - 1 and L > 1
+        flops += 2 * n * fin * H * C + 2 * (E0 + n) * D * H + 4 * n * H * C + 2 * (E0 + n) * H * C
+        fin = H * C if (concat and H > 1) else C
+    out_ch = 1
+    nbytes = 4.0 * (n * F0 + E0 * D + n * out_ch)
+    peak_tf = BF16_MFMA_PEAK_TFLOPS if dtype == "bf16" else F32_MFMA_PEAK_TFLOPS
+    hbm_gps = HBM_PEAK_GBS * 1e9 / nbytes
+    fwd_bound = min(hbm_gps, peak_tf * 1e12 / flops)
+    train_bound = min(hbm_gps, peak_tf * 1e12 / (3 * flops))
+    return {"bytes_per_graph": nbytes, "fwd_flops_per_graph": flops,
+            "compute_peak_TFLOPs": peak_tf, "hbm_bound_gps": round(hbm_gps, 1),
+            "fwd_bound_gps": round(fwd_bound, 1), "train_bound_gps": round(train_bound, 1),
+            "fwd_frac": round(fwd_gps / fwd_bound, 4), "train_frac": round(train_gps / train_bound, 4)}
 
 
 def main():
@@ -352,7 +423,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="graphs per GPU (config default)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (no hipGraph)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-batch", type=int, default=128,
+                    help="graphs per CPU-baseline step (per-graph CPU cost is batch independent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-table", action="store_true")
     args = ap.parse_args()
@@ -406,9 +478,10 @@ def main():
             kname, roof = roofline_entry(table)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            # bounded sample: about as many edges as 512 C2 graphs
-            cpu_batch = max(1, min(args.batch, 445440 // (cfg["n"] * (cfg["n"] - 1))))
-            cpu = cpu_baseline(model, args.cpu_seconds, cpu_batch, cfg)
+            # bounded sample (~10-30 s): at most as many edges as 128 C2 graphs
+            cpu_batch = max(1, min(args.cpu_batch, args.batch,
+                                   111360 // (cfg["n"] * (cfg["n"] - 1))))
+            cpu = cpu_baseline(model, cfg, cpu_batch)
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -427,6 +500,7 @@ def main():
                        "graphs_per_gpu": args.batch, "global_batch": args.batch * world,
                        "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
             "fwd_graphs_per_s": round(fwd_value, 1),
+            "step_roofline": step_roofline(cfg, value, fwd_value, "f32"),
             "final_loss": loss,
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -198,16 +198,22 @@ class OracleGATModel(nn.Module):
         self.gat_layers = nn.ModuleList(first + stacked)
         self.linear = nn.Linear(dim_hidden_layers[-1], output_node_channels)
         self.a = {"relu": F.relu, "tanh": F.tanh, "sigmoid": F.sigmoid}[activation]
+        # test hook: explicit post-layer dropout keep masks, one [N, out] 0/1
+        # tensor per GAT layer (utils/models.py:148 draws them with F.dropout)
+        self.post_keep: Optional[list] = None
 
     def forward(self, data):
         x, edge_index, edge_attr = data.x, data.edge_index, data.edge_attr
         if self.standardize:
             x = self.bnorm_node(x)
             edge_attr = self.bnorm_edge(edge_attr)
-        for l in self.gat_layers:
+        for i, l in enumerate(self.gat_layers):
             x = l(x, edge_index, edge_attr)
             x = self.a(x)
             if self.dropout:
-                x = F.dropout(x, p=self.dropout, training=self.training)
+                if self.post_keep is not None and self.training:
+                    x = x * self.post_keep[i].to(x.dtype) / (1.0 - self.dropout)
+                else:
+                    x = F.dropout(x, p=self.dropout, training=self.training)
         x = self.linear(x)
         return x.view(-1)

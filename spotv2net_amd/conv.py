@@ -159,11 +159,6 @@ class GATConv(nn.Module):
             return None
         return fold_edge_weight(self.lin_edge.weight, self.att_edge)
 
-    def attend(self, xs: Tensor, ae: Optional[Tensor], layout: GraphLayout, act: int) -> Tensor:
-        return ops.gat_attention(xs, ae, self.bias, layout, self.heads, self.out_channels,
-                                 self.concat, act, self.negative_slope, self.dropout,
-                                 self.training)
-
     def forward(self, x: Tensor, edge_index: Tensor, edge_attr: Optional[Tensor] = None,
                 size=None, return_attention_weights=None, *,
                 layout: Optional[GraphLayout] = None) -> Tensor:

@@ -138,12 +138,19 @@ def synthetic_series(T: int, n: int = 30, seed: int = 1234, device=None,
 
 
 def window_batch(vol: torch.Tensor, volvol: torch.Tensor, starts: torch.Tensor,
-                 seq_length: int) -> Batch:
+                 seq_length: int, future_steps: int = 1) -> Batch:
     """Collated batch of the windows beginning at ``starts`` (window k uses
     matrices starts[k] .. starts[k]+S-1 and the target diag(vol[starts[k]+S])),
     built with gathers on the series' device; identical to
-    ``collate([window_graph(...) for ...])``."""
+    ``collate([window_graph(...) for ...])``.
+
+    ``future_steps`` = F > 1 gives CovarianceLaggedMultiOutputDataset's target
+    (reference utils/dataset.py:385-390, :405): y_x[v*F + k] =
+    diag(vol[starts+S+k])[v], k < F — the layout GATModel(output_node_channels=F)
+    predicts (6_results.ipynb cell 52 reads it back as view(-1, 30, F))."""
     S = seq_length
+    if future_steps < 1:
+        raise ValueError("future_steps must be >= 1")
     n = vol.shape[1]
     dev = vol.device
     B = int(starts.numel())
@@ -161,7 +168,12 @@ def window_batch(vol: torch.Tensor, volvol: torch.Tensor, starts: torch.Tensor,
     var = torch.diagonal(W, dim1=2, dim2=3)                                  # [B, S, n]
     ea = torch.stack([cv, var[:, :, src_t], var[:, :, tgt_t]], dim=2)       # [B, S, 3, E0]
     ea = ea.permute(0, 3, 2, 1).reshape(B * len(src), 3 * S)                 # ea[e, k*S+t]
-    y = torch.diagonal(vol[starts + S].float(), dim1=1, dim2=2).reshape(B * n)
+    if future_steps == 1:
+        y = torch.diagonal(vol[starts + S].float(), dim1=1, dim2=2).reshape(B * n)
+    else:
+        fidx = starts.view(B, 1) + S + torch.arange(future_steps, device=dev).view(1, -1)
+        yk = torch.diagonal(vol[fidx].float(), dim1=2, dim2=3)                 # [B, F, n]
+        y = yk.permute(0, 2, 1).reshape(B * n * future_steps)                  # y[v*F + k]
     ei = canonical_edge_index(n, B, dev)
     ptr = torch.arange(B + 1, device=dev) * n
     b = Batch(x=x.contiguous(), edge_index=ei, edge_attr=ea.contiguous(), y_x=y,
@@ -183,18 +195,24 @@ class WindowDataset:
     """Sliding windows over a matrix series, like CovarianceLaggedDataset
     (window i = matrices i .. i+S-1, target diag(vol[i+S]);
     utils/dataset.py:200-262), kept on the series' device; ``cut`` drops the
-    first windows like the reference's ``data_list[8357:]`` (:287-288)."""
+    first windows like the reference's ``data_list[8357:]`` (:287-288).
+    ``future_steps`` > 1 is CovarianceLaggedMultiOutputDataset
+    (utils/dataset.py:293-405): T - S - F + 1 windows (:333), F targets per
+    node, the same cut (:411)."""
 
-    def __init__(self, vol: torch.Tensor, volvol: torch.Tensor, seq_length: int, cut: int = 0):
+    def __init__(self, vol: torch.Tensor, volvol: torch.Tensor, seq_length: int, cut: int = 0,
+                 future_steps: int = 1):
         self.vol, self.volvol, self.S = vol, volvol, seq_length
-        self.starts = torch.arange(cut, vol.shape[0] - seq_length, device=vol.device)
+        self.future_steps = int(future_steps)
+        last = vol.shape[0] - seq_length - self.future_steps + 1
+        self.starts = torch.arange(cut, max(cut, last), device=vol.device)
 
     def __len__(self) -> int:
         return int(self.starts.numel())
 
     def batch(self, idx: torch.Tensor) -> Batch:
         return window_batch(self.vol, self.volvol, self.starts[idx.to(self.starts.device)],
-                            self.S)
+                            self.S, self.future_steps)
 
     def loader(self, batch_size: int, shuffle: bool, generator: Optional[torch.Generator] = None,
                subset: Optional[torch.Tensor] = None, rank: int = 0, world_size: int = 1):

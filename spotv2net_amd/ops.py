@@ -7,11 +7,11 @@ CPU tensors raise.
 
 Operators
 ---------
-``linear(x, w)``            x @ wᵀ on f32 MFMA (PyG ``Linear``)
-``edge_logits(ea, wf, …)``  folded lin_edge·att_edge logits for L layers (a8)
-``gat_attention(xs, …)``    self loops + leaky_relu + per-target softmax +
-                            dropout + aggregation + concat/mean + bias + act
-                            (a7, a9-a11, GATModel act a4)
+``linear(x, w)``              x @ wᵀ on f32 MFMA (PyG ``Linear``)
+``project / project_planes``  the projection GEMMs of the fused stack
+``pad_columns``               edge-fold column padding (a8)
+
+The GAT layers themselves (a7-a12) run as one fused node: ``stack.gat_stack``.
 """
 from __future__ import annotations
 
@@ -172,142 +172,3 @@ def pad_columns(w: torch.Tensor) -> tuple[torch.Tensor, int]:
     if hp != hl:
         w = torch.nn.functional.pad(w, (0, hp - hl))
     return w.contiguous(), hp
-
-
-class _EdgeLogits(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, edge_attr: torch.Tensor, wfold: torch.Tensor, layout: GraphLayout,
-                num_layers: int, heads: int):
-        lib = _lib.load()
-        dev = edge_attr.device
-        ea = _aligned(edge_attr)
-        E, D = ea.shape
-        wf, hp = pad_columns(wfold)
-        B, n = layout.num_graphs, layout.n
-        outs = [torch.empty(B, n, n, heads, device=dev, dtype=torch.float32)
-                for _ in range(num_layers)]
-        ctx.save_for_backward(ea)
-        ctx.layout = layout
-        ctx.meta = (num_layers, heads, hp, wfold.shape[1])
-        if E == 0:  # no edges: the attention kernels never read ae
-            return tuple(outs)
-        ptrs = _lib.ptr_array([o.data_ptr() for o in outs])
-        ei = layout.edge_index if layout.kind == "block" else None
-        _lib.check(lib.sv2n_edge_logits_fwd(ea.data_ptr(), E, D, _lib.ptr(ei),
-                                            layout.canon.data_ptr(), wf.data_ptr(), hp, ptrs,
-                                            num_layers, heads, B, n, _stream(dev)),
-                   "sv2n_edge_logits_fwd")
-        return tuple(outs)
-
-    @staticmethod
-    def backward(ctx, *grads):
-        (ea,) = ctx.saved_tensors
-        layout: GraphLayout = ctx.layout
-        L, H, hp, hl = ctx.meta
-        lib = _lib.load()
-        dev = ea.device
-        E, D = ea.shape
-        B, n = layout.num_graphs, layout.n
-        if E == 0:
-            return None, torch.zeros(D, hl, device=dev, dtype=torch.float32), None, None, None
-        gs = [g.contiguous() if g is not None else
-              torch.zeros(B, n, n, H, device=dev, dtype=torch.float32) for g in grads]
-        ptrs = _lib.ptr_array([g.data_ptr() for g in gs])
-        ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hp)
-        ws = torch.empty(ws_n, device=dev, dtype=torch.float32)
-        dwf = torch.empty(D, hp, device=dev, dtype=torch.float32)
-        ei = layout.edge_index if layout.kind == "block" else None
-        _lib.check(lib.sv2n_edge_logits_bwd(ea.data_ptr(), E, D, _lib.ptr(ei),
-                                            layout.canon.data_ptr(), ptrs, L, H, B, n,
-                                            ws.data_ptr(), ws_n, dwf.data_ptr(), hp,
-                                            _stream(dev)), "sv2n_edge_logits_bwd")
-        return None, dwf[:, :hl], None, None, None
-
-
-def edge_logits(edge_attr: torch.Tensor, wfold: torch.Tensor, layout: GraphLayout,
-                num_layers: int, heads: int) -> Sequence[torch.Tensor]:
-    """Per-layer dense edge logits [B, n, n, H] for the L layers whose folded
-    edge weights are the column blocks of ``wfold`` [D, L*H]."""
-    _require_device(edge_attr, wfold)
-    if edge_attr.requires_grad:
-        raise NotImplementedError("gradients w.r.t. edge_attr are not supported (the reference "
-                                  "treats edge_attr as data)")
-    if edge_attr.dim() == 1:
-        edge_attr = edge_attr.view(-1, 1)
-    if edge_attr.size(0) != layout.num_edges:
-        raise ValueError("edge_attr rows must match edge_index columns")
-    return _EdgeLogits.apply(edge_attr, wfold, layout, num_layers, heads)
-
-
-# ---------------------------------------------------------------------------
-# fused attention
-# ---------------------------------------------------------------------------
-class _GatAttention(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, xs, ae, bias, layout: GraphLayout, heads: int, channels: int, concat: bool,
-                act: int, slope: float, keep: Optional[torch.Tensor], keep_scale: float):
-        lib = _lib.load()
-        dev = xs.device
-        B, n = layout.num_graphs, layout.n
-        N = layout.num_nodes
-        OC = heads * channels if concat else channels
-        y = torch.empty(N, OC, device=dev, dtype=torch.float32)
-        psave = torch.empty(B, heads, 32, 32, device=dev, dtype=torch.float32)
-        ae_c = ae.contiguous() if ae is not None else None
-        _lib.check(lib.sv2n_gat_attn_fwd(xs.data_ptr(), xs.stride(0), _lib.ptr(ae_c),
-                                         _lib.ptr(layout.rowmask), _lib.ptr(bias), _lib.ptr(keep),
-                                         keep_scale, y.data_ptr(), psave.data_ptr(), B, n, heads,
-                                         channels, int(concat), act, slope, _stream(dev)),
-                   "sv2n_gat_attn_fwd")
-        ctx.save_for_backward(xs, y, psave, keep)
-        ctx.layout = layout
-        ctx.meta = (heads, channels, concat, act, slope, keep_scale, ae is not None,
-                    bias is not None)
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        xs, y, psave, keep = ctx.saved_tensors
-        layout: GraphLayout = ctx.layout
-        heads, channels, concat, act, slope, keep_scale, has_ae, has_bias = ctx.meta
-        lib = _lib.load()
-        dev = xs.device
-        B, n = layout.num_graphs, layout.n
-        OC = heads * channels if concat else channels
-        dy = dy.contiguous()
-        dxs = torch.empty_like(xs)
-        dae = torch.empty(B, n, n, heads, device=dev, dtype=torch.float32) if has_ae else None
-        dbp = torch.empty(B, OC, device=dev, dtype=torch.float32)
-        _lib.check(lib.sv2n_gat_attn_bwd(dy.data_ptr(), y.data_ptr(), xs.data_ptr(),
-                                         xs.stride(0), psave.data_ptr(), _lib.ptr(keep),
-                                         keep_scale, _lib.ptr(layout.rowmask), dxs.data_ptr(),
-                                         _lib.ptr(dae), dbp.data_ptr(), B, n, heads, channels,
-                                         int(concat), act, slope, _stream(dev)),
-                   "sv2n_gat_attn_bwd")
-        dbias = dbp.sum(0) if has_bias else None
-        return dxs, dae, dbias, None, None, None, None, None, None, None, None
-
-
-def gat_attention(xs: torch.Tensor, ae: Optional[torch.Tensor], bias: Optional[torch.Tensor],
-                  layout: GraphLayout, heads: int, channels: int, concat: bool, act: int,
-                  negative_slope: float, attn_dropout: float = 0.0,
-                  training: bool = False) -> torch.Tensor:
-    """Fused GAT attention for one layer; ``xs`` = [lin_src(x) | a_src | a_dst]."""
-    _require_device(xs, ae, bias)
-    if layout.tiled:
-        from .layout import UnsupportedLayout
-        raise UnsupportedLayout("the per-op attention covers n <= 32; larger blocks run through "
-                                "the fused stack (GATConv.forward / gat_stack)")
-    if xs.stride(1) != 1 or xs.stride(0) % 4 or xs.data_ptr() % 16:
-        xs = _aligned(xs)
-    keep, scale = None, 1.0
-    if training and attn_dropout > 0.0:
-        B, n = layout.num_graphs, layout.n
-        if attn_dropout >= 1.0:
-            keep = torch.zeros(B, heads, 32, 32, device=xs.device, dtype=torch.uint8)
-            scale = 0.0
-        else:
-            keep = (torch.rand(B, heads, 32, 32, device=xs.device) >= attn_dropout).to(torch.uint8)
-            scale = 1.0 / (1.0 - attn_dropout)
-    return _GatAttention.apply(xs, ae, bias, layout, heads, channels, bool(concat), int(act),
-                               float(negative_slope), keep, float(scale))

@@ -14,14 +14,20 @@ Backward, layers in reverse:
   sv2n_gat_prep_bwd_node -> ACCUMULATES into W/att_src/att_dst/bias .grad
   then one sv2n_edge_logits_bwd for all layers + sv2n_gat_prep_bwd_edge.
 
-Parameter gradients are written straight into ``p.grad`` (allocated as zeros
-when None), so no per-parameter autograd glue (copies, adds, fold backward)
-runs; the node returns None for the parameters.  Gradient hooks registered on
-these parameters therefore do not fire for this path (documented deviation).
+Parameter gradients.  By default the node RETURNS its parameter gradients to
+autograd (computed into one zero-initialised flat buffer per backward, one view
+per parameter), so ``AccumulateGrad`` fills ``p.grad``: parameter hooks,
+``torch.autograd.grad(loss, params)`` and ``DistributedDataParallel`` see them
+as with PyG.  Inside ``direct_grad_accumulation()`` (what ``train.TrainStep``
+uses, with every ``p.grad`` already a view of its flat gradient buffer) the
+kernels accumulate straight into ``p.grad`` and the node returns None for the
+parameters: no per-parameter autograd launches in the captured step.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import threading
 from typing import Optional, Sequence
 
 import torch
@@ -39,6 +45,67 @@ def _grad_buf(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     elif not p.grad.is_contiguous():
         p.grad = p.grad.contiguous()
     return p.grad
+
+
+_mode = threading.local()
+
+
+@contextlib.contextmanager
+def direct_grad_accumulation():
+    """Within this context the fused nodes accumulate parameter gradients
+    straight into ``p.grad`` (which must be dense fp32) instead of returning
+    them to autograd.  Hooks and ``autograd.grad`` do not see such gradients;
+    ``train.TrainStep`` uses it around its (captured) forward."""
+    prev = getattr(_mode, "direct", False)
+    _mode.direct = True
+    try:
+        yield
+    finally:
+        _mode.direct = prev
+
+
+def _direct_mode() -> bool:
+    return getattr(_mode, "direct", False)
+
+
+class _GradTargets:
+    """Where a fused node's kernels accumulate parameter gradients, and what
+    its backward returns for the parameters (see module docstring)."""
+
+    def __init__(self, params, needs, direct: bool, device):
+        self.direct = direct
+        self._views = {}
+        self._used = set()
+        self._order = [id(p) for p in params]
+        if direct:
+            for p, nd in zip(params, needs):
+                if nd:
+                    self._views[id(p)] = _grad_buf(p)
+            return
+        total = sum(p.numel() for p, nd in zip(params, needs) if nd)
+        if total == 0:
+            return
+        flat = torch.zeros(total, device=device, dtype=torch.float32)
+        off = 0
+        for p, nd in zip(params, needs):
+            if nd:
+                k = p.numel()
+                self._views[id(p)] = flat[off:off + k].view(p.shape)
+                off += k
+
+    def __call__(self, p) -> Optional[torch.Tensor]:
+        """Gradient buffer of p (None when not needed); marks p as written."""
+        if p is None:
+            return None
+        g = self._views.get(id(p))
+        if g is not None:
+            self._used.add(id(p))
+        return g
+
+    def returned(self) -> tuple:
+        if self.direct:
+            return (None,) * len(self._order)
+        return tuple(self._views.get(i) if i in self._used else None for i in self._order)
 
 
 def layer_params(conv) -> list:
@@ -184,6 +251,7 @@ class _GATStack(torch.autograd.Function):
 
         ctx.convs = convs
         ctx.layout = layout
+        ctx.direct = _direct_mode()
         ctx.meta = (L, act, use_edge, hp, H)
         ctx.kscales = [(1.0 / (1.0 - c.dropout)) if (training and 0.0 < c.dropout < 1.0) else
                        (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs]
@@ -215,6 +283,8 @@ class _GATStack(torch.autograd.Function):
         dy = dout.contiguous()
         daes = [None] * L
         need_x0 = ctx.needs_input_grad[0]
+        params = [p for c in convs for p in layer_params(c)]
+        grad_of = _GradTargets(params, ctx.needs_input_grad[7:], ctx.direct, dev)
         for l in range(L - 1, -1, -1):
             c = convs[l]
             Hc, C = c.heads, c.out_channels
@@ -247,10 +317,10 @@ class _GATStack(torch.autograd.Function):
                     n, Hc, C, int(c.concat), act, float(c.negative_slope), st),
                     "sv2n_gat_attn_bwd")
             daes[l] = dae
-            gW = _grad_buf(c.lin_src.weight)
-            gas = _grad_buf(c.att_src)
-            gad = _grad_buf(c.att_dst)
-            gb = _grad_buf(c.bias)
+            gW = grad_of(c.lin_src.weight)
+            gas = grad_of(c.att_src)
+            gad = grad_of(c.att_dst)
+            gb = grad_of(c.bias)
             if any(g is not None for g in (gW, gas, gad, gb)):
                 # split-K dWaugᵀ GEMM + one fused epilogue (fold, transpose,
                 # att and bias grads), accumulated into .grad
@@ -267,7 +337,7 @@ class _GATStack(torch.autograd.Function):
 
         if use_edge and ea is not None:
             # grads exist (zeros) even without edges, as in PyG
-            need_e = [(_grad_buf(c.lin_edge.weight), _grad_buf(c.att_edge)) for c in convs]
+            need_e = [(grad_of(c.lin_edge.weight), grad_of(c.att_edge)) for c in convs]
             if ea.size(0) > 0 and any(a is not None or b is not None for a, b in need_e):
                 E, D = ea.shape
                 ptrs = _lib.ptr_array([d.data_ptr() for d in daes])
@@ -291,20 +361,35 @@ class _GATStack(torch.autograd.Function):
                         c.att_edge.data_ptr(), c.heads, c.out_channels, D, _lib.ptr(gWe),
                         _lib.ptr(gae), st), "sv2n_gat_prep_bwd_edge")
         dx0 = dy if need_x0 else None
-        n_params = len(ctx.needs_input_grad) - 7
-        return (dx0, None, None, None, None, None, None) + (None,) * n_params
+        return (dx0, None, None, None, None, None, None) + grad_of.returned()
+
+
+def _require_params(params) -> None:
+    """The kernels read every parameter as a dense fp32 buffer through its raw
+    pointer: refuse anything else (stock PyTorch raises a dtype mismatch for
+    ``model.double()`` with fp32 data; here it would read garbage)."""
+    for p in params:
+        if p is None:
+            continue
+        if p.dtype != torch.float32:
+            raise TypeError(f"spotv2net_amd parameters must be float32 (got {p.dtype}); the "
+                            "kernels keep fp32 master weights (bf16 is an execution mode, "
+                            "see GATModel.set_precision)")
+        if not p.is_contiguous():
+            raise TypeError("spotv2net_amd parameters must be contiguous")
 
 
 def gat_stack(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs: Sequence,
               layout: GraphLayout, act: int, post_dropout: float, training: bool) -> torch.Tensor:
     """Run ``convs`` (GATConv modules) as one fused autograd node."""
+    params = []
+    for c in convs:
+        params += layer_params(c)
+    _require_params(params)
     _require_device(x, edge_attr)
     if edge_attr is not None and edge_attr.requires_grad:
         raise NotImplementedError("gradients w.r.t. edge_attr are not supported (the reference "
                                   "treats edge_attr as data)")
-    params = []
-    for c in convs:
-        params += layer_params(c)
     for p in params:
         if p.device != x.device:
             raise RuntimeError("parameters and data must be on the same device")
@@ -314,7 +399,7 @@ def gat_stack(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs: Sequenc
 
 class _Head(torch.autograd.Function):
     """GATModel.linear (reference utils/models.py:120, :150) on sv2n_head_*;
-    parameter gradients are accumulated into ``.grad`` like the GAT stack."""
+    parameter gradients are returned (or accumulated directly) like the GAT stack."""
 
     @staticmethod
     def forward(ctx, x, linear, weight, bias):
@@ -326,6 +411,7 @@ class _Head(torch.autograd.Function):
         _lib.check(lib.sv2n_head_fwd(x.data_ptr(), N, C, weight.data_ptr(), _lib.ptr(bias), O,
                                      out.data_ptr(), _lib.stream_handle(x.device)), "sv2n_head_fwd")
         ctx.linear = linear
+        ctx.direct = _direct_mode()
         ctx.save_for_backward(x)
         return out
 
@@ -340,20 +426,21 @@ class _Head(torch.autograd.Function):
         dx = torch.empty_like(x)
         ws_n = lib.sv2n_head_bwd_workspace(N, C, O)
         ws = _lib.persistent_zeros("head", ws_n, x.device)
-        gw = _grad_buf(lin.weight)
-        gb = _grad_buf(lin.bias)
+        grad_of = _GradTargets([lin.weight, lin.bias], ctx.needs_input_grad[2:4], ctx.direct,
+                               x.device)
+        gw = grad_of(lin.weight)
+        gb = grad_of(lin.bias)
         _lib.check(lib.sv2n_head_bwd(x.data_ptr(), N, C, lin.weight.data_ptr(), O,
                                      dout.data_ptr(), dx.data_ptr(), _lib.ptr(gw), _lib.ptr(gb),
                                      ws.data_ptr(), ws_n, _lib.stream_handle(x.device)),
                    "sv2n_head_bwd")
-        return dx if ctx.needs_input_grad[0] else None, None, None, None
+        return (dx if ctx.needs_input_grad[0] else None, None) + grad_of.returned()
 
 
 class _HeadMSE(torch.autograd.Function):
     """``F.mse_loss(linear(x).view(-1), target)`` (reference
     5_train_SpotV2Net.py:150-154) as two launches: sv2n_head_mse_fwd (head,
-    residual, loss) and sv2n_head_mse_bwd (dx and the head's parameter grads,
-    accumulated into ``.grad``)."""
+    residual, loss) and sv2n_head_mse_bwd (dx and the head's parameter grads)."""
 
     @staticmethod
     def forward(ctx, x, target, linear, weight, bias):
@@ -373,6 +460,7 @@ class _HeadMSE(torch.autograd.Function):
                                          loss.data_ptr(), ws.data_ptr(), ws_n,
                                          _lib.stream_handle(x.device)), "sv2n_head_mse_fwd")
         ctx.linear = linear
+        ctx.direct = _direct_mode()
         ctx.save_for_backward(x, diff)
         return loss
 
@@ -387,17 +475,20 @@ class _HeadMSE(torch.autograd.Function):
         dx = torch.empty_like(x)
         ws_n = lib.sv2n_head_mse_workspace(N, C, O)
         ws = _lib.persistent_zeros("head", ws_n, x.device)
-        gw = _grad_buf(lin.weight)
-        gb = _grad_buf(lin.bias)
+        grad_of = _GradTargets([lin.weight, lin.bias], ctx.needs_input_grad[3:5], ctx.direct,
+                               x.device)
+        gw = grad_of(lin.weight)
+        gb = grad_of(lin.bias)
         _lib.check(lib.sv2n_head_mse_bwd(x.data_ptr(), N, C, lin.weight.data_ptr(), O,
                                          diff.data_ptr(), gloss.data_ptr(), dx.data_ptr(),
                                          _lib.ptr(gw), _lib.ptr(gb), ws.data_ptr(), ws_n,
                                          _lib.stream_handle(x.device)), "sv2n_head_mse_bwd")
-        return dx if ctx.needs_input_grad[0] else None, None, None, None, None
+        return (dx if ctx.needs_input_grad[0] else None, None, None) + grad_of.returned()
 
 
 def head_mse_loss(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tensor) -> torch.Tensor:
     """mean((linear(x).view(-1) - target)²) with the head and the loss fused."""
+    _require_params((linear.weight, linear.bias))
     _require_device(x, target)
     if linear.in_features > 128 or linear.out_features > 16:
         return torch.nn.functional.mse_loss(linear(x).view(-1), target)
@@ -407,6 +498,7 @@ def head_mse_loss(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tensor
 def linear_head(x: torch.Tensor, linear: torch.nn.Linear) -> torch.Tensor:
     """``linear(x)`` for GATModel's output layer on the sv2n head kernels
     (in_features <= 128, out_features <= 16; otherwise the nn.Linear itself)."""
+    _require_params((linear.weight, linear.bias))
     _require_device(x)
     if linear.in_features > 128 or linear.out_features > 16:
         return linear(x)

@@ -136,13 +136,17 @@ class TrainStep:
 
     # -- eager pieces -------------------------------------------------------
     def _fwd_bwd(self) -> None:
+        from .stack import direct_grad_accumulation
         if not getattr(self.opt, "zeroes_grads", False):
             self.flat.zero_()
-        if self._fused_mse:
-            loss = self.model.mse_loss(self.data)
-        else:
-            loss = self.loss_fn(self.model(self.data), self.data.y_x)
-        torch.autograd.backward(loss, self._one)
+        # every p.grad is a view of self.flat: the fused nodes accumulate into
+        # it directly (no per-parameter AccumulateGrad launches)
+        with direct_grad_accumulation():
+            if self._fused_mse:
+                loss = self.model.mse_loss(self.data)
+            else:
+                loss = self.loss_fn(self.model(self.data), self.data.y_x)
+            torch.autograd.backward(loss, self._one)
         self.loss = loss.detach()
 
     def _opt_step(self) -> None:
@@ -155,7 +159,43 @@ class TrainStep:
         self._opt_step()
 
     # -- graph capture ------------------------------------------------------
+    def _snapshot(self) -> dict:
+        """Everything the warm-up steps before capture advance: parameters,
+        optimizer state, RNG streams."""
+        snap = {"params": self.flat_params.clone(), "opt": None,
+                "cpu_rng": torch.get_rng_state(),
+                "cuda_rng": torch.cuda.get_rng_state(self.flat.device)}
+        if isinstance(self.opt, FlatAdam):
+            snap["opt"] = (self.opt.m.clone(), self.opt.v.clone(), self.opt.step_t.clone())
+        return snap
+
+    def _restore(self, snap: dict) -> None:
+        """Undo the warm-up (in place: the captured graph keeps pointing at the
+        same buffers), so that construction does not train the model."""
+        with torch.no_grad():
+            self.flat_params.copy_(snap["params"])
+            self.flat.zero_()
+            if isinstance(self.opt, FlatAdam):
+                m, v, t = snap["opt"]
+                self.opt.m.copy_(m)
+                self.opt.v.copy_(v)
+                self.opt.step_t.copy_(t)
+            else:  # torch.optim.Adam: state was empty before the warm-up
+                for st in self.opt.state.values():
+                    for val in st.values():
+                        if torch.is_tensor(val):
+                            val.zero_()
+        torch.set_rng_state(snap["cpu_rng"])
+        try:
+            torch.cuda.set_rng_state(snap["cuda_rng"], self.flat.device)
+        except RuntimeError:  # generator registered with a live capture
+            pass
+
     def _capture(self, warmup: int) -> None:
+        """Warm up (allocator, lazy optimizer state), capture, then restore the
+        pre-warm-up parameters / optimizer state / RNG: constructing a
+        TrainStep applies no update (k calls == k eager reference steps)."""
+        snap = self._snapshot()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -175,6 +215,8 @@ class TrainStep:
             with torch.cuda.graph(self._g_fb):
                 self._fwd_bwd()
                 self._opt_step()
+        torch.cuda.synchronize()
+        self._restore(snap)
         torch.cuda.synchronize()
 
     def __call__(self) -> torch.Tensor:

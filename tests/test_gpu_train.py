@@ -37,9 +37,10 @@ def test_graph_replay_equals_eager(dev):
     data = synthetic_batch(16, 4, seed=2, device=dev)
     m1 = _model(dev, seed=3)
     m2 = copy.deepcopy(m1)
-    s1 = TrainStep(m1, data, use_graph=True, warmup=1)  # capture runs 1 eager step
+    s1 = TrainStep(m1, data, use_graph=True, warmup=3)  # warm-up is undone after capture
     s2 = TrainStep(m2, data, use_graph=False)
-    s2()  # align: both models have taken one step
+    for (n, p), (_, q) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(p, q), f"{n}: constructing a TrainStep must not train"
     for _ in range(4):
         s1()
         s2()
@@ -112,7 +113,7 @@ def test_flat_adam_advances_step_and_zeroes_grads(dev):
     for _ in range(5):
         s()
     torch.cuda.synchronize()
-    assert float(s.opt.step_t.item()) == 2 + 5  # warmup steps + replays (capture runs nothing)
+    assert float(s.opt.step_t.item()) == 5  # replays only: the warm-up steps are undone
     assert int(s.opt.ticket.abs().sum().item()) == 0
     assert float(s.flat.abs().max().item()) == 0.0
 
