@@ -415,6 +415,40 @@ def step_roofline(cfg, train_gps: float, fwd_gps: float, dtype: str) -> dict:
             "fwd_frac": round(fwd_gps / fwd_bound, 4), "train_frac": round(train_gps / train_bound, 4)}
 
 
+def run_c3_loop(args, dev, cfg) -> dict:
+    """C3 as BASELINE.json states it: config/GNN_param.yaml's model and
+    hyper-parameters (S 42, hidden [500], 6 heads, dropout 0.1, Adam 1e-3,
+    batch 128, split 0.8) over the full training loop of 5_train_SpotV2Net.py
+    (train pass with shuffling + test pass per epoch) on 2,157 windows — the
+    count CovarianceLaggedDataset yields from 10,556 matrices after the
+    [8357:] cut (utils/dataset.py:200, :288).  Timed: ``--epochs`` epochs
+    after ``--warmup-epochs``, in bf16 mode and, for comparison, fp32 mode."""
+    from spotv2net_amd import WindowDataset
+    from spotv2net_amd.data import synthetic_series
+    from spotv2net_amd.train import Fit
+    V, W = synthetic_series(10556, cfg["n"], seed=1234, device=dev)
+    ds = WindowDataset(V, W, cfg["S"], cut=8357)
+    out = {}
+    for prec in (args.precision, "f32" if args.precision == "bf16" else "bf16"):
+        model = build_model(dev, cfg).set_precision(prec)
+        f = Fit(model, ds, args.batch, lr=1e-3, split=0.8,
+                generator=torch.Generator().manual_seed(5154), use_graph=not args.no_graph)
+        for _ in range(args.warmup_epochs):
+            f.run_epoch()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.epochs):
+            rec = f.run_epoch()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        steps = args.epochs * (-(-f.n_train // args.batch))
+        out[prec] = {"graphs_per_s": args.epochs * len(ds) / el,
+                     "train_graphs_per_s_upper": args.epochs * f.n_train / el,
+                     "seconds": el, "train_steps": steps, "epoch_record": rec,
+                     "history": f.history}
+    return {"windows": len(ds), "n_train": f.n_train, "n_test": f.n_test, "runs": out}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -427,7 +461,13 @@ def main():
                     help="graphs per CPU-baseline step (per-graph CPU cost is batch independent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-table", action="store_true")
+    ap.add_argument("--precision", default=None, choices=("f32", "bf16"),
+                    help="execution mode (default: f32; bf16 for --config c3)")
+    ap.add_argument("--epochs", type=int, default=3, help="c3: timed epochs (yaml num_epochs)")
+    ap.add_argument("--warmup-epochs", type=int, default=1, help="c3: untimed epochs")
     args = ap.parse_args()
+    if args.precision is None:
+        args.precision = "bf16" if args.config == "c3" else "f32"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -443,7 +483,9 @@ def main():
     cfg = CONFIGS[args.config]
     if args.batch is None:
         args.batch = cfg["batch"]
-    model = build_model(dev, cfg)
+    if args.config == "c3" and world == 1:
+        return main_c3(args, dev, cfg)
+    model = build_model(dev, cfg).set_precision(args.precision)
     if world > 1:  # identical replicas: broadcast rank 0's weights
         for p in model.parameters():
             dist.broadcast(p.data, 0)
@@ -493,14 +535,14 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": args.precision,
             "data": "synthetic (standardized symmetric vol / vol-of-vol matrices, "
                     "CovarianceLaggedDataset layout), device-resident, random-init weights",
             "config": {"workload": cfg["desc"], "name": args.config,
                        "graphs_per_gpu": args.batch, "global_batch": args.batch * world,
                        "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
             "fwd_graphs_per_s": round(fwd_value, 1),
-            "step_roofline": step_roofline(cfg, value, fwd_value, "f32"),
+            "step_roofline": step_roofline(cfg, value, fwd_value, args.precision),
             "final_loss": loss,
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -515,6 +557,48 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def main_c3(args, dev, cfg):
+    res = run_c3_loop(args, dev, cfg)
+    main_run = res["runs"][args.precision]
+    value = main_run["graphs_per_s"]
+    cpu = None
+    if not args.no_cpu_baseline:
+        model = build_model(dev, cfg)
+        cpu = cpu_baseline(model, cfg, min(args.cpu_batch, 16))
+    result = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "graphs/s",
+        "n_gpus": 1,
+        "steps": main_run["train_steps"],
+        "warmup": args.warmup_epochs,
+        "ms_per_step": round(main_run["seconds"] / main_run["train_steps"] * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic standardized vol / vol-of-vol series of 10,556 matrices on the "
+                "device, windows gathered on the device per batch; random-init weights",
+        "config": {"workload": cfg["desc"] + "; full train loop (train + test pass per epoch, "
+                   "shuffle, ragged last batch) over 2,157 windows, split 0.8",
+                   "name": "c3", "graphs_per_gpu": args.batch, "global_batch": args.batch,
+                   "parallelism": "dp1", "hipgraph": not args.no_graph,
+                   "epochs_timed": args.epochs},
+        "value_is": "windows processed (train + test) per second over whole epochs",
+        "c3_loop": {k: {kk: (round(vv, 2) if isinstance(vv, float) else vv)
+                        for kk, vv in v.items() if kk != "history"}
+                    for k, v in res["runs"].items()},
+        "loss_curves": {k: [(round(r["train_loss"], 6), round(r["test_loss"], 6))
+                            for r in v["history"]] for k, v in res["runs"].items()},
+        "step_roofline": step_roofline(cfg, main_run["train_graphs_per_s_upper"], value,
+                                       args.precision),
+        "cpu_baseline": cpu,
+        "peaks_assumed": {"hbm_GBs": HBM_PEAK_GBS, "f32_mfma_TFLOPs": F32_MFMA_PEAK_TFLOPS,
+                          "bf16_mfma_TFLOPs": BF16_MFMA_PEAK_TFLOPS},
+    }
+    print(json.dumps(result), flush=True)
 
 
 if __name__ == "__main__":

@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 2
+#define SV2N_ABI_VERSION 3
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -164,6 +164,14 @@ int sv2n_split3(const float* in, int64_t rows, int64_t K, int64_t ld, int transp
 int sv2n_gemm_f32x3(const float* A, int64_t lda, const uint16_t* Bp, float* C, int64_t ldc,
                     int64_t M, int64_t N, int64_t K, hipStream_t stream);
 
+/* bf16 execution mode of the same projection (the reference run under
+ * torch.autocast(dtype=bfloat16), BASELINE config C3): C = bf16(A)·bf16(B)ᵀ
+ * with fp32 accumulation and fp32 output.  A fp32 k-major as in
+ * sv2n_gemm_f32x3 (rounded to bf16 while staged); Bp is plane 0 of the
+ * sv2n_split3 planes of B (= bf16_rn(B), [N][Kp]); planes 1-2 are not read. */
+int sv2n_gemm_bf16(const float* A, int64_t lda, const uint16_t* Bp, float* C, int64_t ldc,
+                   int64_t M, int64_t N, int64_t K, hipStream_t stream);
+
 /* Weight preparation for one GAT layer (replaces, per step, PyG's separate
  * (x_src*att_src).sum(-1) / (x_dst*att_dst).sum(-1) and lin_edge·att_edge
  * reductions by folded weights):
@@ -237,6 +245,20 @@ int sv2n_gat_wgrad_node(const float* x, int64_t ld_x, const float* dxs, int ldx,
                         float* g_att_src, float* g_att_dst, float* g_bias, float* workspace,
                         int64_t workspace_floats, hipStream_t stream);
 
+/* sv2n_gat_wgrad_node in the bf16 execution mode: the GEMM T = xᵀ·dxs runs
+ * on bf16 operands (rounded while staged) with fp32 accumulation; the fold,
+ * attention-vector and bias epilogue is the fp32 one.  Same arguments;
+ * workspace: sv2n_gat_wgrad_node_bf16_workspace floats; x, dxs 16-B aligned
+ * with leading dims % 4 == 0. */
+int64_t sv2n_gat_wgrad_node_bf16_workspace(int64_t num_nodes, int in_features, int ldx,
+                                           int heads, int channels);
+int sv2n_gat_wgrad_node_bf16(const float* x, int64_t ld_x, const float* dxs, int ldx,
+                             int64_t num_nodes, int in_features, const float* W,
+                             const float* att_src, const float* att_dst, int heads, int channels,
+                             const float* dbias_partial, int num_parts, int bias_len, float* gW,
+                             float* g_att_src, float* g_att_dst, float* g_bias, float* workspace,
+                             int64_t workspace_floats, hipStream_t stream);
+
 /* Backward of the edge fold: ACCUMULATE gW_edge[h*C+c][d] += dwfold[d][col0+h]·att_edge[h*C+c]
  * and g_att_edge[h*C+c] += Σ_d W_edge[h*C+c][d]·dwfold[d][col0+h]. */
 int sv2n_gat_prep_bwd_edge(const float* dwfold, int hl_pad, int col0,
@@ -260,7 +282,7 @@ int sv2n_adam_f32_step(float* param, float* grad, float* exp_avg, float* exp_avg
 
 /* Output head (GATModel.linear, reference utils/models.py:120/:150):
  *   out[i][o] = Σ_c x[i][c]·weight[o][c] + bias[o]      x [rows][in], weight [out][in]
- * in_features <= 128, out_features <= 16.  The backward writes dx and
+ * in_features <= 1024, out_features <= 16.  The backward writes dx and
  * ACCUMULATES into g_weight / g_bias (either may be NULL).
  * workspace: sv2n_head_bwd_workspace(rows, in, out) floats, 16-B aligned; its
  * first SV2N_TICKET_WORDS (288) floats are ticket counters that must be zero

@@ -14,7 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p
@@ -58,6 +58,7 @@ _SIGNATURES = {
     "sv2n_split3_kpad": (_i64, [_i64]),
     "sv2n_split3": (_i32, [_p, _i64, _i64, _i64, _i32, _p, _p]),
     "sv2n_gemm_f32x3": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "sv2n_gemm_bf16": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "sv2n_gemm_f32_workspace": (_i64, [_i64, _i64, _i64]),
     "sv2n_gemm_f32_slabs_count": (_i32, [_i64, _i64, _i64]),
     "sv2n_gemm_f32_slabs": (_i32, [_i32, _i32, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
@@ -70,6 +71,9 @@ _SIGNATURES = {
     "sv2n_gat_wgrad_node_workspace": (_i64, [_i64, _i32, _i32, _i32, _i32]),
     "sv2n_gat_wgrad_node": (_i32, [_p, _i64, _p, _i32, _i64, _i32, _p, _p, _p, _i32, _i32, _p,
                                    _i32, _i32, _p, _p, _p, _p, _p, _i64, _p]),
+    "sv2n_gat_wgrad_node_bf16_workspace": (_i64, [_i64, _i32, _i32, _i32, _i32]),
+    "sv2n_gat_wgrad_node_bf16": (_i32, [_p, _i64, _p, _i32, _i64, _i32, _p, _p, _p, _i32, _i32,
+                                        _p, _i32, _i32, _p, _p, _p, _p, _p, _i64, _p]),
     "sv2n_gat_prep_bwd_node": (_i32, [_p, _i32, _p, _p, _p, _i32, _i32, _i32, _p, _i32, _i32, _p,
                                       _p, _p, _p, _p, _i64, _p]),
     "sv2n_gat_prep_bwd_edge": (_i32, [_p, _i32, _i32, _p, _p, _i32, _i32, _i32, _p, _p, _p]),

@@ -100,6 +100,7 @@ class GATConv(nn.Module):
         self.add_self_loops = add_self_loops
         self.edge_dim = edge_dim
         self.fill_value = fill_value
+        self.precision: Optional[str] = None  # see GATModel.set_precision
 
         # registration order follows PyG 2.3.0 (state_dict key order)
         self.lin_src = Linear(in_channels, heads * out_channels)
@@ -170,7 +171,8 @@ class GATConv(nn.Module):
             raise ValueError("x must be [N, in_channels]")
         if layout is None:
             layout = analyze_edge_index(edge_index, x.size(0))
-        return gat_stack(x, edge_attr, (self,), layout, ops.ACT_CODES[None], 0.0, self.training)
+        return gat_stack(x, edge_attr, (self,), layout, ops.ACT_CODES[None], 0.0, self.training,
+                         self.precision)
 
     def __repr__(self) -> str:
         return (f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, "

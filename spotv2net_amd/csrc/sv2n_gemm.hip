@@ -17,6 +17,7 @@
 //   same box (tools/gemm_ref_blas.py).
 #include "sv2n_common.h"
 #include "sv2n_gemm_kernel.h"
+#include "sv2n_gemm3_kernel.h"
 
 namespace sv2n {
 
@@ -286,6 +287,44 @@ extern "C" int64_t sv2n_gat_wgrad_node_workspace(int64_t num_nodes, int in_featu
   return (int64_t)in_features * ldx + wgrad_slab_floats(num_nodes, in_features, ldx);
 }
 
+// bf16-operand weight-gradient GEMM (k_gemm3_t, one plane): tiles 128 x 208
+// (or 128 x 112), K slices of multiples of 64 aiming at ~480 workgroups
+static GemmPlan plan_gemm_bf16t(int64_t M, int64_t N, int64_t K) {
+  GemmPlan p{};
+  p.nt = N > 256 ? 13 : 7;
+  const int64_t tiles = ((M + 127) / 128) * ((N + 16 * p.nt - 1) / (16 * p.nt));
+  int64_t sk = 1;
+  if (tiles < 240 && K >= 1024) {
+    sk = std::min<int64_t>(32, (480 + tiles - 1) / tiles);
+    sk = std::min<int64_t>(sk, std::max<int64_t>(1, K / 256));
+  }
+  int64_t ks = (K + sk - 1) / sk;
+  ks = (ks + 63) / 64 * 64;
+  p.splitk = (int)((K + ks - 1) / ks);
+  p.kslice = ks;
+  p.pf = 1;
+  return p;
+}
+
+template <int NT>
+static void launch_wgrad_bf16(const GemmPlan& p, hipStream_t st, const float* x, int64_t ld_x,
+                              const float* dxs, int64_t ldx, int64_t F, int64_t K, float* out) {
+  using Cfg = Gemm3TCfg<8, 1, NT, 64, 1>;
+  constexpr size_t lds = Cfg::LDS;
+  static_assert(lds <= 64 * 1024, "LDS budget");
+  const dim3 grid((unsigned)((F + Cfg::BM - 1) / Cfg::BM), (unsigned)((ldx + Cfg::BN - 1) / Cfg::BN),
+                  (unsigned)p.splitk);
+  hipLaunchKernelGGL((k_gemm3_t<8, 1, NT, 64, 1>), grid, dim3(Cfg::THREADS), lds, st, x, ld_x, dxs,
+                     ldx, out, ldx, F, ldx, K, p.kslice);
+}
+
+static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* dxs, int ldx,
+                      int64_t num_nodes, int in_features, const float* W, const float* att_src,
+                      const float* att_dst, int heads, int channels, const float* dbias_partial,
+                      int num_parts, int bias_len, float* gW, float* g_att_src, float* g_att_dst,
+                      float* g_bias, float* workspace, int64_t workspace_floats,
+                      hipStream_t stream);
+
 extern "C" int sv2n_gat_wgrad_node(const float* x, int64_t ld_x, const float* dxs, int ldx,
                                    int64_t num_nodes, int in_features, const float* W,
                                    const float* att_src, const float* att_dst, int heads,
@@ -293,6 +332,36 @@ extern "C" int sv2n_gat_wgrad_node(const float* x, int64_t ld_x, const float* dx
                                    int bias_len, float* gW, float* g_att_src, float* g_att_dst,
                                    float* g_bias, float* workspace, int64_t workspace_floats,
                                    hipStream_t stream) {
+  return wgrad_node(0, x, ld_x, dxs, ldx, num_nodes, in_features, W, att_src, att_dst, heads,
+                    channels, dbias_partial, num_parts, bias_len, gW, g_att_src, g_att_dst,
+                    g_bias, workspace, workspace_floats, stream);
+}
+
+extern "C" int64_t sv2n_gat_wgrad_node_bf16_workspace(int64_t num_nodes, int in_features, int ldx,
+                                                      int heads, int channels) {
+  if (num_nodes <= 0 || in_features <= 0 || ldx <= 0 || heads <= 0 || channels <= 0) return 0;
+  const GemmPlan p = plan_gemm_bf16t(in_features, ldx, num_nodes);
+  return (int64_t)in_features * ldx * (p.splitk > 1 ? 1 + p.splitk : 1);
+}
+
+extern "C" int sv2n_gat_wgrad_node_bf16(const float* x, int64_t ld_x, const float* dxs, int ldx,
+                                        int64_t num_nodes, int in_features, const float* W,
+                                        const float* att_src, const float* att_dst, int heads,
+                                        int channels, const float* dbias_partial, int num_parts,
+                                        int bias_len, float* gW, float* g_att_src,
+                                        float* g_att_dst, float* g_bias, float* workspace,
+                                        int64_t workspace_floats, hipStream_t stream) {
+  return wgrad_node(1, x, ld_x, dxs, ldx, num_nodes, in_features, W, att_src, att_dst, heads,
+                    channels, dbias_partial, num_parts, bias_len, gW, g_att_src, g_att_dst,
+                    g_bias, workspace, workspace_floats, stream);
+}
+
+static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* dxs, int ldx,
+                      int64_t num_nodes, int in_features, const float* W, const float* att_src,
+                      const float* att_dst, int heads, int channels, const float* dbias_partial,
+                      int num_parts, int bias_len, float* gW, float* g_att_src, float* g_att_dst,
+                      float* g_bias, float* workspace, int64_t workspace_floats,
+                      hipStream_t stream) {
   const bool weights = gW || g_att_src || g_att_dst;
   const int F = in_features, H = heads, C = channels, HC = heads * channels;
   if (H < 1 || C < 1 || F < 1 || num_nodes < 1) return SV2N_ERR_ARG;
@@ -304,11 +373,28 @@ extern "C" int sv2n_gat_wgrad_node(const float* x, int64_t ld_x, const float* dx
   const bool bias = g_bias && dbias_partial && bias_len > 0 && num_parts > 0;
   if (!weights && !bias) return 0;
   if ((int64_t)num_parts * bias_len >= (int64_t)1 << 29) return SV2N_ERR_SHAPE;
-  if (!workspace || workspace_floats < sv2n_gat_wgrad_node_workspace(num_nodes, F, ldx, H, C))
-    return SV2N_ERR_WORKSPACE;
+  const int64_t need = precision ? sv2n_gat_wgrad_node_bf16_workspace(num_nodes, F, ldx, H, C)
+                                 : sv2n_gat_wgrad_node_workspace(num_nodes, F, ldx, H, C);
+  if (!workspace || workspace_floats < need) return SV2N_ERR_WORKSPACE;
   float* T = workspace;  // reduced dWaugᵀ [F][ldx]
   float* slabs = T + (int64_t)F * ldx;
-  if (weights) {
+  if (weights && precision) {
+    // bf16 operands: both k-strided, rounded while staged (k_gemm3_t, NP = 1)
+    if (((uintptr_t)x & 15) || (ld_x & 3) || ((uintptr_t)dxs & 15) || (ldx & 3) || F < 4 ||
+        ldx < 4)
+      return SV2N_ERR_ALIGN;
+    const GemmPlan p = plan_gemm_bf16t(F, ldx, num_nodes);
+    float* out = p.splitk > 1 ? slabs : T;
+    if (p.nt == 13)
+      launch_wgrad_bf16<13>(p, stream, x, ld_x, dxs, ldx, F, num_nodes, out);
+    else
+      launch_wgrad_bf16<7>(p, stream, x, ld_x, dxs, ldx, F, num_nodes, out);
+    if (p.splitk > 1) {
+      const int64_t tot = (int64_t)F * ldx;
+      hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                         stream, slabs, p.splitk, (int64_t)F, (int64_t)ldx, T, (int64_t)ldx);
+    }
+  } else if (weights) {
     // T[f][o] = Σ_k x[k][f] · dxs[k][o]   (both operands k-strided)
     const GemmPlan p = plan_gemm(F, ldx, num_nodes);
     const bool avec = ((uintptr_t)x % 16 == 0) && (ld_x % 4 == 0);

@@ -54,9 +54,37 @@ static int launch_gemm3(hipStream_t st, const float* A, int64_t lda, const unsig
   return (int)hipGetLastError();
 }
 
+// bf16 operands (one plane), fp32 accumulation: the bf16 execution mode
+template <int NW, int MT, int NT, int BK>
+static int launch_gemm_bf16(hipStream_t st, const float* A, int64_t lda, const unsigned short* Bp,
+                            int64_t Kp, int64_t N, float* C, int64_t ldc, int64_t M, int64_t K) {
+  using Cfg = Gemm3Cfg<NW, MT, NT, BK, 1>;
+  constexpr size_t lds = Cfg::LDS;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)k_gemm3<NW, MT, NT, BK, 1, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  const dim3 grid((unsigned)((M + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN));
+  hipLaunchKernelGGL((k_gemm3<NW, MT, NT, BK, 1, 1>), grid, dim3(Cfg::THREADS), lds, st, A, lda,
+                     Bp, Kp, N * Kp, C, ldc, M, N, K);
+  return (int)hipGetLastError();
+}
+
 }  // namespace sv2n
 
 using namespace sv2n;
+
+extern "C" int sv2n_gemm_bf16(const float* A, int64_t lda, const uint16_t* Bp, float* C,
+                              int64_t ldc, int64_t M, int64_t N, int64_t K, hipStream_t stream) {
+  if (!A || !Bp || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldc < N) return SV2N_ERR_ARG;
+  if (((uintptr_t)A & 15) || (lda & 3) || ((uintptr_t)Bp & 15)) return SV2N_ERR_ALIGN;
+  const int64_t Kp = sv2n_split3_kpad(K);
+  const unsigned short* B = reinterpret_cast<const unsigned short*>(Bp);
+  const int64_t mb = (M + 127) / 128;
+  const bool wide = mb * ((N + 207) / 208) >= 240;
+  if (wide) return launch_gemm_bf16<8, 1, 13, 64>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+  return launch_gemm_bf16<8, 1, 7, 64>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+}
 
 extern "C" int64_t sv2n_split3_kpad(int64_t K) {
   return (K + SPLIT3_KALIGN - 1) / SPLIT3_KALIGN * SPLIT3_KALIGN;

@@ -80,7 +80,10 @@ static __global__ __attribute__((unused)) void k_split3(const float* __restrict_
   out[2 * rows * Kp + i] = h2;
 }
 
-template <int NW, int MT, int NT, int BK>
+// NP = number of bf16 planes per operand: 3 = the f32-accurate split (six
+// products), 1 = plain bf16 operands (bf16(a)·bf16(b), fp32 accumulation: the
+// "bf16 autocast" execution mode, one product; B's plane 0 is bf16_rn(w)).
+template <int NW, int MT, int NT, int BK, int NP = 3>
 struct Gemm3Cfg {
   static constexpr int THREADS = 64 * NW;
   static constexpr int BM = 16 * MT * NW, BN = 16 * NT;
@@ -89,27 +92,42 @@ struct Gemm3Cfg {
   // MI355X_MICROARCH.md §LDS) in 16 distinct 16-B bank slots
   static constexpr int ROW = BK + 16;
   static constexpr int AV = BM * (BK / 4) / THREADS;         // float4 per thread
-  static constexpr int BV = (3 * BN * (BK / 8) + THREADS - 1) / THREADS;  // uint4 per thread
-  static constexpr size_t LDS = sizeof(unsigned short) * 3 * (BM + BN) * ROW;
+  static constexpr int BV = (NP * BN * (BK / 8) + THREADS - 1) / THREADS;  // uint4 per thread
+  static constexpr size_t LDS = sizeof(unsigned short) * NP * (BM + BN) * ROW;
   static_assert(BM * (BK / 4) % THREADS == 0, "A staging must tile the threads");
 };
+
+// the MFMA products of one (A, B) fragment pair: NP = 3 keeps the six with
+// plane orders p + q <= 2 (small terms first), NP = 1 the single bf16 product
+template <int NP>
+__device__ __forceinline__ f32x4 mfma_planes(const bf16x8 (&a)[NP], const bf16x8 (&b)[NP],
+                                             f32x4 acc) {
+  if constexpr (NP == 3) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  }
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+}
 
 // Workgroup = NW waves stacked along M (wave tile MT x NT 16x16 tiles), K
 // blocks of BK, PF register sets of staged operands in flight (the loads for
 // block kb+PF are issued while block kb is computed from LDS).
-template <int NW, int MT, int NT, int BK, int PF>
+template <int NW, int MT, int NT, int BK, int PF, int NP = 3>
 __global__ __launch_bounds__(64 * NW) void k_gemm3(const float* __restrict__ A, int64_t lda,
                                                    const unsigned short* __restrict__ Bp,
                                                    int64_t ldb, int64_t bplane,
                                                    float* __restrict__ C, int64_t ldc, int64_t M,
                                                    int64_t N, int64_t K) {
-  using Cfg = Gemm3Cfg<NW, MT, NT, BK>;
+  using Cfg = Gemm3Cfg<NW, MT, NT, BK, NP>;
   constexpr int TH = Cfg::THREADS, BM = Cfg::BM, BN = Cfg::BN, ROW = Cfg::ROW;
   constexpr int AV = Cfg::AV, BV = Cfg::BV;
   constexpr int AC = BK / 4, BC = BK / 8;  // float4 / uint4 per row
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
-  unsigned short* sA = lds;                    // [3][BM][ROW]
-  unsigned short* sB = lds + 3 * BM * ROW;     // [3][BN][ROW]
+  unsigned short* sA = lds;                    // [NP][BM][ROW]
+  unsigned short* sB = lds + NP * BM * ROW;    // [NP][BN][ROW]
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
@@ -143,7 +161,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3(const float* __restrict__ A, 
     for (int s = 0; s < BV; ++s) {
       const int idx = t + TH * s;
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (idx < 3 * BN * BC) {
+      if (idx < NP * BN * BC) {
         const int p = idx / (BN * BC), rem = idx - p * BN * BC;
         const int r = rem / BC, c = rem - r * BC;
         const int64_t gn = min(n0 + r, N - 1);
@@ -159,16 +177,21 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3(const float* __restrict__ A, 
       const int r = idx / AC, c4 = idx - r * AC;
       const float4 v = ra[set][s];
       uint2 w[3];
-      split3_pk(v.x, v.y, w[0].x, w[1].x, w[2].x);
-      split3_pk(v.z, v.w, w[0].y, w[1].y, w[2].y);
+      if constexpr (NP == 3) {
+        split3_pk(v.x, v.y, w[0].x, w[1].x, w[2].x);
+        split3_pk(v.z, v.w, w[0].y, w[1].y, w[2].y);
+      } else {
+        w[0].x = bf16_pk(v.x, v.y);
+        w[0].y = bf16_pk(v.z, v.w);
+      }
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+      for (int p = 0; p < NP; ++p)
         *reinterpret_cast<uint2*>(sA + (p * BM + r) * ROW + 4 * c4) = w[p];
     }
 #pragma unroll
     for (int s = 0; s < BV; ++s) {
       const int idx = t + TH * s;
-      if (idx < 3 * BN * BC) {
+      if (idx < NP * BN * BC) {
         const int p = idx / (BN * BC), rem = idx - p * BN * BC;
         const int r = rem / BC, c = rem - r * BC;
         *reinterpret_cast<uint4*>(sB + (p * BN + r) * ROW + 8 * c) = rb[set][s];
@@ -178,29 +201,21 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3(const float* __restrict__ A, 
   auto compute = [&]() {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
-      bf16x8 af[MT][3];
+      bf16x8 af[MT][NP];
 #pragma unroll
       for (int a = 0; a < MT; ++a)
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
           af[a][p] = *reinterpret_cast<const bf16x8*>(
               sA + (p * BM + wave * 16 * MT + 16 * a + li) * ROW + kk + 8 * lg);
 #pragma unroll
       for (int b = 0; b < NT; ++b) {
-        bf16x8 bf[3];
+        bf16x8 bf[NP];
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
           bf[p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + 16 * b + li) * ROW + kk + 8 * lg);
 #pragma unroll
-        for (int a = 0; a < MT; ++a) {
-          // small terms first
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][2], bf[0], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][1], bf[1], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[2], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][1], bf[0], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[1], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[0], acc[a][b], 0, 0, 0);
-        }
+        for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<NP>(af[a], bf, acc[a][b]);
       }
     }
   };
@@ -246,14 +261,14 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3(const float* __restrict__ A, 
 // the contiguous row index, transposes them in registers and writes 4
 // consecutive k per plane (ds_write_b64) into the same [plane][row][k] LDS
 // image the k-major kernel reads.
-template <int NW, int MT, int NT, int BK>
+template <int NW, int MT, int NT, int BK, int NP = 3>
 struct Gemm3TCfg {
   static constexpr int THREADS = 64 * NW;
   static constexpr int BM = 16 * MT * NW, BN = 16 * NT;
   static constexpr int ROW = BK + 16;
   static constexpr int AU = BM * BK / 16, BU = BN * BK / 16;   // 4x4 micro-tiles
   static constexpr int AV = (AU + THREADS - 1) / THREADS, BV = (BU + THREADS - 1) / THREADS;
-  static constexpr size_t LDS = sizeof(unsigned short) * 3 * (BM + BN) * ROW;
+  static constexpr size_t LDS = sizeof(unsigned short) * NP * (BM + BN) * ROW;
 };
 
 template <int BK, int ROWS, int TH, int V>
@@ -277,7 +292,7 @@ __device__ __forceinline__ void t_load(float4 (&r)[V][4], const float* __restric
   }
 }
 
-template <int BK, int ROWS, int TH, int V, int ROW>
+template <int BK, int ROWS, int TH, int V, int ROW, int NP = 3>
 __device__ __forceinline__ void t_store(const float4 (&r)[V][4], unsigned short* __restrict__ sX,
                                         int t) {
   constexpr int UR = ROWS / 4;
@@ -288,6 +303,17 @@ __device__ __forceinline__ void t_store(const float4 (&r)[V][4], unsigned short*
     const int ug = idx % UR, kg = idx / UR;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {  // row 4ug + c, k = 4kg .. 4kg+3
+      if constexpr (NP == 1) {
+        const float* p0 = &r[s][0].x;
+        const float* p1 = &r[s][1].x;
+        const float* p2 = &r[s][2].x;
+        const float* p3 = &r[s][3].x;
+        uint2 w;
+        w.x = bf16_pk(p0[c], p1[c]);
+        w.y = bf16_pk(p2[c], p3[c]);
+        *reinterpret_cast<uint2*>(sX + (4 * ug + c) * ROW + 4 * kg) = w;
+        continue;
+      }
       unsigned short h[3][4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -305,18 +331,18 @@ __device__ __forceinline__ void t_store(const float4 (&r)[V][4], unsigned short*
   }
 }
 
-template <int NW, int MT, int NT, int BK>
+template <int NW, int MT, int NT, int BK, int NP = 3>
 __global__ __launch_bounds__(64 * NW) void k_gemm3_t(const float* __restrict__ A, int64_t lda,
                                                      const float* __restrict__ B, int64_t ldb,
                                                      float* __restrict__ C, int64_t ldc,
                                                      int64_t M, int64_t N, int64_t K,
                                                      int64_t kslice) {
-  using Cfg = Gemm3TCfg<NW, MT, NT, BK>;
+  using Cfg = Gemm3TCfg<NW, MT, NT, BK, NP>;
   constexpr int TH = Cfg::THREADS, BM = Cfg::BM, BN = Cfg::BN, ROW = Cfg::ROW;
   constexpr int AV = Cfg::AV, BV = Cfg::BV;
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
-  unsigned short* sA = lds;                    // [3][BM][ROW]
-  unsigned short* sB = lds + 3 * BM * ROW;     // [3][BN][ROW]
+  unsigned short* sA = lds;                    // [NP][BM][ROW]
+  unsigned short* sB = lds + NP * BM * ROW;    // [NP][BN][ROW]
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
@@ -334,8 +360,8 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3_t(const float* __restrict__ A
   t_load<BK, BN, TH, BV>(rb, B, ldb, n0, N, kbeg, kend, t);
   for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
     __syncthreads();
-    t_store<BK, BM, TH, AV, ROW>(ra, sA, t);
-    t_store<BK, BN, TH, BV, ROW>(rb, sB, t);
+    t_store<BK, BM, TH, AV, ROW, NP>(ra, sA, t);
+    t_store<BK, BN, TH, BV, ROW, NP>(rb, sB, t);
     __syncthreads();
     if (k0 + BK < kend) {
       t_load<BK, BM, TH, AV>(ra, A, lda, m0, M, k0 + BK, kend, t);
@@ -343,28 +369,21 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3_t(const float* __restrict__ A
     }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
-      bf16x8 af[MT][3];
+      bf16x8 af[MT][NP];
 #pragma unroll
       for (int a = 0; a < MT; ++a)
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
           af[a][p] = *reinterpret_cast<const bf16x8*>(
               sA + (p * BM + wave * 16 * MT + 16 * a + li) * ROW + kk + 8 * lg);
 #pragma unroll
       for (int b = 0; b < NT; ++b) {
-        bf16x8 bf[3];
+        bf16x8 bf[NP];
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
           bf[p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + 16 * b + li) * ROW + kk + 8 * lg);
 #pragma unroll
-        for (int a = 0; a < MT; ++a) {
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][2], bf[0], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][1], bf[1], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[2], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][1], bf[0], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[1], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][0], bf[0], acc[a][b], 0, 0, 0);
-        }
+        for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<NP>(af[a], bf, acc[a][b]);
       }
     }
   }

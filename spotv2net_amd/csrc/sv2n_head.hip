@@ -10,14 +10,32 @@
 // (last_block_sc1_2): deterministic, and no separate reduce launch.
 //
 // Workspace layout (floats): [0, 288) ticket counters (zero before the first
-// call; every launch leaves it zero) | [16, ...) partial slabs.
+// call; every launch leaves it zero) | [288, ...) partial slabs.
+//
+// Rows per workgroup R = 256 for in_features <= 128 (one row per thread);
+// wider heads (C1/C3: 500) stage fewer rows, R ∈ {128, 64, 32}, so the
+// [R][C+1] image and the weights fit the 160 KiB LDS, and 256/R threads share
+// a row (strided over c, partials added in a fixed order).
 #include "sv2n_common.h"
 
 namespace sv2n {
 
 constexpr int HEAD_MAX_OUT = 16;
-constexpr int HEAD_ROWS = 256;  // rows per workgroup (one per thread)
+constexpr int HEAD_MAX_IN = 1024;
+constexpr int HEAD_ROWS = 256;  // rows per workgroup at most (one per thread)
 constexpr int HEAD_WS_HDR = SV2N_TICKET_WORDS;  // two-level ticket counters
+constexpr size_t HEAD_LDS_BUDGET = 160 * 1024 - 20 * 1024;  // dynamic part (statics below)
+
+// rows per workgroup for in_features C, out_features O (0: does not fit)
+__host__ __device__ inline int head_rows_per_block(int C, int O) {
+  if (C <= 128) return 256;
+  for (int R = 128; R >= 32; R >>= 1)
+    if ((size_t)4 * ((size_t)R * (C + 1) + (size_t)O * C) <= HEAD_LDS_BUDGET) return R;
+  return 0;
+}
+__host__ __device__ inline size_t head_lds_bytes(int C, int O) {
+  return (size_t)4 * ((size_t)head_rows_per_block(C, O) * (C + 1) + (size_t)O * C);
+}
 
 // x rows staged through LDS so the global reads are coalesced.  The block's
 // rows are one contiguous span of nr*C floats: it is read as 16-B buffer
@@ -63,30 +81,58 @@ __device__ __forceinline__ void head_rows(const float* __restrict__ x, int64_t r
   }
 }
 
+// acc[o] = Σ_c x[row][c]·W[o][c] of the block's row r = t % R over the c of
+// thread part q = t / R (c ≡ q mod 256/R); with more than one part per row the
+// parts are added in a fixed order through s_part.  Returns true for the
+// thread that holds row r's total (q == 0, r < nr).
+template <int OUT>
+__device__ __forceinline__ bool head_dot(const float* __restrict__ sx, const float* __restrict__ sw,
+                                         int C, int R, int nr, int t, float (&acc)[OUT],
+                                         float* __restrict__ s_part) {
+  const int CP = C + 1;
+  const int r = t % R, q = t / R, Q = 256 / R;
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) acc[o] = 0.f;
+  if (r < nr) {
+    for (int c = q; c < C; c += Q) {
+      const float xv = sx[r * CP + c];
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) acc[o] = fmaf(xv, sw[o * C + c], acc[o]);
+    }
+  }
+  if (Q == 1) return r < nr;
+  __syncthreads();
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) s_part[(q * R + r) * OUT + o] = acc[o];
+  __syncthreads();
+  if (q != 0) return false;
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) {
+    float v = 0.f;
+    for (int k = 0; k < Q; ++k) v += s_part[(k * R + r) * OUT + o];
+    acc[o] = v;
+  }
+  return r < nr;
+}
+
 template <int OUT>
 __global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ x, int64_t N, int C,
                                                   const float* __restrict__ W,
                                                   const float* __restrict__ b,
-                                                  float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float sx[];  // [256][C+1]
-  __shared__ float sw[HEAD_MAX_OUT * 128];
+                                                  float* __restrict__ out, int R) {
+  extern __shared__ __attribute__((aligned(16))) float sx[];  // [R][C+1] | sw [OUT][C]
+  __shared__ float s_part[256 * OUT];
+  float* sw = sx + R * (C + 1);
   const int t = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * HEAD_ROWS;
-  const int nr = (int)min((int64_t)HEAD_ROWS, N - r0);
-  const int CP = C + 1;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int nr = (int)min((int64_t)R, N - r0);
   head_rows<OUT>(x, r0, nr, C, sx, W, sw, t);
   __syncthreads();
-  if (t < nr) {
-    float acc[OUT];
+  float acc[OUT];
+  if (head_dot<OUT>(sx, sw, C, R, nr, t, acc, s_part)) {
+    const int r = t % R;
 #pragma unroll
-    for (int o = 0; o < OUT; ++o) acc[o] = 0.f;
-    for (int c = 0; c < C; ++c) {
-      const float xv = sx[t * CP + c];
-#pragma unroll
-      for (int o = 0; o < OUT; ++o) acc[o] = fmaf(xv, sw[o * C + c], acc[o]);
-    }
-#pragma unroll
-    for (int o = 0; o < OUT; ++o) out[(r0 + t) * OUT + o] = acc[o] + (b ? b[o] : 0.f);
+    for (int o = 0; o < OUT; ++o) out[(r0 + r) * OUT + o] = acc[o] + (b ? b[o] : 0.f);
   }
 }
 
@@ -96,29 +142,24 @@ template <int OUT>
 __global__ __launch_bounds__(256) void k_head_mse_fwd(
     const float* __restrict__ x, int64_t N, int C, const float* __restrict__ W,
     const float* __restrict__ b, const float* __restrict__ target, float* __restrict__ yhat,
-    float* __restrict__ diff, float* __restrict__ ws, float* __restrict__ loss, float inv_count) {
-  extern __shared__ __attribute__((aligned(16))) float sx[];  // [256][C+1]
-  __shared__ float sw[HEAD_MAX_OUT * 128];
+    float* __restrict__ diff, float* __restrict__ ws, float* __restrict__ loss, float inv_count,
+    int R) {
+  extern __shared__ __attribute__((aligned(16))) float sx[];  // [R][C+1] | sw [OUT][C]
+  __shared__ float s_part[256 * OUT];
   __shared__ float s_red[256];
+  float* sw = sx + R * (C + 1);
   const int t = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * HEAD_ROWS;
-  const int nr = (int)min((int64_t)HEAD_ROWS, N - r0);
-  const int CP = C + 1;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int nr = (int)min((int64_t)R, N - r0);
   head_rows<OUT>(x, r0, nr, C, sx, W, sw, t);
   __syncthreads();
   float sq = 0.f;
-  if (t < nr) {
-    float acc[OUT];
-#pragma unroll
-    for (int o = 0; o < OUT; ++o) acc[o] = 0.f;
-    for (int c = 0; c < C; ++c) {
-      const float xv = sx[t * CP + c];
-#pragma unroll
-      for (int o = 0; o < OUT; ++o) acc[o] = fmaf(xv, sw[o * C + c], acc[o]);
-    }
+  float acc[OUT];
+  if (head_dot<OUT>(sx, sw, C, R, nr, t, acc, s_part)) {
+    const int r = t % R;
 #pragma unroll
     for (int o = 0; o < OUT; ++o) {
-      const int64_t k = (r0 + t) * OUT + o;
+      const int64_t k = (r0 + r) * OUT + o;
       const float v = acc[o] + (b ? b[o] : 0.f);
       if (yhat) yhat[k] = v;
       const float d = v - target[k];
@@ -134,7 +175,7 @@ __global__ __launch_bounds__(256) void k_head_mse_fwd(
   }
   float* part = ws + HEAD_WS_HDR;
   if (t == 0) st_sc1(part + blockIdx.x, s_red[0]);
-  int* s_flag = reinterpret_cast<int*>(sw);
+  int* s_flag = reinterpret_cast<int*>(s_part);
   if (last_block_sc1_2(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
     float a = 0.f;
     for (int k = t; k < (int)gridDim.x; k += 256) a += ld_sc1(part + k);
@@ -162,20 +203,21 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ x, i
                                                   const float* __restrict__ src, float scale,
                                                   const float* __restrict__ dscale,
                                                   float* __restrict__ dx, float* __restrict__ ws,
-                                                  float* __restrict__ gW, float* __restrict__ gb) {
-  extern __shared__ __attribute__((aligned(16))) float sx[];  // [256][C+1] x rows
-  __shared__ float sw[HEAD_MAX_OUT * 128];
+                                                  float* __restrict__ gW, float* __restrict__ gb,
+                                                  int R) {
+  extern __shared__ __attribute__((aligned(16))) float sx[];  // [R][C+1] x rows | sw [OUT][C]
   __shared__ float sd[HEAD_ROWS][HEAD_MAX_OUT];
   __shared__ float s_grp[256];
+  float* sw = sx + R * (C + 1);
   const int t = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * HEAD_ROWS;
-  const int nr = (int)min((int64_t)HEAD_ROWS, N - r0);
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int nr = (int)min((int64_t)R, N - r0);
   const int CP = C + 1;
   const int tot = OUT * CP;
   const int RG = tot <= 256 ? 256 / tot : 1;
   const float sc = dscale ? scale * dscale[0] : scale;
   head_rows<OUT>(x, r0, nr, C, sx, W, sw, t);
-  for (int k = t; k < HEAD_ROWS * OUT; k += 256) {
+  for (int k = t; k < R * OUT; k += 256) {
     const int r = k / OUT;
     sd[r][k - r * OUT] = (r < nr) ? src[(r0 + r) * OUT + (k - r * OUT)] * sc : 0.f;
   }
@@ -258,8 +300,9 @@ using namespace sv2n;
 
 static int head_check(int64_t N, int C, int out_ch) {
   if (N <= 0 || C <= 0 || out_ch <= 0) return SV2N_ERR_ARG;
-  if (out_ch > HEAD_MAX_OUT || C > 128 || out_ch * C > HEAD_MAX_OUT * 128) return SV2N_ERR_SHAPE;
-  if (N > (int64_t)HEAD_ROWS * 0x7fffffff) return SV2N_ERR_SHAPE;
+  if (out_ch > HEAD_MAX_OUT || C > HEAD_MAX_IN || head_rows_per_block(C, out_ch) == 0)
+    return SV2N_ERR_SHAPE;
+  if (N / head_rows_per_block(C, out_ch) >= 0x7fffffff) return SV2N_ERR_SHAPE;
   return 0;
 }
 
@@ -290,19 +333,22 @@ extern "C" int sv2n_head_fwd(const float* x, int64_t num_rows, int in_features,
   const int out_ch = out_features;
   if (!x || !weight || !out) return SV2N_ERR_ARG;
   if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
-  const unsigned grid = (unsigned)((num_rows + HEAD_ROWS - 1) / HEAD_ROWS);
-  const size_t lds = sizeof(float) * HEAD_ROWS * (in_features + 1);
+  const int R = head_rows_per_block(in_features, out_ch);
+  const unsigned grid = (unsigned)((num_rows + R - 1) / R);
+  const size_t lds = head_lds_bytes(in_features, out_ch);
   SV2N_HEAD_DISPATCH(k_head_fwd, dim3(grid), dim3(256), lds, stream, x, num_rows, in_features,
-                     weight, bias, out)
+                     weight, bias, out, R)
   return (int)hipGetLastError();
 }
 
-static int64_t head_bwd_blocks(int64_t num_rows) {
-  return (num_rows + HEAD_ROWS - 1) / HEAD_ROWS;
+static int64_t head_bwd_blocks(int64_t num_rows, int C, int O) {
+  const int R = head_rows_per_block(C, O);
+  return R ? (num_rows + R - 1) / R : 0;
 }
 
 extern "C" int64_t sv2n_head_bwd_workspace(int64_t num_rows, int in_features, int out_features) {
-  return HEAD_WS_HDR + head_bwd_blocks(num_rows) * (int64_t)out_features * (in_features + 1);
+  return HEAD_WS_HDR + head_bwd_blocks(num_rows, in_features, out_features) *
+                           (int64_t)out_features * (in_features + 1);
 }
 
 static int head_bwd_launch(const float* x, int64_t num_rows, int in_features, const float* weight,
@@ -311,13 +357,14 @@ static int head_bwd_launch(const float* x, int64_t num_rows, int in_features, co
                            int64_t workspace_floats, hipStream_t stream) {
   if (!x || !weight || !src || !dx || !workspace) return SV2N_ERR_ARG;
   if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
-  const int64_t nb = head_bwd_blocks(num_rows);
+  const int64_t nb = head_bwd_blocks(num_rows, in_features, out_ch);
   if (workspace_floats < sv2n_head_bwd_workspace(num_rows, in_features, out_ch))
     return SV2N_ERR_WORKSPACE;
   if ((uintptr_t)workspace & 15) return SV2N_ERR_ALIGN;
-  const size_t lds = sizeof(float) * HEAD_ROWS * (in_features + 1);
+  const int R = head_rows_per_block(in_features, out_ch);
+  const size_t lds = head_lds_bytes(in_features, out_ch);
   SV2N_HEAD_DISPATCH(k_head_bwd, dim3((unsigned)nb), dim3(256), lds, stream, x, num_rows,
-                     in_features, weight, src, scale, dscale, dx, workspace, g_weight, g_bias)
+                     in_features, weight, src, scale, dscale, dx, workspace, g_weight, g_bias, R)
   return (int)hipGetLastError();
 }
 
@@ -330,7 +377,7 @@ extern "C" int sv2n_head_bwd(const float* x, int64_t num_rows, int in_features,
 }
 
 extern "C" int64_t sv2n_head_mse_workspace(int64_t num_rows, int in_features, int out_features) {
-  const int64_t nb = (num_rows + HEAD_ROWS - 1) / HEAD_ROWS;
+  const int64_t nb = head_bwd_blocks(num_rows, in_features, out_features);
   return std::max<int64_t>(sv2n_head_bwd_workspace(num_rows, in_features, out_features),
                            HEAD_WS_HDR + nb);
 }
@@ -345,11 +392,12 @@ extern "C" int sv2n_head_mse_fwd(const float* x, int64_t num_rows, int in_featur
   if (workspace_floats < sv2n_head_mse_workspace(num_rows, in_features, out_ch))
     return SV2N_ERR_WORKSPACE;
   if ((uintptr_t)workspace & 15) return SV2N_ERR_ALIGN;
-  const unsigned grid = (unsigned)((num_rows + HEAD_ROWS - 1) / HEAD_ROWS);
-  const size_t lds = sizeof(float) * HEAD_ROWS * (in_features + 1);
+  const int R = head_rows_per_block(in_features, out_ch);
+  const unsigned grid = (unsigned)((num_rows + R - 1) / R);
+  const size_t lds = head_lds_bytes(in_features, out_ch);
   const float inv_count = 1.f / (float)(num_rows * out_ch);
   SV2N_HEAD_DISPATCH(k_head_mse_fwd, dim3(grid), dim3(256), lds, stream, x, num_rows,
-                     in_features, weight, bias, target, yhat, diff, workspace, loss, inv_count)
+                     in_features, weight, bias, target, yhat, diff, workspace, loss, inv_count, R)
   return (int)hipGetLastError();
 }
 

@@ -206,6 +206,56 @@ class WindowDataset:
         self.future_steps = int(future_steps)
         last = vol.shape[0] - seq_length - self.future_steps + 1
         self.starts = torch.arange(cut, max(cut, last), device=vol.device)
+        n = vol.shape[1]
+        self.n = n
+        dev = vol.device
+        src, tgt = canonical_pairs(n)
+        P = len(src) // 2
+        # index vectors of the capturable gather (fill): no host->device copies
+        self._src = torch.tensor(src, dtype=torch.long).to(dev)
+        self._tgt = torch.tensor(tgt, dtype=torch.long).to(dev)
+        self._up_s, self._up_t = self._src[:P], self._tgt[:P]
+        self._arS = torch.arange(seq_length, device=dev)
+        self._arF = torch.arange(self.future_steps, device=dev)
+
+    def empty_batch(self, batch_size: int) -> Batch:
+        """Static device buffers of one batch of ``batch_size`` windows (the
+        layout of ``batch``), for ``fill``: a hipGraph-captured train step
+        reads the same tensors every replay."""
+        B, n, S = batch_size, self.n, self.S
+        E0 = n * (n - 1)
+        dev = self.vol.device
+        b = Batch(x=torch.empty(B * n, n * S, device=dev),
+                  edge_index=canonical_edge_index(n, B, dev),
+                  edge_attr=torch.empty(B * E0, 3 * S, device=dev),
+                  y_x=torch.empty(B * n * self.future_steps, device=dev),
+                  batch=torch.arange(B, device=dev).repeat_interleave(n),
+                  ptr=torch.arange(B + 1, device=dev) * n)
+        b.nodes_per_graph = n
+        return b
+
+    def fill(self, out: Batch, idx: torch.Tensor) -> None:
+        """Gather the windows ``self.starts[idx]`` into ``out``'s buffers
+        (from ``empty_batch(idx.numel())``), on the device, with no host
+        synchronisation or host->device copy: capturable into a hipGraph.
+        Same values as ``batch(idx)``."""
+        B, n, S, Fs = idx.numel(), self.n, self.S, self.future_steps
+        P = self._up_s.numel()
+        st = self.starts.index_select(0, idx)
+        tidx = st.view(B, 1) + self._arS.view(1, S)                               # [B, S]
+        V = self.vol[tidx]                                                        # [B, S, n, n]
+        W = self.volvol[tidx]
+        out.x.view(B, n, n, S).copy_(V.permute(0, 2, 3, 1))                       # x[v, c*S+t]
+        ea = out.edge_attr.view(B, 2 * P, 3, S)                                   # ea[e, k*S+t]
+        cv = W[:, :, self._up_s, self._up_t].permute(0, 2, 1)                     # [B, P, S]
+        ea[:, :P, 0].copy_(cv)
+        ea[:, P:, 0].copy_(cv)
+        var = torch.diagonal(W, dim1=2, dim2=3).permute(0, 2, 1)                  # [B, n, S]
+        ea[:, :, 1].copy_(var[:, self._src])
+        ea[:, :, 2].copy_(var[:, self._tgt])
+        fidx = st.view(B, 1) + S + self._arF.view(1, Fs)                          # [B, F]
+        yk = torch.diagonal(self.vol[fidx], dim1=2, dim2=3)                       # [B, F, n]
+        out.y_x.view(B, n, Fs).copy_(yk.permute(0, 2, 1))
 
     def __len__(self) -> int:
         return int(self.starts.numel())

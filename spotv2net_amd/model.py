@@ -68,6 +68,10 @@ class GATModel(nn.Module):
         self.gat_layers = nn.ModuleList(first + stacked)
         self.linear = nn.Linear(dim_hidden_layers[-1], output_node_channels)
 
+        # execution mode of the GAT stack: None = fp32 unless inside
+        # torch.autocast("cuda", dtype=torch.bfloat16); "f32" / "bf16" force it
+        self.precision: Optional[str] = None
+
         acts = {"relu": F.relu, "tanh": F.tanh, "sigmoid": F.sigmoid}
         if activation not in acts:
             raise ValueError("Choose an available activation function")
@@ -82,7 +86,15 @@ class GATModel(nn.Module):
                 edge_attr = self.bnorm_edge(edge_attr)
         layout = _layout_of(data, x, edge_index)
         return gat_stack(x, edge_attr, tuple(self.gat_layers), layout, self._act_code,
-                         float(self.dropout or 0.0), self.training)
+                         float(self.dropout or 0.0), self.training, self.precision)
+
+    def set_precision(self, precision: Optional[str]) -> "GATModel":
+        """"bf16": projection / weight-gradient GEMMs on bf16 operands with
+        fp32 accumulation (the reference under bf16 autocast, BASELINE C3);
+        "f32": fp32-accurate everywhere (1e-5 parity); None: follow autocast."""
+        ops.resolve_precision(precision)  # validates
+        self.precision = precision
+        return self
 
     def forward(self, data):
         return linear_head(self._hidden(data), self.linear).view(-1)

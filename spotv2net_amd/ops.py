@@ -111,18 +111,48 @@ def project(a: torch.Tensor, w: torch.Tensor, transpose_w: bool) -> torch.Tensor
 
 
 def project_planes(a: torch.Tensor, planes: Optional[torch.Tensor], w: torch.Tensor,
-                   transpose_w: bool) -> torch.Tensor:
+                   transpose_w: bool, bf16: bool = False) -> torch.Tensor:
     """project(a, w, transpose_w) with w's bf16 split planes already made
-    (sv2n_gat_prep_fwd_all); exact-f32 fallback on w as in project()."""
-    if planes is None or not _split_ok(a):
-        return project(a, w, transpose_w)
+    (sv2n_gat_prep_fwd_all); exact-f32 fallback on w as in project().
+    ``bf16``: the bf16 execution mode (sv2n_gemm_bf16: bf16 operands, fp32
+    accumulation, on plane 0 = bf16_rn(w))."""
     lib = _lib.load()
     M, K = a.shape
     N = w.shape[1] if transpose_w else w.shape[0]
+    if bf16:
+        if planes is None:
+            planes = weight_planes(w, transpose_w)
+        if not (a.stride(1) == 1 and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0):
+            a = _aligned(a) if a.size(1) % 4 == 0 else \
+                torch.nn.functional.pad(a, (0, (-a.size(1)) % 4))[:, :K]
+        out = torch.empty(M, N, device=a.device, dtype=torch.float32)
+        _lib.check(lib.sv2n_gemm_bf16(a.data_ptr(), a.stride(0), planes.data_ptr(),
+                                      out.data_ptr(), out.stride(0), M, N, K, _stream(a.device)),
+                   "sv2n_gemm_bf16")
+        return out
+    if planes is None or not _split_ok(a):
+        return project(a, w, transpose_w)
     out = torch.empty(M, N, device=a.device, dtype=torch.float32)
     _lib.check(lib.sv2n_gemm_f32x3(a.data_ptr(), a.stride(0), planes.data_ptr(), out.data_ptr(),
                                    out.stride(0), M, N, K, _stream(a.device)), "sv2n_gemm_f32x3")
     return out
+
+
+PRECISIONS = ("f32", "bf16")
+
+
+def resolve_precision(precision: Optional[str]) -> str:
+    """The execution mode of a fused GAT node: an explicit ``precision``, else
+    bf16 inside ``torch.autocast("cuda", dtype=torch.bfloat16)`` (the
+    reference run with autocast, BASELINE config C3), else f32."""
+    if precision is not None:
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {PRECISIONS}, got {precision!r}")
+        return precision
+    if torch.is_autocast_enabled("cuda") and \
+            torch.get_autocast_dtype("cuda") == torch.bfloat16:
+        return "bf16"
+    return "f32"
 
 
 class _Linear(torch.autograd.Function):

@@ -34,7 +34,7 @@ import torch
 
 from . import _lib
 from .layout import GraphLayout
-from .ops import _aligned, _require_device, gemm_f32, pad_columns, project, project_planes
+from .ops import _aligned, _require_device, pad_columns, project_planes, resolve_precision
 
 
 def _grad_buf(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -46,6 +46,18 @@ def _grad_buf(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
         p.grad = p.grad.contiguous()
     return p.grad
 
+
+HEAD_MAX_IN, HEAD_MAX_OUT = 1024, 16   # sv2n_head_* limits (include/sv2n.h)
+
+
+def head_fits(in_features: int, out_features: int) -> bool:
+    """Whether sv2n_head_* take this head (sv2n_head.hip head_rows_per_block:
+    at least 32 staged rows of in_features + 1 floats plus the weights in the
+    kernels' 140 KiB dynamic LDS)."""
+    if not (0 < in_features <= HEAD_MAX_IN and 0 < out_features <= HEAD_MAX_OUT):
+        return False
+    return in_features <= 128 or 4 * (32 * (in_features + 1) + out_features * in_features) \
+        <= 140 * 1024
 
 _mode = threading.local()
 
@@ -124,7 +136,7 @@ def _ldx(conv) -> int:
 class _GATStack(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, edge_attr, convs, layout: GraphLayout, act: int, post_dropout: float,
-                training: bool, *params):
+                training: bool, precision: str, *params):
         lib = _lib.load()
         dev = x.device
         st = _lib.stream_handle(dev)
@@ -133,6 +145,7 @@ class _GATStack(torch.autograd.Function):
         use_edge = edge_attr is not None and all(c.lin_edge is not None for c in convs)
         H = convs[0].heads
         tiled = layout.tiled
+        bf16 = precision == "bf16"
         if use_edge and any(c.heads != H for c in convs):
             raise NotImplementedError("fused edge pass needs equal head counts across layers")
 
@@ -203,7 +216,7 @@ class _GATStack(torch.autograd.Function):
             F = c.in_channels
             if xin.size(1) != F:
                 raise ValueError(f"layer {l}: expected {F} input features, got {xin.size(1)}")
-            xs = project_planes(xin, planes[l], waugs[l], False)  # x · Waugᵀ
+            xs = project_planes(xin, planes[l], waugs[l], False, bf16)  # x · Waugᵀ
             keep, kscale = None, 1.0
             kn = n if tiled else 32  # keep-mask tile: [B][H][n][n] tiled, [B][H][32][32] per-graph
             if training and c.dropout > 0.0:
@@ -252,6 +265,7 @@ class _GATStack(torch.autograd.Function):
         ctx.convs = convs
         ctx.layout = layout
         ctx.direct = _direct_mode()
+        ctx.bf16 = bf16
         ctx.meta = (L, act, use_edge, hp, H)
         ctx.kscales = [(1.0 / (1.0 - c.dropout)) if (training and 0.0 < c.dropout < 1.0) else
                        (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs]
@@ -284,7 +298,7 @@ class _GATStack(torch.autograd.Function):
         daes = [None] * L
         need_x0 = ctx.needs_input_grad[0]
         params = [p for c in convs for p in layer_params(c)]
-        grad_of = _GradTargets(params, ctx.needs_input_grad[7:], ctx.direct, dev)
+        grad_of = _GradTargets(params, ctx.needs_input_grad[8:], ctx.direct, dev)
         for l in range(L - 1, -1, -1):
             c = convs[l]
             Hc, C = c.heads, c.out_channels
@@ -325,15 +339,20 @@ class _GATStack(torch.autograd.Function):
                 # split-K dWaugᵀ GEMM + one fused epilogue (fold, transpose,
                 # att and bias grads), accumulated into .grad
                 x_l = xs_in[l]
-                ws_n = lib.sv2n_gat_wgrad_node_workspace(N, F, xs.size(1), Hc, C)
+                # bf16 mode: bf16-operand GEMM when x_l's rows are 16-B multiples
+                wg_bf16 = ctx.bf16 and x_l.stride(0) % 4 == 0 and F >= 4
+                ws_fn = lib.sv2n_gat_wgrad_node_bf16_workspace if wg_bf16 else \
+                    lib.sv2n_gat_wgrad_node_workspace
+                wg_fn = lib.sv2n_gat_wgrad_node_bf16 if wg_bf16 else lib.sv2n_gat_wgrad_node
+                ws_n = ws_fn(N, F, xs.size(1), Hc, C)
                 ws = torch.empty(max(ws_n, 1), device=dev, dtype=torch.float32)
-                _lib.check(lib.sv2n_gat_wgrad_node(
+                _lib.check(wg_fn(
                     x_l.data_ptr(), x_l.stride(0), dxs.data_ptr(), dxs.stride(0), N, F,
                     c.lin_src.weight.data_ptr(), c.att_src.data_ptr(), c.att_dst.data_ptr(), Hc, C,
                     dbp.data_ptr(), B, OC, _lib.ptr(gW), _lib.ptr(gas), _lib.ptr(gad),
                     _lib.ptr(gb), ws.data_ptr(), ws_n, st), "sv2n_gat_wgrad_node")
             if l > 0 or need_x0:
-                dy = project_planes(dxs, planes_t[l], waugs[l], True)  # dxs · Waug
+                dy = project_planes(dxs, planes_t[l], waugs[l], True, ctx.bf16)  # dxs · Waug
 
         if use_edge and ea is not None:
             # grads exist (zeros) even without edges, as in PyG
@@ -361,7 +380,7 @@ class _GATStack(torch.autograd.Function):
                         c.att_edge.data_ptr(), c.heads, c.out_channels, D, _lib.ptr(gWe),
                         _lib.ptr(gae), st), "sv2n_gat_prep_bwd_edge")
         dx0 = dy if need_x0 else None
-        return (dx0, None, None, None, None, None, None) + grad_of.returned()
+        return (dx0, None, None, None, None, None, None, None) + grad_of.returned()
 
 
 def _require_params(params) -> None:
@@ -380,8 +399,15 @@ def _require_params(params) -> None:
 
 
 def gat_stack(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs: Sequence,
-              layout: GraphLayout, act: int, post_dropout: float, training: bool) -> torch.Tensor:
-    """Run ``convs`` (GATConv modules) as one fused autograd node."""
+              layout: GraphLayout, act: int, post_dropout: float, training: bool,
+              precision: Optional[str] = None) -> torch.Tensor:
+    """Run ``convs`` (GATConv modules) as one fused autograd node.
+
+    ``precision``: "f32" (f32-accurate GEMMs, 1e-5 parity with PyG fp32) or
+    "bf16" (projection and weight-gradient GEMMs on bf16 operands with fp32
+    accumulation; softmax, aggregation and edge logits stay fp32); None =
+    bf16 inside torch.autocast(cuda, bfloat16), else f32."""
+    precision = resolve_precision(precision)
     params = []
     for c in convs:
         params += layer_params(c)
@@ -394,7 +420,7 @@ def gat_stack(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs: Sequenc
         if p.device != x.device:
             raise RuntimeError("parameters and data must be on the same device")
     return _GATStack.apply(x, edge_attr, tuple(convs), layout, int(act), float(post_dropout),
-                           bool(training), *params)
+                           bool(training), precision, *params)
 
 
 class _Head(torch.autograd.Function):
@@ -490,16 +516,16 @@ def head_mse_loss(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tensor
     """mean((linear(x).view(-1) - target)²) with the head and the loss fused."""
     _require_params((linear.weight, linear.bias))
     _require_device(x, target)
-    if linear.in_features > 128 or linear.out_features > 16:
+    if not head_fits(linear.in_features, linear.out_features):
         return torch.nn.functional.mse_loss(linear(x).view(-1), target)
     return _HeadMSE.apply(x, target, linear, linear.weight, linear.bias)
 
 
 def linear_head(x: torch.Tensor, linear: torch.nn.Linear) -> torch.Tensor:
     """``linear(x)`` for GATModel's output layer on the sv2n head kernels
-    (in_features <= 128, out_features <= 16; otherwise the nn.Linear itself)."""
+    (in_features <= 1024, out_features <= 16; otherwise the nn.Linear itself)."""
     _require_params((linear.weight, linear.bias))
     _require_device(x)
-    if linear.in_features > 128 or linear.out_features > 16:
+    if not head_fits(linear.in_features, linear.out_features):
         return linear(x)
     return _Head.apply(x, linear, linear.weight, linear.bias)

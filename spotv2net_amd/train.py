@@ -104,20 +104,38 @@ def make_adam(params, lr: float):
         return torch.optim.Adam(params, lr=lr, capturable=True, foreach=True)
 
 
+class _Shape:
+    """One captured batch shape of a TrainStep: its static data, the optional
+    capturable ``prepare`` (e.g. WindowDataset.fill from an index buffer),
+    its graphs and its loss output."""
+
+    def __init__(self, data, prepare: Optional[Callable[[], None]]):
+        self.data, self.prepare = data, prepare
+        self.g_fb = self.g_opt = None
+        self.loss: Optional[torch.Tensor] = None
+
+
 class TrainStep:
     """One optimisation step over a static device-resident batch.
 
     ``data`` is read through ``data.x / edge_index / edge_attr / y_x``; for
-    graph replay the same tensors must stay alive (refresh them in place to
-    feed new batches)."""
+    graph replay the same tensors must stay alive (refresh them in place, or
+    pass ``prepare``: a capturable callable run at the start of every step that
+    refills them, e.g. ``lambda: dataset.fill(data, idx_buffer)``).
+    ``add_shape`` captures further batch shapes (a ragged last batch) that
+    share the parameters, gradients and optimizer state.
+
+    Constructing it applies no update: the warm-up steps before capture are
+    undone (parameters, optimizer state, RNG)."""
 
     def __init__(self, model: torch.nn.Module, data, lr: float = 1e-3,
                  loss_fn: Callable = torch.nn.functional.mse_loss, use_graph: bool = True,
-                 group=None, warmup: int = 3, optimizer: str = "sv2n"):
+                 group=None, warmup: int = 3, optimizer: str = "sv2n",
+                 prepare: Optional[Callable[[], None]] = None):
         self.model = model
-        self.data = data
         self.loss_fn = loss_fn
         self.group = group
+        self.warmup = warmup
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.flat_params = flatten_params(self.params)
         self.flat = flatten_grads(self.params)
@@ -130,33 +148,49 @@ class TrainStep:
         self._one = torch.ones((), device=self.flat.device)
         # fused head + MSE (two launches) when the model offers it
         self._fused_mse = loss_fn is torch.nn.functional.mse_loss and hasattr(model, "mse_loss")
-        self._g_fb = self._g_opt = None
-        if use_graph:
-            self._capture(warmup)
+        self._shapes = []
+        self.add_shape(data, prepare)
+
+    @property
+    def data(self):
+        return self._shapes[0].data
+
+    def add_shape(self, data, prepare: Optional[Callable[[], None]] = None) -> int:
+        """Capture the step for another static batch; returns its index for
+        ``__call__(shape)``."""
+        sh = _Shape(data, prepare)
+        self._shapes.append(sh)
+        if self.use_graph:
+            self._capture(sh, self.warmup)
+        return len(self._shapes) - 1
 
     # -- eager pieces -------------------------------------------------------
-    def _fwd_bwd(self) -> None:
+    def _fwd_bwd(self, sh: _Shape) -> None:
         from .stack import direct_grad_accumulation
+        if sh.prepare is not None:
+            sh.prepare()
         if not getattr(self.opt, "zeroes_grads", False):
             self.flat.zero_()
         # every p.grad is a view of self.flat: the fused nodes accumulate into
         # it directly (no per-parameter AccumulateGrad launches)
         with direct_grad_accumulation():
             if self._fused_mse:
-                loss = self.model.mse_loss(self.data)
+                loss = self.model.mse_loss(sh.data)
             else:
-                loss = self.loss_fn(self.model(self.data), self.data.y_x)
+                loss = self.loss_fn(self.model(sh.data), sh.data.y_x)
             torch.autograd.backward(loss, self._one)
-        self.loss = loss.detach()
+        sh.loss = loss.detach()
 
     def _opt_step(self) -> None:
         self.opt.step()
 
-    def eager_step(self) -> None:
-        self._fwd_bwd()
+    def eager_step(self, sh: Optional[_Shape] = None) -> None:
+        sh = sh or self._shapes[0]
+        self._fwd_bwd(sh)
         if self.distributed:
             allreduce_mean_(self.flat, self.group)
         self._opt_step()
+        self.loss = sh.loss
 
     # -- graph capture ------------------------------------------------------
     def _snapshot(self) -> dict:
@@ -167,10 +201,14 @@ class TrainStep:
                 "cuda_rng": torch.cuda.get_rng_state(self.flat.device)}
         if isinstance(self.opt, FlatAdam):
             snap["opt"] = (self.opt.m.clone(), self.opt.v.clone(), self.opt.step_t.clone())
+        else:
+            snap["opt"] = {id(p): {k: (v.clone() if torch.is_tensor(v) else v)
+                                   for k, v in st.items()}
+                           for p, st in self.opt.state.items()}
         return snap
 
     def _restore(self, snap: dict) -> None:
-        """Undo the warm-up (in place: the captured graph keeps pointing at the
+        """Undo the warm-up (in place: the captured graphs keep pointing at the
         same buffers), so that construction does not train the model."""
         with torch.no_grad():
             self.flat_params.copy_(snap["params"])
@@ -180,18 +218,22 @@ class TrainStep:
                 self.opt.m.copy_(m)
                 self.opt.v.copy_(v)
                 self.opt.step_t.copy_(t)
-            else:  # torch.optim.Adam: state was empty before the warm-up
-                for st in self.opt.state.values():
-                    for val in st.values():
+            else:  # torch.optim.Adam: state tensors back to their pre-warm-up values
+                for p, st in self.opt.state.items():
+                    old = snap["opt"].get(id(p))
+                    for k, val in st.items():
                         if torch.is_tensor(val):
-                            val.zero_()
+                            if old is not None and k in old:
+                                val.copy_(old[k])
+                            else:
+                                val.zero_()
         torch.set_rng_state(snap["cpu_rng"])
         try:
             torch.cuda.set_rng_state(snap["cuda_rng"], self.flat.device)
         except RuntimeError:  # generator registered with a live capture
             pass
 
-    def _capture(self, warmup: int) -> None:
+    def _capture(self, sh: _Shape, warmup: int) -> None:
         """Warm up (allocator, lazy optimizer state), capture, then restore the
         pre-warm-up parameters / optimizer state / RNG: constructing a
         TrainStep applies no update (k calls == k eager reference steps)."""
@@ -200,41 +242,49 @@ class TrainStep:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(max(1, warmup)):
-                self.eager_step()
+                self.eager_step(sh)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         if self.distributed:
-            self._g_fb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_fb):
-                self._fwd_bwd()
-            self._g_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_opt):
+            sh.g_fb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(sh.g_fb):
+                self._fwd_bwd(sh)
+            sh.g_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(sh.g_opt):
                 self._opt_step()
         else:
-            self._g_fb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_fb):
-                self._fwd_bwd()
+            sh.g_fb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(sh.g_fb):
+                self._fwd_bwd(sh)
                 self._opt_step()
         torch.cuda.synchronize()
         self._restore(snap)
         torch.cuda.synchronize()
 
-    def __call__(self) -> torch.Tensor:
+    def __call__(self, shape: int = 0) -> torch.Tensor:
+        sh = self._shapes[shape]
         if not self.use_graph:
-            self.eager_step()
+            self.eager_step(sh)
             return self.loss
-        self._g_fb.replay()
+        sh.g_fb.replay()
         if self.distributed:
             allreduce_mean_(self.flat, self.group)
-            self._g_opt.replay()
+            sh.g_opt.replay()
+        self.loss = sh.loss
         return self.loss
 
 
 class ForwardStep:
-    """Inference forward (eval mode, no grad) captured into a hipGraph."""
+    """Inference forward (eval mode, no grad) captured into a hipGraph.
+    ``fn(model, data)`` is what runs (default ``model(data)``; e.g.
+    ``lambda m, d: m.mse_loss(d)`` for the evaluation loss); ``prepare`` as in
+    TrainStep."""
 
-    def __init__(self, model: torch.nn.Module, data, use_graph: bool = True, warmup: int = 2):
+    def __init__(self, model: torch.nn.Module, data, use_graph: bool = True, warmup: int = 2,
+                 fn: Optional[Callable] = None, prepare: Optional[Callable[[], None]] = None):
         self.model, self.data = model, data
+        self.fn = fn or (lambda m, d: m(d))
+        self.prepare = prepare
         self.out: Optional[torch.Tensor] = None
         self.graph = None
         with torch.no_grad():
@@ -242,19 +292,144 @@ class ForwardStep:
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 for _ in range(max(1, warmup)):
-                    self.out = model(data)
+                    self._run()
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
             if use_graph:
                 self.graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.graph):
-                    self.out = model(data)
+                    self._run()
                 torch.cuda.synchronize()
+
+    def _run(self) -> None:
+        if self.prepare is not None:
+            self.prepare()
+        self.out = self.fn(self.model, self.data)
 
     def __call__(self) -> torch.Tensor:
         if self.graph is None:
             with torch.no_grad():
-                self.out = self.model(self.data)
+                self._run()
         else:
             self.graph.replay()
         return self.out
+
+
+# ---------------------------------------------------------------------------
+# the reference's training loop (5_train_SpotV2Net.py:86-197) on the device
+# ---------------------------------------------------------------------------
+class Fit:
+    """5_train_SpotV2Net.py's loop over a device-resident WindowDataset:
+    train/test split ``int(split * len)`` (:86-88), DataLoader(shuffle=True)
+    order for training and sequential order for testing (:90-91), per batch
+    MSE + zero_grad + backward + Adam (:150-159), per epoch the mean batch
+    loss of each phase (:163, :180), and the checkpoint rule (:186-191).
+
+    The steps are hipGraph replays: the window gather (WindowDataset.fill from
+    a device index buffer), forward, fused head + MSE, backward and Adam of
+    one batch are ONE graph; the ragged last batch has its own graph; batch
+    losses are summed on the device, so the host synchronises once per epoch
+    (the reference calls loss.item() per batch, :160)."""
+
+    def __init__(self, model: torch.nn.Module, dataset, batch_size: int, lr: float = 1e-3,
+                 split: float = 0.8, generator: Optional[torch.Generator] = None,
+                 use_graph: bool = True, optimizer: str = "sv2n",
+                 step_hook: Optional[Callable[[int, int], None]] = None):
+        self.model, self.ds, self.bs = model, dataset, int(batch_size)
+        n = len(dataset)
+        self.n_train = int(split * n)
+        self.n_test = n - self.n_train
+        dev = dataset.vol.device
+        self.dev = dev
+        self.gen = generator if generator is not None else torch.Generator()
+        self.step_hook = step_hook
+        self.use_graph = use_graph and step_hook is None
+        self.epoch = 0
+        self._idx = {}     # batch size -> static index buffer
+        self._batch = {}   # batch size -> static Batch
+        sizes = [self.bs] if self.n_train >= self.bs else []
+        if self.n_train % self.bs:
+            sizes.append(self.n_train % self.bs)
+        self._train_shape = {}
+        self.step = None
+        model.train()  # the training graphs are captured in train mode (dropout on)
+        for b in sizes:
+            data, prep = self._static(b)
+            if self.step is None:
+                self.step = TrainStep(model, data, lr=lr, use_graph=self.use_graph,
+                                      optimizer=optimizer, prepare=prep)
+                self._train_shape[b] = 0
+            else:
+                self._train_shape[b] = self.step.add_shape(data, prep)
+        self._eval = {}
+        self.history: list = []
+        self.best_test = float("inf")
+
+    def _static(self, b: int):
+        if b not in self._batch:
+            self._idx[b] = torch.zeros(b, dtype=torch.long, device=self.dev)
+            self._batch[b] = self.ds.empty_batch(b)
+            self.ds.fill(self._batch[b], self._idx[b])
+        data, idx = self._batch[b], self._idx[b]
+        return data, (lambda: self.ds.fill(data, idx))
+
+    def _eval_step(self, b: int) -> ForwardStep:
+        if b not in self._eval:
+            data, prep = self._static(b)
+            was = self.model.training
+            self.model.eval()
+            self._eval[b] = ForwardStep(self.model, data, use_graph=self.use_graph,
+                                        fn=lambda m, d: m.mse_loss(d).reshape(()), prepare=prep)
+            self.model.train(was)
+        return self._eval[b]
+
+    def run_epoch(self, checkpoint_path: Optional[str] = None, tolerance: float = 1e-9) -> dict:
+        """One epoch: training pass, test pass, history entry (and checkpoint)."""
+        dev = self.dev
+        perm = torch.randperm(self.n_train, generator=self.gen).to(dev, non_blocking=True)
+        tot_train = torch.zeros((), device=dev)
+        self.model.train()
+        nb = 0
+        for k in range(0, self.n_train, self.bs):
+            b = min(self.bs, self.n_train - k)
+            self._idx[b].copy_(perm[k:k + b])
+            if self.step_hook is not None:
+                self.step_hook(self.epoch, nb)
+            tot_train += self.step(self._train_shape[b])
+            nb += 1
+        tot_test = torch.zeros((), device=dev)
+        nt = 0
+        self.model.eval()
+        test_idx = torch.arange(self.n_train, self.n_train + self.n_test, device=dev)
+        for k in range(0, self.n_test, self.bs):
+            b = min(self.bs, self.n_test - k)
+            fs = self._eval_step(b)
+            self._idx[b].copy_(test_idx[k:k + b])
+            tot_test += fs()
+            nt += 1
+        self.model.train()
+        train_loss = float(tot_train) / max(nb, 1)   # one host sync per epoch
+        test_loss = float(tot_test) / max(nt, 1)
+        rec = {"epoch": self.epoch + 1, "train_loss": train_loss, "test_loss": test_loss,
+               "train_rmse": train_loss ** 0.5, "test_rmse": test_loss ** 0.5}
+        if checkpoint_path is not None and (self.epoch == 0 or
+                                            test_loss + tolerance < self.best_test):
+            torch.save({k: v.detach().clone() for k, v in self.model.state_dict().items()},
+                       checkpoint_path)
+        if self.epoch == 0 or test_loss + tolerance < self.best_test:
+            self.best_test = test_loss
+        self.history.append(rec)
+        self.epoch += 1
+        return rec
+
+
+def fit(model: torch.nn.Module, dataset, num_epochs: int, batch_size: int, lr: float = 1e-3,
+        split: float = 0.8, generator: Optional[torch.Generator] = None, use_graph: bool = True,
+        checkpoint_path: Optional[str] = None, tolerance: float = 1e-9,
+        step_hook: Optional[Callable[[int, int], None]] = None) -> list:
+    """Train like 5_train_SpotV2Net.py:139-197 and return the per-epoch history
+    (train/test loss and RMSE).  See ``Fit``."""
+    f = Fit(model, dataset, batch_size, lr, split, generator, use_graph, step_hook=step_hook)
+    for _ in range(num_epochs):
+        f.run_epoch(checkpoint_path, tolerance)
+    return f.history
