@@ -429,7 +429,9 @@ def run_c3_loop(args, dev, cfg) -> dict:
     V, W = synthetic_series(10556, cfg["n"], seed=1234, device=dev)
     ds = WindowDataset(V, W, cfg["S"], cut=8357)
     out = {}
-    for prec in (args.precision, "f32" if args.precision == "bf16" else "bf16"):
+    precs = [args.precision] + ([] if args.no_compare else
+                                ["f32" if args.precision == "bf16" else "bf16"])
+    for prec in precs:
         model = build_model(dev, cfg).set_precision(prec)
         f = Fit(model, ds, args.batch, lr=1e-3, split=0.8,
                 generator=torch.Generator().manual_seed(5154), use_graph=not args.no_graph)
@@ -465,6 +467,8 @@ def main():
                     help="execution mode (default: f32; bf16 for --config c3)")
     ap.add_argument("--epochs", type=int, default=3, help="c3: timed epochs (yaml num_epochs)")
     ap.add_argument("--warmup-epochs", type=int, default=1, help="c3: untimed epochs")
+    ap.add_argument("--no-compare", action="store_true",
+                    help="c3: skip the run in the other precision")
     args = ap.parse_args()
     if args.precision is None:
         args.precision = "bf16" if args.config == "c3" else "f32"

@@ -26,7 +26,7 @@ def _rel_to_abs_sum(got, a, b):
     return ((got.double() - ref).abs() / absum.clamp_min(1e-30)).max().item()
 
 
-@pytest.mark.parametrize("M,N,K", [(3840, 3012, 1260), (15360, 408, 1260), (97, 37, 70)])
+@pytest.mark.parametrize("M,N,K", [(3840, 3012, 1260), (15360, 408, 1260), (97, 37, 72)])
 def test_gemm_bf16_is_exact_bf16_products(dev, M, N, K):
     from spotv2net_amd import _lib
     from spotv2net_amd.ops import weight_planes
@@ -40,6 +40,18 @@ def test_gemm_bf16_is_exact_bf16_products(dev, M, N, K):
                                   N, M, N, K, _lib.stream_handle(dev)), "gemm_bf16")
     err = _rel_to_abs_sum(out.cpu(), _bf(a).cpu(), _bf(w).cpu())
     assert err < 2e-6, err  # fp32 accumulation of exact bf16 x bf16 products
+
+
+def test_project_planes_bf16_unaligned_rows(dev):
+    """The bf16 projection on activations whose row length is not a multiple of
+    4 floats (e.g. a 50-wide layer input): padded to 16-B rows, same products."""
+    from spotv2net_amd.ops import project_planes
+    g = torch.Generator().manual_seed(5)
+    a = torch.randn(300, 70, generator=g).to(dev)
+    w = (torch.randn(37, 70, generator=g) * 0.1).to(dev)
+    out = project_planes(a, None, w, False, bf16=True)
+    err = _rel_to_abs_sum(out.cpu(), _bf(a).cpu(), _bf(w).cpu())
+    assert err < 2e-6, err
 
 
 @pytest.mark.parametrize("F,H,C,nodes", [(1260, 6, 500, 3840), (1260, 4, 100, 15360),
