@@ -370,6 +370,21 @@ int sv2n_block_eid(const int64_t* edge_index, int64_t num_edges, int64_t num_nod
 int sv2n_block_rowmask(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
                        int n, uint32_t* rowmask, hipStream_t stream);
 
+/* Device-side CovarianceLaggedDataset window builder (reference
+ * utils/dataset.py:200-282; multi-output targets :385-405): for window b with
+ * first matrix starts[b] (int64, device), fills the PyG batch layout
+ *   x         [B*n][n*S]      x[b*n+v][c*S+t] = vol[starts[b]+t][v][c]
+ *   edge_attr [B*n(n-1)][3S]  canonical edge order (canon = target<<8|source):
+ *             [0*S+t] upper-triangle volvol[t][min][max], [1*S+t] volvol[t][s][s],
+ *             [2*S+t] volvol[t][g][g]
+ *   y         [B*n*F]         y[(b*n+v)*F+k] = vol[starts[b]+S+k][v][v]
+ * vol / volvol: [T][n][n] fp32 series; the caller guarantees
+ * starts[b] + S + F - 1 < T. */
+int sv2n_window_gather(const float* vol, const float* volvol, int n, const int64_t* starts,
+                       int64_t num_windows, int seq_length, int future_steps,
+                       const uint16_t* canon, float* x, float* edge_attr, float* y,
+                       hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

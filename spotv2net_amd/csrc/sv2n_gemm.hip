@@ -18,6 +18,7 @@
 #include "sv2n_common.h"
 #include "sv2n_gemm_kernel.h"
 #include "sv2n_gemm3_kernel.h"
+#include "sv2n_gemm_tt.h"
 
 namespace sv2n {
 
@@ -287,35 +288,37 @@ extern "C" int64_t sv2n_gat_wgrad_node_workspace(int64_t num_nodes, int in_featu
   return (int64_t)in_features * ldx + wgrad_slab_floats(num_nodes, in_features, ldx);
 }
 
-// bf16-operand weight-gradient GEMM (k_gemm3_t, one plane): tiles 128 x 208
-// (or 128 x 112), K slices of multiples of 64 aiming at ~480 workgroups
+// bf16-operand weight-gradient GEMM: k_gemm_tt<128, 128, 1> (transposed LDS
+// reads, sv2n_gemm_tt.h), K slices of multiples of 32 aiming at ~480
+// workgroups (tools/gemm_tt_tune.hip: C3 dWaugᵀ 1260 x 3012 x 3840 in 78 us,
+// 374 TF/s, vs 340 us for the split kernel k_gemm3_t)
+constexpr int TT_BM = 128, TT_BN = 128;
 static GemmPlan plan_gemm_bf16t(int64_t M, int64_t N, int64_t K) {
   GemmPlan p{};
-  p.nt = N > 256 ? 13 : 7;
-  const int64_t tiles = ((M + 127) / 128) * ((N + 16 * p.nt - 1) / (16 * p.nt));
+  p.nt = TT_BN / 16;
+  const int64_t tiles = ((M + TT_BM - 1) / TT_BM) * ((N + TT_BN - 1) / TT_BN);
   int64_t sk = 1;
-  if (tiles < 240 && K >= 1024) {
+  if (tiles < 400 && K >= 512) {
     sk = std::min<int64_t>(32, (480 + tiles - 1) / tiles);
     sk = std::min<int64_t>(sk, std::max<int64_t>(1, K / 256));
   }
   int64_t ks = (K + sk - 1) / sk;
-  ks = (ks + 63) / 64 * 64;
+  ks = (ks + 31) / 32 * 32;
   p.splitk = (int)((K + ks - 1) / ks);
   p.kslice = ks;
   p.pf = 1;
   return p;
 }
 
-template <int NT>
 static void launch_wgrad_bf16(const GemmPlan& p, hipStream_t st, const float* x, int64_t ld_x,
                               const float* dxs, int64_t ldx, int64_t F, int64_t K, float* out) {
-  using Cfg = Gemm3TCfg<8, 1, NT, 64, 1>;
+  using Cfg = GemmTTCfg<TT_BM, TT_BN, 1>;
   constexpr size_t lds = Cfg::LDS;
   static_assert(lds <= 64 * 1024, "LDS budget");
-  const dim3 grid((unsigned)((F + Cfg::BM - 1) / Cfg::BM), (unsigned)((ldx + Cfg::BN - 1) / Cfg::BN),
+  const dim3 grid((unsigned)((F + TT_BM - 1) / TT_BM), (unsigned)((ldx + TT_BN - 1) / TT_BN),
                   (unsigned)p.splitk);
-  hipLaunchKernelGGL((k_gemm3_t<8, 1, NT, 64, 1>), grid, dim3(Cfg::THREADS), lds, st, x, ld_x, dxs,
-                     ldx, out, ldx, F, ldx, K, p.kslice);
+  hipLaunchKernelGGL((k_gemm_tt<TT_BM, TT_BN, 1>), grid, dim3(256), lds, st, x, ld_x, dxs, ldx,
+                     out, ldx, F, ldx, K, p.kslice);
 }
 
 static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* dxs, int ldx,
@@ -379,16 +382,14 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
   float* T = workspace;  // reduced dWaugᵀ [F][ldx]
   float* slabs = T + (int64_t)F * ldx;
   if (weights && precision) {
-    // bf16 operands: both k-strided, rounded while staged (k_gemm3_t, NP = 1)
+    // bf16 operands: both k-strided, rounded while staged (k_gemm_tt, NP = 1)
     if (((uintptr_t)x & 15) || (ld_x & 3) || ((uintptr_t)dxs & 15) || (ldx & 3) || F < 4 ||
         ldx < 4)
       return SV2N_ERR_ALIGN;
+    if (num_nodes * std::max<int64_t>(ld_x, ldx) * 4 > 0x7fffffff) return SV2N_ERR_SHAPE;
     const GemmPlan p = plan_gemm_bf16t(F, ldx, num_nodes);
     float* out = p.splitk > 1 ? slabs : T;
-    if (p.nt == 13)
-      launch_wgrad_bf16<13>(p, stream, x, ld_x, dxs, ldx, F, num_nodes, out);
-    else
-      launch_wgrad_bf16<7>(p, stream, x, ld_x, dxs, ldx, F, num_nodes, out);
+    launch_wgrad_bf16(p, stream, x, ld_x, dxs, ldx, F, num_nodes, out);
     if (p.splitk > 1) {
       const int64_t tot = (int64_t)F * ldx;
       hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,

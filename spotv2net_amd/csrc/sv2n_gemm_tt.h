@@ -1,0 +1,189 @@
+// Weight-gradient GEMM with BOTH operands k-strided, on bf16 MFMA:
+//
+//   C[m][n] = Σ_k A[k][m] · B[k][n]      (A = x [K][lda], B = dxs [K][ldb])
+//
+// i.e. dWaugᵀ = xᵀ·dxs of a GAT layer, K = the batch's
+// node count.  The operands are staged as they lie in HBM — row k of the tile
+// is BM (BN) contiguous floats — converted to bf16 planes on the way into LDS
+// ([k][m] images, no register transpose), and the MFMA fragments are read
+// with ds_read_b64_tr_b16 (gfx950's transposing LDS read: a 16-lane group
+// gets a 4-row x 16-column block column-major).
+//
+// Fragment k order.  v_mfma_f32_16x16x32_bf16 wants lane (i, g) (i = l & 15,
+// g = l >> 4) to hold 8 k values of row/column i.  Two transposed reads give
+// it rows {4g .. 4g+3} and {16+4g .. 16+4g+3} of the 32-row tile: a fixed
+// bijection of the 32 k of the step, the same for A and B, so the products
+// sum over every k exactly once.  With LDS rows of BM + 16 bf16 (72 dwords
+// for BM = 128) the 8 rows one 32-lane half reads fall in 8 distinct 8-bank
+// windows: conflict-free.
+//
+// NP = 1: bf16 operands (bf16 execution mode).  NP = 3: the f32-accurate
+// split (x = x0 + x1 + x2 in bf16, six products with plane order p + q <= 2,
+// sv2n_gemm3_kernel.h) for the fp32 path.
+//
+// Workgroup: 4 waves as 2 x 2, wave tile (BM/2) x (BN/2); K steps of 32 with
+// the next step's global loads in registers while this step computes (one
+// barrier per step, two LDS stages).  gridDim.z K slices write slabs
+// C + z*M*ldc (summed in a fixed order by the caller).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "sv2n_common.h"
+#include "sv2n_gemm3_kernel.h"
+
+namespace sv2n {
+
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+
+template <int BM, int BN, int NP>
+struct GemmTTCfg {
+  static constexpr int BK = 32;
+  static constexpr int SA = BM + 16, SB = BN + 16;          // bf16 per LDS row
+  static constexpr int PLANE_A = BK * SA, PLANE_B = BK * SB;
+  static constexpr int STAGE = NP * (PLANE_A + PLANE_B);    // bf16 per stage
+  static constexpr size_t LDS = sizeof(unsigned short) * 2 * STAGE;
+  static constexpr int AV = BK * BM / 4 / 256, BV = BK * BN / 4 / 256;  // float4 / thread
+  static constexpr int MT = BM / 32, NT = BN / 32;           // 16x16 tiles per wave
+  static_assert(BK * BM / 4 % 256 == 0 && BK * BN / 4 % 256 == 0, "staging tiles threads");
+};
+
+__device__ __forceinline__ bf16x8 tr_frag(const unsigned short* p0, const unsigned short* p1) {
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p0));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p1));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+template <int BM, int BN, int NP>
+__global__ __launch_bounds__(256) void k_gemm_tt(const float* __restrict__ A, int64_t lda,
+                                                 const float* __restrict__ B, int64_t ldb,
+                                                 float* __restrict__ C, int64_t ldc, int64_t M,
+                                                 int64_t N, int64_t K, int64_t kslice) {
+  using Cfg = GemmTTCfg<BM, BN, NP>;
+  constexpr int BK = Cfg::BK, SA = Cfg::SA, SB = Cfg::SB, AV = Cfg::AV, BV = Cfg::BV;
+  constexpr int MT = Cfg::MT, NT = Cfg::NT, STAGE = Cfg::STAGE;
+  constexpr int PA = Cfg::PLANE_A, PB = Cfg::PLANE_B;
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int li = lane & 15, lg = lane >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
+  const int64_t kbeg = (int64_t)blockIdx.z * kslice, kend = min(K, kbeg + kslice);
+  if (gridDim.z > 1) C += (int64_t)blockIdx.z * M * ldc;
+
+  // whole-operand buffer descriptors: rows past K / columns past the array
+  // read 0; columns in [M, lda) only feed output rows that are never stored
+  const rsrc_t ra = make_rsrc(A, (uint32_t)min<int64_t>(K * lda * 4, 0x7fffffff));
+  const rsrc_t rb = make_rsrc(B, (uint32_t)min<int64_t>(K * ldb * 4, 0x7fffffff));
+
+  f32x4 va[AV], vb[BV];
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int s = 0; s < AV; ++s) {
+      const int idx = t + 256 * s;
+      const int r = idx / (BM / 4), c4 = idx - r * (BM / 4);
+      const int64_t k = k0 + r, m = m0 + 4 * c4;
+      va[s] = bld4(ra, (k < kend && m < lda) ? (int)((k * lda + m) * 4) : OOB);
+    }
+#pragma unroll
+    for (int s = 0; s < BV; ++s) {
+      const int idx = t + 256 * s;
+      const int r = idx / (BN / 4), c4 = idx - r * (BN / 4);
+      const int64_t k = k0 + r, n = n0 + 4 * c4;
+      vb[s] = bld4(rb, (k < kend && n < ldb) ? (int)((k * ldb + n) * 4) : OOB);
+    }
+  };
+  auto put = [&](unsigned short* dst, int plane_elems, int stride, int r, int c, const f32x4& v) {
+    uint2 w[3];
+    if constexpr (NP == 3) {
+      split3_pk(v[0], v[1], w[0].x, w[1].x, w[2].x);
+      split3_pk(v[2], v[3], w[0].y, w[1].y, w[2].y);
+    } else {
+      w[0].x = bf16_pk(v[0], v[1]);
+      w[0].y = bf16_pk(v[2], v[3]);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      *reinterpret_cast<uint2*>(dst + p * plane_elems + r * stride + c) = w[p];
+  };
+  auto store = [&](unsigned short* st) {
+#pragma unroll
+    for (int s = 0; s < AV; ++s) {
+      const int idx = t + 256 * s;
+      const int r = idx / (BM / 4), c4 = idx - r * (BM / 4);
+      put(st, PA, SA, r, 4 * c4, va[s]);
+    }
+    unsigned short* sb = st + NP * PA;
+#pragma unroll
+    for (int s = 0; s < BV; ++s) {
+      const int idx = t + 256 * s;
+      const int r = idx / (BN / 4), c4 = idx - r * (BN / 4);
+      put(sb, PB, SB, r, 4 * c4, vb[s]);
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read addresses: lane 4q+p of its 16-lane group -> row q, columns 4p..4p+3
+  const int q = li >> 2, p4 = 4 * (li & 3);
+  const int rowA0 = (4 * lg + q) * SA, rowA1 = (16 + 4 * lg + q) * SA;
+  const int rowB0 = (4 * lg + q) * SB, rowB1 = (16 + 4 * lg + q) * SB;
+  auto compute = [&](const unsigned short* st) {
+    const unsigned short* sa = st;
+    const unsigned short* sb = st + NP * PA;
+    bf16x8 af[MT][NP];
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+      const int col = wm * (BM / 2) + 16 * a + p4;
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl)
+        af[a][pl] = tr_frag(sa + pl * PA + rowA0 + col, sa + pl * PA + rowA1 + col);
+    }
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int col = wn * (BN / 2) + 16 * b + p4;
+      bf16x8 bf[NP];
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl)
+        bf[pl] = tr_frag(sb + pl * PB + rowB0 + col, sb + pl * PB + rowB1 + col);
+#pragma unroll
+      for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<NP>(af[a], bf, acc[a][b]);
+    }
+  };
+
+  const int nsteps = (int)((kend - kbeg + BK - 1) / BK);
+  if (nsteps > 0) {
+    load(kbeg);
+    store(lds);
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+      if (s + 1 < nsteps) load(kbeg + (int64_t)(s + 1) * BK);
+      compute(lds + (s & 1) * STAGE);
+      if (s + 1 < nsteps) store(lds + ((s + 1) & 1) * STAGE);
+      __syncthreads();
+    }
+  }
+  // acc[a][b][r] = C[row 16a + 4lg + r][col 16b + li] of the wave tile
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int64_t gn = n0 + wn * (BN / 2) + 16 * b + li;
+      if (gn < N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t gm = m0 + wm * (BM / 2) + 16 * a + 4 * lg + r;
+          if (gm < M) C[gm * ldc + gn] = acc[a][b][r];
+        }
+      }
+    }
+}
+
+}  // namespace sv2n

@@ -26,15 +26,23 @@ constexpr int HEAD_ROWS = 256;  // rows per workgroup at most (one per thread)
 constexpr int HEAD_WS_HDR = SV2N_TICKET_WORDS;  // two-level ticket counters
 constexpr size_t HEAD_LDS_BUDGET = 160 * 1024 - 20 * 1024;  // dynamic part (statics below)
 
-// rows per workgroup for in_features C, out_features O (0: does not fit)
-__host__ __device__ inline int head_rows_per_block(int C, int O) {
-  if (C <= 128) return 256;
-  for (int R = 128; R >= 32; R >>= 1)
-    if ((size_t)4 * ((size_t)R * (C + 1) + (size_t)O * C) <= HEAD_LDS_BUDGET) return R;
-  return 0;
+// rows per workgroup for in_features C, out_features O, N rows (0: does not
+// fit): the largest of 256 .. 32 whose [R][C+1] image and weights fit the LDS,
+// lowered (down to 8) until the launch has ~256 workgroups (a C2 batch of
+// 15,360 rows at R = 256 was 60 workgroups on 256 CUs)
+__host__ __device__ inline int head_rows_per_block(int C, int O, int64_t N) {
+  int R = 0;
+  for (int r = 256; r >= 32; r >>= 1)
+    if ((size_t)4 * ((size_t)r * (C + 1) + (size_t)O * C) <= HEAD_LDS_BUDGET) {
+      R = r;
+      break;
+    }
+  if (R == 0) return 0;
+  while (R > 8 && (N + R / 2 - 1) / (R / 2) <= 256) R >>= 1;
+  return R;
 }
-__host__ __device__ inline size_t head_lds_bytes(int C, int O) {
-  return (size_t)4 * ((size_t)head_rows_per_block(C, O) * (C + 1) + (size_t)O * C);
+__host__ __device__ inline size_t head_lds_bytes(int C, int O, int64_t N) {
+  return (size_t)4 * ((size_t)head_rows_per_block(C, O, N) * (C + 1) + (size_t)O * C);
 }
 
 // x rows staged through LDS so the global reads are coalesced.  The block's
@@ -300,9 +308,9 @@ using namespace sv2n;
 
 static int head_check(int64_t N, int C, int out_ch) {
   if (N <= 0 || C <= 0 || out_ch <= 0) return SV2N_ERR_ARG;
-  if (out_ch > HEAD_MAX_OUT || C > HEAD_MAX_IN || head_rows_per_block(C, out_ch) == 0)
+  if (out_ch > HEAD_MAX_OUT || C > HEAD_MAX_IN || head_rows_per_block(C, out_ch, N) == 0)
     return SV2N_ERR_SHAPE;
-  if (N / head_rows_per_block(C, out_ch) >= 0x7fffffff) return SV2N_ERR_SHAPE;
+  if (N / head_rows_per_block(C, out_ch, N) >= 0x7fffffff) return SV2N_ERR_SHAPE;
   return 0;
 }
 
@@ -333,16 +341,16 @@ extern "C" int sv2n_head_fwd(const float* x, int64_t num_rows, int in_features,
   const int out_ch = out_features;
   if (!x || !weight || !out) return SV2N_ERR_ARG;
   if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
-  const int R = head_rows_per_block(in_features, out_ch);
+  const int R = head_rows_per_block(in_features, out_ch, num_rows);
   const unsigned grid = (unsigned)((num_rows + R - 1) / R);
-  const size_t lds = head_lds_bytes(in_features, out_ch);
+  const size_t lds = head_lds_bytes(in_features, out_ch, num_rows);
   SV2N_HEAD_DISPATCH(k_head_fwd, dim3(grid), dim3(256), lds, stream, x, num_rows, in_features,
                      weight, bias, out, R)
   return (int)hipGetLastError();
 }
 
 static int64_t head_bwd_blocks(int64_t num_rows, int C, int O) {
-  const int R = head_rows_per_block(C, O);
+  const int R = head_rows_per_block(C, O, num_rows);
   return R ? (num_rows + R - 1) / R : 0;
 }
 
@@ -361,8 +369,8 @@ static int head_bwd_launch(const float* x, int64_t num_rows, int in_features, co
   if (workspace_floats < sv2n_head_bwd_workspace(num_rows, in_features, out_ch))
     return SV2N_ERR_WORKSPACE;
   if ((uintptr_t)workspace & 15) return SV2N_ERR_ALIGN;
-  const int R = head_rows_per_block(in_features, out_ch);
-  const size_t lds = head_lds_bytes(in_features, out_ch);
+  const int R = head_rows_per_block(in_features, out_ch, num_rows);
+  const size_t lds = head_lds_bytes(in_features, out_ch, num_rows);
   SV2N_HEAD_DISPATCH(k_head_bwd, dim3((unsigned)nb), dim3(256), lds, stream, x, num_rows,
                      in_features, weight, src, scale, dscale, dx, workspace, g_weight, g_bias, R)
   return (int)hipGetLastError();
@@ -392,9 +400,9 @@ extern "C" int sv2n_head_mse_fwd(const float* x, int64_t num_rows, int in_featur
   if (workspace_floats < sv2n_head_mse_workspace(num_rows, in_features, out_ch))
     return SV2N_ERR_WORKSPACE;
   if ((uintptr_t)workspace & 15) return SV2N_ERR_ALIGN;
-  const int R = head_rows_per_block(in_features, out_ch);
+  const int R = head_rows_per_block(in_features, out_ch, num_rows);
   const unsigned grid = (unsigned)((num_rows + R - 1) / R);
-  const size_t lds = head_lds_bytes(in_features, out_ch);
+  const size_t lds = head_lds_bytes(in_features, out_ch, num_rows);
   const float inv_count = 1.f / (float)(num_rows * out_ch);
   SV2N_HEAD_DISPATCH(k_head_mse_fwd, dim3(grid), dim3(256), lds, stream, x, num_rows,
                      in_features, weight, bias, target, yhat, diff, workspace, loss, inv_count, R)

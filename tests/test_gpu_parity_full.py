@@ -123,3 +123,20 @@ def test_device_window_dataset_matches_restatement(dev):
         assert torch.equal(got.x[k * 30:(k + 1) * 30].cpu(), r["x"])
         assert torch.equal(got.edge_attr[k * E0:(k + 1) * E0].cpu(), r["edge_attr"])
         assert torch.equal(got.y_x[k * 30:(k + 1) * 30].cpu(), r["y_x"])
+
+
+@pytest.mark.parametrize("n,S,Fs", [(30, 42, 1), (30, 4, 14), (7, 3, 2)])
+def test_window_gather_kernel_matches_builder(dev, n, S, Fs):
+    """sv2n_window_gather (WindowDataset.fill on the device, one launch) is
+    bit-exact with the torch-op builder window_batch (itself checked against
+    the restatement of utils/dataset.py), including a ragged index set."""
+    from spotv2net_amd import WindowDataset
+    from spotv2net_amd.data import synthetic_series
+    V, W = synthetic_series(S + Fs + 60, n, seed=n + S)
+    ds = WindowDataset(V.to(dev), W.to(dev), S, cut=3, future_steps=Fs)
+    idx = torch.randperm(len(ds), generator=torch.Generator().manual_seed(1))[:37].to(dev)
+    want = ds.batch(idx)
+    got = ds.empty_batch(idx.numel())
+    ds.fill(got, idx)
+    for key in ("x", "edge_attr", "y_x", "edge_index"):
+        assert torch.equal(getattr(got, key), getattr(want, key)), key
