@@ -38,7 +38,14 @@ __host__ __device__ inline int head_rows_per_block(int C, int O, int64_t N) {
       break;
     }
   if (R == 0) return 0;
-  while (R > 8 && (N + R / 2 - 1) / (R / 2) <= 256) R >>= 1;
+  // halve while the launch stays <= 256 workgroups and the weight-gradient
+  // partials the last workgroup combines stay <= 32K floats
+  const int64_t tot = (int64_t)O * (C + 1);
+  while (R > 8) {
+    const int64_t nb = (N + R / 2 - 1) / (R / 2);
+    if (nb > 256 || nb * tot > 32768) break;
+    R >>= 1;
+  }
   return R;
 }
 __host__ __device__ inline size_t head_lds_bytes(int C, int O, int64_t N) {
@@ -282,7 +289,18 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ x, i
       if (t < PG * cols) {
         const int oc = base + t % cols, g = t / cols;
         float s = 0.f;
-        for (int bb = g; bb < nparts; bb += PG) s += ld_sc1(part + (int64_t)bb * tot + oc);
+        // 8 independent loads in flight per round (a dependent chain of
+        // agent-scope loads is one memory round trip per part)
+        for (int b0 = g; b0 < nparts; b0 += 8 * PG) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int bb = b0 + u * PG;
+            v[u] = bb < nparts ? ld_sc1(part + (int64_t)bb * tot + oc) : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) s += v[u];
+        }
         s_grp[t] = s;
       }
       __syncthreads();

@@ -64,6 +64,63 @@ __global__ __launch_bounds__(256) void k_window_gather(
   }
 }
 
+// One workgroup per (window b, node u): the S rows vol[st+t][u][:] and
+// volvol[st+t][u][:] and the volvol diagonal are staged in LDS ([t][v]
+// images, read along v = coalesced), then written transposed:
+//   x row b*n+u                       (n*S floats, contiguous)
+//   the edge rows of the upper pairs (u, w), w > u, and of their swapped
+//   copies (canonical order: both runs are contiguous, 3S floats per row)
+//   y[(b*n+u)*F .. +F)
+// 3 * S * (n+1) floats of LDS.
+__global__ __launch_bounds__(256) void k_window_rows(
+    const float* __restrict__ vol, const float* __restrict__ volvol, int n,
+    const int64_t* __restrict__ starts, int S, int F, float* __restrict__ x,
+    float* __restrict__ ea, float* __restrict__ y) {
+  extern __shared__ float lds[];
+  const int NP = n + 1;
+  float* sv = lds;             // [S][NP] vol[t][u][v]
+  float* sw = sv + S * NP;     // [S][NP] volvol[t][u][v]
+  float* sd = sw + S * NP;     // [S][NP] volvol[t][v][v]
+  const int u = blockIdx.x % n;
+  const int64_t b = blockIdx.x / n;
+  const int t = threadIdx.x;
+  const int64_t nn = (int64_t)n * n;
+  const int64_t st = starts[b];
+  const int E0 = n * (n - 1), P = E0 / 2;
+  for (int k = t; k < S * n; k += 256) {
+    const int tt = k / n, v = k - tt * n;
+    const int64_t base = (st + tt) * nn;
+    sv[tt * NP + v] = vol[base + (int64_t)u * n + v];
+    sw[tt * NP + v] = volvol[base + (int64_t)u * n + v];
+    sd[tt * NP + v] = volvol[base + (int64_t)v * n + v];
+  }
+  if (t < F) y[(b * n + u) * F + t] = vol[(st + S + t) * nn + (int64_t)u * n + u];
+  __syncthreads();
+  // x[b*n+u][c*S + tt] = vol[tt][u][c]
+  float* xr = x + (b * n + u) * (int64_t)n * S;
+  for (int j = t; j < n * S; j += 256) {
+    const int c = j / S, tt = j - c * S;
+    xr[j] = sv[tt * NP + c];
+  }
+  // upper pairs (u, w > u): e = off(u) + (w - u - 1), off(u) = u*(2n-u-1)/2
+  const int m = n - 1 - u;
+  if (m == 0) return;
+  const int e0 = u * (2 * n - u - 1) / 2;
+  const int RW = 3 * S;
+  float* up = ea + (b * E0 + e0) * (int64_t)RW;
+  float* lo = ea + (b * E0 + P + e0) * (int64_t)RW;
+  for (int j = t; j < m * RW; j += 256) {
+    const int r = j / RW, q = j - r * RW;
+    const int kind = q / S, tt = q - kind * S;
+    const int w = u + 1 + r;
+    const float cov = sw[tt * NP + w];
+    // upper edge u -> w: (covol, var_u, var_w); swapped edge w -> u: (covol, var_w, var_u)
+    const float du = sw[tt * NP + u], dw = sd[tt * NP + w];
+    up[j] = kind == 0 ? cov : (kind == 1 ? du : dw);
+    lo[j] = kind == 0 ? cov : (kind == 1 ? dw : du);
+  }
+}
+
 }  // namespace sv2n
 
 using namespace sv2n;
@@ -78,6 +135,12 @@ extern "C" int sv2n_window_gather(const float* vol, const float* volvol, int n,
   const int64_t total = num_windows * ((int64_t)n * n * seq_length +
                                        (int64_t)n * (n - 1) * 3 * seq_length +
                                        (int64_t)n * future_steps);
+  const size_t lds = sizeof(float) * 3 * (size_t)seq_length * (n + 1);
+  if (lds <= 64 * 1024 && future_steps <= 256) {
+    hipLaunchKernelGGL(k_window_rows, dim3((unsigned)(num_windows * n)), dim3(256), lds, stream,
+                       vol, volvol, n, starts, seq_length, future_steps, x, edge_attr, y);
+    return (int)hipGetLastError();
+  }
   const int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);
   hipLaunchKernelGGL(k_window_gather, dim3((unsigned)blocks), dim3(256), 0, stream, vol, volvol,
                      n, starts, num_windows, seq_length, future_steps, canon, x, edge_attr, y);
