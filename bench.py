@@ -415,6 +415,33 @@ def step_roofline(cfg, train_gps: float, fwd_gps: float, dtype: str) -> dict:
             "fwd_frac": round(fwd_gps / fwd_bound, 4), "train_frac": round(train_gps / train_bound, 4)}
 
 
+def reference_loop_rate(dev, cfg, data, args, world) -> float:
+    """5_train_SpotV2Net.py:142-160 as written, eager: a NEW batch object with
+    a new edge_index every step (as PyG's DataLoader yields; layout analysed
+    without a host sync), model(data), nn.MSELoss, zero_grad, backward,
+    torch.optim.Adam(fused) step and the per-step loss.item() sync.  Inputs
+    stay device-resident (the DataLoader's CPU collation and H2D copy are
+    not on the GPU path)."""
+    from spotv2net_amd import Batch
+    model = build_model(dev, cfg).set_precision(args.precision)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    crit = torch.nn.MSELoss()
+
+    def step():
+        b = Batch(x=data.x, edge_index=data.edge_index.clone(), edge_attr=data.edge_attr,
+                  y_x=data.y_x, batch=data.batch, ptr=data.ptr)
+        loss = crit(model(b), b.y_x)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        return loss.item()
+
+    for _ in range(max(2, args.warmup)):
+        step()
+    el = max_over_ranks(time_replays(step, args.steps), dev)
+    return world * args.batch * args.steps / el
+
+
 def run_c3_loop(args, dev, cfg) -> dict:
     """C3 as BASELINE.json states it: config/GNN_param.yaml's model and
     hyper-parameters (S 42, hidden [500], 6 heads, dropout 0.1, Adam 1e-3,
@@ -463,6 +490,8 @@ def main():
                     help="graphs per CPU-baseline step (per-graph CPU cost is batch independent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-table", action="store_true")
+    ap.add_argument("--no-ref-loop", action="store_true",
+                    help="skip the eager reference-loop (new batch per step) measurement")
     ap.add_argument("--precision", default=None, choices=("f32", "bf16"),
                     help="execution mode (default: f32; bf16 for --config c3)")
     ap.add_argument("--epochs", type=int, default=3, help="c3: timed epochs (yaml num_epochs)")
@@ -503,6 +532,9 @@ def main():
     value = world * args.batch * args.steps / el
     loss = float(step.loss.item())
 
+    ref_loop = None
+    if not args.no_ref_loop:
+        ref_loop = reference_loop_rate(dev, cfg, data, args, world)
     model.eval()
     fstep = ForwardStep(model, data, use_graph=not args.no_graph)
     for _ in range(max(1, args.warmup)):
@@ -546,6 +578,7 @@ def main():
                        "graphs_per_gpu": args.batch, "global_batch": args.batch * world,
                        "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
             "fwd_graphs_per_s": round(fwd_value, 1),
+            "ref_loop_graphs_per_s": round(ref_loop, 1) if ref_loop else None,
             "step_roofline": step_roofline(cfg, value, fwd_value, args.precision),
             "final_loss": loss,
             "roofline": roof,

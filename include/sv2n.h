@@ -370,6 +370,15 @@ int sv2n_block_eid(const int64_t* edge_index, int64_t num_edges, int64_t num_nod
 int sv2n_block_rowmask(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
                        int n, uint32_t* rowmask, hipStream_t stream);
 
+/* sv2n_block_rowmask that also validates, with no host round trip: adds to
+ * *violations (int32, device) the number of edges the dense-block kernels
+ * cannot take — an end outside [0, num_nodes), source and target in
+ * different n-node blocks, or a repeated (target, source) pair.  The host
+ * reads the count later (deferred error) instead of synchronising per batch. */
+int sv2n_block_rowmask_checked(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
+                               int n, uint32_t* rowmask, int32_t* violations,
+                               hipStream_t stream);
+
 /* Device-side CovarianceLaggedDataset window builder (reference
  * utils/dataset.py:200-282; multi-output targets :385-405): for window b with
  * first matrix starts[b] (int64, device), fills the PyG batch layout

@@ -64,6 +64,7 @@ _SIGNATURES = {
     "sv2n_gemm_f32_slabs": (_i32, [_i32, _i32, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "sv2n_gemm_f32": (_i32, [_i32, _i32, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "sv2n_block_rowmask": (_i32, [_p, _i64, _i64, _i32, _p, _p]),
+    "sv2n_block_rowmask_checked": (_i32, [_p, _i64, _i64, _i32, _p, _p, _p]),
     "sv2n_gat_prep_fwd": (_i32, [_p, _p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _i32, _p, _i32,
                                  _i32, _p]),
     "sv2n_gat_prep_bwd_workspace": (_i64, [_i32, _i32]),

@@ -349,6 +349,27 @@ __global__ void k_block_rowmask(const int64_t* __restrict__ ei, int64_t E, int64
   atomicOr(&rowmask[t * W + (j >> 5)], 1u << (int)(j & 31));
 }
 
+// rowmask plus validation without a host round trip: counts into *bad the
+// edges the dense-block kernels cannot take (an end outside [0, N), source
+// and target in different n-node blocks, a repeated (target, source) pair —
+// the atomicOr that finds its bit already set)
+__global__ void k_block_rowmask_checked(const int64_t* __restrict__ ei, int64_t E, int64_t N,
+                                        int n, uint32_t* __restrict__ rowmask,
+                                        int* __restrict__ bad) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int64_t s = ei[e], t = ei[E + e];
+  if (s < 0 || s >= N || t < 0 || t >= N || s / n != t / n) {
+    atomicAdd(bad, 1);
+    return;
+  }
+  if (s == t) return;  // input self loops: PyG removes them
+  const int64_t j = s - (t / n) * n;
+  const int W = (n + 31) >> 5;
+  const uint32_t bit = 1u << (int)(j & 31);
+  if (atomicOr(&rowmask[t * W + (j >> 5)], bit) & bit) atomicAdd(bad, 1);
+}
+
 // ---------------------------------------------------------------------------
 // narrow edge features (D <= 16, e.g. the C5 stress shapes, D = 12): a 64-edge
 // chunk is only 3 KB there, too little in flight per workgroup, so one thread
@@ -835,5 +856,18 @@ extern "C" int sv2n_block_rowmask(const int64_t* edge_index, int64_t num_edges, 
   if (num_edges == 0) return 0;
   hipLaunchKernelGGL(k_block_rowmask, dim3((unsigned)((num_edges + 255) / 256)), dim3(256), 0,
                      stream, edge_index, num_edges, num_nodes, n, rowmask);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_block_rowmask_checked(const int64_t* edge_index, int64_t num_edges,
+                                          int64_t num_nodes, int n, uint32_t* rowmask,
+                                          int32_t* violations, hipStream_t stream) {
+  if (!edge_index || !rowmask || !violations || num_edges < 0 || num_nodes <= 0)
+    return SV2N_ERR_ARG;
+  if (n < 1 || n > SV2N_MAX_N_TILED) return SV2N_ERR_SHAPE;
+  if (num_edges == 0) return 0;
+  hipLaunchKernelGGL(k_block_rowmask_checked, dim3((unsigned)((num_edges + 255) / 256)),
+                     dim3(256), 0, stream, edge_index, num_edges, num_nodes, n, rowmask,
+                     violations);
   return (int)hipGetLastError();
 }

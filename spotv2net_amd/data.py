@@ -244,15 +244,12 @@ class WindowDataset:
         st = self.starts.index_select(0, idx)
         if self.vol.is_cuda and self.vol.dtype == torch.float32 and \
                 self.volvol.dtype == torch.float32:
-            # one sv2n_window_gather launch (include/sv2n.h)
-            from . import _lib
+            # one sv2n::window_gather launch (include/sv2n.h sv2n_window_gather)
+            from . import library  # noqa: F401
             from .layout import canonical_table
-            vol, volvol = self.vol.contiguous(), self.volvol.contiguous()
-            _lib.check(_lib.load().sv2n_window_gather(
-                vol.data_ptr(), volvol.data_ptr(), n, st.data_ptr(), B, S, Fs,
-                canonical_table(n, vol.device).data_ptr(), out.x.data_ptr(),
-                out.edge_attr.data_ptr(), out.y_x.data_ptr(), _lib.stream_handle(vol.device)),
-                "sv2n_window_gather")
+            torch.ops.sv2n.window_gather(self.vol.contiguous(), self.volvol.contiguous(), st, S,
+                                         Fs, canonical_table(n, self.vol.device), out.x,
+                                         out.edge_attr, out.y_x)
             return
         tidx = st.view(B, 1) + self._arS.view(1, S)                               # [B, S]
         V = self.vol[tidx]                                                        # [B, S, n, n]

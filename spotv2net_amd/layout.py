@@ -19,8 +19,20 @@ on the tensor object (keyed by its version counter):
 Blocks of n <= 32 nodes run on the one-workgroup-per-graph attention
 kernels; 32 < n <= 256 (the C5 stress shapes) on the target-row-tiled ones.
 Anything else (ragged graph sizes, duplicate edges, n > 256) raises
-``UnsupportedLayout``.  Analysis runs on the device with torch ops and costs
-one host synchronisation per new edge_index tensor.
+``UnsupportedLayout``.
+
+Host synchronisation.  ``canonical_edge_index`` tensors (what the window
+builders emit) carry their layout: no analysis at all.  When the caller knows
+the graph size (``n``: a Batch's ``nodes_per_graph``, or N / ``num_graphs``),
+a new edge_index is analysed WITHOUT a host round trip — the reference loop
+builds a new PyG Batch every step (5_train_SpotV2Net.py:142-143) and would
+otherwise stall the stream once per batch: it takes the block path (valid for
+any edge order) and one kernel (sv2n_block_rowmask_checked) builds the row
+mask while counting the edges the kernels cannot take.  That count is a
+DEFERRED error: the forward's output is poisoned with NaN when it is non-zero
+(``GraphLayout.poison``) and the next analysis (or ``check_pending()``)
+raises ``UnsupportedLayout`` for it.  Without a size hint the analysis finds
+the block size on the device and synchronises once per new edge_index.
 """
 from __future__ import annotations
 
@@ -50,6 +62,14 @@ class GraphLayout:
     rowmask: Optional[torch.Tensor]     # int32 [N][ceil(n/32)] source bitmask; None = complete
     canon: Optional[torch.Tensor]       # int16 [n(n-1)] (target<<8 | source) table
     eid: Optional[torch.Tensor] = None  # int32 [N][n] edge ids (tiled 'block' layouts only)
+    pending: Optional[torch.Tensor] = None  # int32 [1] device count of invalid edges (deferred)
+
+    def poison(self, out: torch.Tensor) -> torch.Tensor:
+        """``out`` with NaN everywhere if the deferred validation found invalid
+        edges (device-side select: no host synchronisation)."""
+        if self.pending is None:
+            return out
+        return torch.where(self.pending != 0, torch.full_like(out, float("nan")), out)
 
     @property
     def tiled(self) -> bool:
@@ -87,7 +107,8 @@ def canonical_table(n: int, device: torch.device) -> torch.Tensor:
 
 
 def canonical_edge_index(n: int, num_graphs: int = 1, device=None) -> torch.Tensor:
-    """Batched canonical edge_index [2, B*n(n-1)] with PyG Batch node offsets."""
+    """Batched canonical edge_index [2, B*n(n-1)] with PyG Batch node offsets.
+    The tensor carries its (canonical) layout, so models never analyse it."""
     device = torch.device(device) if device is not None else torch.device("cpu")
     key = ("ei", n, num_graphs, str(device))
     if key not in _canon_cache:
@@ -96,6 +117,12 @@ def canonical_edge_index(n: int, num_graphs: int = 1, device=None) -> torch.Tens
         off = (torch.arange(num_graphs, dtype=torch.long) * n).repeat_interleave(len(s))
         ei = one.repeat(1, num_graphs) + off.unsqueeze(0)
         ei = ei.to(device)
+        if 1 <= n <= MAX_N:
+            N = n * num_graphs
+            lay = GraphLayout("canonical", n, num_graphs, N, ei.size(1), None, None,
+                              canonical_table(n, device))
+            for hint in (None, n):
+                _attach(ei, (N, hint), lay)
         if num_graphs * len(s) > 10_000_000:
             return ei  # do not pin very large batches in the cache
         _canon_cache[key] = ei
@@ -108,10 +135,81 @@ def _words(n: int) -> int:
 
 def _attach(edge_index: torch.Tensor, key, layout: GraphLayout) -> GraphLayout:
     try:
-        edge_index._sv2n_layout = (edge_index._version, key, layout)
+        cache = getattr(edge_index, "_sv2n_layouts", None)
+        if cache is None:
+            cache = {}
+            edge_index._sv2n_layouts = cache
+        cache[key] = (edge_index._version, layout)
     except (AttributeError, RuntimeError):
         pass
     return layout
+
+
+def _cached(edge_index: torch.Tensor, key) -> Optional[GraphLayout]:
+    cache = getattr(edge_index, "_sv2n_layouts", None)
+    if cache is None or key not in cache:
+        return None
+    ver, lay = cache[key]
+    return lay if ver == edge_index._version else None
+
+
+# deferred validations: (pinned host count, event, what) of layouts analysed
+# without a host synchronisation; checked at the next analysis / check_pending()
+_pending: list = []
+
+
+def check_pending(block: bool = False) -> None:
+    """Raise UnsupportedLayout for any earlier sync-free analysis whose device
+    check found invalid edges.  ``block`` waits for checks still in flight."""
+    keep = []
+    err = None
+    for host, ev, what in _pending:
+        if not block and not ev.query():
+            keep.append((host, ev, what))
+            continue
+        ev.synchronize()
+        if int(host[0]) != 0 and err is None:
+            err = UnsupportedLayout(
+                f"{what}: {int(host[0])} edge(s) outside the node range, across n-node blocks "
+                "or repeated; the affected forward returned NaN")
+    _pending[:] = keep
+    if err is not None:
+        raise err
+
+
+def _analyze_deferred(edge_index: torch.Tensor, N: int, n: int, key) -> GraphLayout:
+    """Block-path layout with no host synchronisation (module docstring)."""
+    device = edge_index.device
+    if N % n != 0:
+        raise UnsupportedLayout(f"{N} nodes are not a union of {n}-node graphs")
+    if n > MAX_N:
+        raise UnsupportedLayout(f"graphs of {n} > {MAX_N} nodes")
+    E = edge_index.size(1)
+    B = N // n
+    if E > 0x7FFFFFFF:
+        raise UnsupportedLayout("more than 2^31 edges in one batch")
+    lib = _lib.load()
+    st = _lib.stream_handle(device)
+    ei = edge_index.contiguous()
+    rowmask = torch.zeros(N * _words(n), dtype=torch.int32, device=device)
+    bad = torch.zeros(1, dtype=torch.int32, device=device)
+    if E > 0:
+        _lib.check(lib.sv2n_block_rowmask_checked(ei.data_ptr(), E, N, n, rowmask.data_ptr(),
+                                                  bad.data_ptr(), st), "sv2n_block_rowmask")
+    eid = None
+    if n > SMALL_N:
+        eid = torch.full((N * n,), -1, dtype=torch.int32, device=device)
+        if E > 0:
+            _lib.check(lib.sv2n_block_eid(ei.data_ptr(), E, N, n, eid.data_ptr(), st),
+                       "sv2n_block_eid")
+    if not torch.cuda.is_current_stream_capturing():
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(bad, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        _pending.append((host, ev, f"edge_index of {B} graphs x {n} nodes"))
+    lay = GraphLayout("block", n, B, N, E, ei, rowmask, canonical_table(n, device), eid, bad)
+    return _attach(edge_index, key, lay)
 
 
 def analyze_edge_index(edge_index: torch.Tensor, num_nodes: int,
@@ -122,15 +220,19 @@ def analyze_edge_index(edge_index: torch.Tensor, num_nodes: int,
     if edge_index.dtype != torch.long:
         raise TypeError("edge_index must be int64 (PyG convention)")
     key = (num_nodes, n)
-    cached = getattr(edge_index, "_sv2n_layout", None)
-    if cached is not None and cached[0] == edge_index._version and cached[1] == key:
-        return cached[2]
+    lay = _cached(edge_index, key)
+    if lay is not None:
+        return lay
 
     device = edge_index.device
     E = edge_index.size(1)
     N = int(num_nodes)
     if N <= 0:
         raise UnsupportedLayout("empty graph batch")
+    if _pending:
+        check_pending()
+    if n is not None and device.type == "cuda":
+        return _analyze_deferred(edge_index, N, int(n), key)
 
     # 1) block size
     cands = []

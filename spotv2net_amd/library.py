@@ -1,0 +1,517 @@
+"""``torch.ops.sv2n.*``: the C-ABI (include/sv2n.h) registered as PyTorch
+operators, with fake (meta) implementations for shape propagation.
+
+This is the operator boundary SURVEY.md §8b names: every kernel group the
+fused GAT stack, the output head, the optimizer and the window builder launch
+is one ``sv2n::`` op.  The real implementations check shapes / dtypes /
+devices, allocate outputs and workspaces from the caching allocator and
+launch on the current HIP stream (so every op is capturable into a hipGraph);
+the fake implementations return correctly shaped empty tensors, which is what
+``torch.compile`` / FakeTensor tracing and ``torch.library.opcheck`` need.
+
+Ops that ACCUMULATE into parameter gradients (``gat_wgrad``,
+``prep_bwd_edge``, ``head_bwd``, ``head_mse_bwd``) and the optimizer step
+declare those arguments as mutated (``Tensor(a!)``) in their schema.
+
+Reference ops each entry replaces: the comments in include/sv2n.h
+(PyG 2.3.0 GATConv pieces, reference utils/models.py:146; GATModel.linear,
+utils/models.py:150; Adam, 5_train_SpotV2Net.py:127/:159;
+CovarianceLaggedDataset windows, utils/dataset.py:200-282).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import torch
+
+from . import _lib
+
+LIB = torch.library.Library("sv2n", "DEF")
+
+_SCHEMAS = {
+    "gat_prep": "(Tensor[] W, Tensor[] att_src, Tensor[] att_dst, Tensor[] W_edge, "
+                "Tensor[] att_edge, int[] heads, int[] channels, int hl_pad, bool[] need_t, "
+                "bool use_edge) -> (Tensor[], Tensor[], Tensor[], Tensor)",
+    "edge_logits": "(Tensor edge_attr, Tensor wfold, Tensor? edge_index, Tensor canon, "
+                   "int num_layers, int heads, int num_graphs, int n, bool planes) -> Tensor[]",
+    "project": "(Tensor a, Tensor? planes, Tensor w, bool transpose_w, bool bf16) -> Tensor",
+    "gat_attn_fwd": "(Tensor xs, Tensor? ae, Tensor? rowmask, Tensor? bias, Tensor? keep, "
+                    "float keep_scale, int num_graphs, int n, int heads, int channels, "
+                    "bool concat, int act, float slope) -> (Tensor, Tensor)",
+    "gat_attn_tiled_fwd": "(Tensor xs, Tensor? ae, int num_edges, Tensor? eid, Tensor? rowmask, "
+                          "Tensor? bias, Tensor? keep, float keep_scale, int num_graphs, int n, "
+                          "int heads, int channels, bool concat, int act, float slope) -> Tensor",
+    "gat_attn_bwd": "(Tensor dy, Tensor y, Tensor xs, Tensor psave, Tensor? keep, "
+                    "float keep_scale, Tensor? rowmask, bool with_ae, int num_graphs, int n, "
+                    "int heads, int channels, bool concat, int act, float slope) "
+                    "-> (Tensor, Tensor, Tensor)",
+    "gat_attn_tiled_bwd": "(Tensor dy, Tensor y, Tensor xs, Tensor? ae, int num_edges, "
+                          "Tensor? eid, Tensor? keep, float keep_scale, Tensor? rowmask, "
+                          "int num_graphs, int n, int heads, int channels, bool concat, int act, "
+                          "float slope) -> (Tensor, Tensor, Tensor)",
+    "gat_wgrad": "(Tensor? x, Tensor dxs, Tensor W, Tensor att_src, Tensor att_dst, "
+                 "Tensor dbias_partial, int heads, int channels, bool bf16, Tensor(a!)? gW, "
+                 "Tensor(b!)? g_att_src, Tensor(c!)? g_att_dst, Tensor(d!)? g_bias) -> ()",
+    "edge_logits_bwd": "(Tensor edge_attr, Tensor? edge_index, Tensor canon, Tensor[] dae, "
+                       "int heads, int num_graphs, int n, int hl_pad, bool planes) -> Tensor",
+    "prep_bwd_edge": "(Tensor dwfold, int col0, Tensor W_edge, Tensor att_edge, int heads, "
+                     "int channels, Tensor(a!)? gW_edge, Tensor(b!)? g_att_edge) -> ()",
+    "head_fwd": "(Tensor x, Tensor weight, Tensor? bias) -> Tensor",
+    "head_bwd": "(Tensor x, Tensor weight, Tensor dout, Tensor(a!)? g_weight, "
+                "Tensor(b!)? g_bias) -> Tensor",
+    "head_mse_fwd": "(Tensor x, Tensor weight, Tensor? bias, Tensor target) -> (Tensor, Tensor)",
+    "head_mse_bwd": "(Tensor x, Tensor weight, Tensor diff, Tensor grad_loss, "
+                    "Tensor(a!)? g_weight, Tensor(b!)? g_bias) -> Tensor",
+    "adam_step": "(Tensor(a!) param, Tensor(b!) grad, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "
+                 "Tensor(e!) step, Tensor(f!) ticket, float lr, float beta1, float beta2, "
+                 "float eps, float weight_decay) -> ()",
+    "window_gather": "(Tensor vol, Tensor volvol, Tensor starts, int seq_length, "
+                     "int future_steps, Tensor canon, Tensor(a!) x, Tensor(b!) edge_attr, "
+                     "Tensor(c!) y) -> ()",
+}
+for _name, _schema in _SCHEMAS.items():
+    LIB.define(_name + _schema)
+
+
+def _impl(name):
+    def deco(fn):
+        LIB.impl(name, fn, "CUDA")
+        return fn
+    return deco
+
+
+def _fake(name):
+    return torch.library.register_fake("sv2n::" + name)
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None or t.numel() == 0 else t.data_ptr()
+
+
+def _st(t: torch.Tensor) -> int:
+    return _lib.stream_handle(t.device)
+
+
+def _need(cond: bool, msg: str) -> None:
+    if not cond:
+        raise RuntimeError("sv2n: " + msg)
+
+
+def _f32(*ts) -> None:
+    for t in ts:
+        if t is not None:
+            _need(t.dtype == torch.float32, f"expected float32, got {t.dtype}")
+            _need(t.is_cuda, "expected a ROCm device tensor")
+
+
+def _ldx(H: int, C: int) -> int:
+    return (H * C + 2 * H + 3) // 4 * 4
+
+
+# --------------------------------------------------------------------------
+# weight preparation (sv2n_gat_prep_fwd_all)
+# --------------------------------------------------------------------------
+def _prep_shapes(W, heads, channels, need_t, kpad):
+    out = []
+    for l, w in enumerate(W):
+        F = w.shape[1]
+        ldx = _ldx(heads[l], channels[l])
+        out.append(((ldx, F), (3, ldx, kpad(F)), (3, F, kpad(ldx)) if need_t[l] else (0,)))
+    return out
+
+
+def _kpad(K: int) -> int:
+    return (K + 63) // 64 * 64  # sv2n_split3_kpad
+
+
+@_impl("gat_prep")
+def _gat_prep(W, att_src, att_dst, W_edge, att_edge, heads, channels, hl_pad, need_t, use_edge):
+    lib = _lib.load()
+    L = len(W)
+    _f32(*W, *att_src, *att_dst, *W_edge, *att_edge)
+    dev = W[0].device
+    D = W_edge[0].shape[1] if use_edge else 0
+    wf = torch.empty(D, hl_pad, device=dev) if use_edge else torch.empty(0, device=dev)
+    arr = (_lib.PrepLayer * L)()
+    waugs, planes, planes_t = [], [], []
+    for l, (s_w, s_p, s_t) in enumerate(_prep_shapes(W, heads, channels, need_t, _kpad)):
+        waug = torch.empty(s_w, device=dev)
+        pl = torch.empty(s_p, device=dev, dtype=torch.int16)
+        plt = torch.empty(s_t, device=dev, dtype=torch.int16)
+        arr[l] = _lib.PrepLayer(
+            W[l].data_ptr(), att_src[l].data_ptr(), att_dst[l].data_ptr(), heads[l], channels[l],
+            W[l].shape[1], s_w[0], waug.data_ptr(), pl.data_ptr(), _p(plt),
+            W_edge[l].data_ptr() if use_edge else None,
+            att_edge[l].data_ptr() if use_edge else None, D, hl_pad, l * heads[0],
+            _p(wf) if use_edge else None)
+        waugs.append(waug)
+        planes.append(pl)
+        planes_t.append(plt)
+    _lib.check(lib.sv2n_gat_prep_fwd_all(ctypes.addressof(arr), L, _st(W[0])),
+               "sv2n_gat_prep_fwd_all")
+    return waugs, planes, planes_t, wf
+
+
+@_fake("gat_prep")
+def _gat_prep_fake(W, att_src, att_dst, W_edge, att_edge, heads, channels, hl_pad, need_t,
+                   use_edge):
+    D = W_edge[0].shape[1] if use_edge else 0
+    w0 = W[0]
+    shp = _prep_shapes(W, heads, channels, need_t, _kpad)
+    return ([w0.new_empty(a) for a, _, _ in shp],
+            [w0.new_empty(b, dtype=torch.int16) for _, b, _ in shp],
+            [w0.new_empty(c, dtype=torch.int16) for _, _, c in shp],
+            w0.new_empty((D, hl_pad) if use_edge else (0,)))
+
+
+# --------------------------------------------------------------------------
+# edge logits (sv2n_edge_logits_fwd / _planes) and their weight gradient
+# --------------------------------------------------------------------------
+def _ae_shape(planes, E, num_graphs, n, heads):
+    return (heads, E) if planes else (num_graphs, n, n, heads)
+
+
+@_impl("edge_logits")
+def _edge_logits(edge_attr, wfold, edge_index, canon, num_layers, heads, num_graphs, n, planes):
+    lib = _lib.load()
+    _f32(edge_attr, wfold)
+    E, D = edge_attr.shape
+    outs = [torch.empty(_ae_shape(planes, E, num_graphs, n, heads), device=edge_attr.device)
+            for _ in range(num_layers)]
+    if E == 0:
+        return outs
+    _need(edge_attr.is_contiguous() and edge_attr.data_ptr() % 16 == 0, "edge_attr alignment")
+    ptrs = _lib.ptr_array([o.data_ptr() for o in outs])
+    hp = wfold.shape[1]
+    if planes:
+        rc = lib.sv2n_edge_logits_fwd_planes(edge_attr.data_ptr(), E, D, wfold.data_ptr(), hp,
+                                             ptrs, num_layers, heads, _st(edge_attr))
+    else:
+        rc = lib.sv2n_edge_logits_fwd(edge_attr.data_ptr(), E, D, _p(edge_index),
+                                      canon.data_ptr(), wfold.data_ptr(), hp, ptrs, num_layers,
+                                      heads, num_graphs, n, _st(edge_attr))
+    _lib.check(rc, "sv2n_edge_logits_fwd")
+    return outs
+
+
+@_fake("edge_logits")
+def _edge_logits_fake(edge_attr, wfold, edge_index, canon, num_layers, heads, num_graphs, n,
+                      planes):
+    E = edge_attr.shape[0]
+    return [edge_attr.new_empty(_ae_shape(planes, E, num_graphs, n, heads))
+            for _ in range(num_layers)]
+
+
+@_impl("edge_logits_bwd")
+def _edge_logits_bwd(edge_attr, edge_index, canon, dae, heads, num_graphs, n, hl_pad, planes):
+    lib = _lib.load()
+    E, D = edge_attr.shape
+    dev = edge_attr.device
+    L = len(dae)
+    ptrs = _lib.ptr_array([d.data_ptr() for d in dae])
+    ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hl_pad)
+    ws = torch.empty(ws_n, device=dev)
+    dwf = torch.empty(D, hl_pad, device=dev)
+    if planes:
+        rc = lib.sv2n_edge_logits_bwd_planes(edge_attr.data_ptr(), E, D, _p(edge_index), ptrs, L,
+                                             heads, ws.data_ptr(), ws_n, dwf.data_ptr(), hl_pad,
+                                             _st(edge_attr))
+    else:
+        rc = lib.sv2n_edge_logits_bwd(edge_attr.data_ptr(), E, D, _p(edge_index),
+                                      canon.data_ptr(), ptrs, L, heads, num_graphs, n,
+                                      ws.data_ptr(), ws_n, dwf.data_ptr(), hl_pad, _st(edge_attr))
+    _lib.check(rc, "sv2n_edge_logits_bwd")
+    return dwf
+
+
+@_fake("edge_logits_bwd")
+def _edge_logits_bwd_fake(edge_attr, edge_index, canon, dae, heads, num_graphs, n, hl_pad,
+                          planes):
+    return edge_attr.new_empty((edge_attr.shape[1], hl_pad))
+
+
+@_impl("prep_bwd_edge")
+def _prep_bwd_edge(dwfold, col0, W_edge, att_edge, heads, channels, gW_edge, g_att_edge):
+    lib = _lib.load()
+    _lib.check(lib.sv2n_gat_prep_bwd_edge(dwfold.data_ptr(), dwfold.shape[1], col0,
+                                          W_edge.data_ptr(), att_edge.data_ptr(), heads, channels,
+                                          W_edge.shape[1], _p(gW_edge), _p(g_att_edge),
+                                          _st(dwfold)), "sv2n_gat_prep_bwd_edge")
+
+
+@_fake("prep_bwd_edge")
+def _prep_bwd_edge_fake(dwfold, col0, W_edge, att_edge, heads, channels, gW_edge, g_att_edge):
+    return None
+
+
+# --------------------------------------------------------------------------
+# projection GEMMs (sv2n_gemm_f32x3 / sv2n_gemm_bf16 / sv2n_gemm_f32)
+# --------------------------------------------------------------------------
+@_impl("project")
+def _project(a, planes, w, transpose_w, bf16):
+    from .ops import project_planes
+    _f32(a, w)
+    return project_planes(a, planes, w, transpose_w, bf16)
+
+
+@_fake("project")
+def _project_fake(a, planes, w, transpose_w, bf16):
+    N = w.shape[1] if transpose_w else w.shape[0]
+    return a.new_empty((a.shape[0], N))
+
+
+# --------------------------------------------------------------------------
+# fused attention (sv2n_gat_attn_* and the tiled forms)
+# --------------------------------------------------------------------------
+def _oc(heads, channels, concat):
+    return heads * channels if concat else channels
+
+
+@_impl("gat_attn_fwd")
+def _gat_attn_fwd(xs, ae, rowmask, bias, keep, keep_scale, num_graphs, n, heads, channels,
+                  concat, act, slope):
+    lib = _lib.load()
+    _f32(xs, ae, bias)
+    N = num_graphs * n
+    _need(xs.shape[0] == N and xs.stride(1) == 1, "xs shape")
+    y = torch.empty(N, _oc(heads, channels, concat), device=xs.device)
+    ps = torch.empty(num_graphs, heads, 32, 32, device=xs.device)
+    _lib.check(lib.sv2n_gat_attn_fwd(xs.data_ptr(), xs.stride(0), _p(ae), _p(rowmask), _p(bias),
+                                     _p(keep), keep_scale, y.data_ptr(), ps.data_ptr(),
+                                     num_graphs, n, heads, channels, int(concat), act, slope,
+                                     _st(xs)), "sv2n_gat_attn_fwd")
+    return y, ps
+
+
+@_fake("gat_attn_fwd")
+def _gat_attn_fwd_fake(xs, ae, rowmask, bias, keep, keep_scale, num_graphs, n, heads, channels,
+                       concat, act, slope):
+    return (xs.new_empty((num_graphs * n, _oc(heads, channels, concat))),
+            xs.new_empty((num_graphs, heads, 32, 32)))
+
+
+@_impl("gat_attn_tiled_fwd")
+def _gat_attn_tiled_fwd(xs, ae, num_edges, eid, rowmask, bias, keep, keep_scale, num_graphs, n,
+                        heads, channels, concat, act, slope):
+    lib = _lib.load()
+    _f32(xs, ae, bias)
+    N = num_graphs * n
+    y = torch.empty(N, _oc(heads, channels, concat), device=xs.device)
+    ws_n = lib.sv2n_gat_attn_tiled_workspace(num_graphs, n, heads, channels, int(concat))
+    ws = torch.empty(max(ws_n, 1), device=xs.device)
+    _lib.check(lib.sv2n_gat_attn_tiled_fwd(
+        xs.data_ptr(), xs.stride(0), _p(ae), num_edges, _p(eid), _p(rowmask), _p(bias), _p(keep),
+        keep_scale, y.data_ptr(), ws.data_ptr(), ws_n, num_graphs, n, heads, channels,
+        int(concat), act, slope, _st(xs)), "sv2n_gat_attn_tiled_fwd")
+    return y
+
+
+@_fake("gat_attn_tiled_fwd")
+def _gat_attn_tiled_fwd_fake(xs, ae, num_edges, eid, rowmask, bias, keep, keep_scale, num_graphs,
+                             n, heads, channels, concat, act, slope):
+    return xs.new_empty((num_graphs * n, _oc(heads, channels, concat)))
+
+
+@_impl("gat_attn_bwd")
+def _gat_attn_bwd(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_graphs, n, heads,
+                  channels, concat, act, slope):
+    lib = _lib.load()
+    _f32(dy, y, xs, psave)
+    dev = xs.device
+    dxs = torch.empty_like(xs)
+    dae = torch.empty(num_graphs, n, n, heads, device=dev) if with_ae else \
+        torch.empty(0, device=dev)
+    dbp = torch.empty(num_graphs, _oc(heads, channels, concat), device=dev)
+    _lib.check(lib.sv2n_gat_attn_bwd(dy.data_ptr(), y.data_ptr(), xs.data_ptr(), xs.stride(0),
+                                     psave.data_ptr(), _p(keep), keep_scale, _p(rowmask),
+                                     dxs.data_ptr(), _p(dae), dbp.data_ptr(), num_graphs, n,
+                                     heads, channels, int(concat), act, slope, _st(xs)),
+               "sv2n_gat_attn_bwd")
+    return dxs, dae, dbp
+
+
+@_fake("gat_attn_bwd")
+def _gat_attn_bwd_fake(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_graphs, n,
+                       heads, channels, concat, act, slope):
+    return (torch.empty_like(xs),
+            xs.new_empty((num_graphs, n, n, heads) if with_ae else (0,)),
+            xs.new_empty((num_graphs, _oc(heads, channels, concat))))
+
+
+@_impl("gat_attn_tiled_bwd")
+def _gat_attn_tiled_bwd(dy, y, xs, ae, num_edges, eid, keep, keep_scale, rowmask, num_graphs, n,
+                        heads, channels, concat, act, slope):
+    lib = _lib.load()
+    _f32(dy, y, xs, ae)
+    dev = xs.device
+    dxs = torch.empty_like(xs)
+    dae = torch.empty(heads, num_edges, device=dev) if (ae is not None and num_edges > 0) else \
+        torch.empty(0, device=dev)
+    dbp = torch.empty(num_graphs, _oc(heads, channels, concat), device=dev)
+    _lib.check(lib.sv2n_gat_attn_tiled_bwd(
+        dy.data_ptr(), y.data_ptr(), xs.data_ptr(), xs.stride(0), _p(ae), num_edges, _p(eid),
+        _p(keep), keep_scale, _p(rowmask), dxs.data_ptr(), _p(dae), dbp.data_ptr(), num_graphs,
+        n, heads, channels, int(concat), act, slope, _st(xs)), "sv2n_gat_attn_tiled_bwd")
+    return dxs, dae, dbp
+
+
+@_fake("gat_attn_tiled_bwd")
+def _gat_attn_tiled_bwd_fake(dy, y, xs, ae, num_edges, eid, keep, keep_scale, rowmask,
+                             num_graphs, n, heads, channels, concat, act, slope):
+    return (torch.empty_like(xs),
+            xs.new_empty((heads, num_edges) if (ae is not None and num_edges > 0) else (0,)),
+            xs.new_empty((num_graphs, _oc(heads, channels, concat))))
+
+
+# --------------------------------------------------------------------------
+# weight gradients of one layer (sv2n_gat_wgrad_node / _bf16), accumulating
+# --------------------------------------------------------------------------
+@_impl("gat_wgrad")
+def _gat_wgrad(x, dxs, W, att_src, att_dst, dbias_partial, heads, channels, bf16, gW, g_att_src,
+               g_att_dst, g_bias):
+    lib = _lib.load()
+    _f32(x, dxs, W, att_src, att_dst, dbias_partial, gW, g_att_src, g_att_dst, g_bias)
+    N, ldx = dxs.shape
+    F = W.shape[1]
+    weights = gW is not None or g_att_src is not None or g_att_dst is not None
+    use_bf16 = bf16 and weights and x.stride(0) % 4 == 0 and F >= 4 and \
+        x.data_ptr() % 16 == 0 and dxs.data_ptr() % 16 == 0
+    ws_fn = lib.sv2n_gat_wgrad_node_bf16_workspace if use_bf16 else \
+        lib.sv2n_gat_wgrad_node_workspace
+    fn = lib.sv2n_gat_wgrad_node_bf16 if use_bf16 else lib.sv2n_gat_wgrad_node
+    ws_n = ws_fn(N, F, ldx, heads, channels)
+    ws = torch.empty(max(ws_n, 1), device=dxs.device)
+    B, OC = dbias_partial.shape
+    _lib.check(fn(_p(x) if weights else None, x.stride(0) if weights else 0, dxs.data_ptr(), ldx,
+                  N, F, W.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), heads, channels,
+                  dbias_partial.data_ptr(), B, OC, _p(gW), _p(g_att_src), _p(g_att_dst),
+                  _p(g_bias), ws.data_ptr(), ws_n, _st(dxs)), "sv2n_gat_wgrad_node")
+
+
+@_fake("gat_wgrad")
+def _gat_wgrad_fake(x, dxs, W, att_src, att_dst, dbias_partial, heads, channels, bf16, gW,
+                    g_att_src, g_att_dst, g_bias):
+    return None
+
+
+# --------------------------------------------------------------------------
+# output head (sv2n_head_*), fused with the MSE loss
+# --------------------------------------------------------------------------
+@_impl("head_fwd")
+def _head_fwd(x, weight, bias):
+    lib = _lib.load()
+    _f32(x, weight, bias)
+    N, C = x.shape
+    O = weight.shape[0]
+    out = torch.empty(N, O, device=x.device)
+    _lib.check(lib.sv2n_head_fwd(x.data_ptr(), N, C, weight.data_ptr(), _p(bias), O,
+                                 out.data_ptr(), _st(x)), "sv2n_head_fwd")
+    return out
+
+
+@_fake("head_fwd")
+def _head_fwd_fake(x, weight, bias):
+    return x.new_empty((x.shape[0], weight.shape[0]))
+
+
+@_impl("head_bwd")
+def _head_bwd(x, weight, dout, g_weight, g_bias):
+    lib = _lib.load()
+    N, C = x.shape
+    O = weight.shape[0]
+    dout = dout.contiguous()
+    dx = torch.empty_like(x)
+    ws_n = lib.sv2n_head_bwd_workspace(N, C, O)
+    ws = _lib.persistent_zeros("head", ws_n, x.device)
+    _lib.check(lib.sv2n_head_bwd(x.data_ptr(), N, C, weight.data_ptr(), O, dout.data_ptr(),
+                                 dx.data_ptr(), _p(g_weight), _p(g_bias), ws.data_ptr(), ws_n,
+                                 _st(x)), "sv2n_head_bwd")
+    return dx
+
+
+@_fake("head_bwd")
+def _head_bwd_fake(x, weight, dout, g_weight, g_bias):
+    return torch.empty_like(x)
+
+
+@_impl("head_mse_fwd")
+def _head_mse_fwd(x, weight, bias, target):
+    lib = _lib.load()
+    _f32(x, weight, bias, target)
+    N, C = x.shape
+    O = weight.shape[0]
+    target = target.reshape(-1).contiguous()
+    _need(target.numel() == N * O, f"target has {target.numel()} elements, expected {N * O}")
+    diff = torch.empty(N * O, device=x.device)
+    loss = torch.empty((), device=x.device)
+    ws_n = lib.sv2n_head_mse_workspace(N, C, O)
+    ws = _lib.persistent_zeros("head", ws_n, x.device)
+    _lib.check(lib.sv2n_head_mse_fwd(x.data_ptr(), N, C, weight.data_ptr(), _p(bias), O,
+                                     target.data_ptr(), None, diff.data_ptr(), loss.data_ptr(),
+                                     ws.data_ptr(), ws_n, _st(x)), "sv2n_head_mse_fwd")
+    return loss, diff
+
+
+@_fake("head_mse_fwd")
+def _head_mse_fwd_fake(x, weight, bias, target):
+    return x.new_empty(()), x.new_empty((x.shape[0] * weight.shape[0],))
+
+
+@_impl("head_mse_bwd")
+def _head_mse_bwd(x, weight, diff, grad_loss, g_weight, g_bias):
+    lib = _lib.load()
+    N, C = x.shape
+    O = weight.shape[0]
+    gl = grad_loss.reshape(()).contiguous().to(torch.float32)
+    dx = torch.empty_like(x)
+    ws_n = lib.sv2n_head_mse_workspace(N, C, O)
+    ws = _lib.persistent_zeros("head", ws_n, x.device)
+    _lib.check(lib.sv2n_head_mse_bwd(x.data_ptr(), N, C, weight.data_ptr(), O, diff.data_ptr(),
+                                     gl.data_ptr(), dx.data_ptr(), _p(g_weight), _p(g_bias),
+                                     ws.data_ptr(), ws_n, _st(x)), "sv2n_head_mse_bwd")
+    return dx
+
+
+@_fake("head_mse_bwd")
+def _head_mse_bwd_fake(x, weight, diff, grad_loss, g_weight, g_bias):
+    return torch.empty_like(x)
+
+
+# --------------------------------------------------------------------------
+# optimizer step and window builder
+# --------------------------------------------------------------------------
+@_impl("adam_step")
+def _adam_step(param, grad, exp_avg, exp_avg_sq, step, ticket, lr, beta1, beta2, eps,
+               weight_decay):
+    lib = _lib.load()
+    _lib.check(lib.sv2n_adam_f32_step(param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(),
+                                      exp_avg_sq.data_ptr(), param.numel(), step.data_ptr(),
+                                      ticket.data_ptr(), lr, beta1, beta2, eps, weight_decay,
+                                      _st(param)), "sv2n_adam_f32_step")
+
+
+@_fake("adam_step")
+def _adam_step_fake(param, grad, exp_avg, exp_avg_sq, step, ticket, lr, beta1, beta2, eps,
+                    weight_decay):
+    return None
+
+
+@_impl("window_gather")
+def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y):
+    lib = _lib.load()
+    _f32(vol, volvol, x, edge_attr, y)
+    _need(vol.is_contiguous() and volvol.is_contiguous(), "series must be contiguous")
+    _need(starts.dtype == torch.long, "starts must be int64")
+    _lib.check(lib.sv2n_window_gather(vol.data_ptr(), volvol.data_ptr(), vol.shape[1],
+                                      starts.data_ptr(), starts.numel(), seq_length, future_steps,
+                                      canon.data_ptr(), x.data_ptr(), edge_attr.data_ptr(),
+                                      y.data_ptr(), _st(vol)), "sv2n_window_gather")
+
+
+@_fake("window_gather")
+def _window_gather_fake(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y):
+    return None
+
+
+OPS = tuple(_SCHEMAS)

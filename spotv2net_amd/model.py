@@ -32,11 +32,22 @@ from .stack import gat_stack, head_mse_loss, linear_head
 
 
 def _layout_of(data, x: torch.Tensor, edge_index: torch.Tensor) -> GraphLayout:
+    """The batch's graph layout: attached to it, cached on its edge_index, or
+    analysed — without a host synchronisation when the graph size is known
+    (``nodes_per_graph``, or N / ``num_graphs`` of a PyG / sv2n Batch)."""
     lay = getattr(data, "sv2n_layout", None)
     if isinstance(lay, GraphLayout) and lay.num_nodes == x.size(0):
         return lay
+    N = x.size(0)
     hint = getattr(data, "nodes_per_graph", None)
-    return analyze_edge_index(edge_index, x.size(0), hint)
+    if hint is None:
+        try:
+            ng = int(data.num_graphs)  # PyG Batch: host int; sv2n Batch: ptr length
+        except (AttributeError, TypeError, RuntimeError):
+            ng = 0
+        if ng > 0 and N % ng == 0:
+            hint = N // ng
+    return analyze_edge_index(edge_index, N, hint)
 
 
 class GATModel(nn.Module):

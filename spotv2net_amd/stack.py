@@ -1,18 +1,18 @@
 """Fused GAT stack: all GATConv layers of a GATModel (or one standalone
 GATConv) as ONE autograd node whose forward and backward are sequences of
-sv2n kernel launches.
+``torch.ops.sv2n`` operators (library.py; each one C-ABI kernel group).
 
 Forward (reference utils/models.py:145-148 with PyG GATConv inside):
-  per layer  sv2n_gat_prep_fwd   W -> [W ; Wᵀatt_src ; Wᵀatt_dst] and W̃_edge columns
-  once       sv2n_edge_logits_fwd  edge_attr · W̃ for every layer (one HBM pass)
-  per layer  sv2n_gemm_f32       xs = x · Waugᵀ  (f32 MFMA)
-             sv2n_gat_attn_fwd   loops/leaky/softmax/dropout/aggregate/bias/act
+  once       sv2n::gat_prep     W -> [W ; Wᵀatt_src ; Wᵀatt_dst], its bf16 planes, W̃_edge
+  once       sv2n::edge_logits  edge_attr · W̃ for every layer (one HBM pass)
+  per layer  sv2n::project      xs = x · Waugᵀ  (f32-accurate split MFMA, or bf16)
+             sv2n::gat_attn_fwd loops/leaky/softmax/dropout/aggregate/bias/act
              dropout between layers (model-level, torch RNG mask)
 Backward, layers in reverse:
-  sv2n_gat_attn_bwd  -> d xs, d ae, bias partials
-  sv2n_gemm_f32      -> dWaugᵀ = xᵀ·dxs (split-K), and dx = dxs·Waug (if needed)
-  sv2n_gat_prep_bwd_node -> ACCUMULATES into W/att_src/att_dst/bias .grad
-  then one sv2n_edge_logits_bwd for all layers + sv2n_gat_prep_bwd_edge.
+  sv2n::gat_attn_bwd  -> d xs, d ae, bias partials
+  sv2n::gat_wgrad     -> dWaugᵀ = xᵀ·dxs (split-K) + fold epilogue, ACCUMULATED
+  sv2n::project       -> dx = dxs·Waug (if needed)
+  then one sv2n::edge_logits_bwd for all layers + sv2n::prep_bwd_edge per layer.
 
 Parameter gradients.  By default the node RETURNS its parameter gradients to
 autograd (computed into one zero-initialised flat buffer per backward, one view
@@ -26,15 +26,14 @@ parameters: no per-parameter autograd launches in the captured step.
 from __future__ import annotations
 
 import contextlib
-import ctypes
 import threading
 from typing import Optional, Sequence
 
 import torch
 
-from . import _lib
+from . import _lib, library  # noqa: F401  (library registers torch.ops.sv2n)
 from .layout import GraphLayout
-from .ops import _aligned, _require_device, pad_columns, project_planes, resolve_precision
+from .ops import _aligned, _require_device, resolve_precision
 
 
 def _grad_buf(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -133,13 +132,24 @@ def _ldx(conv) -> int:
     return (conv.heads * conv.out_channels + 2 * conv.heads + 3) // 4 * 4
 
 
+def _hp(L: int, H: int) -> int:
+    """Edge-fold column padding: L*H -> 4, 8, 16 or 32 (ops.pad_columns)."""
+    for hp in (4, 8, 16, 32):
+        if L * H <= hp:
+            return hp
+    raise ValueError(f"at most 32 (layers x heads) edge-logit columns supported, got {L * H}")
+
+
+def _opt(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    return None if t is None or t.numel() == 0 else t
+
+
 class _GATStack(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, edge_attr, convs, layout: GraphLayout, act: int, post_dropout: float,
                 training: bool, precision: str, *params):
-        lib = _lib.load()
+        ops = torch.ops.sv2n
         dev = x.device
-        st = _lib.stream_handle(dev)
         L = len(convs)
         B, n, N = layout.num_graphs, layout.n, layout.num_nodes
         use_edge = edge_attr is not None and all(c.lin_edge is not None for c in convs)
@@ -150,63 +160,31 @@ class _GATStack(torch.autograd.Function):
             raise NotImplementedError("fused edge pass needs equal head counts across layers")
 
         ea = None
-        wf = None
         hp = 0
         if use_edge:
             ea = edge_attr.view(-1, 1) if edge_attr.dim() == 1 else edge_attr
             ea = _aligned(ea)
             if ea.size(0) != layout.num_edges:
                 raise ValueError("edge_attr rows must match edge_index columns")
-            D = ea.size(1)
-            _, hp = pad_columns(torch.empty(0, L * H))
-            wf = torch.empty(D, hp, device=dev, dtype=torch.float32)
+            hp = _hp(L, H)
 
         # 1) weight preparation: every layer's folded Waug, its bf16 split planes
         #    (and the transposed ones the backward's dx GEMM needs) and the edge
-        #    fold, in one launch
-        waugs, planes, planes_t = [], [], []
-        arr = (_lib.PrepLayer * L)()
-        for l, c in enumerate(convs):
-            F = c.in_channels
-            ldx = _ldx(c)
-            waug = torch.empty(ldx, F, device=dev, dtype=torch.float32)
-            pl = torch.empty(3, ldx, lib.sv2n_split3_kpad(F), device=dev, dtype=torch.int16)
-            need_t = training and (l > 0 or x.requires_grad)
-            plt = (torch.empty(3, F, lib.sv2n_split3_kpad(ldx), device=dev, dtype=torch.int16)
-                   if need_t else None)
-            We = c.lin_edge.weight if use_edge else None
-            arr[l] = _lib.PrepLayer(
-                c.lin_src.weight.data_ptr(), c.att_src.data_ptr(), c.att_dst.data_ptr(), c.heads,
-                c.out_channels, F, ldx, waug.data_ptr(), pl.data_ptr(), _lib.ptr(plt),
-                _lib.ptr(We), _lib.ptr(c.att_edge if use_edge else None),
-                ea.size(1) if use_edge else 0, hp, l * H, _lib.ptr(wf))
-            waugs.append(waug)
-            planes.append(pl)
-            planes_t.append(plt)
-        _lib.check(lib.sv2n_gat_prep_fwd_all(ctypes.addressof(arr), L, st),
-                   "sv2n_gat_prep_fwd_all")
+        #    fold, in one launch (sv2n::gat_prep)
+        need_t = [bool(training and (l > 0 or x.requires_grad)) for l in range(L)]
+        waugs, planes, planes_t, wf = ops.gat_prep(
+            [c.lin_src.weight for c in convs], [c.att_src for c in convs],
+            [c.att_dst for c in convs], [c.lin_edge.weight for c in convs] if use_edge else [],
+            [c.att_edge for c in convs] if use_edge else [], [c.heads for c in convs],
+            [c.out_channels for c in convs], hp, need_t, use_edge)
 
-        # 2) edge logits of every layer in one pass over edge_attr
+        # 2) edge logits of every layer in one pass over edge_attr (sv2n::edge_logits)
         aes = [None] * L
         if use_edge:
-            E = ea.size(0)
-            if tiled:  # head planes [H][E] in edge order
-                aes = [torch.empty(H, E, device=dev, dtype=torch.float32) if E > 0 else None
-                       for _ in range(L)]
-                if E > 0:
-                    ptrs = _lib.ptr_array([a.data_ptr() for a in aes])
-                    _lib.check(lib.sv2n_edge_logits_fwd_planes(ea.data_ptr(), E, ea.size(1),
-                                                               wf.data_ptr(), hp, ptrs, L, H, st),
-                               "sv2n_edge_logits_fwd_planes")
-            else:
-                aes = [torch.empty(B, n, n, H, device=dev, dtype=torch.float32) for _ in range(L)]
-                if E > 0:
-                    ptrs = _lib.ptr_array([a.data_ptr() for a in aes])
-                    ei = layout.edge_index if layout.kind == "block" else None
-                    _lib.check(lib.sv2n_edge_logits_fwd(ea.data_ptr(), E, ea.size(1),
-                                                        _lib.ptr(ei), layout.canon.data_ptr(),
-                                                        wf.data_ptr(), hp, ptrs, L, H, B, n, st),
-                               "sv2n_edge_logits_fwd")
+            ei = layout.edge_index if layout.kind == "block" else None
+            aes = list(ops.edge_logits(ea, wf, ei, layout.canon, L, H, B, n, tiled))
+            if tiled and ea.size(0) == 0:
+                aes = [None] * L
 
         # 3) layers
         xin = _aligned(x)
@@ -216,7 +194,7 @@ class _GATStack(torch.autograd.Function):
             F = c.in_channels
             if xin.size(1) != F:
                 raise ValueError(f"layer {l}: expected {F} input features, got {xin.size(1)}")
-            xs = project_planes(xin, planes[l], waugs[l], False, bf16)  # x · Waugᵀ
+            xs = ops.project(xin, planes[l], waugs[l], False, bf16)  # x · Waugᵀ
             keep, kscale = None, 1.0
             kn = n if tiled else 32  # keep-mask tile: [B][H][n][n] tiled, [B][H][32][32] per-graph
             if training and c.dropout > 0.0:
@@ -226,25 +204,15 @@ class _GATStack(torch.autograd.Function):
                 else:
                     keep = (torch.rand(B, Hc, kn, kn, device=dev) >= c.dropout).to(torch.uint8)
                     kscale = 1.0 / (1.0 - c.dropout)
-            OC = Hc * C if c.concat else C
-            y = torch.empty(N, OC, device=dev, dtype=torch.float32)
             if tiled:
                 # nothing saved: the backward recomputes the attention from xs and ae
-                ps = None
-                ws_n = lib.sv2n_gat_attn_tiled_workspace(B, n, Hc, C, int(c.concat))
-                ws = torch.empty(max(ws_n, 1), device=dev, dtype=torch.float32)
-                _lib.check(lib.sv2n_gat_attn_tiled_fwd(
-                    xs.data_ptr(), xs.stride(0), _lib.ptr(aes[l]), layout.num_edges,
-                    _lib.ptr(layout.eid), _lib.ptr(layout.rowmask),
-                    _lib.ptr(c.bias), _lib.ptr(keep), kscale, y.data_ptr(), ws.data_ptr(), ws_n,
-                    B, n, Hc, C, int(c.concat), act, float(c.negative_slope), st),
-                    "sv2n_gat_attn_tiled_fwd")
+                y = ops.gat_attn_tiled_fwd(xs, aes[l], layout.num_edges, layout.eid,
+                                           layout.rowmask, c.bias, keep, kscale, B, n, Hc, C,
+                                           c.concat, act, float(c.negative_slope))
+                ps = aes[l]
             else:
-                ps = torch.empty(B, Hc, 32, 32, device=dev, dtype=torch.float32)
-                _lib.check(lib.sv2n_gat_attn_fwd(
-                    xs.data_ptr(), xs.stride(0), _lib.ptr(aes[l]), _lib.ptr(layout.rowmask),
-                    _lib.ptr(c.bias), _lib.ptr(keep), kscale, y.data_ptr(), ps.data_ptr(), B, n,
-                    Hc, C, int(c.concat), act, float(c.negative_slope), st), "sv2n_gat_attn_fwd")
+                y, ps = ops.gat_attn_fwd(xs, aes[l], layout.rowmask, c.bias, keep, kscale, B, n,
+                                         Hc, C, c.concat, act, float(c.negative_slope))
             out = y
             dmask = None
             if training and post_dropout > 0.0:
@@ -257,7 +225,7 @@ class _GATStack(torch.autograd.Function):
             saved_x.append(xin)
             saved_xs.append(xs)
             saved_y.append(y)
-            saved_p.append(aes[l] if tiled else ps)
+            saved_p.append(ps)
             saved_keep.append(keep)
             saved_drop.append(dmask)
             xin = out
@@ -275,7 +243,7 @@ class _GATStack(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        lib = _lib.load()
+        ops = torch.ops.sv2n
         convs = ctx.convs
         layout: GraphLayout = ctx.layout
         L, act, use_edge, hp, H = ctx.meta
@@ -291,7 +259,6 @@ class _GATStack(torch.autograd.Function):
         waugs = sv[k:k + L]; k += L
         planes_t = sv[k:k + L]
         dev = dout.device
-        st = _lib.stream_handle(dev)
         B, n, N = layout.num_graphs, layout.n, layout.num_nodes
 
         dy = dout.contiguous()
@@ -302,83 +269,41 @@ class _GATStack(torch.autograd.Function):
         for l in range(L - 1, -1, -1):
             c = convs[l]
             Hc, C = c.heads, c.out_channels
-            F = c.in_channels
-            OC = Hc * C if c.concat else C
             if drops[l] is not None:
                 dy = dy * drops[l]
             xs = xss[l]
-            dxs = torch.empty_like(xs)
-            dae = None
-            if use_edge and layout.tiled:
-                dae = torch.empty(Hc, ea.size(0), device=dev, dtype=torch.float32) \
-                    if ea.size(0) > 0 else None
-            elif use_edge:
-                dae = torch.empty(B, n, n, Hc, device=dev, dtype=torch.float32)
-            dbp = torch.empty(B, OC, device=dev, dtype=torch.float32)
             if layout.tiled:  # pss[l] holds the layer's ae (or None without edges)
-                _lib.check(lib.sv2n_gat_attn_tiled_bwd(
-                    dy.data_ptr(), ys[l].data_ptr(), xs.data_ptr(), xs.stride(0),
-                    _lib.ptr(pss[l]), layout.num_edges, _lib.ptr(layout.eid),
-                    _lib.ptr(keeps[l]), ctx.kscales[l],
-                    _lib.ptr(layout.rowmask), dxs.data_ptr(), _lib.ptr(dae), dbp.data_ptr(), B,
-                    n, Hc, C, int(c.concat), act, float(c.negative_slope), st),
-                    "sv2n_gat_attn_tiled_bwd")
+                dxs, dae, dbp = ops.gat_attn_tiled_bwd(
+                    dy, ys[l], xs, pss[l], layout.num_edges, layout.eid, keeps[l],
+                    ctx.kscales[l], layout.rowmask, B, n, Hc, C, c.concat, act,
+                    float(c.negative_slope))
             else:
-                _lib.check(lib.sv2n_gat_attn_bwd(
-                    dy.data_ptr(), ys[l].data_ptr(), xs.data_ptr(), xs.stride(0),
-                    pss[l].data_ptr(), _lib.ptr(keeps[l]), ctx.kscales[l],
-                    _lib.ptr(layout.rowmask), dxs.data_ptr(), _lib.ptr(dae), dbp.data_ptr(), B,
-                    n, Hc, C, int(c.concat), act, float(c.negative_slope), st),
-                    "sv2n_gat_attn_bwd")
-            daes[l] = dae
+                dxs, dae, dbp = ops.gat_attn_bwd(
+                    dy, ys[l], xs, pss[l], keeps[l], ctx.kscales[l], layout.rowmask, use_edge,
+                    B, n, Hc, C, c.concat, act, float(c.negative_slope))
+            daes[l] = _opt(dae)
             gW = grad_of(c.lin_src.weight)
             gas = grad_of(c.att_src)
             gad = grad_of(c.att_dst)
             gb = grad_of(c.bias)
             if any(g is not None for g in (gW, gas, gad, gb)):
                 # split-K dWaugᵀ GEMM + one fused epilogue (fold, transpose,
-                # att and bias grads), accumulated into .grad
-                x_l = xs_in[l]
-                # bf16 mode: bf16-operand GEMM when x_l's rows are 16-B multiples
-                wg_bf16 = ctx.bf16 and x_l.stride(0) % 4 == 0 and F >= 4
-                ws_fn = lib.sv2n_gat_wgrad_node_bf16_workspace if wg_bf16 else \
-                    lib.sv2n_gat_wgrad_node_workspace
-                wg_fn = lib.sv2n_gat_wgrad_node_bf16 if wg_bf16 else lib.sv2n_gat_wgrad_node
-                ws_n = ws_fn(N, F, xs.size(1), Hc, C)
-                ws = torch.empty(max(ws_n, 1), device=dev, dtype=torch.float32)
-                _lib.check(wg_fn(
-                    x_l.data_ptr(), x_l.stride(0), dxs.data_ptr(), dxs.stride(0), N, F,
-                    c.lin_src.weight.data_ptr(), c.att_src.data_ptr(), c.att_dst.data_ptr(), Hc, C,
-                    dbp.data_ptr(), B, OC, _lib.ptr(gW), _lib.ptr(gas), _lib.ptr(gad),
-                    _lib.ptr(gb), ws.data_ptr(), ws_n, st), "sv2n_gat_wgrad_node")
+                # att and bias grads), accumulated into the gradient buffers
+                ops.gat_wgrad(xs_in[l], dxs, c.lin_src.weight, c.att_src, c.att_dst, dbp, Hc, C,
+                              ctx.bf16, gW, gas, gad, gb)
             if l > 0 or need_x0:
-                dy = project_planes(dxs, planes_t[l], waugs[l], True, ctx.bf16)  # dxs · Waug
+                dy = ops.project(dxs, _opt(planes_t[l]), waugs[l], True, ctx.bf16)  # dxs · Waug
 
         if use_edge and ea is not None:
             # grads exist (zeros) even without edges, as in PyG
             need_e = [(grad_of(c.lin_edge.weight), grad_of(c.att_edge)) for c in convs]
             if ea.size(0) > 0 and any(a is not None or b is not None for a, b in need_e):
-                E, D = ea.shape
-                ptrs = _lib.ptr_array([d.data_ptr() for d in daes])
-                ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hp)
-                ws = torch.empty(ws_n, device=dev, dtype=torch.float32)
-                dwf = torch.empty(D, hp, device=dev, dtype=torch.float32)
                 ei = layout.edge_index if layout.kind == "block" else None
-                if layout.tiled:
-                    _lib.check(lib.sv2n_edge_logits_bwd_planes(
-                        ea.data_ptr(), E, D, _lib.ptr(ei), ptrs, L, H, ws.data_ptr(), ws_n,
-                        dwf.data_ptr(), hp, st), "sv2n_edge_logits_bwd_planes")
-                else:
-                    _lib.check(lib.sv2n_edge_logits_bwd(ea.data_ptr(), E, D, _lib.ptr(ei),
-                                                        layout.canon.data_ptr(), ptrs, L, H, B,
-                                                        n, ws.data_ptr(), ws_n, dwf.data_ptr(),
-                                                        hp, st), "sv2n_edge_logits_bwd")
+                dwf = ops.edge_logits_bwd(ea, ei, layout.canon, daes, H, B, n, hp, layout.tiled)
                 for l, c in enumerate(convs):
                     gWe, gae = need_e[l]
-                    _lib.check(lib.sv2n_gat_prep_bwd_edge(
-                        dwf.data_ptr(), hp, l * H, c.lin_edge.weight.data_ptr(),
-                        c.att_edge.data_ptr(), c.heads, c.out_channels, D, _lib.ptr(gWe),
-                        _lib.ptr(gae), st), "sv2n_gat_prep_bwd_edge")
+                    ops.prep_bwd_edge(dwf, l * H, c.lin_edge.weight, c.att_edge, c.heads,
+                                      c.out_channels, gWe, gae)
         dx0 = dy if need_x0 else None
         return (dx0, None, None, None, None, None, None, None) + grad_of.returned()
 
@@ -419,23 +344,19 @@ def gat_stack(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs: Sequenc
     for p in params:
         if p.device != x.device:
             raise RuntimeError("parameters and data must be on the same device")
-    return _GATStack.apply(x, edge_attr, tuple(convs), layout, int(act), float(post_dropout),
-                           bool(training), precision, *params)
+    out = _GATStack.apply(x, edge_attr, tuple(convs), layout, int(act), float(post_dropout),
+                          bool(training), precision, *params)
+    return layout.poison(out)  # NaN if a deferred layout check failed (layout.py)
 
 
 class _Head(torch.autograd.Function):
-    """GATModel.linear (reference utils/models.py:120, :150) on sv2n_head_*;
+    """GATModel.linear (reference utils/models.py:120, :150) on sv2n::head_*;
     parameter gradients are returned (or accumulated directly) like the GAT stack."""
 
     @staticmethod
     def forward(ctx, x, linear, weight, bias):
-        lib = _lib.load()
         x = _aligned(x)
-        N, C = x.shape
-        O = weight.shape[0]
-        out = torch.empty(N, O, device=x.device, dtype=torch.float32)
-        _lib.check(lib.sv2n_head_fwd(x.data_ptr(), N, C, weight.data_ptr(), _lib.ptr(bias), O,
-                                     out.data_ptr(), _lib.stream_handle(x.device)), "sv2n_head_fwd")
+        out = torch.ops.sv2n.head_fwd(x, weight, bias)
         ctx.linear = linear
         ctx.direct = _direct_mode()
         ctx.save_for_backward(x)
@@ -443,48 +364,23 @@ class _Head(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        lib = _lib.load()
         (x,) = ctx.saved_tensors
         lin = ctx.linear
-        N, C = x.shape
-        O = lin.weight.shape[0]
-        dout = dout.contiguous()
-        dx = torch.empty_like(x)
-        ws_n = lib.sv2n_head_bwd_workspace(N, C, O)
-        ws = _lib.persistent_zeros("head", ws_n, x.device)
         grad_of = _GradTargets([lin.weight, lin.bias], ctx.needs_input_grad[2:4], ctx.direct,
                                x.device)
-        gw = grad_of(lin.weight)
-        gb = grad_of(lin.bias)
-        _lib.check(lib.sv2n_head_bwd(x.data_ptr(), N, C, lin.weight.data_ptr(), O,
-                                     dout.data_ptr(), dx.data_ptr(), _lib.ptr(gw), _lib.ptr(gb),
-                                     ws.data_ptr(), ws_n, _lib.stream_handle(x.device)),
-                   "sv2n_head_bwd")
+        dx = torch.ops.sv2n.head_bwd(x, lin.weight, dout, grad_of(lin.weight), grad_of(lin.bias))
         return (dx if ctx.needs_input_grad[0] else None, None) + grad_of.returned()
 
 
 class _HeadMSE(torch.autograd.Function):
     """``F.mse_loss(linear(x).view(-1), target)`` (reference
-    5_train_SpotV2Net.py:150-154) as two launches: sv2n_head_mse_fwd (head,
-    residual, loss) and sv2n_head_mse_bwd (dx and the head's parameter grads)."""
+    5_train_SpotV2Net.py:150-154) as two launches: sv2n::head_mse_fwd (head,
+    residual, loss) and sv2n::head_mse_bwd (dx and the head's parameter grads)."""
 
     @staticmethod
     def forward(ctx, x, target, linear, weight, bias):
-        lib = _lib.load()
         x = _aligned(x)
-        N, C = x.shape
-        O = weight.shape[0]
-        target = target.reshape(-1).contiguous()
-        if target.numel() != N * O:
-            raise ValueError(f"target has {target.numel()} elements, expected {N * O}")
-        diff = torch.empty(N * O, device=x.device, dtype=torch.float32)
-        loss = torch.empty((), device=x.device, dtype=torch.float32)
-        ws_n = lib.sv2n_head_mse_workspace(N, C, O)
-        ws = _lib.persistent_zeros("head", ws_n, x.device)
-        _lib.check(lib.sv2n_head_mse_fwd(x.data_ptr(), N, C, weight.data_ptr(), _lib.ptr(bias), O,
-                                         target.data_ptr(), None, diff.data_ptr(),
-                                         loss.data_ptr(), ws.data_ptr(), ws_n,
-                                         _lib.stream_handle(x.device)), "sv2n_head_mse_fwd")
+        loss, diff = torch.ops.sv2n.head_mse_fwd(x, weight, bias, target)
         ctx.linear = linear
         ctx.direct = _direct_mode()
         ctx.save_for_backward(x, diff)
@@ -492,23 +388,12 @@ class _HeadMSE(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gloss):
-        lib = _lib.load()
         x, diff = ctx.saved_tensors
         lin = ctx.linear
-        N, C = x.shape
-        O = lin.weight.shape[0]
-        gloss = gloss.reshape(()).contiguous().to(torch.float32)
-        dx = torch.empty_like(x)
-        ws_n = lib.sv2n_head_mse_workspace(N, C, O)
-        ws = _lib.persistent_zeros("head", ws_n, x.device)
         grad_of = _GradTargets([lin.weight, lin.bias], ctx.needs_input_grad[3:5], ctx.direct,
                                x.device)
-        gw = grad_of(lin.weight)
-        gb = grad_of(lin.bias)
-        _lib.check(lib.sv2n_head_mse_bwd(x.data_ptr(), N, C, lin.weight.data_ptr(), O,
-                                         diff.data_ptr(), gloss.data_ptr(), dx.data_ptr(),
-                                         _lib.ptr(gw), _lib.ptr(gb), ws.data_ptr(), ws_n,
-                                         _lib.stream_handle(x.device)), "sv2n_head_mse_bwd")
+        dx = torch.ops.sv2n.head_mse_bwd(x, lin.weight, diff, gloss, grad_of(lin.weight),
+                                         grad_of(lin.bias))
         return (dx if ctx.needs_input_grad[0] else None, None, None) + grad_of.returned()
 
 

@@ -60,8 +60,7 @@ class FlatAdam:
 
     def __init__(self, flat_params: torch.Tensor, flat_grads: torch.Tensor, lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
-        from . import _lib
-        self._lib = _lib
+        from . import library  # noqa: F401  (torch.ops.sv2n.adam_step)
         self.p, self.g = flat_params, flat_grads
         self.m = torch.zeros_like(flat_params)
         self.v = torch.zeros_like(flat_params)
@@ -73,12 +72,9 @@ class FlatAdam:
     zeroes_grads = True
 
     def step(self) -> None:
-        lib = self._lib.load()
-        self._lib.check(lib.sv2n_adam_f32_step(
-            self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
-            self.p.numel(), self.step_t.data_ptr(), self.ticket.data_ptr(), self.lr,
-            float(self.betas[0]), float(self.betas[1]), self.eps, self.wd,
-            self._lib.stream_handle(self.p.device)), "sv2n_adam_f32_step")
+        torch.ops.sv2n.adam_step(self.p, self.g, self.m, self.v, self.step_t, self.ticket,
+                                 self.lr, float(self.betas[0]), float(self.betas[1]), self.eps,
+                                 self.wd)
 
 
 def allreduce_mean_(flat: torch.Tensor, group=None) -> None:

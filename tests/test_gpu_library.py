@@ -1,0 +1,140 @@
+"""The torch.ops.sv2n operator boundary: schemas and fake
+implementations (torch.library.opcheck), torch.compile over GATModel, and
+the sync-free layout analysis with its deferred error."""
+import pytest
+import torch
+
+from helpers import assert_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _small(dev, B=3, S=2, n=30):
+    from spotv2net_amd import synthetic_batch
+    return synthetic_batch(B, S, n=n, seed=5, device=dev)
+
+
+def test_opcheck_forward_ops(dev):
+    """opcheck: schema, fake (meta) implementation and dispatcher registration
+    of the forward operators on real inputs."""
+    from spotv2net_amd import GATModel, library  # noqa: F401
+    from spotv2net_amd.layout import analyze_edge_index
+    ops = torch.ops.sv2n
+    torch.manual_seed(0)
+    m = GATModel(60, 6, 2, 1, [8, 4], concat_heads=True).to(dev)
+    d = _small(dev)
+    lay = analyze_edge_index(d.edge_index, d.x.shape[0])
+    c0, c1 = m.gat_layers
+    prep_args = ([c0.lin_src.weight, c1.lin_src.weight], [c0.att_src, c1.att_src],
+                 [c0.att_dst, c1.att_dst], [c0.lin_edge.weight, c1.lin_edge.weight],
+                 [c0.att_edge, c1.att_edge], [2, 2], [8, 4], 4, [False, True], True)
+    torch.library.opcheck(ops.gat_prep, prep_args, test_utils=("test_schema", "test_faketensor"))
+    waugs, planes, _, wf = ops.gat_prep(*prep_args)
+    ea_args = (d.edge_attr, wf, None, lay.canon, 2, 2, 3, 30, False)
+    torch.library.opcheck(ops.edge_logits, ea_args, test_utils=("test_schema", "test_faketensor"))
+    aes = ops.edge_logits(*ea_args)
+    pj = (d.x, planes[0], waugs[0], False, False)
+    torch.library.opcheck(ops.project, pj)
+    xs = ops.project(*pj)
+    att = (xs, aes[0], None, c0.bias, None, 1.0, 3, 30, 2, 8, True, 1, 0.2)
+    torch.library.opcheck(ops.gat_attn_fwd, att)
+    h = torch.randn(90, 4, device=dev)
+    torch.library.opcheck(ops.head_fwd, (h, m.linear.weight, m.linear.bias))
+    torch.library.opcheck(ops.head_mse_fwd, (h, m.linear.weight, m.linear.bias,
+                                             torch.randn(90, device=dev)))
+
+
+def test_opcheck_backward_ops(dev):
+    from spotv2net_amd import library  # noqa: F401
+    ops = torch.ops.sv2n
+    g = torch.Generator().manual_seed(1)
+    B, n, H, C = 2, 30, 2, 8
+    ldx = (H * C + 2 * H + 3) // 4 * 4
+    xs = torch.randn(B * n, ldx, generator=g).to(dev)
+    ae = torch.randn(B, n, n, H, generator=g).to(dev)
+    y, ps = ops.gat_attn_fwd(xs, ae, None, None, None, 1.0, B, n, H, C, True, 1, 0.2)
+    dy = torch.randn_like(y)
+    torch.library.opcheck(ops.gat_attn_bwd, (dy, y, xs, ps, None, 1.0, None, True, B, n, H, C,
+                                             True, 1, 0.2))
+    dxs, dae, dbp = ops.gat_attn_bwd(dy, y, xs, ps, None, 1.0, None, True, B, n, H, C, True, 1,
+                                     0.2)
+    x = torch.randn(B * n, 12, generator=g).to(dev)
+    W = torch.randn(H * C, 12, generator=g).to(dev)
+    a_s = torch.randn(1, H, C, generator=g).to(dev)
+    a_d = torch.randn(1, H, C, generator=g).to(dev)
+    grads = [torch.zeros_like(W), torch.zeros_like(a_s), torch.zeros_like(a_d),
+             torch.zeros(H * C, device=dev)]
+    torch.library.opcheck(ops.gat_wgrad, (x, dxs, W, a_s, a_d, dbp, H, C, False, *grads),
+                          test_utils=("test_schema", "test_faketensor"))
+    lin = torch.nn.Linear(4, 1).to(dev)
+    h = torch.randn(60, 4, device=dev)
+    torch.library.opcheck(ops.head_bwd, (h, lin.weight, torch.randn(60, 1, device=dev),
+                                         torch.zeros_like(lin.weight),
+                                         torch.zeros_like(lin.bias)),
+                          test_utils=("test_schema", "test_faketensor"))
+
+
+def test_torch_compile_matches_eager(dev):
+    """torch.compile(GATModel) (inductor) on a batch whose layout is attached:
+    the sv2n ops appear in the traced graph as custom ops (no graph break
+    inside the GAT stack) and the forward / gradients equal eager."""
+    import copy
+
+    from spotv2net_amd import GATModel
+    torch.manual_seed(2)
+    m1 = GATModel(60, 6, 2, 1, [8, 4], concat_heads=True).to(dev)
+    m2 = copy.deepcopy(m1)
+    d = _small(dev)
+    torch._dynamo.reset()
+    explain = torch._dynamo.explain(m2)(d)
+    cm = torch.compile(m2)
+    out1 = m1(d)
+    out2 = cm(d)
+    assert_close(out2, out1, tol=1e-6, what="compiled forward")
+    out1.sum().backward()
+    out2.sum().backward()
+    for (name, p), (_, q) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert_close(q.grad, p.grad, tol=1e-6, what=name)
+    # the stack is one traceable region: breaks, if any, are outside sv2n ops
+    for br in explain.break_reasons:
+        assert "sv2n" not in str(br.reason), br
+
+
+def test_layout_analysis_has_no_host_sync(dev):
+    """A fresh edge_index per batch (the reference's PyG DataLoader loop,
+    5_train_SpotV2Net.py:142-143) with a known graph size: forward and
+    backward run with CUDA sync debugging set to error."""
+    from spotv2net_amd import Batch, GATModel
+    torch.manual_seed(3)
+    m = GATModel(60, 6, 2, 1, [8, 4], concat_heads=True).to(dev)
+    d = _small(dev, B=4)
+    m(d).sum().backward()  # warm caches (canonical table, workspaces)
+    fresh = Batch(x=d.x, edge_index=d.edge_index.clone(), edge_attr=d.edge_attr, y_x=d.y_x,
+                  ptr=d.ptr, batch=d.batch)
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        out = m(fresh)
+        out.sum().backward()
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    assert_close(out, m(d), tol=1e-6, what="block path == canonical path")
+
+
+def test_invalid_edges_poison_then_raise(dev):
+    """Duplicate edges under the sync-free analysis: the forward returns NaN
+    and the deferred check raises UnsupportedLayout."""
+    from spotv2net_amd import Batch, GATModel, UnsupportedLayout
+    from spotv2net_amd.layout import check_pending
+    torch.manual_seed(4)
+    m = GATModel(60, 6, 2, 1, [8, 4], concat_heads=True).to(dev)
+    d = _small(dev, B=2)
+    ei = d.edge_index.clone()
+    ei[:, 5] = ei[:, 6]  # a repeated (target, source) pair
+    bad = Batch(x=d.x, edge_index=ei, edge_attr=d.edge_attr, y_x=d.y_x, ptr=d.ptr,
+                batch=d.batch)
+    out = m(bad)
+    assert torch.isnan(out).all()
+    with pytest.raises(UnsupportedLayout):
+        check_pending(block=True)
+    check_pending(block=True)  # reported once
