@@ -142,7 +142,9 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
       const int o = tt + ATT_THREADS * v;
       const int hh = o / cw, cc = o - hh * cw;
       const bool ok = bias && o < k.span && cc < k.cwv;
-      const float b = bias[ok ? (CONCAT ? (k.h0 + hh) * C : 0) + k.c0 + cc : 0];
+      // bias may be NULL (bias=False): read a valid address, discard the value
+      const float* bsrc = bias ? bias : xs;
+      const float b = bsrc[ok ? (CONCAT ? (k.h0 + hh) * C : 0) + k.c0 + cc : 0];
       br[v] = ok ? b : 0.f;
     }
   };

@@ -105,6 +105,21 @@ def _f32(*ts) -> None:
             _need(t.is_cuda, "expected a ROCm device tensor")
 
 
+def _dense(*ts) -> None:
+    """The kernels address these through raw pointers as dense row-major
+    buffers: refuse anything else (an error, never a wrong read)."""
+    for t in ts:
+        if t is not None and t.numel() > 0:
+            _need(t.is_contiguous(), f"expected a contiguous tensor of shape {tuple(t.shape)}")
+            _need(t.is_cuda, "expected a ROCm device tensor")
+
+
+def _rows(xs: torch.Tensor, rows: int, min_cols: int, what: str) -> None:
+    _need(xs.dim() == 2 and xs.shape[0] == rows and xs.shape[1] >= min_cols and
+          xs.stride(1) == 1 and xs.stride(0) >= xs.shape[1], f"{what}: expected [{rows}, >= "
+          f"{min_cols}] rows with unit column stride, got {tuple(xs.shape)} / {xs.stride()}")
+
+
 def _ldx(H: int, C: int) -> int:
     return (H * C + 2 * H + 3) // 4 * 4
 
@@ -176,7 +191,11 @@ def _ae_shape(planes, E, num_graphs, n, heads):
 def _edge_logits(edge_attr, wfold, edge_index, canon, num_layers, heads, num_graphs, n, planes):
     lib = _lib.load()
     _f32(edge_attr, wfold)
+    _dense(edge_attr, wfold, edge_index, canon)
     E, D = edge_attr.shape
+    _need(wfold.shape[0] == D and num_layers * heads <= wfold.shape[1], "wfold shape")
+    _need(edge_index is None or tuple(edge_index.shape) == (2, E), "edge_index shape")
+    _need(canon.numel() == n * (n - 1), "canonical table shape")
     outs = [torch.empty(_ae_shape(planes, E, num_graphs, n, heads), device=edge_attr.device)
             for _ in range(num_layers)]
     if E == 0:
@@ -206,9 +225,12 @@ def _edge_logits_fake(edge_attr, wfold, edge_index, canon, num_layers, heads, nu
 @_impl("edge_logits_bwd")
 def _edge_logits_bwd(edge_attr, edge_index, canon, dae, heads, num_graphs, n, hl_pad, planes):
     lib = _lib.load()
+    _dense(edge_attr, edge_index, canon, *dae)
     E, D = edge_attr.shape
     dev = edge_attr.device
     L = len(dae)
+    for d in dae:
+        _need(d.numel() == (heads * E if planes else num_graphs * n * n * heads), "dae shape")
     ptrs = _lib.ptr_array([d.data_ptr() for d in dae])
     ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hl_pad)
     ws = torch.empty(ws_n, device=dev)
@@ -274,7 +296,12 @@ def _gat_attn_fwd(xs, ae, rowmask, bias, keep, keep_scale, num_graphs, n, heads,
     lib = _lib.load()
     _f32(xs, ae, bias)
     N = num_graphs * n
-    _need(xs.shape[0] == N and xs.stride(1) == 1, "xs shape")
+    _rows(xs, N, heads * channels + 2 * heads, "xs")
+    _dense(ae, rowmask, bias, keep)
+    _need(ae is None or ae.numel() == num_graphs * n * n * heads, "ae shape")
+    _need(bias is None or bias.numel() == _oc(heads, channels, concat), "bias shape")
+    _need(keep is None or keep.numel() == num_graphs * heads * 1024, "keep shape")
+    _need(rowmask is None or rowmask.numel() >= N, "rowmask shape")
     y = torch.empty(N, _oc(heads, channels, concat), device=xs.device)
     ps = torch.empty(num_graphs, heads, 32, 32, device=xs.device)
     _lib.check(lib.sv2n_gat_attn_fwd(xs.data_ptr(), xs.stride(0), _p(ae), _p(rowmask), _p(bias),
@@ -297,6 +324,12 @@ def _gat_attn_tiled_fwd(xs, ae, num_edges, eid, rowmask, bias, keep, keep_scale,
     lib = _lib.load()
     _f32(xs, ae, bias)
     N = num_graphs * n
+    _rows(xs, N, heads * channels + 2 * heads, "xs")
+    _dense(ae, eid, rowmask, bias, keep)
+    _need(ae is None or ae.numel() == heads * num_edges, "ae shape")
+    _need(eid is None or eid.numel() == N * n, "eid shape")
+    _need(bias is None or bias.numel() == _oc(heads, channels, concat), "bias shape")
+    _need(keep is None or keep.numel() == num_graphs * heads * n * n, "keep shape")
     y = torch.empty(N, _oc(heads, channels, concat), device=xs.device)
     ws_n = lib.sv2n_gat_attn_tiled_workspace(num_graphs, n, heads, channels, int(concat))
     ws = torch.empty(max(ws_n, 1), device=xs.device)
@@ -318,6 +351,12 @@ def _gat_attn_bwd(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_grap
                   channels, concat, act, slope):
     lib = _lib.load()
     _f32(dy, y, xs, psave)
+    N, OC = num_graphs * n, _oc(heads, channels, concat)
+    _rows(xs, N, heads * channels + 2 * heads, "xs")
+    _dense(dy, y, psave, keep, rowmask)
+    _need(dy.numel() == N * OC and y.numel() == N * OC, "dy / y shape")
+    _need(psave.numel() == num_graphs * heads * 1024, "psave shape")
+    _need(keep is None or keep.numel() == num_graphs * heads * 1024, "keep shape")
     dev = xs.device
     dxs = torch.empty_like(xs)
     dae = torch.empty(num_graphs, n, n, heads, device=dev) if with_ae else \
@@ -344,6 +383,12 @@ def _gat_attn_tiled_bwd(dy, y, xs, ae, num_edges, eid, keep, keep_scale, rowmask
                         heads, channels, concat, act, slope):
     lib = _lib.load()
     _f32(dy, y, xs, ae)
+    N, OC = num_graphs * n, _oc(heads, channels, concat)
+    _rows(xs, N, heads * channels + 2 * heads, "xs")
+    _dense(dy, y, ae, eid, keep, rowmask)
+    _need(dy.numel() == N * OC and y.numel() == N * OC, "dy / y shape")
+    _need(ae is None or ae.numel() == heads * num_edges, "ae shape")
+    _need(eid is None or eid.numel() == N * n, "eid shape")
     dev = xs.device
     dxs = torch.empty_like(xs)
     dae = torch.empty(heads, num_edges, device=dev) if (ae is not None and num_edges > 0) else \
@@ -372,8 +417,16 @@ def _gat_wgrad(x, dxs, W, att_src, att_dst, dbias_partial, heads, channels, bf16
                g_att_dst, g_bias):
     lib = _lib.load()
     _f32(x, dxs, W, att_src, att_dst, dbias_partial, gW, g_att_src, g_att_dst, g_bias)
+    _dense(dxs, W, att_src, att_dst, dbias_partial, gW, g_att_src, g_att_dst, g_bias)
     N, ldx = dxs.shape
     F = W.shape[1]
+    HC = heads * channels
+    _need(W.shape[0] == HC and ldx >= HC + 2 * heads, "W / dxs shapes")
+    if x is not None:
+        _rows(x, N, F, "x")
+    _need(gW is None or gW.shape == W.shape, "gW shape")
+    _need(g_att_src is None or g_att_src.numel() == HC, "g_att_src shape")
+    _need(g_att_dst is None or g_att_dst.numel() == HC, "g_att_dst shape")
     weights = gW is not None or g_att_src is not None or g_att_dst is not None
     use_bf16 = bf16 and weights and x.stride(0) % 4 == 0 and F >= 4 and \
         x.data_ptr() % 16 == 0 and dxs.data_ptr() % 16 == 0
@@ -402,8 +455,10 @@ def _gat_wgrad_fake(x, dxs, W, att_src, att_dst, dbias_partial, heads, channels,
 def _head_fwd(x, weight, bias):
     lib = _lib.load()
     _f32(x, weight, bias)
+    _dense(x, weight, bias)
     N, C = x.shape
     O = weight.shape[0]
+    _need(weight.shape[1] == C and (bias is None or bias.numel() == O), "head shapes")
     out = torch.empty(N, O, device=x.device)
     _lib.check(lib.sv2n_head_fwd(x.data_ptr(), N, C, weight.data_ptr(), _p(bias), O,
                                  out.data_ptr(), _st(x)), "sv2n_head_fwd")
@@ -418,9 +473,11 @@ def _head_fwd_fake(x, weight, bias):
 @_impl("head_bwd")
 def _head_bwd(x, weight, dout, g_weight, g_bias):
     lib = _lib.load()
+    _dense(x, weight, g_weight, g_bias)
     N, C = x.shape
     O = weight.shape[0]
     dout = dout.contiguous()
+    _need(dout.numel() == N * O, "dout shape")
     dx = torch.empty_like(x)
     ws_n = lib.sv2n_head_bwd_workspace(N, C, O)
     ws = _lib.persistent_zeros("head", ws_n, x.device)
@@ -439,6 +496,7 @@ def _head_bwd_fake(x, weight, dout, g_weight, g_bias):
 def _head_mse_fwd(x, weight, bias, target):
     lib = _lib.load()
     _f32(x, weight, bias, target)
+    _dense(x, weight, bias)
     N, C = x.shape
     O = weight.shape[0]
     target = target.reshape(-1).contiguous()
@@ -461,8 +519,10 @@ def _head_mse_fwd_fake(x, weight, bias, target):
 @_impl("head_mse_bwd")
 def _head_mse_bwd(x, weight, diff, grad_loss, g_weight, g_bias):
     lib = _lib.load()
+    _dense(x, weight, diff, g_weight, g_bias)
     N, C = x.shape
     O = weight.shape[0]
+    _need(diff.numel() == N * O, "diff shape")
     gl = grad_loss.reshape(()).contiguous().to(torch.float32)
     dx = torch.empty_like(x)
     ws_n = lib.sv2n_head_mse_workspace(N, C, O)
@@ -485,6 +545,10 @@ def _head_mse_bwd_fake(x, weight, diff, grad_loss, g_weight, g_bias):
 def _adam_step(param, grad, exp_avg, exp_avg_sq, step, ticket, lr, beta1, beta2, eps,
                weight_decay):
     lib = _lib.load()
+    _f32(param, grad, exp_avg, exp_avg_sq)
+    _dense(param, grad, exp_avg, exp_avg_sq, step, ticket)
+    _need(grad.numel() == param.numel() == exp_avg.numel() == exp_avg_sq.numel(), "adam sizes")
+    _need(ticket.numel() >= 288 and ticket.dtype == torch.int32, "adam ticket words")
     _lib.check(lib.sv2n_adam_f32_step(param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(),
                                       exp_avg_sq.data_ptr(), param.numel(), step.data_ptr(),
                                       ticket.data_ptr(), lr, beta1, beta2, eps, weight_decay,
@@ -503,6 +567,11 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
     _f32(vol, volvol, x, edge_attr, y)
     _need(vol.is_contiguous() and volvol.is_contiguous(), "series must be contiguous")
     _need(starts.dtype == torch.long, "starts must be int64")
+    _dense(starts, canon, x, edge_attr, y)
+    n, B = vol.shape[1], starts.numel()
+    _need(x.numel() == B * n * n * seq_length and
+          edge_attr.numel() == B * n * (n - 1) * 3 * seq_length and
+          y.numel() == B * n * future_steps, "window output buffer sizes")
     _lib.check(lib.sv2n_window_gather(vol.data_ptr(), volvol.data_ptr(), vol.shape[1],
                                       starts.data_ptr(), starts.numel(), seq_length, future_steps,
                                       canon.data_ptr(), x.data_ptr(), edge_attr.data_ptr(),

