@@ -164,10 +164,11 @@ def check_pending(block: bool = False) -> None:
     keep = []
     err = None
     for host, ev, what in _pending:
-        if not block and not ev.query():
+        if block:
+            ev.synchronize()
+        elif not ev.query():  # still in flight: look again next time
             keep.append((host, ev, what))
             continue
-        ev.synchronize()
         if int(host[0]) != 0 and err is None:
             err = UnsupportedLayout(
                 f"{what}: {int(host[0])} edge(s) outside the node range, across n-node blocks "
