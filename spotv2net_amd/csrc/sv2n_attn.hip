@@ -89,6 +89,15 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
   const int OC = CONCAT ? HC : C;
   const int nhb = (H + hpc - 1) / hpc, ncb = (C + cw - 1) / cw;
   const int nchunk = CONCAT ? nhb * ncb : ncb;
+  // chunk group: this workgroup takes chunks cg, cg + ncg, ... of graph g
+  // (gridDim.y > 1 spreads one graph over several workgroups); with exactly
+  // one head-aligned chunk per workgroup (concat) its softmax covers only
+  // that chunk's heads [hs, hs + hn)
+  const int cg = blockIdx.y, ncg = gridDim.y;
+  const bool own_heads = CONCAT && ncg == nchunk && cw == C && ncg > 1;
+  const int hs = own_heads ? (cg / ncb) * hpc : 0;
+  const int hn = own_heads ? min(hpc, H - hs) : H;
+  const bool write_psave = own_heads || cg == 0;
   const bool row_vec = ((ldx & 3) == 0) && ((((uintptr_t)xs) & 15) == 0);
   const bool contig = cw == C;  // a chunk = contiguous columns [h0*C, (h0+nh)*C) of a row
 
@@ -204,12 +213,12 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
   const float as_v = arow[0], ad_v = arow[aok ? H : 0];
   // softmax inputs from global: each lane-row's source bitmask and keep bytes
   // (clamped, unconditional loads)
-  const int nlr = 64 * H;  // lane-rows: two lanes per (head, target) row
+  const int nlr = 64 * hn;  // lane-rows: two lanes per (head, target) row
   uint32_t rbits[RPT], kw[RPT][4];
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
     const int rr = t + ATT_THREADS * q;
-    const int r = rr >> 1, i = r & 31, h = r >> 5;
+    const int r = rr >> 1, i = r & 31, h = hs + (r >> 5);
     const bool ok = rr < nlr && i < n;
     const uint32_t* rm = rowmask ? rowmask : reinterpret_cast<const uint32_t*>(xs);
     const uint32_t w = rm[rowmask && ok ? row0 + i : 0];
@@ -220,7 +229,7 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
     for (int w4 = 0; w4 < 4; ++w4) kw[q][w4] = *reinterpret_cast<const uint32_t*>(kp + kb + 4 * w4);
   }
 
-  Chunk cur = chunk_of(0);  // issued last: only the aggregation waits for it
+  Chunk cur = chunk_of(cg);  // issued last: only the aggregation waits for it
   load_chunk(cur);
 
   if (ae) {
@@ -263,7 +272,7 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
     if (q * ATT_THREADS >= nlr) break;
     if (rr >= nlr) continue;  // wave-uniform: nlr is a multiple of 64
     const int r = rr >> 1, part = rr & 1;
-    const int h = r >> 5, i = r & 31;
+    const int h = hs + (r >> 5), i = r & 31;
     const int jb = 16 * part;
     const bool rv = i < n;
     const uint32_t bits = rbits[q];
@@ -330,8 +339,8 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
     const int rr = t + ATT_THREADS * q;
-    const int r = rr >> 1, h = r >> 5, i = r & 31;
-    if (rr < nlr && i < n) {
+    const int r = rr >> 1, h = hs + (r >> 5), i = r & 31;
+    if (write_psave && rr < nlr && i < n) {
       float4* dst = reinterpret_cast<float4*>(psave + (((int64_t)g * H + h) * 32 + i) * 32 + 16 * (rr & 1));
 #pragma unroll
       for (int c4 = 0; c4 < 4; ++c4) dst[c4] = psv[q][c4];
@@ -340,12 +349,12 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
 
   // ---- aggregation per chunk: out[i][c] = Σ_j P[h][i][j] · xs[j][h*C + c] ----
   const float invH = 1.f / (float)H;
-  for (int ch = 0; ch < nchunk; ++ch) {
+  for (int ch = cg; ch < nchunk; ch += ncg) {
     const Chunk k = cur;
     const int XS = x_stride(k.span);
     __syncthreads();
-    if (ch + 1 < nchunk) {
-      cur = chunk_of(ch + 1);
+    if (ch + ncg < nchunk) {
+      cur = chunk_of(ch + ncg);
       load_chunk(cur);
     }
     const int ntc = (k.cwv + 31) >> 5;  // 32-column tiles per head
@@ -379,7 +388,7 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
         }
       }
     }
-    if (ch + 1 < nchunk) {
+    if (ch + ncg < nchunk) {
       __syncthreads();  // chunk consumed before the next one overwrites sX / sB
       store_chunk(cur, x_stride(cur.span));
     }
@@ -840,16 +849,45 @@ static void raise_lds(K kernel, size_t bytes) {
                               160 * 1024);
 }
 
+// Workgroups per graph for the forward: a batch of fewer than ~4 graphs per CU
+// leaves CUs waiting on single-workgroup memory round trips, so a graph is
+// spread over ncg workgroups — head groups (concat; each computes only its
+// heads' softmax) or 32-column windows (head mean; each recomputes the small
+// softmax) — up to ATT_TARGET_WG workgroups in total.
+constexpr int64_t ATT_TARGET_WG = 1024;
+struct FwdSplit { FwdChunking ck; int ncg; };
+static inline FwdSplit fwd_split(int64_t B, int H, int C, bool concat) {
+  FwdChunking ck = fwd_chunking(H, C, concat);
+  const int ncb = (C + ck.cw - 1) / ck.cw;
+  int nchunk = concat ? ((H + ck.hpc - 1) / ck.hpc) * ncb : ncb;
+  const int want = (int)std::min<int64_t>(8, (ATT_TARGET_WG + B - 1) / B);
+  if (want <= 1) return {ck, 1};
+  if (concat) {
+    if (ck.cw == C) {  // head-aligned chunks: one per workgroup, hpc heads each
+      const int hpc = std::max(1, std::min(ck.hpc, (H + want - 1) / want));
+      const int nc = (H + hpc - 1) / hpc;
+      return {{hpc, C}, nc};
+    }
+    return {ck, std::min(want, nchunk)};
+  }
+  if (nchunk == 1 && C > 32) {  // one chunk: split its columns into 32-wide windows
+    const int cw = std::max(32, ((C + want - 1) / want + 31) & ~31);
+    ck = {H, cw};
+    nchunk = (C + cw - 1) / cw;
+  }
+  return {ck, std::min(want, nchunk)};
+}
+
 template <int ACT, bool CONCAT>
 static void launch_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
                        const uint32_t* rowmask, const float* bias, const uint8_t* keep,
                        float keep_scale, float* y, float* psave, int n, int H, int C, float slope) {
-  const FwdChunking ck = fwd_chunking(H, C, CONCAT);
-  const size_t lds = fwd_lds(H, ck);
+  const FwdSplit sp = fwd_split(B, H, C, CONCAT);
+  const size_t lds = fwd_lds(H, sp.ck);
   raise_lds(k_attn_fwd<ACT, CONCAT>, lds);
-  hipLaunchKernelGGL((k_attn_fwd<ACT, CONCAT>), dim3((unsigned)B), dim3(ATT_THREADS), lds, st, xs,
-                     ldx, ae, rowmask, bias, keep, keep_scale, y, psave, n, H, C, slope, ck.hpc,
-                     ck.cw);
+  hipLaunchKernelGGL((k_attn_fwd<ACT, CONCAT>), dim3((unsigned)B, (unsigned)sp.ncg),
+                     dim3(ATT_THREADS), lds, st, xs, ldx, ae, rowmask, bias, keep, keep_scale, y,
+                     psave, n, H, C, slope, sp.ck.hpc, sp.ck.cw);
 }
 
 template <int ACT, bool CONCAT>
