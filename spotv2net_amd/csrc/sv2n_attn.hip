@@ -21,6 +21,7 @@
 // leaky_relu's negative side for the backward.
 #include "sv2n_common.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace sv2n {
 
@@ -849,32 +850,27 @@ static void raise_lds(K kernel, size_t bytes) {
                               160 * 1024);
 }
 
-// Workgroups per graph for the forward: a batch of fewer than ~4 graphs per CU
-// leaves CUs waiting on single-workgroup memory round trips, so a graph is
-// spread over ncg workgroups — head groups (concat; each computes only its
-// heads' softmax) or 32-column windows (head mean; each recomputes the small
-// softmax) — up to ATT_TARGET_WG workgroups in total.
-constexpr int64_t ATT_TARGET_WG = 1024;
+// Workgroups per graph for the forward.  A graph whose xs span needs several
+// sequential chunks (C3: 6 heads x 500 columns, 8 chunks) is spread over up to
+// ncg workgroups (tools/attn_sweep.py, MI355X: C3 69 -> 61 us).  Single-chunk
+// graphs (C2) stay one workgroup each: splitting them (head groups, column
+// windows) only repeats the per-graph softmax chain (C2 L0 24 -> 32 us,
+// L1 18 -> 39 us).
+static int64_t att_target_wg() {
+  static int64_t v = [] {
+    const char* e = getenv("SV2N_ATT_TARGET_WG");  // tuning override (0: no split)
+    return e ? (int64_t)atoll(e) : (int64_t)1024;
+  }();
+  return v;
+}
 struct FwdSplit { FwdChunking ck; int ncg; };
 static inline FwdSplit fwd_split(int64_t B, int H, int C, bool concat) {
   FwdChunking ck = fwd_chunking(H, C, concat);
   const int ncb = (C + ck.cw - 1) / ck.cw;
   int nchunk = concat ? ((H + ck.hpc - 1) / ck.hpc) * ncb : ncb;
-  const int want = (int)std::min<int64_t>(8, (ATT_TARGET_WG + B - 1) / B);
-  if (want <= 1) return {ck, 1};
-  if (concat) {
-    if (ck.cw == C) {  // head-aligned chunks: one per workgroup, hpc heads each
-      const int hpc = std::max(1, std::min(ck.hpc, (H + want - 1) / want));
-      const int nc = (H + hpc - 1) / hpc;
-      return {{hpc, C}, nc};
-    }
-    return {ck, std::min(want, nchunk)};
-  }
-  if (nchunk == 1 && C > 32) {  // one chunk: split its columns into 32-wide windows
-    const int cw = std::max(32, ((C + want - 1) / want + 31) & ~31);
-    ck = {H, cw};
-    nchunk = (C + cw - 1) / cw;
-  }
+  const int64_t target = att_target_wg();
+  const int want = target <= 0 ? 1 : (int)std::min<int64_t>(8, (target + B - 1) / B);
+  if (want <= 1 || nchunk == 1) return {ck, 1};
   return {ck, std::min(want, nchunk)};
 }
 
