@@ -447,6 +447,13 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
   const int HC = H * C;
   const int OC = CONCAT ? HC : C;
   const float invH = 1.f / (float)H;
+  // head groups: with gridDim.y > 1 this workgroup owns heads [hs, hs + hpc)
+  // (the chunks of head block blockIdx.y): every quantity of the backward is
+  // then complete inside it (G_h sums over that head's own columns only).
+  // Shared per graph (head mean: dz and its bias sums) is written by group 0.
+  const int hgi = blockIdx.y, nhg = gridDim.y;
+  const int hs = nhg > 1 ? hgi * hpc : 0, hn = nhg > 1 ? min(hpc, H - hs) : H;
+  const bool lead = hgi == 0;
   float* sP = smem;
   uint32_t* sKB = reinterpret_cast<uint32_t*>(sP + H * 32 * TS);
   uint32_t* sRB = sKB + H * 32;
@@ -467,7 +474,8 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
 
   // ---- chunk geometry ----
   const int nhb = (H + hpc - 1) / hpc, ncb = (C + cw - 1) / cw;
-  const int nchunk = nhb * ncb;
+  const int ch_begin = nhg > 1 ? hgi * ncb : 0;
+  const int nchunk = nhg > 1 ? ch_begin + ncb : nhb * ncb;  // end of this group's chunks
   const bool contig = cw == C;
   struct Chunk { int h0, nh, c0, cwv, span, zw; bool vec; };
   auto chunk_of = [&](int ch) {
@@ -622,7 +630,7 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
   const u32x4 kw0 = bld4_u32(rkp, krow ? t * 32 : OOB);
   const u32x4 kw1 = bld4_u32(rkp, krow ? t * 32 + 16 : OOB);
   const uint32_t rmw = bld_u32(rrm, t < n ? t * 4 : OOB);
-  Chunk cur = chunk_of(0);
+  Chunk cur = chunk_of(ch_begin);
   load_chunk(cur);
 
 #pragma unroll
@@ -653,7 +661,7 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
   floatx16 G0, G1;  // G_h for heads wave and wave + 4
 #pragma unroll
   for (int r = 0; r < 16; ++r) { G0[r] = 0.f; G1[r] = 0.f; }
-  for (int ch = 0; ch < nchunk; ++ch) {
+  for (int ch = ch_begin; ch < nchunk; ++ch) {
     const Chunk k = cur;
     const int XS = k.span | 1, ZS = k.zw | 1;
     float* sX = sArea;
@@ -672,7 +680,7 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
       for (int j = 0; j < 32; ++j) sb += sZ[j * ZS + L];
       const int seg = L / cw, cc = L - seg * cw;
       const int oc = (CONCAT ? (k.h0 + seg) * C : 0) + k.c0 + cc;
-      bst(rdb, cc < k.cwv ? oc * 4 : OOB, sb);
+      bst(rdb, (cc < k.cwv && (CONCAT || lead)) ? oc * 4 : OOB, sb);
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -724,7 +732,7 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
     const int h = wave + 4 * s2;
-    if (h >= H) continue;  // wave-uniform
+    if (h >= H || h < hs || h >= hs + hn) continue;  // wave-uniform
     const floatx16 G = s2 ? G1 : G0;
     const int i = l32;
     const bool iv = i < n;
@@ -780,7 +788,7 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
       const bool e = j != i && ((sRB[i] >> j) & 1u);
       return e ? sDL[(h * 32 + i) * TS + j] + sSh[h * 32 + i] : 0.f;
     };
-    if ((nae & 3) == 0 && ((((uintptr_t)dae) & 15) == 0)) {
+    if (nhg == 1 && (nae & 3) == 0 && ((((uintptr_t)dae) & 15) == 0)) {
       const int kb = 4 * t;
       int h = kb % H, ij = kb / H;
       int i = ij / n, j = ij - i * n;
@@ -806,7 +814,8 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
       for (int kk = t; kk < nae; kk += ATT_THREADS) {
         const int h = kk % H, ij = kk / H;
         const int i = ij / n, j = ij - i * n;
-        bst(rdae, kk * 4, dae_val(i, j, h));
+        const bool own = h >= hs && h < hs + hn;
+        bst(rdae, own ? kk * 4 : OOB, own ? dae_val(i, j, h) : 0.f);
       }
     }
   }
@@ -815,6 +824,8 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
   for (int e = t; e < n * ntail; e += ATT_THREADS) {
     const int j = e / ntail, c2 = e - j * ntail;
     float v = 0.f;
+    const int hc = c2 < H ? c2 : c2 - H;  // the head of a d a_src / d a_dst column
+    const bool own = c2 < 2 * H ? (hc >= hs && hc < hs + hn) : lead;
     if (c2 < H) {
       const float* col = sDL + c2 * 32 * TS + j;
 #pragma unroll 8
@@ -822,7 +833,7 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
     } else if (c2 < 2 * H) {
       v = sDad[(c2 - H) * 32 + j];
     }
-    bst(rdx, (j * ldx + HC + c2) * 4, v);
+    bst(rdx, own ? (j * ldx + HC + c2) * 4 : OOB, v);
   }
 }
 
@@ -886,17 +897,44 @@ static void launch_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, cons
                      psave, n, H, C, slope, sp.ck.hpc, sp.ck.cw);
 }
 
+// Head groups for the backward: a graph whose backward walks many sequential
+// chunks (C3: 14 column windows of all 6 heads) is split into head groups, each
+// workgroup owning hpc heads and walking only their columns — no cross-
+// workgroup reduction (G_h of a head sums over that head's columns alone), at
+// the price of re-reading dy / y per group for a head mean.
+static int att_bwd_hpc() {
+  static int v = [] {
+    const char* e = getenv("SV2N_ATT_BWD_HPC");  // tuning override: heads per group
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+struct BwdSplit { BwdChunking ck; int nhg; };
+static inline BwdSplit bwd_split(int64_t B, int H, int C, bool concat) {
+  const BwdChunking ck = bwd_chunking(H, C, concat);
+  const int nchunk = ((H + ck.hpc - 1) / ck.hpc) * ((C + ck.cw - 1) / ck.cw);
+  const int hpc = att_bwd_hpc();
+  if (nchunk < 4 || hpc <= 0 || hpc >= H || B * ((H + hpc - 1) / hpc) > 4096 ||
+      (C & 3) != 0)
+    return {ck, 1};
+  // head-aligned chunks of hpc heads, balanced column windows within XB
+  const int cwmax = (XB / hpc) & ~3;
+  const int nch = (C + cwmax - 1) / cwmax;
+  const int cw = (((C + nch - 1) / nch) + 3) & ~3;
+  return {{hpc, cw}, (H + hpc - 1) / hpc};
+}
+
 template <int ACT, bool CONCAT>
 static void launch_bwd(int64_t B, hipStream_t st, const float* dy, const float* y,
                        const float* xs, int ldx, const float* psave, const uint8_t* keep,
                        float keep_scale, const uint32_t* rowmask, float* dxs, float* dae,
                        float* dbias, int n, int H, int C, float slope) {
-  const BwdChunking ck = bwd_chunking(H, C, CONCAT);
-  const size_t lds = bwd_lds(H, ck, CONCAT);
+  const BwdSplit sp = bwd_split(B, H, C, CONCAT);
+  const size_t lds = bwd_lds(H, sp.ck, CONCAT);
   raise_lds(k_attn_bwd<ACT, CONCAT>, lds);
-  hipLaunchKernelGGL((k_attn_bwd<ACT, CONCAT>), dim3((unsigned)B), dim3(ATT_THREADS), lds, st, dy,
-                     y, xs, ldx, psave, keep, keep_scale, rowmask, dxs, dae, dbias, n, H, C, slope,
-                     ck.hpc, ck.cw);
+  hipLaunchKernelGGL((k_attn_bwd<ACT, CONCAT>), dim3((unsigned)B, (unsigned)sp.nhg),
+                     dim3(ATT_THREADS), lds, st, dy, y, xs, ldx, psave, keep, keep_scale, rowmask,
+                     dxs, dae, dbias, n, H, C, slope, sp.ck.hpc, sp.ck.cw);
 }
 
 static int check_attn_args(int64_t B, int n, int H, int C, int ldx, int act) {
