@@ -902,18 +902,20 @@ static void launch_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, cons
 // workgroup owning hpc heads and walking only their columns — no cross-
 // workgroup reduction (G_h of a head sums over that head's columns alone), at
 // the price of re-reading dy / y per group for a head mean.
-static int att_bwd_hpc() {
+static int att_bwd_hpc(int H) {
   static int v = [] {
     const char* e = getenv("SV2N_ATT_BWD_HPC");  // tuning override: heads per group
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : -1;
   }();
-  return v;
+  // default: two head groups (tools/attn_sweep.py, C3 shapes on MI355X: bwd
+  // 190 us unsplit, 150 / 103 / 95 us at 1 / 2 / 3 heads per group)
+  return v >= 0 ? v : (H + 1) / 2;
 }
 struct BwdSplit { BwdChunking ck; int nhg; };
 static inline BwdSplit bwd_split(int64_t B, int H, int C, bool concat) {
   const BwdChunking ck = bwd_chunking(H, C, concat);
   const int nchunk = ((H + ck.hpc - 1) / ck.hpc) * ((C + ck.cw - 1) / ck.cw);
-  const int hpc = att_bwd_hpc();
+  const int hpc = att_bwd_hpc(H);
   if (nchunk < 4 || hpc <= 0 || hpc >= H || B * ((H + hpc - 1) / hpc) > 4096 ||
       (C & 3) != 0)
     return {ck, 1};
