@@ -259,7 +259,8 @@ extern "C" int sv2n_gemm_f32_slabs(int a_kmajor, int b_kmajor, const float* A, i
   const bool avec = ((uintptr_t)A % 16 == 0) && (lda % 4 == 0);
   const bool bvec = ((uintptr_t)B % 16 == 0) && (ldb % 4 == 0);
 #define SV2N_SLABS(NT, AK, BK)                                                                    \
-  launch_gemm_slabs<8, 1, NT, 16, AK, BK, 2>(p.splitk, p.kslice, stream, A, lda, B, ldb, M, N, K, \
+  launch_gemm_slabs<8, 1, NT, 16, AK, BK, 2, 0, true>(p.splitk, p.kslice, stream, A, lda, B, ldb, \
+                                                    M, N, K, \
                                              avec, bvec, slabs)
   if (p.nt == 13) {
     if (a_kmajor && b_kmajor) SV2N_SLABS(13, true, true);
@@ -401,12 +402,15 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
     const bool avec = ((uintptr_t)x % 16 == 0) && (ld_x % 4 == 0);
     const bool bvec = ((uintptr_t)dxs % 16 == 0) && (ldx % 4 == 0);
     float* out = p.splitk > 1 ? slabs : T;
+    // K slices grouped per XCD (sv2n_gemm_kernel.h, XR): every tile of a slice
+    // shares that XCD's L2 (C2 L0: HBM fetch 374 -> 122 MB, 178 -> 174 us;
+    // tools/gemm_tt_tune.hip)
     if (p.nt == 13)
-      launch_gemm_slabs<8, 1, 13, 16, false, false, 2>(p.splitk, p.kslice, stream, x, ld_x, dxs,
-                                                       ldx, F, ldx, num_nodes, avec, bvec, out);
+      launch_gemm_slabs<8, 1, 13, 16, false, false, 2, 0, true>(
+          p.splitk, p.kslice, stream, x, ld_x, dxs, ldx, F, ldx, num_nodes, avec, bvec, out);
     else
-      launch_gemm_slabs<8, 1, 8, 16, false, false, 2>(p.splitk, p.kslice, stream, x, ld_x, dxs,
-                                                      ldx, F, ldx, num_nodes, avec, bvec, out);
+      launch_gemm_slabs<8, 1, 8, 16, false, false, 2, 0, true>(
+          p.splitk, p.kslice, stream, x, ld_x, dxs, ldx, F, ldx, num_nodes, avec, bvec, out);
     if (p.splitk > 1) {
       const int64_t tot = (int64_t)F * ldx;
       hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,

@@ -142,21 +142,40 @@ struct GemmCfg {
   static constexpr int LDS_BYTES = 2 * BUF * 4;
 };
 
+// XR (XCD-grouped K slices, split-K only): workgroups are dealt round-robin
+// over the 8 XCDs, so with the plain (x, y, z) order the output tiles of one K
+// slice — which all read that slice's A and B panels — land on all eight L2s
+// and every panel is fetched up to 8 times.  With XR the linear block id
+// b = xcd + 8*slot is mapped to K slice z = xcd + 8*(slot / tiles) and tile
+// slot % tiles: every tile of a slice runs on ONE XCD and the panels are read
+// into its L2 once.  The grid's z extent is the slice count rounded up to 8;
+// blocks with z >= nz exit at once.
 template <int NW, int MT, int NT, int KB, bool AK, bool BK, int PF, int ABL = 0, bool AV = true,
-          bool BV = true>
+          bool BV = true, bool XR = false>
 __global__ __launch_bounds__(64 * NW) void k_gemm_f32(
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
     float* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int64_t kslice,
-    float* __restrict__ part) {
+    float* __restrict__ part, int nz = 0) {
   using Cfg = GemmCfg<NW, MT, NT, KB, AK, BK, PF>;
   using TA = typename Cfg::TA;
   using TB = typename Cfg::TB;
   constexpr int AOFF = Cfg::AOFF, BUF = Cfg::BUF;
   __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
 
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if constexpr (XR) {
+    const int tiles = gridDim.x * gridDim.y;
+    const int id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = id & 7, slot = id >> 3;
+    bz = xcd + 8 * (slot / tiles);
+    const int tile = slot - (slot / tiles) * tiles;
+    by = tile / gridDim.x;
+    bx = tile - by * gridDim.x;
+    if (bz >= nz) return;
+  }
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * Cfg::BM, n0 = (int64_t)blockIdx.y * Cfg::BN;
-  const int64_t kb = (int64_t)blockIdx.z * kslice;
+  const int64_t m0 = (int64_t)bx * Cfg::BM, n0 = (int64_t)by * Cfg::BN;
+  const int64_t kb = (int64_t)bz * kslice;
   const int64_t ke = min(K, kb + kslice);
   const int nk = (int)((ke - kb + KB - 1) / KB);
 
@@ -256,7 +275,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_f32(
     }
   }
 
-  float* out = part ? part + (int64_t)blockIdx.z * M * N : C;
+  float* out = part ? part + (int64_t)bz * M * N : C;
   const int64_t ldo = part ? N : ldc;
 #pragma unroll
   for (int a = 0; a < MT; ++a) {
@@ -315,22 +334,31 @@ inline void launch_gemm_cfg(int splitk, int64_t kslice, hipStream_t st, const fl
 
 // As launch_gemm_cfg, but the K slices stay as slabs part[z][M][N] for a
 // consumer that reduces them itself (splitk == 1 writes slab 0).
-template <int NW, int MT, int NT, int KB, bool AK, bool BK, int PF, int ABL = 0>
+template <int NW, int MT, int NT, int KB, bool AK, bool BK, int PF, int ABL = 0, bool XR = false>
 inline void launch_gemm_slabs(int splitk, int64_t kslice, hipStream_t st, const float* A,
                               int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N,
                               int64_t K, bool avec, bool bvec, float* part) {
   using Cfg = GemmCfg<NW, MT, NT, KB, AK, BK, PF>;
+  const bool xr = XR && splitk > 1;
   dim3 grid((unsigned)((M + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN),
-            (unsigned)splitk);
+            (unsigned)(xr ? (splitk + 7) / 8 * 8 : splitk));
   const bool av = avec && ((AK ? K : M) % 4 == 0);
   const bool bv = bvec && ((BK ? K : N) % 4 == 0);
   float* pp = splitk > 1 ? part : nullptr;
-  if (av && bv)
-    hipLaunchKernelGGL((k_gemm_f32<NW, MT, NT, KB, AK, BK, PF, ABL, true, true>), grid,
-                       dim3(Cfg::THREADS), 0, st, A, lda, B, ldb, part, N, M, N, K, kslice, pp);
-  else
+  if (av && bv) {
+    if (xr)
+      hipLaunchKernelGGL((k_gemm_f32<NW, MT, NT, KB, AK, BK, PF, ABL, true, true, true>), grid,
+                         dim3(Cfg::THREADS), 0, st, A, lda, B, ldb, part, N, M, N, K, kslice, pp,
+                         splitk);
+    else
+      hipLaunchKernelGGL((k_gemm_f32<NW, MT, NT, KB, AK, BK, PF, ABL, true, true>), grid,
+                         dim3(Cfg::THREADS), 0, st, A, lda, B, ldb, part, N, M, N, K, kslice, pp,
+                         splitk);
+  } else {
     hipLaunchKernelGGL((k_gemm_f32<NW, MT, NT, KB, AK, BK, PF, ABL, false, false>), grid,
-                       dim3(Cfg::THREADS), 0, st, A, lda, B, ldb, part, N, M, N, K, kslice, pp);
+                       dim3(Cfg::THREADS), 0, st, A, lda, B, ldb, part, N, M, N, K, kslice, pp,
+                       splitk);
+  }
 }
 
 }  // namespace sv2n

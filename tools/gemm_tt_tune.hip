@@ -112,8 +112,7 @@ void run_tt(const Shape& sh, int splitk, hipStream_t st, const float* A, const f
 }
 
 int main() {
-  std::vector<Shape> shapes = {{"C3 dWT (bf16)", 1260, 3012, 3840, 2},
-                               {"C2 dWT L0", 1260, 408, 15360, 24},
+  std::vector<Shape> shapes = {{"C2 dWT L0", 1260, 408, 15360, 24},
                                {"C2 dWT L1", 400, 208, 15360, 32}};
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -150,8 +149,24 @@ int main() {
       char tag[64];
       snprintf(tag, sizeof tag, "f32 MFMA slabs split%d", sk);
       report(tag, sh, slabs, sk, us, ref, absr);
+      for (int sk2 : {sk, sk / 2 > 0 ? sk / 2 : 1}) {  // XCD-grouped K slices
+        int64_t ks2 = (K + sk2 - 1) / sk2;
+        ks2 = (ks2 + 15) / 16 * 16;
+        const int s2 = (int)((K + ks2 - 1) / ks2);
+        auto fx = [&]() {
+          if (N > 256)
+            launch_gemm_slabs<8, 1, 13, 16, false, false, 2, 0, true>(s2, ks2, st, A, M, B, N, M,
+                                                                      N, K, true, true, slabs);
+          else
+            launch_gemm_slabs<8, 1, 8, 16, false, false, 2, 0, true>(s2, ks2, st, A, M, B, N, M,
+                                                                     N, K, true, true, slabs);
+        };
+        const double usx = time_us(fx, st);
+        snprintf(tag, sizeof tag, "f32 MFMA slabs XCD-grouped split%d", s2);
+        report(tag, sh, slabs, s2, usx, ref, absr);
+      }
     }
-    for (int sk : {sh.splitk / 2, sh.splitk, sh.splitk * 2}) {
+    for (int sk : {sh.splitk}) {
       if (sk < 1) continue;
       run_tt<128, 128, 1>(sh, sk, st, A, B, slabs, ref, absr);
       run_tt<64, 128, 1>(sh, sk, st, A, B, slabs, ref, absr);
