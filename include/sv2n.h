@@ -195,12 +195,14 @@ typedef struct sv2n_prep_layer {
   const float* att_dst;   /* [H*C] */
   int heads, channels, in_features, ldx;
   float* waug;            /* [ldx][F] */
-  uint16_t* planes;       /* [3][ldx][kp] */
-  uint16_t* planes_t;     /* [3][F][kpt] or NULL */
+  uint16_t* planes;       /* [nplanes][ldx][kp] */
+  uint16_t* planes_t;     /* [nplanes][F][kpt] or NULL */
   const float* W_edge;    /* lin_edge.weight [H*C][edge_dim] or NULL */
   const float* att_edge;  /* [H*C] */
   int edge_dim, hl_pad, col0;
   float* wfold;           /* [edge_dim][hl_pad] */
+  int nplanes;            /* planes written per operand: 3 (split, default when 0)
+                             or 1 (bf16 mode: plane 0 = bf16_rn(w) only) */
 } sv2n_prep_layer;
 int sv2n_gat_prep_fwd_all(const sv2n_prep_layer* layers, int num_layers, hipStream_t stream);
 

@@ -30,7 +30,7 @@ class PrepLayer(ctypes.Structure):
         ("waug", _p), ("planes", _p), ("planes_t", _p),
         ("W_edge", _p), ("att_edge", _p),
         ("edge_dim", _i32), ("hl_pad", _i32), ("col0", _i32),
-        ("wfold", _p),
+        ("wfold", _p), ("nplanes", _i32),
     ]
 
 

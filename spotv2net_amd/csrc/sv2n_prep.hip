@@ -209,6 +209,7 @@ struct PrepAllArgs {
   sv2n_prep_layer l[SV2N_MAX_LAYERS];
   int64_t kp[SV2N_MAX_LAYERS], kpt[SV2N_MAX_LAYERS];
   int px[SV2N_MAX_LAYERS];       // P blocks along columns
+  int rp[SV2N_MAX_LAYERS];       // row parts of the node copy (part 0 also folds)
   int pstart[SV2N_MAX_LAYERS];   // first P block of the layer
   int tf[SV2N_MAX_LAYERS];       // T tiles along f
   int tstart[SV2N_MAX_LAYERS];   // first T block of the layer
@@ -217,12 +218,15 @@ struct PrepAllArgs {
   int L;
 };
 
-__device__ __forceinline__ void put3(uint16_t* planes, int64_t plane, int64_t idx, float v) {
+__device__ __forceinline__ void put3(uint16_t* planes, int64_t plane, int64_t idx, float v,
+                                     int np = 3) {
   unsigned short h0, h1, h2;
   split3(v, h0, h1, h2);
   planes[idx] = h0;
-  planes[plane + idx] = h1;
-  planes[2 * plane + idx] = h2;
+  if (np == 3) {
+    planes[plane + idx] = h1;
+    planes[2 * plane + idx] = h2;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_prep_fwd_all(const PrepAllArgs a) {
@@ -241,25 +245,32 @@ __global__ __launch_bounds__(256) void k_prep_fwd_all(const PrepAllArgs a) {
   if (local < 0) return;
   const sv2n_prep_layer& P = a.l[l];
   const int H = P.heads, C = P.channels, F = P.in_features, ldx = P.ldx, HC = H * C;
+  const int np = P.nplanes == 1 ? 1 : 3;
   if (!tblock) {
     const int64_t kp = a.kp[l], plane = (int64_t)ldx * kp;
     const int lane = t & 63, grp = t >> 6;
-    const int bx = local % a.px[l], y = local / a.px[l];
+    const int nxy = a.px[l] * (P.W_edge ? 2 * H : H);
+    const int part = local / nxy, lxy = local - part * nxy;
+    const int bx = lxy % a.px[l], y = lxy / a.px[l];
     const int col = bx * 64 + lane;
+    // the block's copy rows [cb, ce) of head h; part 0 also folds all C rows
+    const int RPn = a.rp[l], CR = (C + RPn - 1) / RPn;
+    const int cb = part * CR, ce = min(C, cb + CR);
     if (y < H) {
       const int h = y;
       float ss = 0.f, sd = 0.f;
-      // rows c = grp, grp+4, ...: 8 rows' loads issued before any store (W
+      const int cend = part == 0 ? C : ce;
+      // rows c = grp, grp+4, ...: 16 rows' loads issued before any store (W
       // is reached through the argument struct, so the compiler cannot move
       // a load above an earlier store itself)
-      constexpr int RB = 8;
-      for (int c0 = grp; c0 < C; c0 += 4 * RB) {
+      constexpr int RB = 16;
+      for (int c0 = (part == 0 ? 0 : cb) + grp; c0 < cend; c0 += 4 * RB) {
         float w[RB], as[RB], ad[RB];
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
           const int c = c0 + 4 * u;
           const int row = h * C + min(c, C - 1);
-          const bool ok = c < C && col < F;
+          const bool ok = c < cend && col < F;
           w[u] = ok ? P.W[(int64_t)row * F + min(col, F - 1)] : 0.f;
           as[u] = P.att_src[row];
           ad[u] = P.att_dst[row];
@@ -267,15 +278,18 @@ __global__ __launch_bounds__(256) void k_prep_fwd_all(const PrepAllArgs a) {
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
           const int c = c0 + 4 * u;
-          if (c < C) {
+          if (c < cend) {
             const int row = h * C + c;
-            if (col < F) P.waug[(int64_t)row * F + col] = w[u];
-            if (col < kp) put3(P.planes, plane, (int64_t)row * kp + col, w[u]);
+            if (c >= cb && c < ce) {
+              if (col < F) P.waug[(int64_t)row * F + col] = w[u];
+              if (col < kp) put3(P.planes, plane, (int64_t)row * kp + col, w[u], np);
+            }
             ss = fmaf(as[u], w[u], ss);
             sd = fmaf(ad[u], w[u], sd);
           }
         }
       }
+      if (part != 0) return;
       s_red[0][grp][lane] = ss;
       s_red[1][grp][lane] = sd;
       __syncthreads();
@@ -284,16 +298,16 @@ __global__ __launch_bounds__(256) void k_prep_fwd_all(const PrepAllArgs a) {
                         (s_red[grp][2][lane] + s_red[grp][3][lane]);
         const int row = HC + grp * H + h;
         if (col < F) P.waug[(int64_t)row * F + col] = v;
-        put3(P.planes, plane, (int64_t)row * kp + col, v);
+        put3(P.planes, plane, (int64_t)row * kp + col, v, np);
       }
       if (h == 0 && col < kp) {  // zero padding rows
         for (int r = HC + 2 * H + grp; r < ldx; r += 4) {
           if (col < F) P.waug[(int64_t)r * F + col] = 0.f;
-          put3(P.planes, plane, (int64_t)r * kp + col, 0.f);
+          put3(P.planes, plane, (int64_t)r * kp + col, 0.f, np);
         }
       }
     } else {
-      if (!P.W_edge) return;
+      if (!P.W_edge || part != 0) return;
       const int h = y - H, D = P.edge_dim;
       float se = 0.f;
       if (col < D) {
@@ -350,7 +364,7 @@ __global__ __launch_bounds__(256) void k_prep_fwd_all(const PrepAllArgs a) {
     const int o = o0 + ol;
     for (int fi = fg; fi < 32; fi += 8) {
       const int f = f0 + fi;
-      if (f < F && o < kpt) put3(P.planes_t, plane, (int64_t)f * kpt + o, tile[ol][fi]);
+      if (f < F && o < kpt) put3(P.planes_t, plane, (int64_t)f * kpt + o, tile[ol][fi], np);
     }
   }
 }
@@ -445,7 +459,12 @@ extern "C" int sv2n_gat_prep_fwd_all(const sv2n_prep_layer* layers, int num_laye
     const int64_t cols = std::max<int64_t>(a.kp[l], edge ? P.edge_dim : 0);
     a.px[l] = (int)((cols + 63) / 64);
     a.pstart[l] = nb;
-    a.pcount[l] = a.px[l] * (edge ? 2 * P.heads : P.heads);
+    const int nxy = a.px[l] * (edge ? 2 * P.heads : P.heads);
+    // split the row copy so the launch has ~512 blocks (C3: 20 x 6 blocks of
+    // 500 rows each were a serial 42 us); part 0 keeps the fold
+    a.rp[l] = (int)std::max<int64_t>(1, std::min<int64_t>((512 + nxy - 1) / nxy,
+                                                          (P.channels + 63) / 64));
+    a.pcount[l] = nxy * a.rp[l];
     nb += a.pcount[l];
   }
   for (int l = 0; l < num_layers; ++l) {

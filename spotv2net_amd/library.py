@@ -32,7 +32,7 @@ LIB = torch.library.Library("sv2n", "DEF")
 _SCHEMAS = {
     "gat_prep": "(Tensor[] W, Tensor[] att_src, Tensor[] att_dst, Tensor[] W_edge, "
                 "Tensor[] att_edge, int[] heads, int[] channels, int hl_pad, bool[] need_t, "
-                "bool use_edge) -> (Tensor[], Tensor[], Tensor[], Tensor)",
+                "bool use_edge, bool bf16=False) -> (Tensor[], Tensor[], Tensor[], Tensor)",
     "edge_logits": "(Tensor edge_attr, Tensor wfold, Tensor? edge_index, Tensor canon, "
                    "int num_layers, int heads, int num_graphs, int n, bool planes) -> Tensor[]",
     "project": "(Tensor a, Tensor? planes, Tensor w, bool transpose_w, bool bf16) -> Tensor",
@@ -127,12 +127,12 @@ def _ldx(H: int, C: int) -> int:
 # --------------------------------------------------------------------------
 # weight preparation (sv2n_gat_prep_fwd_all)
 # --------------------------------------------------------------------------
-def _prep_shapes(W, heads, channels, need_t, kpad):
+def _prep_shapes(W, heads, channels, need_t, kpad, np=3):
     out = []
     for l, w in enumerate(W):
         F = w.shape[1]
         ldx = _ldx(heads[l], channels[l])
-        out.append(((ldx, F), (3, ldx, kpad(F)), (3, F, kpad(ldx)) if need_t[l] else (0,)))
+        out.append(((ldx, F), (np, ldx, kpad(F)), (np, F, kpad(ldx)) if need_t[l] else (0,)))
     return out
 
 
@@ -141,7 +141,8 @@ def _kpad(K: int) -> int:
 
 
 @_impl("gat_prep")
-def _gat_prep(W, att_src, att_dst, W_edge, att_edge, heads, channels, hl_pad, need_t, use_edge):
+def _gat_prep(W, att_src, att_dst, W_edge, att_edge, heads, channels, hl_pad, need_t, use_edge,
+              bf16=False):
     lib = _lib.load()
     L = len(W)
     _f32(*W, *att_src, *att_dst, *W_edge, *att_edge)
@@ -150,7 +151,8 @@ def _gat_prep(W, att_src, att_dst, W_edge, att_edge, heads, channels, hl_pad, ne
     wf = torch.empty(D, hl_pad, device=dev) if use_edge else torch.empty(0, device=dev)
     arr = (_lib.PrepLayer * L)()
     waugs, planes, planes_t = [], [], []
-    for l, (s_w, s_p, s_t) in enumerate(_prep_shapes(W, heads, channels, need_t, _kpad)):
+    np = 1 if bf16 else 3
+    for l, (s_w, s_p, s_t) in enumerate(_prep_shapes(W, heads, channels, need_t, _kpad, np)):
         waug = torch.empty(s_w, device=dev)
         pl = torch.empty(s_p, device=dev, dtype=torch.int16)
         plt = torch.empty(s_t, device=dev, dtype=torch.int16)
@@ -159,7 +161,7 @@ def _gat_prep(W, att_src, att_dst, W_edge, att_edge, heads, channels, hl_pad, ne
             W[l].shape[1], s_w[0], waug.data_ptr(), pl.data_ptr(), _p(plt),
             W_edge[l].data_ptr() if use_edge else None,
             att_edge[l].data_ptr() if use_edge else None, D, hl_pad, l * heads[0],
-            _p(wf) if use_edge else None)
+            _p(wf) if use_edge else None, np)
         waugs.append(waug)
         planes.append(pl)
         planes_t.append(plt)
@@ -170,10 +172,10 @@ def _gat_prep(W, att_src, att_dst, W_edge, att_edge, heads, channels, hl_pad, ne
 
 @_fake("gat_prep")
 def _gat_prep_fake(W, att_src, att_dst, W_edge, att_edge, heads, channels, hl_pad, need_t,
-                   use_edge):
+                   use_edge, bf16=False):
     D = W_edge[0].shape[1] if use_edge else 0
     w0 = W[0]
-    shp = _prep_shapes(W, heads, channels, need_t, _kpad)
+    shp = _prep_shapes(W, heads, channels, need_t, _kpad, 1 if bf16 else 3)
     return ([w0.new_empty(a) for a, _, _ in shp],
             [w0.new_empty(b, dtype=torch.int16) for _, b, _ in shp],
             [w0.new_empty(c, dtype=torch.int16) for _, _, c in shp],

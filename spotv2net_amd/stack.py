@@ -176,7 +176,7 @@ class _GATStack(torch.autograd.Function):
             [c.lin_src.weight for c in convs], [c.att_src for c in convs],
             [c.att_dst for c in convs], [c.lin_edge.weight for c in convs] if use_edge else [],
             [c.att_edge for c in convs] if use_edge else [], [c.heads for c in convs],
-            [c.out_channels for c in convs], hp, need_t, use_edge)
+            [c.out_channels for c in convs], hp, need_t, use_edge, bf16)
 
         # 2) edge logits of every layer in one pass over edge_attr (sv2n::edge_logits)
         aes = [None] * L
