@@ -114,7 +114,7 @@ def kernel_table(model, data, reps=50):
     sh = stream.cuda_stream
     E, D = data.edge_attr.shape
     wfp, hp = ops.pad_columns(wf)
-    ae = [torch.empty(B, N_NODES, N_NODES, HEADS, device=dev) for _ in range(L)]
+    ae = [torch.empty(E, HEADS, device=dev) for _ in range(L)]  # canonical: edge order
     ptrs = ops._lib.ptr_array([a.data_ptr() for a in ae])
 
     def edge_fwd():
@@ -126,7 +126,7 @@ def kernel_table(model, data, reps=50):
     ps0 = torch.empty(B, HEADS, 32, 32, device=dev)
 
     def attn_fwd():
-        lib.sv2n_gat_attn_fwd(xs0.data_ptr(), xs0.stride(0), ae[0].data_ptr(), None,
+        lib.sv2n_gat_attn_fwd(xs0.data_ptr(), xs0.stride(0), ae[0].data_ptr(), 1, None,
                               conv0.bias.data_ptr(), None, 1.0, y0.data_ptr(), ps0.data_ptr(),
                               B, N_NODES, HEADS, conv0.out_channels, 1, 1, 0.2, sh)
 
@@ -138,7 +138,7 @@ def kernel_table(model, data, reps=50):
     def attn_bwd():
         lib.sv2n_gat_attn_bwd(dy0.data_ptr(), y0.data_ptr(), xs0.data_ptr(), xs0.stride(0),
                               ps0.data_ptr(), None, 1.0, None, dxs0.data_ptr(), dae0.data_ptr(),
-                              dbp.data_ptr(), B, N_NODES, HEADS, conv0.out_channels, 1, 1, 0.2,
+                              1, dbp.data_ptr(), B, N_NODES, HEADS, conv0.out_channels, 1, 1, 0.2,
                               sh)
 
     ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hp)

@@ -43,10 +43,16 @@
  *    utils/dataset.py:212-226: the n(n-1)/2 row-major upper-triangle pairs,
  *    then the same pairs swapped), described by `canon` ([n(n-1)] uint16,
  *    entry = target<<8 | source).
- *  - Dense attention layout ("AE"): per layer, float [num_graphs][n][n][H],
- *    entry [g][i][j][h] = edge logit of edge j->i for head h.  The diagonal
- *    (self loop) is never stored: the attention kernel derives it as the
- *    mean over i's incoming edges, which is PyG's add_self_loops
+ *  - Attention-logit layouts ("AE"), per layer:
+ *      edge order  float [num_graphs*n(n-1)][H] = [E][H], entry [e][h] = edge
+ *                  logit of canonical edge e for head h.  Written when
+ *                  `edge_index` is NULL (canonical batches, complete graphs):
+ *                  both the edge pass and the attention pass touch it in
+ *                  contiguous runs (ae_edge_order = 1 on the attention calls);
+ *      dense       float [num_graphs][n][n][H], entry [g][i][j][h] = edge
+ *                  logit of edge j->i (any edge set, via edge_index).
+ *    The diagonal (self loop) is never stored: the attention kernel derives
+ *    it as the mean over i's incoming edges, which is PyG's add_self_loops
  *    fill_value='mean' pushed through the linear edge projection.
  *  - Activation codes: 0 identity, 1 relu, 2 tanh, 3 sigmoid
  *    (reference utils/models.py:125-130).
@@ -61,7 +67,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 3
+#define SV2N_ABI_VERSION 4
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -85,7 +91,8 @@ const char* sv2n_strerror(int code);
  *   edge_attr [E][D] row-major, 16-B aligned base.
  *   wfold     [D][hl_pad] with column l*H+h = Σ_c W_edge[l][h*C+c][:]·att_edge[l][h][c];
  *             hl_pad ∈ {4,8,16,32} and L*H <= hl_pad (padding columns are ignored).
- *   ae_layers host array of L device pointers, each [num_graphs][n][n][H].
+ *   ae_layers host array of L device pointers, each [num_edges][H] (edge
+ *             order) when edge_index is NULL, else [num_graphs][n][n][H].
  * Self loops present in edge_index are skipped (PyG remove_self_loops). */
 int sv2n_edge_logits_fwd(const float* edge_attr, int64_t num_edges, int edge_dim,
                          const int64_t* edge_index, const uint16_t* canon,
@@ -93,7 +100,8 @@ int sv2n_edge_logits_fwd(const float* edge_attr, int64_t num_edges, int edge_dim
                          float* const* ae_layers, int num_layers, int heads,
                          int64_t num_graphs, int n, hipStream_t stream);
 
-/* dW̃ = edge_attrᵀ·dAE over all layers: dwfold [D][hl_pad] (overwritten).
+/* dW̃ = edge_attrᵀ·dAE over all layers: dwfold [D][hl_pad] (overwritten);
+ * dae_layers in the layout sv2n_edge_logits_fwd wrote.
  * workspace: sv2n_edge_logits_bwd_workspace(edge_dim, hl_pad) floats. */
 int64_t sv2n_edge_logits_bwd_workspace(int edge_dim, int hl_pad);
 int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, int edge_dim,
@@ -106,7 +114,9 @@ int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, int edge_dim
 /* Fused per-graph attention forward for one layer.
  *   xs      [N][ldx]: columns [0,H*C) = lin_src(x), [H*C, H*C+H) = a_src,
  *           [H*C+H, H*C+2H) = a_dst (the projection GEMM emits all three).
- *   ae      [num_graphs][n][n][H] or NULL (edge_attr=None: no edge term).
+ *   ae      [num_graphs][n][n][H], or [num_graphs*n(n-1)][H] when
+ *           ae_edge_order (complete graphs: rowmask must be NULL), or NULL
+ *           (edge_attr=None: no edge term).
  *   rowmask [N] uint32 (bit j of row g*n+i: edge j->i present) or NULL for
  *           complete graphs.
  *   bias    [H*C] (concat) or [C] (mean).
@@ -117,7 +127,8 @@ int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, int edge_dim
  *   psave   [num_graphs][H][32][32] softmax probabilities (pre-dropout; rows
  *           padded to 32, absent edges 0) whose sign bit records leaky_relu's
  *           negative side (for the backward). */
-int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, const uint32_t* rowmask,
+int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, int ae_edge_order,
+                      const uint32_t* rowmask,
                       const float* bias, const uint8_t* keep, float keep_scale,
                       float* y, float* psave,
                       int64_t num_graphs, int n, int heads, int channels, int concat,
@@ -126,12 +137,14 @@ int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, const uint32_t*
 /* Backward of sv2n_gat_attn_fwd.
  *   dy, y   [N][OC] (OC = concat ? H*C : C); y is the forward output.
  *   dxs     [N][ldx] gradient w.r.t. xs (all ldx columns written; padding 0).
- *   dae     [num_graphs][n][n][H] gradient w.r.t. ae (diagonal / absent 0), or
- *           NULL when the forward ran without ae.
+ *   dae     gradient w.r.t. ae in the layout ae_edge_order names
+ *           ([num_graphs][n][n][H] with diagonal / absent entries 0, or
+ *           [num_graphs*n(n-1)][H]), or NULL when the forward ran without ae.
  *   dbias_partial [num_graphs][OC] per-graph bias-gradient partial sums. */
 int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* xs, int ldx,
                       const float* psave, const uint8_t* keep, float keep_scale,
-                      const uint32_t* rowmask, float* dxs, float* dae, float* dbias_partial,
+                      const uint32_t* rowmask, float* dxs, float* dae, int ae_edge_order,
+                      float* dbias_partial,
                       int64_t num_graphs, int n, int heads, int channels, int concat,
                       int act, float negative_slope, hipStream_t stream);
 

@@ -69,7 +69,7 @@ static inline FwdChunking fwd_chunking(int H, int C, bool concat) {
 
 template <int ACT, bool CONCAT>
 __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
-    const float* __restrict__ xs, int ldx, const float* __restrict__ ae,
+    const float* __restrict__ xs, int ldx, const float* __restrict__ ae, int ae_edge_order,
     const uint32_t* __restrict__ rowmask, const float* __restrict__ bias,
     const uint8_t* __restrict__ keep, float keep_scale, float* __restrict__ y,
     float* __restrict__ psave, int n, int H, int C, float slope, int hpc, int cw) {
@@ -189,10 +189,14 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
   };
 
   // ---- every load of the softmax phase, then chunk 0's ----
-  const int nae = n * n * H;
-  const int nv = nae >> 2;
-  const float* aesrc = ae ? ae + row0 * n * H : xs;
-  const bool ae_vec = (((uintptr_t)aesrc) & 15) == 0;
+  // AE block of the graph: canonical edge order [n(n-1)][H] (ae_edge_order,
+  // what the edge pass writes for canonical batches: coalesced both ways) or
+  // the dense [n][n][H] form (block layouts)
+  const int E0 = n * (n - 1);
+  const int nae = ae_edge_order ? E0 * H : n * n * H;
+  const int nv = (nae + 3) >> 2;  // slots of four elements (the last may be partial)
+  const float* aesrc = ae ? ae + (int64_t)g * nae : xs;
+  const bool ae_vec = (((uintptr_t)aesrc) & 15) == 0 && (nae & 3) == 0;
   float4 av[AEV];
   if (ae) {
 #pragma unroll
@@ -202,8 +206,12 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
       float4 w;
       if (ae_vec) {
         w = reinterpret_cast<const float4*>(aesrc)[kc];
-      } else {
-        w.x = aesrc[4 * kc]; w.y = aesrc[4 * kc + 1]; w.z = aesrc[4 * kc + 2]; w.w = aesrc[4 * kc + 3];
+      } else {  // clamped scalar loads: the tail elements past nae are never scattered
+        const int b0 = 4 * kc, lim = nae - 1;
+        w.x = aesrc[min(b0, lim)];
+        w.y = aesrc[min(b0 + 1, lim)];
+        w.z = aesrc[min(b0 + 2, lim)];
+        w.w = aesrc[min(b0 + 3, lim)];
       }
       av[q] = w;
     }
@@ -233,7 +241,24 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_fwd(
   Chunk cur = chunk_of(cg);  // issued last: only the aggregation waits for it
   load_chunk(cur);
 
-  if (ae) {
+  if (ae && ae_edge_order) {
+    // element kk = e*H + h of the edge-ordered block -> sE[h][i][j]
+#pragma unroll
+    for (int q = 0; q < AEV; ++q) {
+      const int kk0 = 4 * (t + ATT_THREADS * q);
+      if (kk0 < nae) {
+        const float* pa = &av[q].x;
+        int e = kk0 / H, h2 = kk0 - e * H;
+        CanonIt it;
+        it.init(e, n);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (kk0 + c < nae) sE[(h2 * 32 + it.i()) * TS + it.j()] = pa[c];
+          if (++h2 == H) { h2 = 0; it.next(n); }
+        }
+      }
+    }
+  } else if (ae) {
     // element kk = 4k + e of AE [n][n][H] -> (i, j, h), kk = (i*n + j)*H + h
     const int kb = 4 * t;
     int h = kb % H, ij = kb / H;
@@ -438,7 +463,8 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ xs,
     int ldx, const float* __restrict__ psave, const uint8_t* __restrict__ keep, float keep_scale,
     const uint32_t* __restrict__ rowmask, float* __restrict__ dxs, float* __restrict__ dae,
-    float* __restrict__ dbias_part, int n, int H, int C, float slope, int hpc, int cw) {
+    int ae_edge_order, float* __restrict__ dbias_part, int n, int H, int C, float slope, int hpc,
+    int cw) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int g = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -780,8 +806,35 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
   }
   __syncthreads();
 
-  // ---- d ae: the graph's [n][n][H] block, four elements per slot ----
-  if (dae) {
+  // ---- d ae, canonical edge order [n(n-1)][H]: complete graph, every (i, j != i) ----
+  if (dae && ae_edge_order) {
+    const int nae = n * (n - 1) * H;
+    const rsrc_t rdae = make_rsrc(dae + (int64_t)g * nae, (uint32_t)nae * 4u);
+    if (nhg == 1 && (nae & 3) == 0 && ((((uintptr_t)dae) & 15) == 0)) {
+      for (int k4 = 4 * t; k4 < nae; k4 += 4 * ATT_THREADS) {
+        int e = k4 / H, h = k4 - e * H;
+        CanonIt it;
+        it.init(e, n);
+        f32x4 v;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int i = it.i();
+          v[c] = sDL[(h * 32 + i) * TS + it.j()] + sSh[h * 32 + i];
+          if (++h == H) { h = 0; it.next(n); }
+        }
+        bst4(rdae, k4 * 4, v);
+      }
+    } else {
+      for (int kk = t; kk < nae; kk += ATT_THREADS) {
+        const int e = kk / H, h = kk - e * H;
+        int i, j;
+        canon_decode(e, n, i, j);
+        const bool own = h >= hs && h < hs + hn;
+        bst(rdae, own ? kk * 4 : OOB, own ? sDL[(h * 32 + i) * TS + j] + sSh[h * 32 + i] : 0.f);
+      }
+    }
+  } else if (dae) {
+    // ---- d ae: the graph's [n][n][H] block, four elements per slot ----
     const int nae = n * n * H;
     const rsrc_t rdae = make_rsrc(dae + row0 * n * H, (uint32_t)nae * 4u);
     auto dae_val = [&](int i, int j, int h) {
@@ -887,13 +940,13 @@ static inline FwdSplit fwd_split(int64_t B, int H, int C, bool concat) {
 
 template <int ACT, bool CONCAT>
 static void launch_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
-                       const uint32_t* rowmask, const float* bias, const uint8_t* keep,
+                       int ae_edge_order, const uint32_t* rowmask, const float* bias, const uint8_t* keep,
                        float keep_scale, float* y, float* psave, int n, int H, int C, float slope) {
   const FwdSplit sp = fwd_split(B, H, C, CONCAT);
   const size_t lds = fwd_lds(H, sp.ck);
   raise_lds(k_attn_fwd<ACT, CONCAT>, lds);
   hipLaunchKernelGGL((k_attn_fwd<ACT, CONCAT>), dim3((unsigned)B, (unsigned)sp.ncg),
-                     dim3(ATT_THREADS), lds, st, xs, ldx, ae, rowmask, bias, keep, keep_scale, y,
+                     dim3(ATT_THREADS), lds, st, xs, ldx, ae, ae_edge_order, rowmask, bias, keep, keep_scale, y,
                      psave, n, H, C, slope, sp.ck.hpc, sp.ck.cw);
 }
 
@@ -930,13 +983,13 @@ template <int ACT, bool CONCAT>
 static void launch_bwd(int64_t B, hipStream_t st, const float* dy, const float* y,
                        const float* xs, int ldx, const float* psave, const uint8_t* keep,
                        float keep_scale, const uint32_t* rowmask, float* dxs, float* dae,
-                       float* dbias, int n, int H, int C, float slope) {
+                       int ae_edge_order, float* dbias, int n, int H, int C, float slope) {
   const BwdSplit sp = bwd_split(B, H, C, CONCAT);
   const size_t lds = bwd_lds(H, sp.ck, CONCAT);
   raise_lds(k_attn_bwd<ACT, CONCAT>, lds);
   hipLaunchKernelGGL((k_attn_bwd<ACT, CONCAT>), dim3((unsigned)B, (unsigned)sp.nhg),
                      dim3(ATT_THREADS), lds, st, dy, y, xs, ldx, psave, keep, keep_scale, rowmask,
-                     dxs, dae, dbias, n, H, C, slope, sp.ck.hpc, sp.ck.cw);
+                     dxs, dae, ae_edge_order, dbias, n, H, C, slope, sp.ck.hpc, sp.ck.cw);
 }
 
 static int check_attn_args(int64_t B, int n, int H, int C, int ldx, int act) {
@@ -955,19 +1008,20 @@ static int check_attn_args(int64_t B, int n, int H, int C, int ldx, int act) {
     default: FN<3, CONCAT>(__VA_ARGS__); break;         \
   }
 
-extern "C" int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae,
+extern "C" int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, int ae_edge_order,
                                  const uint32_t* rowmask, const float* bias, const uint8_t* keep,
                                  float keep_scale, float* y, float* psave, int64_t num_graphs,
                                  int n, int heads, int channels, int concat, int act,
                                  float negative_slope, hipStream_t stream) {
   if (!xs || !y || !psave) return SV2N_ERR_ARG;
   if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
+  if (ae_edge_order && (rowmask || n < 2)) return SV2N_ERR_ARG;  // complete graphs only
   if (concat) {
-    SV2N_DISPATCH_ACT(launch_fwd, true, num_graphs, stream, xs, ldx, ae, rowmask, bias, keep,
-                      keep_scale, y, psave, n, heads, channels, negative_slope)
+    SV2N_DISPATCH_ACT(launch_fwd, true, num_graphs, stream, xs, ldx, ae, ae_edge_order, rowmask,
+                      bias, keep, keep_scale, y, psave, n, heads, channels, negative_slope)
   } else {
-    SV2N_DISPATCH_ACT(launch_fwd, false, num_graphs, stream, xs, ldx, ae, rowmask, bias, keep,
-                      keep_scale, y, psave, n, heads, channels, negative_slope)
+    SV2N_DISPATCH_ACT(launch_fwd, false, num_graphs, stream, xs, ldx, ae, ae_edge_order, rowmask,
+                      bias, keep, keep_scale, y, psave, n, heads, channels, negative_slope)
   }
   return (int)hipGetLastError();
 }
@@ -975,19 +1029,20 @@ extern "C" int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae,
 extern "C" int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* xs, int ldx,
                                  const float* psave, const uint8_t* keep, float keep_scale,
                                  const uint32_t* rowmask, float* dxs, float* dae,
-                                 float* dbias_partial, int64_t num_graphs, int n, int heads,
-                                 int channels, int concat, int act, float negative_slope,
-                                 hipStream_t stream) {
+                                 int ae_edge_order, float* dbias_partial, int64_t num_graphs, int n,
+                                 int heads, int channels, int concat, int act,
+                                 float negative_slope, hipStream_t stream) {
   if (!dy || !y || !xs || !psave || !dxs || !dbias_partial) return SV2N_ERR_ARG;
   if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
+  if (ae_edge_order && (rowmask || n < 2)) return SV2N_ERR_ARG;  // complete graphs only
   if (concat) {
     SV2N_DISPATCH_ACT(launch_bwd, true, num_graphs, stream, dy, y, xs, ldx, psave, keep,
-                      keep_scale, rowmask, dxs, dae, dbias_partial, n, heads, channels,
-                      negative_slope)
+                      keep_scale, rowmask, dxs, dae, ae_edge_order, dbias_partial, n, heads,
+                      channels, negative_slope)
   } else {
     SV2N_DISPATCH_ACT(launch_bwd, false, num_graphs, stream, dy, y, xs, ldx, psave, keep,
-                      keep_scale, rowmask, dxs, dae, dbias_partial, n, heads, channels,
-                      negative_slope)
+                      keep_scale, rowmask, dxs, dae, ae_edge_order, dbias_partial, n, heads,
+                      channels, negative_slope)
   }
   return (int)hipGetLastError();
 }

@@ -164,6 +164,45 @@ __device__ __forceinline__ uint32_t row_bits(const uint32_t* rowmask, int64_t ro
 }
 
 // edge e -> (graph g, target i, source j); false for self loops / out-of-block
+// Canonical edge e of an n-node graph (CovarianceLaggedDataset order,
+// reference utils/dataset.py:216-226: the P = n(n-1)/2 row-major upper pairs
+// (u, w) as u -> w, then the same pairs swapped) -> (target i, source j),
+// without a table: the pair index p inverts tri_off(n, u) = u(2n-u-1)/2.
+__device__ __forceinline__ void canon_decode(int e, int n, int& i, int& j) {
+  const int P = n * (n - 1) / 2;
+  const bool lo = e >= P;
+  const int p = lo ? e - P : e;
+  const float b = 2.f * (float)n - 1.f;
+  int u = (int)((b - sqrtf(fmaxf(b * b - 8.f * (float)p, 0.f))) * 0.5f);
+  u = max(0, min(u, n - 2));
+  while (u < n - 2 && (u + 1) * (2 * n - u - 2) / 2 <= p) ++u;
+  while (u > 0 && u * (2 * n - u - 1) / 2 > p) --u;
+  const int w = u + 1 + (p - u * (2 * n - u - 1) / 2);
+  i = lo ? u : w;
+  j = lo ? w : u;
+}
+// the canonical edge after (i, j): advances the pair state (lo, u, w)
+struct CanonIt {
+  int lo, u, w;
+  __device__ __forceinline__ void init(int e, int n) {
+    const int P = n * (n - 1) / 2;
+    int i, j;
+    canon_decode(e, n, i, j);
+    lo = e >= P;
+    u = lo ? i : j;
+    w = lo ? j : i;
+  }
+  __device__ __forceinline__ void next(int n) {
+    if (++w == n) {
+      ++u;
+      w = u + 1;
+      if (u == n - 1) { lo ^= 1; u = 0; w = 1; }
+    }
+  }
+  __device__ __forceinline__ int i() const { return lo ? u : w; }
+  __device__ __forceinline__ int j() const { return lo ? w : u; }
+};
+
 __device__ __forceinline__ bool decode_edge(int64_t e, const int64_t* __restrict__ ei, int64_t E,
                                             const uint16_t* __restrict__ canon, int E0, int n,
                                             int64_t B, int64_t& g, int& i, int& j) {

@@ -163,6 +163,13 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_fwd(
         const int l = k / H, h = k - l * H;
         s_ptr[l][(int64_t)h * E + e0 + le] = s_out[le * HLP + k];
       }
+    } else if (!ei) {  // canonical batch: edge order [E][H] per layer, contiguous runs
+      const int nh = ne * H;
+      for (int idx = t; idx < L * nh; idx += EDGE_THREADS) {
+        const int l = idx / nh, r = idx - l * nh;
+        const int le = r / H, h = r - le * H;
+        s_ptr[l][e0 * H + r] = s_out[le * HLP + l * H + h];
+      }
     } else {
       for (int idx = t; idx < ne * HL; idx += EDGE_THREADS) {
         const int le = idx / HL, k = idx - le * HL;
@@ -199,6 +206,12 @@ __device__ __forceinline__ void gather_dae(float (&gd)[(EDGE_CHUNK * HLP + EDGE_
       if (le < ne && k < HL && !(ei && ei[e] == ei[E + e])) {
         const int l = k / H, h = k - l * H;
         v = s_ptr[l][(int64_t)h * E + e];
+      }
+    } else if (!ei) {  // canonical batch: edge order [E][H]
+      const int le = idx / HLP, k = idx - le * HLP;
+      if (le < ne && k < HL) {
+        const int l = k / H, h = k - l * H;
+        v = s_ptr[l][(e0 + le) * H + h];
       }
     } else {
       const int le = idx / HLP, k = idx - le * HLP;
@@ -413,8 +426,12 @@ __global__ __launch_bounds__(256) void k_edge_fwd_small(
     if constexpr (!PLANES) {
       int64_t g;
       int i, j;
-      if (!decode_edge(e, ei, E, canon, E0, n, B, g, i, j)) continue;
-      off = ((g * n + i) * n + j) * H;
+      if (!ei) {
+        off = e * H;  // canonical batch: edge order
+      } else {
+        if (!decode_edge(e, ei, E, canon, E0, n, B, g, i, j)) continue;
+        off = ((g * n + i) * n + j) * H;
+      }
     }
     // 4 output columns at a time (not unrolled: W̃ stays in LDS as broadcast
     // reads instead of D*HLP live VGPRs)
@@ -455,6 +472,9 @@ __global__ __launch_bounds__(256) void k_edge_bwd_small(
     bool ok;
     if constexpr (PLANES) {
       ok = !(ei && ei[e] == ei[E + e]);
+    } else if (!ei) {
+      ok = true;
+      off = e * H;  // canonical batch: edge order
     } else {
       int64_t g;
       int i, j;

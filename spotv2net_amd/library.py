@@ -38,14 +38,14 @@ _SCHEMAS = {
     "project": "(Tensor a, Tensor? planes, Tensor w, bool transpose_w, bool bf16) -> Tensor",
     "gat_attn_fwd": "(Tensor xs, Tensor? ae, Tensor? rowmask, Tensor? bias, Tensor? keep, "
                     "float keep_scale, int num_graphs, int n, int heads, int channels, "
-                    "bool concat, int act, float slope) -> (Tensor, Tensor)",
+                    "bool concat, int act, float slope, bool edge_order=False) -> (Tensor, Tensor)",
     "gat_attn_tiled_fwd": "(Tensor xs, Tensor? ae, int num_edges, Tensor? eid, Tensor? rowmask, "
                           "Tensor? bias, Tensor? keep, float keep_scale, int num_graphs, int n, "
                           "int heads, int channels, bool concat, int act, float slope) -> Tensor",
     "gat_attn_bwd": "(Tensor dy, Tensor y, Tensor xs, Tensor psave, Tensor? keep, "
                     "float keep_scale, Tensor? rowmask, bool with_ae, int num_graphs, int n, "
-                    "int heads, int channels, bool concat, int act, float slope) "
-                    "-> (Tensor, Tensor, Tensor)",
+                    "int heads, int channels, bool concat, int act, float slope, "
+                    "bool edge_order=False) -> (Tensor, Tensor, Tensor)",
     "gat_attn_tiled_bwd": "(Tensor dy, Tensor y, Tensor xs, Tensor? ae, int num_edges, "
                           "Tensor? eid, Tensor? keep, float keep_scale, Tensor? rowmask, "
                           "int num_graphs, int n, int heads, int channels, bool concat, int act, "
@@ -185,8 +185,18 @@ def _gat_prep_fake(W, att_src, att_dst, W_edge, att_edge, heads, channels, hl_pa
 # --------------------------------------------------------------------------
 # edge logits (sv2n_edge_logits_fwd / _planes) and their weight gradient
 # --------------------------------------------------------------------------
-def _ae_shape(planes, E, num_graphs, n, heads):
-    return (heads, E) if planes else (num_graphs, n, n, heads)
+def _ae_shape(planes, E, num_graphs, n, heads, edge_index):
+    """[H][E] planes (tiled path); edge order [E][H] for a canonical batch
+    (edge_index None, n > 1); else the dense per-graph [B][n][n][H] block."""
+    if planes:
+        return (heads, E)
+    return (E, heads) if edge_order(edge_index, n) else (num_graphs, n, n, heads)
+
+
+def edge_order(edge_index, n: int) -> bool:
+    """Whether sv2n_edge_logits_fwd writes (and the attention kernels take)
+    the edge-ordered AE layout: canonical batches of complete graphs."""
+    return edge_index is None and n > 1
 
 
 @_impl("edge_logits")
@@ -198,7 +208,10 @@ def _edge_logits(edge_attr, wfold, edge_index, canon, num_layers, heads, num_gra
     _need(wfold.shape[0] == D and num_layers * heads <= wfold.shape[1], "wfold shape")
     _need(edge_index is None or tuple(edge_index.shape) == (2, E), "edge_index shape")
     _need(canon.numel() == n * (n - 1), "canonical table shape")
-    outs = [torch.empty(_ae_shape(planes, E, num_graphs, n, heads), device=edge_attr.device)
+    _need(planes or edge_index is not None or E == num_graphs * n * (n - 1),
+          "canonical batch edge count")
+    outs = [torch.empty(_ae_shape(planes, E, num_graphs, n, heads, edge_index),
+                        device=edge_attr.device)
             for _ in range(num_layers)]
     if E == 0:
         return outs
@@ -220,7 +233,7 @@ def _edge_logits(edge_attr, wfold, edge_index, canon, num_layers, heads, num_gra
 def _edge_logits_fake(edge_attr, wfold, edge_index, canon, num_layers, heads, num_graphs, n,
                       planes):
     E = edge_attr.shape[0]
-    return [edge_attr.new_empty(_ae_shape(planes, E, num_graphs, n, heads))
+    return [edge_attr.new_empty(_ae_shape(planes, E, num_graphs, n, heads, edge_index))
             for _ in range(num_layers)]
 
 
@@ -232,7 +245,8 @@ def _edge_logits_bwd(edge_attr, edge_index, canon, dae, heads, num_graphs, n, hl
     dev = edge_attr.device
     L = len(dae)
     for d in dae:
-        _need(d.numel() == (heads * E if planes else num_graphs * n * n * heads), "dae shape")
+        _need(d.numel() == (heads * E if planes or edge_order(edge_index, n)
+                            else num_graphs * n * n * heads), "dae shape")
     ptrs = _lib.ptr_array([d.data_ptr() for d in dae])
     ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hl_pad)
     ws = torch.empty(ws_n, device=dev)
@@ -294,19 +308,21 @@ def _oc(heads, channels, concat):
 
 @_impl("gat_attn_fwd")
 def _gat_attn_fwd(xs, ae, rowmask, bias, keep, keep_scale, num_graphs, n, heads, channels,
-                  concat, act, slope):
+                  concat, act, slope, edge_order=False):
     lib = _lib.load()
     _f32(xs, ae, bias)
     N = num_graphs * n
     _rows(xs, N, heads * channels + 2 * heads, "xs")
     _dense(ae, rowmask, bias, keep)
-    _need(ae is None or ae.numel() == num_graphs * n * n * heads, "ae shape")
+    _need(ae is None or ae.numel() == num_graphs * n * (n - int(edge_order)) * heads, "ae shape")
+    _need(not edge_order or rowmask is None, "edge-ordered ae needs complete graphs")
     _need(bias is None or bias.numel() == _oc(heads, channels, concat), "bias shape")
     _need(keep is None or keep.numel() == num_graphs * heads * 1024, "keep shape")
     _need(rowmask is None or rowmask.numel() >= N, "rowmask shape")
     y = torch.empty(N, _oc(heads, channels, concat), device=xs.device)
     ps = torch.empty(num_graphs, heads, 32, 32, device=xs.device)
-    _lib.check(lib.sv2n_gat_attn_fwd(xs.data_ptr(), xs.stride(0), _p(ae), _p(rowmask), _p(bias),
+    _lib.check(lib.sv2n_gat_attn_fwd(xs.data_ptr(), xs.stride(0), _p(ae), int(edge_order),
+                                     _p(rowmask), _p(bias),
                                      _p(keep), keep_scale, y.data_ptr(), ps.data_ptr(),
                                      num_graphs, n, heads, channels, int(concat), act, slope,
                                      _st(xs)), "sv2n_gat_attn_fwd")
@@ -315,7 +331,7 @@ def _gat_attn_fwd(xs, ae, rowmask, bias, keep, keep_scale, num_graphs, n, heads,
 
 @_fake("gat_attn_fwd")
 def _gat_attn_fwd_fake(xs, ae, rowmask, bias, keep, keep_scale, num_graphs, n, heads, channels,
-                       concat, act, slope):
+                       concat, act, slope, edge_order=False):
     return (xs.new_empty((num_graphs * n, _oc(heads, channels, concat))),
             xs.new_empty((num_graphs, heads, 32, 32)))
 
@@ -348,9 +364,13 @@ def _gat_attn_tiled_fwd_fake(xs, ae, num_edges, eid, rowmask, bias, keep, keep_s
     return xs.new_empty((num_graphs * n, _oc(heads, channels, concat)))
 
 
+def _dae_shape(edge_order, num_graphs, n, heads):
+    return (num_graphs * n * (n - 1), heads) if edge_order else (num_graphs, n, n, heads)
+
+
 @_impl("gat_attn_bwd")
 def _gat_attn_bwd(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_graphs, n, heads,
-                  channels, concat, act, slope):
+                  channels, concat, act, slope, edge_order=False):
     lib = _lib.load()
     _f32(dy, y, xs, psave)
     N, OC = num_graphs * n, _oc(heads, channels, concat)
@@ -361,12 +381,14 @@ def _gat_attn_bwd(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_grap
     _need(keep is None or keep.numel() == num_graphs * heads * 1024, "keep shape")
     dev = xs.device
     dxs = torch.empty_like(xs)
-    dae = torch.empty(num_graphs, n, n, heads, device=dev) if with_ae else \
+    _need(not edge_order or rowmask is None, "edge-ordered ae needs complete graphs")
+    dae = torch.empty(_dae_shape(edge_order, num_graphs, n, heads), device=dev) if with_ae else \
         torch.empty(0, device=dev)
     dbp = torch.empty(num_graphs, _oc(heads, channels, concat), device=dev)
     _lib.check(lib.sv2n_gat_attn_bwd(dy.data_ptr(), y.data_ptr(), xs.data_ptr(), xs.stride(0),
                                      psave.data_ptr(), _p(keep), keep_scale, _p(rowmask),
-                                     dxs.data_ptr(), _p(dae), dbp.data_ptr(), num_graphs, n,
+                                     dxs.data_ptr(), _p(dae), int(edge_order), dbp.data_ptr(),
+                                     num_graphs, n,
                                      heads, channels, int(concat), act, slope, _st(xs)),
                "sv2n_gat_attn_bwd")
     return dxs, dae, dbp
@@ -374,9 +396,9 @@ def _gat_attn_bwd(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_grap
 
 @_fake("gat_attn_bwd")
 def _gat_attn_bwd_fake(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_graphs, n,
-                       heads, channels, concat, act, slope):
+                       heads, channels, concat, act, slope, edge_order=False):
     return (torch.empty_like(xs),
-            xs.new_empty((num_graphs, n, n, heads) if with_ae else (0,)),
+            xs.new_empty(_dae_shape(edge_order, num_graphs, n, heads) if with_ae else (0,)),
             xs.new_empty((num_graphs, _oc(heads, channels, concat))))
 
 

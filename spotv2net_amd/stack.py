@@ -33,6 +33,7 @@ import torch
 
 from . import _lib, library  # noqa: F401  (library registers torch.ops.sv2n)
 from .layout import GraphLayout
+from .library import edge_order
 from .ops import _aligned, _require_device, resolve_precision
 
 
@@ -180,8 +181,10 @@ class _GATStack(torch.autograd.Function):
 
         # 2) edge logits of every layer in one pass over edge_attr (sv2n::edge_logits)
         aes = [None] * L
+        ei = layout.edge_index if layout.kind == "block" else None
+        # canonical batches: AE in edge order [E][H] (coalesced on both sides)
+        eo = bool(use_edge and not tiled and edge_order(ei, n))
         if use_edge:
-            ei = layout.edge_index if layout.kind == "block" else None
             aes = list(ops.edge_logits(ea, wf, ei, layout.canon, L, H, B, n, tiled))
             if tiled and ea.size(0) == 0:
                 aes = [None] * L
@@ -212,7 +215,7 @@ class _GATStack(torch.autograd.Function):
                 ps = aes[l]
             else:
                 y, ps = ops.gat_attn_fwd(xs, aes[l], layout.rowmask, c.bias, keep, kscale, B, n,
-                                         Hc, C, c.concat, act, float(c.negative_slope))
+                                         Hc, C, c.concat, act, float(c.negative_slope), eo)
             out = y
             dmask = None
             if training and post_dropout > 0.0:
@@ -234,7 +237,7 @@ class _GATStack(torch.autograd.Function):
         ctx.layout = layout
         ctx.direct = _direct_mode()
         ctx.bf16 = bf16
-        ctx.meta = (L, act, use_edge, hp, H)
+        ctx.meta = (L, act, use_edge, hp, H, eo)
         ctx.kscales = [(1.0 / (1.0 - c.dropout)) if (training and 0.0 < c.dropout < 1.0) else
                        (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs]
         ctx.save_for_backward(ea, *saved_x, *saved_xs, *saved_y, *saved_p, *saved_keep,
@@ -246,7 +249,7 @@ class _GATStack(torch.autograd.Function):
         ops = torch.ops.sv2n
         convs = ctx.convs
         layout: GraphLayout = ctx.layout
-        L, act, use_edge, hp, H = ctx.meta
+        L, act, use_edge, hp, H, eo = ctx.meta
         sv = ctx.saved_tensors
         ea = sv[0]
         k = 1
@@ -280,7 +283,7 @@ class _GATStack(torch.autograd.Function):
             else:
                 dxs, dae, dbp = ops.gat_attn_bwd(
                     dy, ys[l], xs, pss[l], keeps[l], ctx.kscales[l], layout.rowmask, use_edge,
-                    B, n, Hc, C, c.concat, act, float(c.negative_slope))
+                    B, n, Hc, C, c.concat, act, float(c.negative_slope), eo)
             daes[l] = _opt(dae)
             gW = grad_of(c.lin_src.weight)
             gas = grad_of(c.att_src)

@@ -83,6 +83,17 @@ def test_graph_sizes(dev, n):
     _run(mine, ref, torch.randn(B * n, 8), ei, torch.randn(ei.size(1), 3), dev)
 
 
+@pytest.mark.parametrize("n,heads", [(3, 1), (7, 3), (31, 1), (30, 3)])
+def test_edge_order_partial_slots(dev, n, heads):
+    """Canonical batches carry the edge logits in edge order [B*n(n-1)][H]:
+    with H odd a graph's block is neither a multiple of four floats nor
+    16-B aligned (the attention kernels' clamped scalar path)."""
+    B = 5
+    mine, ref = twin_conv(6, 4, heads, True, 3, seed=n + heads)
+    ei = block_graphs(B, n)
+    _run(mine, ref, torch.randn(B * n, 6), ei, torch.randn(ei.size(1), 3), dev)
+
+
 @pytest.mark.parametrize("slope", [0.05, 0.8])
 def test_negative_slope(dev, slope):
     mine, ref = twin_conv(12, 6, 3, False, 4, slope=slope, seed=8)

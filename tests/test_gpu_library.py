@@ -42,7 +42,8 @@ def test_opcheck_forward_ops(dev):
     pj = (d.x, planes[0], waugs[0], False, False)
     torch.library.opcheck(ops.project, pj, test_utils=UTILS)
     xs = ops.project(*pj)
-    att = (xs, aes[0], None, c0.bias, None, 1.0, 3, 30, 2, 8, True, 1, 0.2)
+    assert aes[0].shape == (3 * 870, 2)  # canonical batch: edge-ordered logits
+    att = (xs, aes[0], None, c0.bias, None, 1.0, 3, 30, 2, 8, True, 1, 0.2, True)
     torch.library.opcheck(ops.gat_attn_fwd, att, test_utils=UTILS)
     h = torch.randn(90, 4, device=dev)
     torch.library.opcheck(ops.head_fwd, (h, m.linear.weight, m.linear.bias), test_utils=UTILS)
@@ -71,6 +72,11 @@ def test_opcheck_backward_ops(dev):
     grads = [torch.zeros_like(W), torch.zeros_like(a_s), torch.zeros_like(a_d),
              torch.zeros(H * C, device=dev)]
     torch.library.opcheck(ops.gat_wgrad, (x, dxs, W, a_s, a_d, dbp, H, C, False, *grads),
+                          test_utils=UTILS)
+    ae_e = torch.randn(B * n * (n - 1), H, generator=g).to(dev)
+    y2, ps2 = ops.gat_attn_fwd(xs, ae_e, None, None, None, 1.0, B, n, H, C, True, 1, 0.2, True)
+    torch.library.opcheck(ops.gat_attn_bwd, (torch.randn_like(y2), y2, xs, ps2, None, 1.0, None,
+                                             True, B, n, H, C, True, 1, 0.2, True),
                           test_utils=UTILS)
     lin = torch.nn.Linear(4, 1).to(dev)
     h = torch.randn(60, 4, device=dev)

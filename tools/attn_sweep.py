@@ -29,13 +29,14 @@ for name, B, H, C, concat in [("C2 L0", 512, 4, 100, True), ("C2 L1", 512, 4, 50
     n = 30
     ldx = (H * C + 2 * H + 3) // 4 * 4
     xs = torch.randn(B * n, ldx, device=dev)
-    ae = torch.randn(B, n, n, H, device=dev)
+    ae = torch.randn(B * n * (n - 1), H, device=dev)  # canonical batches: edge order
     OC = H * C if concat else C
     bias = torch.randn(OC, device=dev)
-    y, ps = ops.gat_attn_fwd(xs, ae, None, bias, None, 1.0, B, n, H, C, concat, 1, 0.2)
+    y, ps = ops.gat_attn_fwd(xs, ae, None, bias, None, 1.0, B, n, H, C, concat, 1, 0.2, True)
     dy = torch.randn_like(y)
-    tf = bench(lambda: ops.gat_attn_fwd(xs, ae, None, bias, None, 1.0, B, n, H, C, concat, 1, 0.2))
+    tf = bench(lambda: ops.gat_attn_fwd(xs, ae, None, bias, None, 1.0, B, n, H, C, concat, 1, 0.2,
+                                        True))
     tb = bench(lambda: ops.gat_attn_bwd(dy, y, xs, ps, None, 1.0, None, True, B, n, H, C, concat,
-                                        1, 0.2))
+                                        1, 0.2, True))
     print(f"{name}: target {os.environ.get('SV2N_ATT_TARGET_WG', '1024')}: fwd {tf:.1f} us  "
           f"bwd {tb:.1f} us", flush=True)
