@@ -25,6 +25,8 @@
  *   sv2n_adam_f32          the reference's Adam step over flat buffers (a13)
  *   sv2n_gat_attn_tiled_*  the same attention fwd/bwd for 32 < n <= 256 (C5
  *                          stress shapes), target-row-tiled
+ *   sv2n_gat_attn_fused_*  32 < n <= 256 with narrow edge features: the edge
+ *                          logits computed inside the attention (no planes)
  *   sv2n_block_rowmask     edge_index -> per-target source bitmask for graph
  *                          batches whose edges are not in canonical order
  *
@@ -67,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 4
+#define SV2N_ABI_VERSION 5
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -357,6 +359,48 @@ int sv2n_gat_attn_tiled_bwd(const float* dy, const float* y, const float* xs, in
                             const float* ae, int64_t num_edges, const int32_t* eid,
                             const uint8_t* keep, float keep_scale, const uint32_t* rowmask,
                             float* dxs, float* dae, float* dbias_partial, int64_t num_graphs,
+                            int n, int heads, int channels, int concat, int act,
+                            float negative_slope, hipStream_t stream);
+
+/* Edge-fused attention for dense-block graphs of 32 < n <= 256 nodes with
+ * narrow edge features (n 256, edge_dim 12, 8 heads x 16).
+ * Replaces, per GATConv layer, PyG's lin_edge + edge_update + softmax +
+ * dropout + propagate + bias (torch_geometric/nn/conv/gat_conv.py, reference
+ * utils/models.py:146) AND this library's separate edge pass: the logit of
+ * (i <- j, h) is edge_attr[e]·wfold[:, col0+h] + a_src[j,h] + a_dst[i,h],
+ * computed where it is consumed in the forward and again in the backward.
+ *   sv2n_gat_attn_fused_supported: 1 if (n, heads, channels, edge_dim) are
+ *            taken (heads <= 8, channels in {4,8,12,16}, edge_dim in {3,6,12})
+ *   edge_attr [num_edges][edge_dim] fp32; canonical order (eid NULL) needs
+ *            num_edges = num_graphs*n*(n-1) and 16-B alignment; block
+ *            layouts pass eid [N][n] (sv2n_block_eid; -1 = absent edge)
+ *   wfold, hl_pad, col0: the layer's columns of the edge fold
+ *            (sv2n_gat_prep_fwd_all), col0 + heads <= hl_pad
+ *   xs       [N][ldx] projection output (ldx % 4 == 0, 16-B aligned)
+ *   keep     [num_graphs][heads][n][n] uint8 attention-dropout mask or NULL
+ *   y        [N][OC] layer output (activation applied)
+ *   agg, stats: training only (both or neither): agg [N][heads*channels] the
+ *            pre-bias head aggregates, stats [N][4*heads] (row max, 1/sum,
+ *            self-loop logit, edge count) — the backward's inputs
+ * Backward: dxs [N][ldx] is overwritten (xs, a_src, a_dst, padding columns);
+ * dbias_partial [num_graphs*ceil(n/32)][OC] overwritten (sum them);
+ * dwfold columns col0..col0+heads-1 overwritten (the layer's dW̃);
+ * workspace sv2n_gat_attn_fused_bwd_workspace floats, no state between calls. */
+int sv2n_gat_attn_fused_supported(int n, int heads, int channels, int edge_dim);
+int sv2n_gat_attn_fused_fwd(const float* xs, int ldx, const float* edge_attr, int edge_dim,
+                            const float* wfold, int hl_pad, int col0, const int32_t* eid,
+                            const float* bias, const uint8_t* keep, float keep_scale, float* y,
+                            float* agg, float* stats, int64_t num_graphs, int n, int heads,
+                            int channels, int concat, int act, float negative_slope,
+                            hipStream_t stream);
+int64_t sv2n_gat_attn_fused_bwd_workspace(int64_t num_graphs, int n, int heads, int channels,
+                                          int edge_dim);
+int sv2n_gat_attn_fused_bwd(const float* dy, const float* y, const float* agg,
+                            const float* stats, const float* xs, int ldx,
+                            const float* edge_attr, int edge_dim, const float* wfold,
+                            int hl_pad, int col0, const int32_t* eid, const uint8_t* keep,
+                            float keep_scale, float* dxs, float* dbias_partial, float* dwfold,
+                            float* workspace, int64_t workspace_floats, int64_t num_graphs,
                             int n, int heads, int channels, int concat, int act,
                             float negative_slope, hipStream_t stream);
 

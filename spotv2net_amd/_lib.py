@@ -14,7 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p
@@ -51,6 +51,13 @@ _SIGNATURES = {
                                        _i64, _i32, _i32, _i32, _i32, _i32, _f32, _p]),
     "sv2n_gat_attn_tiled_bwd": (_i32, [_p, _p, _p, _i32, _p, _i64, _p, _p, _f32, _p, _p, _p, _p,
                                        _i64, _i32, _i32, _i32, _i32, _i32, _f32, _p]),
+    "sv2n_gat_attn_fused_supported": (_i32, [_i32, _i32, _i32, _i32]),
+    "sv2n_gat_attn_fused_fwd": (_i32, [_p, _i32, _p, _i32, _p, _i32, _i32, _p, _p, _p, _f32, _p, _p,
+                                       _p, _i64, _i32, _i32, _i32, _i32, _i32, _f32, _p]),
+    "sv2n_gat_attn_fused_bwd_workspace": (_i64, [_i64, _i32, _i32, _i32, _i32]),
+    "sv2n_gat_attn_fused_bwd": (_i32, [_p, _p, _p, _p, _p, _i32, _p, _i32, _p, _i32, _i32, _p, _p,
+                                       _f32, _p, _p, _p, _p, _i64, _i64, _i32, _i32, _i32, _i32,
+                                       _i32, _f32, _p]),
     "sv2n_edge_logits_fwd_planes": (_i32, [_p, _i64, _i32, _p, _i32, _p, _i32, _i32, _p]),
     "sv2n_edge_logits_bwd_planes": (_i32, [_p, _i64, _i32, _p, _p, _i32, _i32, _p, _i64, _p,
                                            _i32, _p]),

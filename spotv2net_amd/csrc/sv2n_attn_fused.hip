@@ -1,0 +1,1135 @@
+// Edge-fused GAT attention for dense-block graphs of 32 < n <= 256 nodes with
+// narrow edge features (the SURVEY.md §8d C5 stress shapes: D = 12, 8 heads
+// of 16 channels) — PyG 2.3.0 GATConv semantics (reference utils/models.py:146
+// -> GATConv.forward), like sv2n_attn_tiled.hip,
+// but the edge logits are never materialised:
+//
+//   logit(i <- j, h) = edge_attr[e(i,j)] · W̃[:, h] + a_src[j,h] + a_dst[i,h]
+//
+// is computed where it is consumed, from the D-float edge row, in every pass
+// that needs it.  With D·4 bytes per edge below the 4·H bytes one layer's
+// logit plane costs to write and to read back (and the same again for d-logit
+// planes in the backward), re-reading edge_attr once per layer and direction
+// moves fewer HBM bytes than any materialised form: per layer 2·4D bytes per
+// edge against 16·H (C5: 96 vs 128, and no separate edge pass).
+//
+// Forward, one 8-wave workgroup per (graph, 32-target tile), XCD-aware block
+// order (the tiles of a graph share an XCD, so the xs rows they all read hit L2):
+//   * sources in blocks of 32: the block's edge rows and xs rows are loaded one
+//     block ahead into registers (edge slots mapped so each wave reads
+//     contiguous runs of the canonical order: along the targets below the
+//     diagonal, along the sources above it);
+//   * logits of all 8 head columns into LDS (packed FMAs); then wave h runs
+//     head h's online softmax IN the MFMA A-operand layout (running max / sum
+//     per row, row reductions over the 4 lanes of a row with permlane swaps),
+//     keeping the sum of the raw edge logits for the mean-filled self loop;
+//   * aggregation out_h = P_h · xs_h on v_mfma_f32_16x16x4_f32 (exact f32)
+//     with P straight from registers, accumulators rescaled per row as the
+//     max moves;
+//   * self loop last (its logit needs the row's mean edge logit), then
+//     normalisation, bias and activation; training saves the pre-bias head
+//     aggregates and per-row softmax statistics (max, 1/sum, self logit, count).
+//
+// Backward, three launches per layer:
+//   bprep  per node: dOut = act'(y)·dy (÷H for mean), r = dOut·agg
+//          (= Σ_j p·dP, the softmax row term), the self loop's whole gradient,
+//          and per-chunk bias partials;
+//   bwd    one 8-wave workgroup per (graph, 32-source tile) walking all
+//          targets in blocks of 16: recompute logits and P from the saved
+//          statistics, dP = dOut·xsᵀ and dxs += Pᵀ·dOut on MFMA (wave h: head
+//          h, the softmax backward in the MFMA output layout, P in registers),
+//          d a_src complete in the workgroup, d a_dst partial per source tile,
+//          dW̃ = Σ edge_attr ⊗ d logit in registers (edge rows split over 4
+//          lanes; one partial per workgroup);
+//   finish d a_dst = Σ partials + self term, dW̃ = fixed-order sum of partials.
+// No atomics; every sum has a fixed order (deterministic).
+#include "sv2n_common.h"
+
+// tools/fattn_ablate.py builds variants with parts removed (timing only):
+// forward: 1 no edge_attr loads, 2 no softmax / MFMA phase, 3 no logit arithmetic;
+// backward: 4 no edge_attr loads, 5 no per-head phase [B], 6 no dW̃ phase [C]
+#ifndef SV2N_FATTN_ABLATE
+#define SV2N_FATTN_ABLATE 0
+#endif
+
+namespace sv2n {
+namespace fused {
+
+constexpr int WT = 512;   // threads per workgroup of the attention kernels (8 waves)
+constexpr int PT = 256;   // threads per workgroup of the per-node / reduction kernels
+constexpr int MH = 8;     // max heads (one per wave in the MFMA phases)
+constexpr int FT = 32;    // forward: targets per tile
+constexpr int FS = 32;    // forward: sources per block
+constexpr int BS = 32;    // backward: sources per tile
+constexpr int BT = 16;    // backward: targets per block
+constexpr int RS = 36;    // LDS stride (floats) of a 32-wide row (16-B aligned, b128 conflict-free)
+constexpr int XW = 132;   // LDS stride of a [8 heads x 16] row
+constexpr int XCHUNKS = 3;  // forward xs prefetch: ceil(32 rows x 34 chunks / 512)
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int tri_off(int n, int u) { return u * (2 * n - u - 1) / 2; }
+
+// canonical in-graph edge id of (target i <- source j) (reference
+// utils/dataset.py:216-226: upper pairs u->w row-major, then swapped), -1 if
+// (i, j) is not an edge
+__device__ __forceinline__ int canon_id(int i, int j, int n) {
+  const int U = n * (n - 1) / 2;
+  const int id = j > i ? U + tri_off(n, i) + (j - i - 1) : tri_off(n, j) + (i - j - 1);
+  return (i < n && j < n && i != j) ? id : -1;
+}
+
+// blockIdx -> (graph, tile) with the tiles of a graph on one XCD
+__device__ __forceinline__ void block_gt(int NT, int64_t& g, int& tile) {
+  const int64_t nb = (int64_t)gridDim.x;
+  int64_t b = blockIdx.x;
+  if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);
+  g = b / NT;
+  tile = (int)(b - g * NT);
+}
+
+// One edge row of D floats.  Canonical layouts: buffer loads at 32-bit
+// offsets within the graph's edge rows (a miss reads 0).  Edge-id maps
+// (block layouts): global edge ids, 64-bit addresses.
+template <int D>
+__device__ __forceinline__ void load_edge(float (&v)[D], rsrc_t rea, int cid,
+                                          const float* __restrict__ ea, int64_t gid, bool eidm) {
+  if (eidm) {
+    const bool ok = gid >= 0;
+    const float* p = ea + (ok ? gid : 0) * D;
+    if constexpr (D % 4 == 0) {
+#pragma unroll
+      for (int q = 0; q < D / 4; ++q) {
+        const f4 w = ok ? *reinterpret_cast<const f4*>(p + 4 * q) : f4{0.f, 0.f, 0.f, 0.f};
+        v[4 * q] = w.x; v[4 * q + 1] = w.y; v[4 * q + 2] = w.z; v[4 * q + 3] = w.w;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < D; ++d) v[d] = ok ? p[d] : 0.f;
+    }
+  } else {
+    if constexpr (D % 4 == 0) {
+#pragma unroll
+      for (int q = 0; q < D / 4; ++q) {
+        const f32x4 w = bld4(rea, cid >= 0 ? 4 * (cid * D + 4 * q) : OOB);
+        v[4 * q] = w.x; v[4 * q + 1] = w.y; v[4 * q + 2] = w.z; v[4 * q + 3] = w.w;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < D; ++d) v[d] = bld(rea, cid >= 0 ? 4 * (cid * D + d) : OOB);
+    }
+  }
+}
+
+__device__ __forceinline__ float act_fwd_rt(int act, float z) {
+  switch (act) {
+    case ACT_RELU: return act_fwd<ACT_RELU>(z);
+    case ACT_TANH: return act_fwd<ACT_TANH>(z);
+    case ACT_SIGMOID: return act_fwd<ACT_SIGMOID>(z);
+    default: return z;
+  }
+}
+__device__ __forceinline__ float act_bwd_rt(int act, float dy, float y) {
+  switch (act) {
+    case ACT_RELU: return act_bwd<ACT_RELU>(dy, y);
+    case ACT_TANH: return act_bwd<ACT_TANH>(dy, y);
+    case ACT_SIGMOID: return act_bwd<ACT_SIGMOID>(dy, y);
+    default: return dy;
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// 16-lane row sum (every lane of the row ends with the same value)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dppf<0x128>(v);
+  v += dppf<0x124>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0xB1>(v);
+  return v;
+}
+
+// Half of an edge row: lane parity `half` holds floats [half*DH, half*DH + DH)
+// (DH = ceil(D/2); past D reads 0).  The backward splits every edge row over a
+// lane pair so that its dW̃ accumulators are D/2 x 8 per thread, not D x 8.
+template <int D>
+__device__ __forceinline__ void load_edge_half(float (&v)[(D + 1) / 2], rsrc_t rea, int cid,
+                                               const float* __restrict__ ea, int64_t gid,
+                                               bool eidm, int half) {
+  constexpr int DH = (D + 1) / 2;
+  const int d0 = half * DH;
+  if (eidm) {
+    const bool ok = gid >= 0;
+    const float* p = ea + (ok ? gid : 0) * D + d0;
+#pragma unroll
+    for (int dd = 0; dd < DH; ++dd) v[dd] = (ok && d0 + dd < D) ? p[dd] : 0.f;
+  } else if constexpr (DH % 2 == 0 && D % 2 == 0) {
+#pragma unroll
+    for (int q = 0; q < DH / 2; ++q) {
+      const auto w = __builtin_amdgcn_raw_buffer_load_b64(
+          rea, cid >= 0 ? 4 * (cid * D + d0 + 2 * q) : OOB, 0, 0);
+      v[2 * q] = __uint_as_float(w[0]);
+      v[2 * q + 1] = __uint_as_float(w[1]);
+    }
+  } else {
+#pragma unroll
+    for (int dd = 0; dd < DH; ++dd)
+      v[dd] = (d0 + dd < D) ? bld(rea, cid >= 0 ? 4 * (cid * D + d0 + dd) : OOB) : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+// Softmax arithmetic in base 2: scaled logits s = leaky(logit)·log2(e), p =
+// exp2(s - m) on v_exp_f32; the saved row max m is in the same units.
+constexpr float L2E = 1.4426950408889634f;
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// logits of K edge rows for all 8 head columns on packed FMAs: the row's
+// floats in natural register pairs (d, d+1) times W̃ᵀ pairs from LDS (sWT
+// [8][DP], broadcast b128 reads), the two halves summed at the end — no
+// broadcast copies of the loaded values (which would make the compiler wait on
+// the prefetch right after issuing it)
+template <int D>
+constexpr int dpad() { return (D + 3) / 4 * 4; }
+template <int D, int K>
+__device__ __forceinline__ void edge_logits_pk(float (&lg)[K][MH], const float (&ev)[K][D],
+                                               const float* __restrict__ sWT) {
+  constexpr int DP = dpad<D>();
+#pragma unroll
+  for (int h = 0; h < MH; ++h) {
+    f2 a2[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a2[k] = f2{0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < DP / 4; ++q) {
+      const f4 w4 = *reinterpret_cast<const f4*>(sWT + h * DP + 4 * q);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int d = 4 * q;
+        const f2 e01 = f2{ev[k][d], d + 1 < D ? ev[k][d + 1] : 0.f};
+        a2[k] = __builtin_elementwise_fma(e01, f2{w4.x, w4.y}, a2[k]);
+        if (d + 2 < D) {
+          const f2 e23 = f2{ev[k][d + 2], d + 3 < D ? ev[k][d + 3] : 0.f};
+          a2[k] = __builtin_elementwise_fma(e23, f2{w4.z, w4.w}, a2[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) lg[k][h] = a2[k].x + a2[k].y;
+  }
+}
+
+// max / sum over the 4 lanes li, li+16, li+32, li+48 of a wave (the rows of an
+// MFMA A operand): gfx950 permlane swaps, no LDS round trip
+__device__ __forceinline__ float lk_max(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float lk_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+constexpr int FHS = FT * RS + 32;  // forward: LDS stride of a head's [32][RS] logit block
+
+template <int D, bool EIDM, bool KEEP>
+__global__ __launch_bounds__(WT, (EIDM || KEEP) ? 2 : 4) void k_fattn_fwd(
+    const float* __restrict__ xs, int ldx, const float* __restrict__ ea,
+    const float* __restrict__ wf, int hl_pad, int col0, const int32_t* __restrict__ eid,
+    const float* __restrict__ bias, const uint8_t* __restrict__ keep, float keep_scale,
+    float* __restrict__ y, float* __restrict__ agg, float* __restrict__ stats, int n, int H,
+    int C, int act, int concat, float slope) {
+  __shared__ __attribute__((aligned(16))) float sE[MH * FHS];       // edge logits of the block
+  __shared__ __attribute__((aligned(16))) float sXT[MH * 16 * RS];  // xs_hᵀ of the block
+  __shared__ __attribute__((aligned(16))) float sA[MH * FS];        // a_src of the block
+  __shared__ __attribute__((aligned(16))) float sAl[MH * FT], sPs[MH * FT], sInv[MH * FT];
+  __shared__ uint32_t sPres[2][FT];  // edge-id maps: present sources per target (by block parity)
+  __shared__ __attribute__((aligned(16))) float sWT[MH * dpad<D>()];  // W̃ᵀ, zero padded
+
+  const int NT = (n + FT - 1) / FT;
+  int64_t g;
+  int tile;
+  block_gt(NT, g, tile);
+  const int t = threadIdx.x, lane = t & 63, hh = t >> 6;  // wave hh: head hh in [B]
+  const int li = lane & 15, lk = lane >> 4;
+  const int i0 = tile * FT;
+  const int HC = H * C;
+  const int64_t row0 = g * n;
+  const int E0 = n * (n - 1);
+  constexpr bool eidm = EIDM;
+  const rsrc_t rea = eidm ? make_rsrc(nullptr, 0u)
+                          : make_rsrc(ea + g * (int64_t)E0 * D, (uint32_t)(4 * E0 * D));
+  const rsrc_t rxs = make_rsrc(xs + row0 * ldx, (uint32_t)(4 * n * ldx));
+  const int CQ = (HC + H + 3) >> 2;  // 16-B chunks of [xs | a_src] per row
+  const float slope2 = slope * L2E;
+  const bool hv = hh < H;
+
+  if (t < MH * dpad<D>()) {
+    const int h = t / dpad<D>(), d = t - h * dpad<D>();
+    sWT[t] = (h < H && d < D) ? wf[d * hl_pad + col0 + h] : 0.f;
+  }
+  if (eidm && t < 2 * FT) sPres[t >> 5][t & 31] = 0u;
+  // padding rows of xs_hᵀ (c >= C or h >= H) stay zero
+  for (int idx = t; idx < MH * 16 * RS; idx += WT) {
+    const int r = idx / RS;
+    if ((r & 15) >= C || (r >> 4) >= H) sXT[idx] = 0.f;
+  }
+  // where this thread's xs chunks go in LDS (fixed over the blocks): -1 none;
+  // < 2^20: 4 rows of sXT from there (stride RS); else a_src elements from
+  // (xd & 0xffff), count (xd >> 20)
+  int xdst[XCHUNKS];
+#pragma unroll
+  for (int q = 0; q < XCHUNKS; ++q) {
+    const int u = t + WT * q, jl = u & 31, cq = u >> 5, cg = 4 * cq;
+    xdst[q] = -1;
+    if (cq < CQ) {
+      if (cg < HC) {
+        const int h = cg / C, c = cg - h * C;
+        xdst[q] = (h * 16 + c) * RS + jl;
+      } else {
+        xdst[q] = (min(4, HC + H - cg) << 20) | ((cg - HC) * FS + jl);
+      }
+    }
+  }
+
+  // per row tile rt: state of row i = i0 + 16rt + li for head hh (replicated over lk)
+  float ad[2], mrow[2], lrow[2], esum[2], cnt[2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int i = i0 + 16 * rt + li;
+    ad[rt] = (hv && i < n) ? xs[(row0 + i) * ldx + HC + H + hh] : 0.f;
+    mrow[rt] = -INFINITY;
+    lrow[rt] = 0.f;  // this lane's share of the row sum
+    esum[rt] = 0.f;
+    cnt[rt] = 0.f;
+  }
+  __syncthreads();
+
+  // edge rows and xs rows of the next block, loaded while this one is computed
+  float ev[2][D];
+  f32x4 xv[XCHUNKS];
+  auto slot = [&](int k, int j0, int& il, int& jl) {
+    const int s = k * WT + t;
+    const bool along_i = !eidm && (j0 + FS <= i0);
+    il = along_i ? (s & 31) : (s >> 5);
+    jl = along_i ? (s >> 5) : (s & 31);
+  };
+  auto issue = [&](int j0) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      int il, jl;
+      slot(k, j0, il, jl);
+      const int i = i0 + il, j = j0 + jl;
+      int cid = -1;
+      int64_t gid = -1;
+      if constexpr (eidm) {
+        gid = (i < n && j < n && i != j) ? eid[(row0 + i) * n + j] : -1;
+      } else {
+        cid = canon_id(i, j, n);
+      }
+      if (SV2N_FATTN_ABLATE == 1) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) ev[k][d] = (float)(cid & 7) * 0.01f;
+      } else {
+        load_edge<D>(ev[k], rea, cid, ea, gid, eidm);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < XCHUNKS; ++q) {
+      const int u = t + WT * q, jl = u & 31, cq = u >> 5, j = j0 + jl;
+      xv[q] = bld4(rxs, (cq < CQ && j < n) ? 4 * (j * ldx + 4 * cq) : OOB);
+    }
+  };
+
+  f4 acc[2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) acc[rt] = f4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  int par = 0;
+  for (int j0 = 0; j0 < n; j0 += FS, par ^= 1) {
+    // ---- [A] logits of the block (all 8 head columns), xs rows into LDS ----
+    {
+      float lg[2][MH];
+      if (SV2N_FATTN_ABLATE == 3) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int h = 0; h < MH; ++h) lg[k][h] = ev[k][h % D];
+      } else {
+        edge_logits_pk<D, 2>(lg, ev, sWT);
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        int il, jl;
+        slot(k, j0, il, jl);
+        float* dst = sE + il * RS + jl;
+#pragma unroll
+        for (int h = 0; h < MH; ++h) dst[h * FHS] = lg[k][h];
+        if constexpr (eidm) {
+          const int i = i0 + il, j = j0 + jl;
+          const bool pres = i < n && j < n && i != j && eid[(row0 + i) * n + j] >= 0;
+          if (pres) atomicOr(&sPres[par][il], 1u << jl);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < XCHUNKS; ++q) {
+      const int xd = xdst[q];
+      if (xd >= 0 && xd < (1 << 20)) {
+        float* dst = sXT + xd;
+        dst[0] = xv[q].x;
+        dst[RS] = xv[q].y;
+        dst[2 * RS] = xv[q].z;
+        dst[3 * RS] = xv[q].w;
+      } else if (xd >= 0) {
+        float* dst = sA + (xd & 0xffff);
+        const int cntq = xd >> 20;
+        const float vv[4] = {xv[q].x, xv[q].y, xv[q].z, xv[q].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (e < cntq) dst[e * FS] = vv[e];
+      }
+    }
+    if (j0 + FS < n) issue(j0 + FS);
+    __syncthreads();
+
+    // ---- [B] wave hh: softmax of head hh in registers, MFMA aggregation ----
+    if (hv && SV2N_FATTN_ABLATE != 2) {
+      const bool clean = !eidm && j0 != i0 && j0 + FS <= n;
+      const f4 as0 = *reinterpret_cast<const f4*>(sA + hh * FS + 4 * lk);
+      const f4 as1 = *reinterpret_cast<const f4*>(sA + hh * FS + 16 + 4 * lk);
+      const float asv[8] = {as0.x, as0.y, as0.z, as0.w, as1.x, as1.y, as1.z, as1.w};
+      const f4 xb0 = *reinterpret_cast<const f4*>(sXT + (hh * 16 + li) * RS + 4 * lk);
+      const f4 xb1 = *reinterpret_cast<const f4*>(sXT + (hh * 16 + li) * RS + 16 + 4 * lk);
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int il = 16 * rt + li, i = i0 + il;
+        const float* er = sE + hh * FHS + il * RS;
+        const f4 e0 = *reinterpret_cast<const f4*>(er + 4 * lk);
+        const f4 e1 = *reinterpret_cast<const f4*>(er + 16 + 4 * lk);
+        const float evv[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+        uint32_t vm = 0xffu;  // bit k: element k (source 4lk + (k&3) + 16(k>>2)) is an edge
+        if (!clean) {
+          uint32_t row = i < n ? 0xffffffffu : 0u;
+          const int lim = n - j0;
+          if (lim < 32) row &= (1u << lim) - 1u;
+          if (i >= j0 && i < j0 + FS) row &= ~(1u << (i - j0));
+          if constexpr (eidm) row &= sPres[par][il];
+          vm = ((row >> (4 * lk)) & 0xfu) | (((row >> (16 + 4 * lk)) & 0xfu) << 4);
+        }
+        float sv[8], bm = -INFINITY, es = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const bool valid = (vm >> k) & 1u;
+          es += valid ? evv[k] : 0.f;
+          const float v = asv[k] + ad[rt] + evv[k];
+          const float s2 = v * (v > 0.f ? L2E : slope2);
+          sv[k] = valid ? s2 : -INFINITY;
+          bm = fmaxf(bm, sv[k]);
+        }
+        esum[rt] += es;
+        if constexpr (eidm) cnt[rt] += (float)__popc(vm);  // canonical: n - 1
+        bm = lk_max(bm);
+        const float mo = mrow[rt];
+        const float mn = fmaxf(mo, bm);
+        const float al = mn == -INFINITY ? 1.f : fexp2(mo - mn);
+        const float mref = mn == -INFINITY ? 0.f : mn;
+        float pk[8], ls = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float p = fexp2(sv[k] - mref);  // exp2(-inf) = 0
+          ls += p;
+          pk[k] = p;
+          if constexpr (KEEP) {
+            const int j = j0 + 4 * lk + (k & 3) + 16 * (k >> 2);
+            pk[k] = (i < n && j < n && keep[((g * H + hh) * (int64_t)n + i) * n + j]) ?
+                        p * keep_scale : 0.f;
+          }
+        }
+        lrow[rt] = lrow[rt] * al + ls;
+        mrow[rt] = mn;
+        // rescale factor of the accumulator rows 4lk + r (wave-local LDS exchange)
+        if (lk == 0) sAl[hh * FT + il] = al;
+        const f4 al4 = *reinterpret_cast<const f4*>(sAl + hh * FT + 16 * rt + 4 * lk);
+        acc[rt].x *= al4.x;
+        acc[rt].y *= al4.y;
+        acc[rt].z *= al4.z;
+        acc[rt].w *= al4.w;
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pk[0], xb0.x, acc[rt], 0, 0, 0);
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pk[1], xb0.y, acc[rt], 0, 0, 0);
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pk[2], xb0.z, acc[rt], 0, 0, 0);
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pk[3], xb0.w, acc[rt], 0, 0, 0);
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pk[4], xb1.x, acc[rt], 0, 0, 0);
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pk[5], xb1.y, acc[rt], 0, 0, 0);
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pk[6], xb1.z, acc[rt], 0, 0, 0);
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pk[7], xb1.w, acc[rt], 0, 0, 0);
+      }
+    }
+    if constexpr (eidm) {
+      if (t < FT) sPres[par ^ 1][t] = 0u;  // the next block's buffer (last read two blocks ago)
+    }
+    __syncthreads();
+  }
+
+  // ---- self loop (logit = a_src + a_dst + mean edge logit), statistics ----
+  if (hv) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int il = 16 * rt + li, i = i0 + il;
+      const float l = lk_sum(lrow[rt]);
+      const float es = lk_sum(esum[rt]);
+      const float cn = eidm ? lk_sum(cnt[rt]) : (float)(n - 1);
+      const float as_self = i < n ? xs[(row0 + i) * ldx + HC + hh] : 0.f;
+      const float loopv = cn > 0.f ? es / cn : 0.f;
+      const float vs = as_self + ad[rt] + loopv;
+      const float lr = vs * (vs > 0.f ? L2E : slope2);
+      const float mo = mrow[rt];
+      const float mn = fmaxf(mo, lr);
+      const float al = fexp2(mo - mn);
+      const float ps = fexp2(lr - mn);
+      const float lt = l * al + ps;
+      const float inv = 1.f / (lt + 1e-16f);
+      float pks = ps;
+      if constexpr (KEEP) pks = (i < n && keep[((g * H + hh) * (int64_t)n + i) * n + i]) ?
+                                    ps * keep_scale : 0.f;
+      if (lk == 0) {
+        sAl[hh * FT + il] = al;
+        sPs[hh * FT + il] = pks;
+        sInv[hh * FT + il] = inv;
+        if (stats && i < n) {
+          float* st = stats + (row0 + i) * 4 * H;
+          st[hh] = mn;
+          st[H + hh] = inv;
+          st[2 * H + hh] = vs;
+          st[3 * H + hh] = cn;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  float* sOut = sE;  // [FT][HC] head aggregates (mean over heads)
+  if (hv) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const float av[4] = {acc[rt].x, acc[rt].y, acc[rt].z, acc[rt].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int il = 16 * rt + 4 * lk + r, i = i0 + il, c = li;
+        if (i < n && c < C) {
+          const int q = hh * FT + il;
+          const int64_t row = row0 + i;
+          const float xv1 = xs[row * ldx + hh * C + c];
+          const float out = fmaf(av[r], sAl[q], sPs[q] * xv1) * sInv[q];
+          if (agg) agg[row * HC + hh * C + c] = out;
+          if (concat) {
+            const float b = bias ? bias[hh * C + c] : 0.f;
+            y[row * HC + hh * C + c] = act_fwd_rt(act, out + b);
+          } else {
+            sOut[il * HC + hh * C + c] = out;
+          }
+        }
+      }
+    }
+  }
+  if (!concat) {
+    __syncthreads();
+    const float invH = 1.f / (float)H;
+    for (int idx = t; idx < FT * C; idx += WT) {
+      const int il = idx / C, c = idx - il * C, i = i0 + il;
+      if (i < n) {
+        float s = 0.f;
+        for (int h = 0; h < H; ++h) s += sOut[il * HC + h * C + c];
+        y[(row0 + i) * C + c] = act_fwd_rt(act, s * invH + (bias ? bias[c] : 0.f));
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward: per-node preparation
+//   dout [N][HC]  dOut_h (concat slice, or dz / H for every head)
+//   rs   [N][4H]  r | d logit of the self loop | its kept prob. | that ÷ count
+//   dbp  [B*NT][OC] bias partials (Σ dz over the chunk's rows)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(PT) void k_fattn_bprep(
+    const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ agg,
+    const float* __restrict__ stats, const float* __restrict__ xs, int ldx,
+    const uint8_t* __restrict__ keep, float keep_scale, float* __restrict__ dout,
+    float* __restrict__ rs, float* __restrict__ dbp, int n, int H, int C, int act, int concat,
+    float slope) {
+  __shared__ float sRt[FT * 128], sDp[FT * 128];
+  __shared__ float sDb[2 * 128];
+  const int NT = (n + FT - 1) / FT;
+  const int64_t g = blockIdx.x / NT;
+  const int chunk = (int)(blockIdx.x - g * NT);
+  const int i0 = chunk * FT;
+  const int t = threadIdx.x;
+  const int HC = H * C, OC = concat ? HC : C;
+  const int64_t row0 = g * n;
+  const int hc = t & 127, rh = t >> 7;
+  const int h = hc / C, c = hc - (hc / C) * C;
+  const int oc = concat ? hc : c;
+  const bool colv = hc < HC;
+  const float oscale = concat ? 1.f : 1.f / (float)H;
+
+  float vdy[FT / 2], vy[FT / 2], vag[FT / 2], vx[FT / 2];
+#pragma unroll
+  for (int q = 0; q < FT / 2; ++q) {
+    const int i = i0 + rh + 2 * q;
+    const bool ok = colv && i < n;
+    const int64_t row = row0 + (ok ? i : 0);
+    vdy[q] = ok ? dy[row * OC + oc] : 0.f;
+    vy[q] = ok ? y[row * OC + oc] : 0.f;
+    vag[q] = ok ? agg[row * HC + hc] : 0.f;
+    vx[q] = ok ? xs[row * ldx + hc] : 0.f;
+  }
+  float db = 0.f;
+#pragma unroll
+  for (int q = 0; q < FT / 2; ++q) {
+    const int il = rh + 2 * q, i = i0 + il;
+    const bool ok = colv && i < n;
+    const float dz = act_bwd_rt(act, vdy[q], vy[q]);
+    const float d = dz * oscale;
+    if (ok) dout[(row0 + i) * HC + hc] = d;
+    sRt[il * 128 + hc] = ok ? d * vag[q] : 0.f;
+    sDp[il * 128 + hc] = ok ? d * vx[q] : 0.f;
+    if (ok && (concat || h == 0)) db += dz;
+  }
+  sDb[rh * 128 + hc] = db;
+  __syncthreads();
+  {
+    const int il = t >> 3, hh = t & 7, i = i0 + il;
+    if (hh < H && i < n) {
+      float r = 0.f, dp = 0.f;
+      for (int cc = 0; cc < C; ++cc) {
+        r += sRt[il * 128 + hh * C + cc];
+        dp += sDp[il * 128 + hh * C + cc];
+      }
+      const int64_t row = row0 + i;
+      const float* st = stats + row * 4 * H;
+      const float mx = st[hh], inv = st[H + hh], vs = st[2 * H + hh], cnt = st[3 * H + hh];
+      const float lr = vs * (vs > 0.f ? L2E : slope * L2E);  // base-2 units, as the forward
+      const float ps = fexp2(lr - mx) * inv;
+      float pd = ps, dP = dp;
+      if (keep) {
+        const bool kp = keep[((g * H + hh) * (int64_t)n + i) * n + i] != 0;
+        pd = kp ? ps * keep_scale : 0.f;
+        dP = kp ? dp * keep_scale : 0.f;
+      }
+      const float ds = ps * (dP - r);
+      const float dl = vs > 0.f ? ds : ds * slope;
+      float* o = rs + row * 4 * H;
+      o[hh] = r;
+      o[H + hh] = dl;
+      o[2 * H + hh] = pd;
+      o[3 * H + hh] = cnt > 0.f ? dl / cnt : 0.f;
+    }
+  }
+  if (t < OC) dbp[(g * NT + chunk) * OC + t] = sDb[t] + sDb[128 + t];
+}
+
+// ---------------------------------------------------------------------------
+// backward: one 8-wave workgroup per (graph, 32-source tile)
+//   [A] slot owners (4 lanes per edge row, D/4 floats each): logits of the
+//       block's edges -> LDS; dOut rows and the per-target vectors staged
+//   [B] wave h: dP = dOut·xsᵀ on MFMA, the softmax / leaky / dropout backward
+//       in the MFMA output layout (lane (li, lk) holds targets 4lk+r, sources
+//       16jt+li), P kept in registers as the A operand of dxs += Pᵀ·dOut;
+//       d a_src accumulated in registers, d a_dst row sums stored per source
+//       tile, d logit (+ the self loop's share) -> LDS
+//   [C] slot owners: dW̃ += edge_attr ⊗ d logit in registers
+// ---------------------------------------------------------------------------
+constexpr int BHS = BT * RS + 16;  // backward: LDS stride of a head's [16][RS] block (≡ 16 mod 64)
+
+template <int D, bool EIDM, bool KEEP>
+__global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
+    const float* __restrict__ xs, int ldx, const float* __restrict__ ea,
+    const float* __restrict__ wf, int hl_pad, int col0, const int32_t* __restrict__ eid,
+    const uint8_t* __restrict__ keep, float keep_scale, const float* __restrict__ dout,
+    const float* __restrict__ stats, const float* __restrict__ rs, float* __restrict__ dxs,
+    float* __restrict__ adst_part, float* __restrict__ wpart, int n, int H, int C, float slope) {
+  __shared__ __attribute__((aligned(16))) float sXs[BS * XW];   // source rows, [j][h*16+c]
+  __shared__ __attribute__((aligned(16))) float sE[MH * BHS];   // edge logits of the block
+  __shared__ __attribute__((aligned(16))) float sD[MH * BHS];   // d logit (+ share) of the block
+  __shared__ __attribute__((aligned(16))) float sO[BT * XW];    // dOut rows of the block
+  __shared__ __attribute__((aligned(16))) float sM[MH * BT], sInv[MH * BT], sR[MH * BT],
+      sAd[MH * BT], sSh[MH * BT];
+  __shared__ uint32_t sPres[2][BT];
+  __shared__ __attribute__((aligned(16))) float sW[D * MH];
+
+  const int NS = (n + BS - 1) / BS;
+  int64_t g;
+  int js;
+  block_gt(NS, g, js);
+  const int t = threadIdx.x, lane = t & 63, hh = t >> 6;  // wave hh: head hh in [B]
+  const int li = lane & 15, lk = lane >> 4;
+  const int j0 = js * BS;
+  const int HC = H * C;
+  const int64_t row0 = g * n;
+  const int64_t Ntot = (int64_t)gridDim.x / NS * n;
+  const int E0 = n * (n - 1);
+  constexpr bool eidm = EIDM;
+  const rsrc_t rea = eidm ? make_rsrc(nullptr, 0u)
+                          : make_rsrc(ea + g * (int64_t)E0 * D, (uint32_t)(4 * E0 * D));
+  const rsrc_t rdo = make_rsrc(dout + row0 * HC, (uint32_t)(4 * n * HC));
+  const int HQ = HC >> 2;  // 16-B chunks per dOut row
+  const float slope2 = slope * L2E;
+  const bool hv = hh < H;
+
+  if (t < D * MH) sW[t] = (t % MH) < H ? wf[(t / MH) * hl_pad + col0 + t % MH] : 0.f;
+  if (eidm && t < 2 * BT) sPres[t >> 4][t & 15] = 0u;
+  // source rows of the tile (constant): xs_h padded to 16 columns per head
+  for (int idx = t; idx < BS * MH * 16; idx += WT) {
+    const int jl = idx >> 7, hc16 = idx & 127, h = hc16 >> 4, c = hc16 & 15, j = j0 + jl;
+    sXs[jl * XW + hc16] = (j < n && h < H && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
+  }
+  for (int idx = t; idx < BT * XW; idx += WT) sO[idx] = 0.f;  // padding columns stay zero
+  // a_src of this lane's sources (j = j0 + 16jt + li) for head hh
+  float asrc[2];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    const int j = j0 + 16 * jt + li;
+    asrc[jt] = (hv && j < n) ? xs[(row0 + j) * ldx + HC + hh] : 0.f;
+  }
+  __syncthreads();
+
+  // edge slots: 512 per block, each split over 4 lanes (quarter = lane & 3)
+  constexpr int DQ = (D + 3) / 4;
+  const int qtr = t & 3, d0 = qtr * DQ;
+  float wacc[DQ][MH];
+#pragma unroll
+  for (int d = 0; d < DQ; ++d)
+#pragma unroll
+    for (int h = 0; h < MH; ++h) wacc[d][h] = 0.f;
+  f4 dacc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  float das[2] = {0.f, 0.f};
+
+  // the next block's edge quarters, dOut chunk and target vectors (prefetch)
+  float evn[4][DQ], evc[4][DQ];
+  f32x4 don;
+  float vecn[5];
+  auto slot = [&](int k, int i0, int& il, int& jl) {
+    const int s = (t >> 2) + 128 * k;
+    const bool along_i = !eidm && (j0 + BS <= i0);
+    il = along_i ? (s & 15) : (s >> 5);
+    jl = along_i ? (s >> 4) : (s & 31);
+  };
+  auto issue = [&](int i0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int il, jl;
+      slot(k, i0, il, jl);
+      const int i = i0 + il, j = j0 + jl;
+      int cid = -1;
+      int64_t gid = -1;
+      if constexpr (eidm) gid = (i < n && j < n && i != j) ? eid[(row0 + i) * n + j] : -1;
+      else cid = canon_id(i, j, n);
+      if constexpr (eidm) {
+        const bool ok = gid >= 0;
+        const float* p = ea + (ok ? gid : 0) * D + d0;
+#pragma unroll
+        for (int dd = 0; dd < DQ; ++dd) evn[k][dd] = (ok && d0 + dd < D) ? p[dd] : 0.f;
+      } else if (SV2N_FATTN_ABLATE == 4) {
+#pragma unroll
+        for (int dd = 0; dd < DQ; ++dd) evn[k][dd] = (float)(cid & 7) * 0.01f;
+      } else {
+#pragma unroll
+        for (int dd = 0; dd < DQ; ++dd)
+          evn[k][dd] = (d0 + dd < D) ? bld(rea, cid >= 0 ? 4 * (cid * D + d0 + dd) : OOB) : 0.f;
+      }
+    }
+    {
+      const int r = t / HQ, cq = t - r * HQ, i = i0 + r;
+      don = bld4(rdo, (r < BT && i < n) ? 4 * (i * HC + 4 * cq) : OOB);
+    }
+    if (t < MH * BT) {
+      const int h = t >> 4, il = t & 15, i = i0 + il;
+      const bool ok = h < H && i < n;
+      const int64_t row = row0 + (ok ? i : 0);
+      vecn[0] = ok ? stats[row * 4 * H + h] : 0.f;
+      vecn[1] = ok ? stats[row * 4 * H + H + h] : 0.f;
+      vecn[2] = ok ? rs[row * 4 * H + h] : 0.f;
+      vecn[3] = ok ? xs[row * ldx + HC + H + h] : 0.f;
+      vecn[4] = ok ? rs[row * 4 * H + 3 * H + h] : 0.f;
+    }
+  };
+
+  issue(0);
+  int par = 0;
+  for (int i0 = 0; i0 < n; i0 += BT, par ^= 1) {
+    // ---- [A] stage the block: logits (2 heads per lane of a quad), dOut, vectors ----
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int d = 0; d < DQ; ++d) evc[k][d] = evn[k][d];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      // partial logits over this lane's quarter of the row (scalar FMAs: no
+      // packed copies of the prefetched values), completed over the quad
+      float lf[MH];
+#pragma unroll
+      for (int h = 0; h < MH; ++h) lf[h] = 0.f;
+#pragma unroll
+      for (int dd = 0; dd < DQ; ++dd) {
+        const float* wr = sW + min(d0 + dd, D - 1) * MH;
+        const f4 wa = *reinterpret_cast<const f4*>(wr);
+        const f4 wb = *reinterpret_cast<const f4*>(wr + 4);
+        const float wv[MH] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+        for (int h = 0; h < MH; ++h) lf[h] = fmaf(evc[k][dd], wv[h], lf[h]);
+      }
+#pragma unroll
+      for (int h = 0; h < MH; ++h) {
+        lf[h] += dpp_xor1(lf[h]);
+        lf[h] += dpp_xor2(lf[h]);
+      }
+      int il, jl;
+      slot(k, i0, il, jl);
+      float* dst = sE + il * RS + jl;
+      // lane quarter q stores heads q and q + 4
+      dst[qtr * BHS] = qtr == 0 ? lf[0] : qtr == 1 ? lf[1] : qtr == 2 ? lf[2] : lf[3];
+      dst[(qtr + 4) * BHS] = qtr == 0 ? lf[4] : qtr == 1 ? lf[5] : qtr == 2 ? lf[6] : lf[7];
+      if (eidm && qtr == 0) {
+        const int i = i0 + il, j = j0 + jl;
+        const bool pres = i < n && j < n && i != j && eid[(row0 + i) * n + j] >= 0;
+        if (pres) atomicOr(&sPres[par][il], 1u << jl);
+      }
+    }
+    {
+      const int r = t / HQ, cq = t - r * HQ;
+      if (r < BT) {
+        const int cg = 4 * cq, h = cg / C, c = cg - h * C;
+        *reinterpret_cast<f4*>(sO + r * XW + h * 16 + c) = f4{don.x, don.y, don.z, don.w};
+      }
+    }
+    if (t < MH * BT) {
+      sM[t] = vecn[0];
+      sInv[t] = vecn[1];
+      sR[t] = vecn[2];
+      sAd[t] = vecn[3];
+      sSh[t] = vecn[4];
+    }
+    if (i0 + BT < n) issue(i0 + BT);
+    __syncthreads();
+
+    // ---- [B] wave hh ----
+    if (hv && SV2N_FATTN_ABLATE != 5) {
+      const bool clean =
+          !eidm && (j0 + BS <= i0 || i0 + BT <= j0) && j0 + BS <= n && i0 + BT <= n;
+      // dP[i][j] = dOut_h[i] · xs_h[j]: rows i = 4lk + r, columns j = 16jt + li
+      f4 pacc[2];
+      const f4 oa = *reinterpret_cast<const f4*>(sO + li * XW + hh * 16 + 4 * lk);
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        const f4 xb = *reinterpret_cast<const f4*>(sXs + (16 * jt + li) * XW + hh * 16 + 4 * lk);
+        f4 pa = {0.f, 0.f, 0.f, 0.f};
+        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.x, xb.x, pa, 0, 0, 0);
+        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.y, xb.y, pa, 0, 0, 0);
+        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.z, xb.z, pa, 0, 0, 0);
+        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.w, xb.w, pa, 0, 0, 0);
+        pacc[jt] = pa;
+      }
+      const int q0 = hh * BT + 4 * lk;
+      const f4 m4 = *reinterpret_cast<const f4*>(sM + q0);
+      const f4 inv4 = *reinterpret_cast<const f4*>(sInv + q0);
+      const f4 r4 = *reinterpret_cast<const f4*>(sR + q0);
+      const f4 ad4 = *reinterpret_cast<const f4*>(sAd + q0);
+      const f4 sh4 = *reinterpret_cast<const f4*>(sSh + q0);
+      const float mv[4] = {m4.x, m4.y, m4.z, m4.w}, iv[4] = {inv4.x, inv4.y, inv4.z, inv4.w};
+      const float rv[4] = {r4.x, r4.y, r4.z, r4.w}, av[4] = {ad4.x, ad4.y, ad4.z, ad4.w};
+      const float shv[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
+      float pd[2][4], rowacc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        const float dpv[4] = {pacc[jt].x, pacc[jt].y, pacc[jt].z, pacc[jt].w};
+        const int jl = 16 * jt + li, j = j0 + jl;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int il = 4 * lk + r, i = i0 + il;
+          bool valid = true;
+          if (!clean) {
+            valid = i < n && j < n && i != j;
+            if constexpr (eidm) valid = valid && ((sPres[par][il] >> jl) & 1u);
+          }
+          const int e = hh * BHS + il * RS + jl;
+          const float v = asrc[jt] + av[r] + sE[e];
+          const float p = valid ? fexp2(v * (v > 0.f ? L2E : slope2) - mv[r]) * iv[r] : 0.f;
+          float pk = p, dP = dpv[r];
+          if constexpr (KEEP) {
+            const bool kp = valid && keep[((g * H + hh) * (int64_t)n + i) * n + j] != 0;
+            pk = kp ? p * keep_scale : 0.f;
+            dP = kp ? dP * keep_scale : 0.f;
+          }
+          const float ds = p * (dP - rv[r]);
+          const float dl = valid ? (v > 0.f ? ds : ds * slope) : 0.f;
+          pd[jt][r] = pk;
+          das[jt] += dl;
+          rowacc[r] += dl;
+          sD[e] = valid ? dl + shv[r] : 0.f;
+        }
+      }
+      // d a_dst partial of this source tile: row sums over the 16 lanes li
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s = row16_sum(rowacc[r]);
+        const int i = i0 + 4 * lk + r;
+        if (li == 0 && i < n) adst_part[((int64_t)js * Ntot + row0 + i) * H + hh] = s;
+      }
+      // dxs_h[j][c] += Σ_i P[i][j] dOut_h[i][c]: A = P from registers (k = 4lk + s)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float ob = sO[(4 * lk + s) * XW + hh * 16 + li];
+          dacc[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pd[jt][s], ob, dacc[jt], 0, 0, 0);
+        }
+      }
+    }
+    if constexpr (eidm) {
+      if (t < BT) sPres[par ^ 1][t] = 0u;
+    }
+    __syncthreads();
+
+    // ---- [C] dW̃ += edge_attr ⊗ (d logit + the self loop's share) ----
+#pragma unroll
+    for (int k = 0; k < (SV2N_FATTN_ABLATE == 6 ? 0 : 4); ++k) {
+      int il, jl;
+      slot(k, i0, il, jl);
+      const float* dr = sD + il * RS + jl;
+#pragma unroll
+      for (int h = 0; h < MH; ++h) {
+        const float dlw = dr[h * BHS];
+#pragma unroll
+        for (int d = 0; d < DQ; ++d) wacc[d][h] = fmaf(evc[k][d], dlw, wacc[d][h]);
+      }
+    }
+  }
+
+  // ---- d a_src (complete: every target was visited) + the self loop ----
+  if (hv) {
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      const float s = lk_sum(das[jt]);
+      const int j = j0 + 16 * jt + li;
+      if (lk == 0 && j < n) {
+        const int64_t row = row0 + j;
+        dxs[row * ldx + HC + hh] = s + rs[row * 4 * H + H + hh];
+      }
+    }
+    // ---- dxs_h rows: accumulated products + the self loop's P·dOut ----
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      const float dv[4] = {dacc[jt].x, dacc[jt].y, dacc[jt].z, dacc[jt].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = j0 + 16 * jt + 4 * lk + r, c = li;
+        if (j < n && c < C) {
+          const int64_t row = row0 + j;
+          dxs[row * ldx + hh * C + c] =
+              fmaf(rs[row * 4 * H + 2 * H + hh], dout[row * HC + hh * C + c], dv[r]);
+        }
+      }
+    }
+  }
+  {
+    const int padc = ldx - HC - 2 * H;
+    for (int idx = t; idx < BS * padc; idx += WT) {
+      const int jl = idx / padc, j = j0 + jl;
+      if (j < n) dxs[(row0 + j) * ldx + HC + 2 * H + (idx - jl * padc)] = 0.f;
+    }
+  }
+  // ---- dW̃ partial of the workgroup: the 4 same-quarter lanes of each 16-lane
+  //      row (DPP), then the 32 rows of the workgroup ----
+  __syncthreads();
+  float* sRed = sE;  // [32][D*MH] <= MH*BHS floats
+#pragma unroll
+  for (int d = 0; d < DQ; ++d)
+#pragma unroll
+    for (int h = 0; h < MH; ++h) {
+      float v = wacc[d][h];
+      v += dppf<0x124>(v);
+      v += dppf<0x128>(v);
+      if (li < 4 && d0 + d < D) sRed[(hh * 4 + lk) * (D * MH) + (d0 + d) * MH + h] = v;
+    }
+  __syncthreads();
+  const int64_t P = (int64_t)gridDim.x;
+  const int64_t part = g * NS + js;
+  if (t < D * MH) {
+    const int d = t / MH, h = t - d * MH;
+    if (h < H) {
+      float s = 0.f;
+#pragma unroll
+      for (int r = 0; r < 32; ++r) s += sRed[r * (D * MH) + t];
+      wpart[(int64_t)(d * H + h) * P + part] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward: d a_dst (Σ over source tiles + self loop) and dW̃ (Σ of partials)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(PT) void k_fattn_bfinish(
+    const float* __restrict__ adst_part, const float* __restrict__ rs, float* __restrict__ dxs,
+    int ldx, int64_t N, int NS, int H, int HC, const float* __restrict__ wpart, int64_t P,
+    float* __restrict__ dwf, int hl_pad, int col0, int64_t nA) {
+  __shared__ float sred[PT];
+  const int t = threadIdx.x;
+  if ((int64_t)blockIdx.x < nA) {
+    const int64_t idx = (int64_t)blockIdx.x * PT + t;
+    if (idx < N * H) {
+      const int64_t i = idx / H;
+      const int h = (int)(idx - i * H);
+      float s = 0.f;
+      for (int q = 0; q < NS; ++q) s += adst_part[(q * N + i) * H + h];
+      dxs[i * ldx + HC + H + h] = s + rs[i * 4 * H + H + h];
+    }
+    return;
+  }
+  const int q = (int)(blockIdx.x - nA);  // output (d, h) = q / H, q % H
+  const float* src = wpart + (int64_t)q * P;
+  float s = 0.f;
+  for (int64_t k = t; k < P; k += PT) s += src[k];
+  sred[t] = s;
+  __syncthreads();
+  for (int w = PT / 2; w > 0; w >>= 1) {
+    if (t < w) sred[t] += sred[t + w];
+    __syncthreads();
+  }
+  if (t == 0) {
+    const int d = q / H, h = q - d * H;
+    dwf[d * hl_pad + col0 + h] = sred[0];
+  }
+}
+
+}  // namespace fused
+}  // namespace sv2n
+
+// ============================ C-ABI ========================================
+using namespace sv2n::fused;
+
+#define SV2N_FVAR(M, DD)                       \
+  if (eid) {                                     \
+    if (keep) M(DD, true, true); else M(DD, true, false);  \
+  } else {                                       \
+    if (keep) M(DD, false, true); else M(DD, false, false); \
+  }
+
+extern "C" int sv2n_gat_attn_fused_supported(int n, int heads, int channels, int edge_dim) {
+  const bool d_ok = edge_dim == 3 || edge_dim == 6 || edge_dim == 12;
+  return (n > 32 && n <= 256 && heads >= 1 && heads <= MH && channels >= 4 && channels <= 16 &&
+          channels % 4 == 0 && d_ok)
+             ? 1
+             : 0;
+}
+
+static int fused_check(const float* xs, int ldx, const float* ea, int edge_dim, const float* wf,
+                       int hl_pad, int col0, int64_t B, int n, int H, int C, int act) {
+  if (!xs || !ea || !wf || B <= 0) return SV2N_ERR_ARG;
+  if (!sv2n_gat_attn_fused_supported(n, H, C, edge_dim) || act < 0 || act > 3)
+    return SV2N_ERR_SHAPE;
+  if (col0 < 0 || col0 + H > hl_pad) return SV2N_ERR_SHAPE;
+  if (ldx < H * C + 2 * H || (ldx & 3) || ((uintptr_t)xs & 15)) return SV2N_ERR_ALIGN;
+  if ((int64_t)n * ldx * 4 > 0x7fffffff) return SV2N_ERR_SHAPE;
+  if ((int64_t)n * (n - 1) * edge_dim * 4 > 0x7fffff00LL) return SV2N_ERR_SHAPE;
+  if (B * ((n + 31) / 32) > 0x7fffffffLL) return SV2N_ERR_SHAPE;
+  return 0;
+}
+
+extern "C" int sv2n_gat_attn_fused_fwd(const float* xs, int ldx, const float* edge_attr,
+                                       int edge_dim, const float* wfold, int hl_pad, int col0,
+                                       const int32_t* eid, const float* bias, const uint8_t* keep,
+                                       float keep_scale, float* y, float* agg, float* stats,
+                                       int64_t num_graphs, int n, int heads, int channels,
+                                       int concat, int act, float negative_slope,
+                                       hipStream_t stream) {
+  if (!y || ((agg == nullptr) != (stats == nullptr))) return SV2N_ERR_ARG;
+  if (int rc = fused_check(xs, ldx, edge_attr, edge_dim, wfold, hl_pad, col0, num_graphs, n,
+                           heads, channels, act))
+    return rc;
+  if (!eid && ((uintptr_t)edge_attr & 15)) return SV2N_ERR_ALIGN;
+  const dim3 grid((unsigned)(num_graphs * ((n + FT - 1) / FT)));
+#define SV2N_FFWD1(DD, EM, KP)                                                                  \
+  hipLaunchKernelGGL((k_fattn_fwd<DD, EM, KP>), grid, dim3(WT), 0, stream, xs, ldx, edge_attr, wfold,     \
+                     hl_pad, col0, eid, bias, keep, keep_scale, y, agg, stats, n, heads,        \
+                     channels, act, concat, negative_slope)
+  switch (edge_dim) {
+    case 3: SV2N_FVAR(SV2N_FFWD1, 3) break;
+    case 6: SV2N_FVAR(SV2N_FFWD1, 6) break;
+    default: SV2N_FVAR(SV2N_FFWD1, 12) break;
+  }
+#undef SV2N_FFWD1
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t sv2n_gat_attn_fused_bwd_workspace(int64_t num_graphs, int n, int heads,
+                                                     int channels, int edge_dim) {
+  const int64_t N = num_graphs * n;
+  const int64_t NS = (n + BS - 1) / BS;
+  return N * heads * channels        // dout
+         + N * 4 * heads            // rs
+         + NS * N * heads           // d a_dst partials
+         + (int64_t)edge_dim * heads * num_graphs * NS;  // dW̃ partials
+}
+
+extern "C" int sv2n_gat_attn_fused_bwd(const float* dy, const float* y, const float* agg,
+                                       const float* stats, const float* xs, int ldx,
+                                       const float* edge_attr, int edge_dim, const float* wfold,
+                                       int hl_pad, int col0, const int32_t* eid,
+                                       const uint8_t* keep, float keep_scale, float* dxs,
+                                       float* dbias_partial, float* dwfold, float* workspace,
+                                       int64_t workspace_floats, int64_t num_graphs, int n,
+                                       int heads, int channels, int concat, int act,
+                                       float negative_slope, hipStream_t stream) {
+  if (!dy || !y || !agg || !stats || !dxs || !dbias_partial || !dwfold || !workspace)
+    return SV2N_ERR_ARG;
+  if (int rc = fused_check(xs, ldx, edge_attr, edge_dim, wfold, hl_pad, col0, num_graphs, n,
+                           heads, channels, act))
+    return rc;
+  if (!eid && ((uintptr_t)edge_attr & 15)) return SV2N_ERR_ALIGN;
+  const int H = heads, C = channels, HC = H * C;
+  if (((uintptr_t)dxs & 15)) return SV2N_ERR_ALIGN;
+  const int64_t need = sv2n_gat_attn_fused_bwd_workspace(num_graphs, n, H, C, edge_dim);
+  if (workspace_floats < need) return SV2N_ERR_WORKSPACE;
+  const int64_t N = num_graphs * n;
+  const int NT = (n + FT - 1) / FT, NS = (n + BS - 1) / BS;
+  float* dout = workspace;
+  float* rs = dout + N * HC;
+  float* adst = rs + N * 4 * H;
+  float* wpart = adst + (int64_t)NS * N * H;
+  if (((uintptr_t)dout & 15)) return SV2N_ERR_ALIGN;
+  hipLaunchKernelGGL(k_fattn_bprep, dim3((unsigned)(num_graphs * NT)), dim3(PT), 0, stream, dy,
+                     y, agg, stats, xs, ldx, keep, keep_scale, dout, rs, dbias_partial, n, H, C,
+                     act, concat, negative_slope);
+  const dim3 grid((unsigned)(num_graphs * NS));
+#define SV2N_FBWD1(DD, EM, KP)                                                                  \
+  hipLaunchKernelGGL((k_fattn_bwd<DD, EM, KP>), grid, dim3(WT), 0, stream, xs, ldx, edge_attr, wfold,     \
+                     hl_pad, col0, eid, keep, keep_scale, dout, stats, rs, dxs, adst, wpart, n, \
+                     H, C, negative_slope)
+  switch (edge_dim) {
+    case 3: SV2N_FVAR(SV2N_FBWD1, 3) break;
+    case 6: SV2N_FVAR(SV2N_FBWD1, 6) break;
+    default: SV2N_FVAR(SV2N_FBWD1, 12) break;
+  }
+#undef SV2N_FBWD1
+  const int64_t nA = (N * H + PT - 1) / PT;
+  hipLaunchKernelGGL(k_fattn_bfinish, dim3((unsigned)(nA + edge_dim * H)), dim3(PT), 0, stream,
+                     adst, rs, dxs, ldx, N, NS, H, HC, wpart, num_graphs * NS, dwfold, hl_pad,
+                     col0, nA);
+  return (int)hipGetLastError();
+}

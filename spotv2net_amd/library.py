@@ -42,6 +42,14 @@ _SCHEMAS = {
     "gat_attn_tiled_fwd": "(Tensor xs, Tensor? ae, int num_edges, Tensor? eid, Tensor? rowmask, "
                           "Tensor? bias, Tensor? keep, float keep_scale, int num_graphs, int n, "
                           "int heads, int channels, bool concat, int act, float slope) -> Tensor",
+    "gat_attn_fused_fwd": "(Tensor xs, Tensor edge_attr, Tensor wfold, int col0, Tensor? eid, "
+                          "Tensor? bias, Tensor? keep, float keep_scale, int num_graphs, int n, "
+                          "int heads, int channels, bool concat, int act, float slope, "
+                          "bool training) -> (Tensor, Tensor, Tensor)",
+    "gat_attn_fused_bwd": "(Tensor dy, Tensor y, Tensor agg, Tensor stats, Tensor xs, "
+                          "Tensor edge_attr, Tensor wfold, int col0, Tensor? eid, Tensor? keep, "
+                          "float keep_scale, Tensor(a!) dwfold, int num_graphs, int n, int heads, "
+                          "int channels, bool concat, int act, float slope) -> (Tensor, Tensor)",
     "gat_attn_bwd": "(Tensor dy, Tensor y, Tensor xs, Tensor psave, Tensor? keep, "
                     "float keep_scale, Tensor? rowmask, bool with_ae, int num_graphs, int n, "
                     "int heads, int channels, bool concat, int act, float slope, "
@@ -362,6 +370,94 @@ def _gat_attn_tiled_fwd(xs, ae, num_edges, eid, rowmask, bias, keep, keep_scale,
 def _gat_attn_tiled_fwd_fake(xs, ae, num_edges, eid, rowmask, bias, keep, keep_scale, num_graphs,
                              n, heads, channels, concat, act, slope):
     return xs.new_empty((num_graphs * n, _oc(heads, channels, concat)))
+
+
+def fused_supported(n: int, heads: int, channels: int, edge_dim: int) -> bool:
+    """Whether sv2n_gat_attn_fused_* take this layer shape (include/sv2n.h)."""
+    return bool(_lib.load().sv2n_gat_attn_fused_supported(n, heads, channels, edge_dim))
+
+
+def _fused_common(xs, edge_attr, wfold, col0, eid, num_graphs, n, heads, channels):
+    N = num_graphs * n
+    _rows(xs, N, heads * channels + 2 * heads, "xs")
+    _need(xs.stride(0) % 4 == 0 and xs.data_ptr() % 16 == 0, "xs: 16-B aligned rows needed")
+    _dense(edge_attr, wfold, eid)
+    _need(edge_attr.dim() == 2, "edge_attr must be [E, D]")
+    _need(wfold.dim() == 2 and wfold.shape[0] == edge_attr.shape[1] and
+          0 <= col0 and col0 + heads <= wfold.shape[1], "wfold / col0 shape")
+    if eid is None:
+        _need(edge_attr.shape[0] == N * (n - 1), "canonical edge_attr needs num_graphs*n*(n-1) rows")
+        _need(edge_attr.data_ptr() % 16 == 0, "edge_attr must be 16-B aligned")
+    else:
+        _need(eid.numel() == N * n and eid.dtype == torch.int32, "eid shape")
+    _need(fused_supported(n, heads, channels, edge_attr.shape[1]), "unsupported fused shape")
+
+
+@_impl("gat_attn_fused_fwd")
+def _gat_attn_fused_fwd(xs, edge_attr, wfold, col0, eid, bias, keep, keep_scale, num_graphs, n,
+                        heads, channels, concat, act, slope, training):
+    lib = _lib.load()
+    _f32(xs, edge_attr, wfold, bias)
+    _fused_common(xs, edge_attr, wfold, col0, eid, num_graphs, n, heads, channels)
+    _dense(bias, keep)
+    N = num_graphs * n
+    _need(bias is None or bias.numel() == _oc(heads, channels, concat), "bias shape")
+    _need(keep is None or keep.numel() == num_graphs * heads * n * n, "keep shape")
+    dev = xs.device
+    y = torch.empty(N, _oc(heads, channels, concat), device=dev)
+    agg = torch.empty(N, heads * channels, device=dev) if training else torch.empty(0, device=dev)
+    stats = torch.empty(N, 4 * heads, device=dev) if training else torch.empty(0, device=dev)
+    _lib.check(lib.sv2n_gat_attn_fused_fwd(
+        xs.data_ptr(), xs.stride(0), edge_attr.data_ptr(), edge_attr.shape[1], wfold.data_ptr(),
+        wfold.shape[1], col0, _p(eid), _p(bias), _p(keep), keep_scale, y.data_ptr(), _p(agg),
+        _p(stats), num_graphs, n, heads, channels, int(concat), act, slope, _st(xs)),
+        "sv2n_gat_attn_fused_fwd")
+    return y, agg, stats
+
+
+@_fake("gat_attn_fused_fwd")
+def _gat_attn_fused_fwd_fake(xs, edge_attr, wfold, col0, eid, bias, keep, keep_scale, num_graphs,
+                             n, heads, channels, concat, act, slope, training):
+    N = num_graphs * n
+    return (xs.new_empty((N, _oc(heads, channels, concat))),
+            xs.new_empty((N, heads * channels) if training else (0,)),
+            xs.new_empty((N, 4 * heads) if training else (0,)))
+
+
+@_impl("gat_attn_fused_bwd")
+def _gat_attn_fused_bwd(dy, y, agg, stats, xs, edge_attr, wfold, col0, eid, keep, keep_scale,
+                        dwfold, num_graphs, n, heads, channels, concat, act, slope):
+    lib = _lib.load()
+    _f32(dy, y, agg, stats, xs, edge_attr, wfold, dwfold)
+    _fused_common(xs, edge_attr, wfold, col0, eid, num_graphs, n, heads, channels)
+    N, OC = num_graphs * n, _oc(heads, channels, concat)
+    _dense(dy, y, agg, stats, keep, dwfold)
+    _need(dy.numel() == N * OC and y.numel() == N * OC, "dy / y shape")
+    _need(agg.numel() == N * heads * channels and stats.numel() == N * 4 * heads,
+          "agg / stats: pass the training forward's outputs")
+    _need(keep is None or keep.numel() == num_graphs * heads * n * n, "keep shape")
+    _need(dwfold.shape == wfold.shape, "dwfold shape")
+    dev = xs.device
+    dxs = torch.empty_like(xs)
+    dbp = torch.empty(num_graphs * ((n + 31) // 32), OC, device=dev)
+    ws_n = lib.sv2n_gat_attn_fused_bwd_workspace(num_graphs, n, heads, channels,
+                                                 edge_attr.shape[1])
+    ws = torch.empty(ws_n, device=dev)
+    _lib.check(lib.sv2n_gat_attn_fused_bwd(
+        dy.data_ptr(), y.data_ptr(), agg.data_ptr(), stats.data_ptr(), xs.data_ptr(),
+        xs.stride(0), edge_attr.data_ptr(), edge_attr.shape[1], wfold.data_ptr(),
+        wfold.shape[1], col0, _p(eid), _p(keep), keep_scale, dxs.data_ptr(), dbp.data_ptr(),
+        dwfold.data_ptr(), ws.data_ptr(), ws_n, num_graphs, n, heads, channels, int(concat), act,
+        slope, _st(xs)), "sv2n_gat_attn_fused_bwd")
+    return dxs, dbp
+
+
+@_fake("gat_attn_fused_bwd")
+def _gat_attn_fused_bwd_fake(dy, y, agg, stats, xs, edge_attr, wfold, col0, eid, keep,
+                             keep_scale, dwfold, num_graphs, n, heads, channels, concat, act,
+                             slope):
+    return (torch.empty_like(xs),
+            xs.new_empty((num_graphs * ((n + 31) // 32), _oc(heads, channels, concat))))
 
 
 def _dae_shape(edge_order, num_graphs, n, heads):

@@ -8,6 +8,10 @@ Forward (reference utils/models.py:145-148 with PyG GATConv inside):
   per layer  sv2n::project      xs = x · Waugᵀ  (f32-accurate split MFMA, or bf16)
              sv2n::gat_attn_fwd loops/leaky/softmax/dropout/aggregate/bias/act
              dropout between layers (model-level, torch RNG mask)
+Edge-fused mode (32 < n <= 256, narrow edge_attr: the C5 shapes, see
+``_use_fused``): no edge pass; sv2n::gat_attn_fused_fwd computes each layer's
+edge logits from edge_attr inside the attention, and sv2n::gat_attn_fused_bwd
+returns the layer's dW̃ columns directly (no logit / d-logit planes).
 Backward, layers in reverse:
   sv2n::gat_attn_bwd  -> d xs, d ae, bias partials
   sv2n::gat_wgrad     -> dWaugᵀ = xᵀ·dxs (split-K) + fold epilogue, ACCUMULATED
@@ -26,6 +30,7 @@ parameters: no per-parameter autograd launches in the captured step.
 from __future__ import annotations
 
 import contextlib
+import os
 import threading
 from typing import Optional, Sequence
 
@@ -33,7 +38,7 @@ import torch
 
 from . import _lib, library  # noqa: F401  (library registers torch.ops.sv2n)
 from .layout import GraphLayout
-from .library import edge_order
+from .library import edge_order, fused_supported
 from .ops import _aligned, _require_device, resolve_precision
 
 
@@ -141,6 +146,31 @@ def _hp(L: int, H: int) -> int:
     raise ValueError(f"at most 32 (layers x heads) edge-logit columns supported, got {L * H}")
 
 
+# "auto" (the rule in _use_fused), "on" (whenever the kernels take the shape) or
+# "off" (always edge pass + planes): an A/B switch for tests and measurements
+EDGE_FUSED = os.environ.get("SV2N_EDGE_FUSED", "auto")
+LAST_PATH = {"attention": None}  # which attention path the last forward took (tests)
+
+
+def _use_fused(layout: GraphLayout, convs, D: int, num_edges: int) -> bool:
+    """Edge-fused attention (sv2n_attn_fused.hip) instead of edge pass + planes.
+
+    Per layer the fused kernels read edge_attr twice (forward, backward):
+    8·D bytes per edge.  The planes path reads it twice for all L layers
+    (8·D/L per layer) but writes and re-reads a logit plane and a d-logit
+    plane: 16·H bytes per edge and layer.  Fused wins when
+    8·D·(1 - 1/L) < 16·H, i.e. D·(L-1) < 2·H·L (C5: D 12, L 3, H 8)."""
+    if EDGE_FUSED == "off" or not layout.tiled or num_edges == 0:
+        return False
+    if layout.kind == "block" and layout.eid is None:
+        return False
+    L = len(convs)
+    H = convs[0].heads
+    if not all(fused_supported(layout.n, c.heads, c.out_channels, D) for c in convs):
+        return False
+    return EDGE_FUSED == "on" or D * (L - 1) < 2 * H * L
+
+
 def _opt(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return None if t is None or t.numel() == 0 else t
 
@@ -179,12 +209,17 @@ class _GATStack(torch.autograd.Function):
             [c.att_edge for c in convs] if use_edge else [], [c.heads for c in convs],
             [c.out_channels for c in convs], hp, need_t, use_edge, bf16)
 
-        # 2) edge logits of every layer in one pass over edge_attr (sv2n::edge_logits)
+        # 2) edge logits of every layer in one pass over edge_attr (sv2n::edge_logits),
+        #    unless the attention computes them itself (edge-fused mode)
         aes = [None] * L
         ei = layout.edge_index if layout.kind == "block" else None
         # canonical batches: AE in edge order [E][H] (coalesced on both sides)
         eo = bool(use_edge and not tiled and edge_order(ei, n))
-        if use_edge:
+        fused = bool(use_edge and _use_fused(layout, convs, ea.size(1), ea.size(0)))
+        feid = layout.eid if (fused and layout.kind == "block") else None
+        need_saved = training or any(ctx.needs_input_grad)
+        LAST_PATH["attention"] = "fused" if fused else ("tiled" if tiled else "small")
+        if use_edge and not fused:
             aes = list(ops.edge_logits(ea, wf, ei, layout.canon, L, H, B, n, tiled))
             if tiled and ea.size(0) == 0:
                 aes = [None] * L
@@ -192,6 +227,7 @@ class _GATStack(torch.autograd.Function):
         # 3) layers
         xin = _aligned(x)
         saved_x, saved_xs, saved_y, saved_p, saved_keep, saved_drop = [], [], [], [], [], []
+        saved_st = []
         for l, c in enumerate(convs):
             Hc, C = c.heads, c.out_channels
             F = c.in_channels
@@ -207,7 +243,13 @@ class _GATStack(torch.autograd.Function):
                 else:
                     keep = (torch.rand(B, Hc, kn, kn, device=dev) >= c.dropout).to(torch.uint8)
                     kscale = 1.0 / (1.0 - c.dropout)
-            if tiled:
+            st = None
+            if fused:
+                # saved: pre-bias head aggregates + per-row softmax statistics
+                y, ps, st = ops.gat_attn_fused_fwd(xs, ea, wf, l * H, feid, c.bias, keep, kscale,
+                                                   B, n, Hc, C, c.concat, act,
+                                                   float(c.negative_slope), need_saved)
+            elif tiled:
                 # nothing saved: the backward recomputes the attention from xs and ae
                 y = ops.gat_attn_tiled_fwd(xs, aes[l], layout.num_edges, layout.eid,
                                            layout.rowmask, c.bias, keep, kscale, B, n, Hc, C,
@@ -229,6 +271,7 @@ class _GATStack(torch.autograd.Function):
             saved_xs.append(xs)
             saved_y.append(y)
             saved_p.append(ps)
+            saved_st.append(st)
             saved_keep.append(keep)
             saved_drop.append(dmask)
             xin = out
@@ -237,11 +280,12 @@ class _GATStack(torch.autograd.Function):
         ctx.layout = layout
         ctx.direct = _direct_mode()
         ctx.bf16 = bf16
-        ctx.meta = (L, act, use_edge, hp, H, eo)
+        ctx.meta = (L, act, use_edge, hp, H, eo, fused)
+        ctx.feid = feid
         ctx.kscales = [(1.0 / (1.0 - c.dropout)) if (training and 0.0 < c.dropout < 1.0) else
                        (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs]
-        ctx.save_for_backward(ea, *saved_x, *saved_xs, *saved_y, *saved_p, *saved_keep,
-                              *saved_drop, *waugs, *planes_t)
+        ctx.save_for_backward(ea, wf if fused else None, *saved_x, *saved_xs, *saved_y,
+                              *saved_p, *saved_st, *saved_keep, *saved_drop, *waugs, *planes_t)
         return xin
 
     @staticmethod
@@ -249,14 +293,15 @@ class _GATStack(torch.autograd.Function):
         ops = torch.ops.sv2n
         convs = ctx.convs
         layout: GraphLayout = ctx.layout
-        L, act, use_edge, hp, H, eo = ctx.meta
+        L, act, use_edge, hp, H, eo, fused = ctx.meta
         sv = ctx.saved_tensors
-        ea = sv[0]
-        k = 1
+        ea, wf = sv[0], sv[1]
+        k = 2
         xs_in = sv[k:k + L]; k += L
         xss = sv[k:k + L]; k += L
         ys = sv[k:k + L]; k += L
         pss = sv[k:k + L]; k += L
+        sts = sv[k:k + L]; k += L
         keeps = sv[k:k + L]; k += L
         drops = sv[k:k + L]; k += L
         waugs = sv[k:k + L]; k += L
@@ -269,13 +314,19 @@ class _GATStack(torch.autograd.Function):
         need_x0 = ctx.needs_input_grad[0]
         params = [p for c in convs for p in layer_params(c)]
         grad_of = _GradTargets(params, ctx.needs_input_grad[8:], ctx.direct, dev)
+        dwf = torch.zeros_like(wf) if fused else None  # every layer writes its own columns
         for l in range(L - 1, -1, -1):
             c = convs[l]
             Hc, C = c.heads, c.out_channels
             if drops[l] is not None:
                 dy = dy * drops[l]
             xs = xss[l]
-            if layout.tiled:  # pss[l] holds the layer's ae (or None without edges)
+            if fused:  # pss[l], sts[l]: the forward's head aggregates and row statistics
+                dxs, dbp = ops.gat_attn_fused_bwd(
+                    dy, ys[l], pss[l], sts[l], xs, ea, wf, l * H, ctx.feid, keeps[l],
+                    ctx.kscales[l], dwf, B, n, Hc, C, c.concat, act, float(c.negative_slope))
+                dae = None
+            elif layout.tiled:  # pss[l] holds the layer's ae (or None without edges)
                 dxs, dae, dbp = ops.gat_attn_tiled_bwd(
                     dy, ys[l], xs, pss[l], layout.num_edges, layout.eid, keeps[l],
                     ctx.kscales[l], layout.rowmask, B, n, Hc, C, c.concat, act,
@@ -302,7 +353,9 @@ class _GATStack(torch.autograd.Function):
             need_e = [(grad_of(c.lin_edge.weight), grad_of(c.att_edge)) for c in convs]
             if ea.size(0) > 0 and any(a is not None or b is not None for a, b in need_e):
                 ei = layout.edge_index if layout.kind == "block" else None
-                dwf = ops.edge_logits_bwd(ea, ei, layout.canon, daes, H, B, n, hp, layout.tiled)
+                if not fused:
+                    dwf = ops.edge_logits_bwd(ea, ei, layout.canon, daes, H, B, n, hp,
+                                              layout.tiled)
                 for l, c in enumerate(convs):
                     gWe, gae = need_e[l]
                     ops.prep_bwd_edge(dwf, l * H, c.lin_edge.weight, c.att_edge, c.heads,
