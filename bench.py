@@ -203,9 +203,13 @@ def kernel_table(model, data, reps=50):
 
 
 def kernel_table_tiled(model, data, cfg, reps=10):
-    """C5 (32 < n <= 256): the tiled attention of layer 0 and the plane edge
-    passes, HIP events on the launch stream.  Algorithmic bytes: every logit
-    plane, xs row, output row read or written once per launch."""
+    """C5 (32 < n <= 256, narrow edge_attr): the layer-0 edge-fused attention
+    forward and backward (sv2n_gat_attn_fused_*: prep + main + finish) and the
+    layer-0 projection / weight-gradient GEMMs, HIP events on the launch stream.
+    Algorithmic bytes per launch: every tensor the call must read or write,
+    once — edge_attr, xs, the layer output and the saved aggregates /
+    statistics (forward); edge_attr, xs, dy, y, agg, statistics and dxs
+    (backward)."""
     from spotv2net_amd import ops
     dev = data.x.device
     stream = torch.cuda.current_stream(dev)
@@ -213,57 +217,72 @@ def kernel_table_tiled(model, data, cfg, reps=10):
     n, H = cfg["n"], cfg["heads"]
     N0 = data.x.shape[0]
     B = N0 // n
-    L = len(model.gat_layers)
     lib = ops._lib.load()
     with torch.no_grad():
         W0 = model.gat_layers[0].projection_weight().contiguous()
         wf = torch.cat([c.edge_fold() for c in model.gat_layers], 1)
     conv0 = model.gat_layers[0]
     C = conv0.out_channels
-    ldx = (H * C + 2 * H + 3) // 4 * 4
+    HC = H * C
+    ldx = (HC + 2 * H + 3) // 4 * 4
     xs0 = torch.zeros(N0, ldx, device=dev)
     xs0[:, :W0.shape[0]] = ops.gemm_f32(data.x, True, W0, True, N0, W0.shape[0], data.x.shape[1])
     E, D = data.edge_attr.shape
     wfp, hp = ops.pad_columns(wf)
-    aes = [torch.empty(H, E, device=dev) for _ in range(L)]
-    ptrs = ops._lib.ptr_array([a.data_ptr() for a in aes])
-    y0 = torch.empty(N0, H * C, device=dev)
+    y0 = torch.empty(N0, HC, device=dev)
+    agg0 = torch.empty(N0, HC, device=dev)
+    st0 = torch.empty(N0, 4 * H, device=dev)
     dy0 = torch.randn_like(y0)
     dxs0 = torch.empty_like(xs0)
-    dae0 = torch.empty(L, H, E, device=dev)
-    dptrs = ops._lib.ptr_array([dae0[l].data_ptr() for l in range(L)])
-    dbp = torch.empty(B, H * C, device=dev)
-    ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hp)
+    NT = (n + 31) // 32
+    dbp = torch.empty(B * NT, HC, device=dev)
+    dwf = torch.zeros(D, hp, device=dev)
+    ws_n = lib.sv2n_gat_attn_fused_bwd_workspace(B, n, H, C, D)
     ws = torch.empty(ws_n, device=dev)
-    dwf = torch.empty(D, hp, device=dev)
-
-    def edge_fwd():
-        lib.sv2n_edge_logits_fwd_planes(data.edge_attr.data_ptr(), E, D, wfp.data_ptr(), hp, ptrs,
-                                        L, H, sh)
-
-    def edge_bwd():
-        lib.sv2n_edge_logits_bwd_planes(data.edge_attr.data_ptr(), E, D, None, dptrs, L, H,
-                                        ws.data_ptr(), ws_n, dwf.data_ptr(), hp, sh)
 
     def attn_fwd():
-        lib.sv2n_gat_attn_tiled_fwd(xs0.data_ptr(), ldx, aes[0].data_ptr(), E, None, None,
-                                    conv0.bias.data_ptr(), None, 1.0, y0.data_ptr(), None, 0, B,
-                                    n, H, C, 1, 1, 0.2, sh)
+        lib.sv2n_gat_attn_fused_fwd(xs0.data_ptr(), ldx, data.edge_attr.data_ptr(), D,
+                                    wfp.data_ptr(), hp, 0, None, conv0.bias.data_ptr(), None, 1.0,
+                                    y0.data_ptr(), agg0.data_ptr(), st0.data_ptr(), B, n, H, C,
+                                    1, 1, 0.2, sh)
 
     def attn_bwd():
-        lib.sv2n_gat_attn_tiled_bwd(dy0.data_ptr(), y0.data_ptr(), xs0.data_ptr(), ldx,
-                                    aes[0].data_ptr(), E, None, None, 1.0, None, dxs0.data_ptr(),
-                                    dae0[0].data_ptr(), dbp.data_ptr(), B, n, H, C, 1, 1, 0.2, sh)
+        lib.sv2n_gat_attn_fused_bwd(dy0.data_ptr(), y0.data_ptr(), agg0.data_ptr(),
+                                    st0.data_ptr(), xs0.data_ptr(), ldx,
+                                    data.edge_attr.data_ptr(), D, wfp.data_ptr(), hp, 0, None,
+                                    None, 1.0, dxs0.data_ptr(), dbp.data_ptr(), dwf.data_ptr(),
+                                    ws.data_ptr(), ws_n, B, n, H, C, 1, 1, 0.2, sh)
 
-    plane, xsb, yb = 4.0 * H * E, 4.0 * N0 * ldx, 4.0 * N0 * H * C
+    x0 = data.x
+    planes0 = ops.weight_planes(W0, False)
+    out0 = torch.empty(N0, W0.shape[0], device=dev)
+
+    def gemm_fwd():
+        lib.sv2n_gemm_f32x3(x0.data_ptr(), x0.stride(0), planes0.data_ptr(), out0.data_ptr(),
+                            out0.stride(0), N0, W0.shape[0], x0.shape[1], sh)
+
+    Fd, Nd = x0.shape[1], ldx
+    nslab = lib.sv2n_gemm_f32_slabs_count(Fd, Nd, N0)
+    slabs = torch.empty(nslab * Fd * Nd, device=dev)
+
+    def gemm_dwt():
+        lib.sv2n_gemm_f32_slabs(0, 0, x0.data_ptr(), x0.stride(0), dxs0.data_ptr(),
+                                dxs0.stride(0), Fd, Nd, N0, slabs.data_ptr(), slabs.numel(), sh)
+
+    attn_fwd()  # the backward reads the training forward's outputs
+    eab, xsb, rowb, stb = 4.0 * E * D, 4.0 * N0 * ldx, 4.0 * N0 * HC, 4.0 * N0 * 4 * H
+    M0, Nc, K0 = N0, W0.shape[0], x0.shape[1]
+    # (fn, bound, algorithmic flops, algorithmic bytes, peak)
     rows = {
-        "edge_logits_fwd": (edge_fwd, "hbm", 4.0 * E * D + L * plane),
-        "edge_logits_bwd": (edge_bwd, "hbm", 4.0 * E * D + L * plane),
-        "gat_attn_tiled_fwd_l0": (attn_fwd, "hbm", plane + xsb + yb),
-        "gat_attn_tiled_bwd_l0": (attn_bwd, "hbm", 2 * plane + 2 * xsb + 2 * yb),
+        "gat_attn_fused_fwd_l0": (attn_fwd, "hbm", 0.0, eab + xsb + 2 * rowb + stb, None),
+        "gat_attn_fused_bwd_l0": (attn_bwd, "hbm", 0.0, eab + 2 * xsb + 3 * rowb + stb, None),
+        "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * Nc * K0, 4.0 * (M0 * K0 + Nc * K0 + M0 * Nc),
+                        BF16X3_PEAK_TFLOPS),
+        "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * Nd * K0, 4.0 * (M0 * K0 + M0 * Nd + Nd * K0),
+                        F32_MFMA_PEAK_TFLOPS),
     }
     res = {}
-    for name, (fn, bound, nbytes) in rows.items():
+    for name, (fn, bound, flops, nbytes, peak) in rows.items():
         fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
@@ -272,8 +291,8 @@ def kernel_table_tiled(model, data, cfg, reps=10):
         e1.record(stream)
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / reps
-        res[name] = dict(avg_us=us, bound=bound, flops=0.0, bytes=nbytes, tflops=0.0,
-                         gbs=nbytes / us / 1e3, peak_tflops=None)
+        res[name] = dict(avg_us=us, bound=bound, flops=flops, bytes=nbytes,
+                         tflops=flops / us / 1e6, gbs=nbytes / us / 1e3, peak_tflops=peak)
     return res
 
 
@@ -554,6 +573,7 @@ def main():
         elif not args.no_kernel_table and args.config == "c5":
             table = kernel_table_tiled(model, data, cfg)
             kname, roof = roofline_entry(table)
+            roof["traffic"] = load_traffic("c5:" + kname)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             # bounded sample (~10-30 s): at most as many edges as 128 C2 graphs

@@ -32,6 +32,14 @@ KERNELS = {
 }
 
 
+# C5 (tools/pmc_c5_traffic.sh): keys prefixed "c5:" in the same JSON
+KERNELS_C5 = {
+    "gat_attn_fused_fwd_l0": "sv2n::fused::k_fattn_fwd<12, false, false>",
+    "gat_attn_fused_bwd_l0": "sv2n::fused::k_fattn_bwd<12, false, false>",
+    "gemm_l0_fwd": "sv2n::k_gemm3<8, 1, 13, 64, 1, 3>",
+}
+
+
 def per_kernel(path, counter):
     """mean over dispatches of the dispatch's counter sum (KiB), keyed by kernel name."""
     disp = defaultdict(float)
@@ -60,13 +68,21 @@ def main():
     ap.add_argument("fetch")
     ap.add_argument("write")
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    ap.add_argument("--config", default="c2", choices=("c2", "c5"))
     a = ap.parse_args()
     fetch = per_kernel(a.fetch, "FETCH_SIZE")
     write = per_kernel(a.write, "WRITE_SIZE")
-    out = {"_note": "hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), "
-                    "gfx950 FETCH_SIZE halving corrected per MI355X_MICROARCH.md; "
-                    "mean over the dispatches of the profiled C2 train/forward steps"}
-    for key, prefix in KERNELS.items():
+    out = {}
+    try:
+        out = json.load(open(a.out))  # merge: C2 and C5 passes share the file
+    except (OSError, ValueError):
+        pass
+    out["_note"] = ("hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), "
+                    "gfx950 FETCH_SIZE halving corrected per MI355X_MICROARCH.md; mean over "
+                    "the dispatches of the profiled C2 train/forward steps (keys 'c5:...': "
+                    "the C5 steps)")
+    table = KERNELS if a.config == "c2" else {"c5:" + k: v for k, v in KERNELS_C5.items()}
+    for key, prefix in table.items():
         f, w = find(fetch, prefix), find(write, prefix)
         if f is None or w is None:
             continue
