@@ -895,6 +895,23 @@ __global__ __launch_bounds__(ATT_THREADS) void k_attn_bwd(
 // ============================ C-ABI ========================================
 using namespace sv2n;
 
+namespace sv2n {
+// sv2n_attn_canon.hip: complete graphs in canonical edge order
+void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
+                    const float* bias, const uint8_t* keep, float keep_scale, float* y,
+                    float* psave, int n, int H, int C, int concat, int act, float slope);
+}  // namespace sv2n
+
+// The lean complete-graph kernels take every canonical batch (edge logits in
+// edge order, or no edge features) unless SV2N_ATTN_CANON=0 (A/B switch).
+static bool canon_path(const float* ae, int ae_edge_order, const uint32_t* rowmask, int n, int H) {
+  static const bool on = [] {
+    const char* e = getenv("SV2N_ATTN_CANON");
+    return !(e && e[0] == '0');
+  }();
+  return on && !rowmask && (!ae || ae_edge_order) && n >= 2 && n <= 32 && H <= 8;
+}
+
 static size_t fwd_lds(int H, FwdChunking ck) {
   const size_t xs = (size_t)x_stride(ck.hpc * ck.cw);
   return sizeof(float) * ((size_t)H * 32 * TS + 2 * (size_t)H * 32 + xs +
@@ -1016,6 +1033,11 @@ extern "C" int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, int 
   if (!xs || !y || !psave) return SV2N_ERR_ARG;
   if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
   if (ae_edge_order && (rowmask || n < 2)) return SV2N_ERR_ARG;  // complete graphs only
+  if (canon_path(ae, ae_edge_order, rowmask, n, heads)) {
+    attn_canon_fwd(num_graphs, stream, xs, ldx, ae, bias, keep, keep_scale, y, psave, n, heads,
+                   channels, concat, act, negative_slope);
+    return (int)hipGetLastError();
+  }
   if (concat) {
     SV2N_DISPATCH_ACT(launch_fwd, true, num_graphs, stream, xs, ldx, ae, ae_edge_order, rowmask,
                       bias, keep, keep_scale, y, psave, n, heads, channels, negative_slope)
