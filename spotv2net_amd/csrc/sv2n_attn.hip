@@ -900,6 +900,10 @@ namespace sv2n {
 void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
                     const float* bias, const uint8_t* keep, float keep_scale, float* y,
                     float* psave, int n, int H, int C, int concat, int act, float slope);
+void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, const float* xs,
+                    int ldx, const float* psave, const uint8_t* keep, float keep_scale,
+                    float* dxs, float* dae, float* dbias, int n, int H, int C, int concat,
+                    int act, float slope);
 }  // namespace sv2n
 
 // The lean complete-graph kernels take every canonical batch (edge logits in
@@ -1057,6 +1061,11 @@ extern "C" int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* x
   if (!dy || !y || !xs || !psave || !dxs || !dbias_partial) return SV2N_ERR_ARG;
   if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
   if (ae_edge_order && (rowmask || n < 2)) return SV2N_ERR_ARG;  // complete graphs only
+  if (canon_path(dae, ae_edge_order, rowmask, n, heads)) {
+    attn_canon_bwd(num_graphs, stream, dy, y, xs, ldx, psave, keep, keep_scale, dxs, dae,
+                   dbias_partial, n, heads, channels, concat, act, negative_slope);
+    return (int)hipGetLastError();
+  }
   if (concat) {
     SV2N_DISPATCH_ACT(launch_bwd, true, num_graphs, stream, dy, y, xs, ldx, psave, keep,
                       keep_scale, rowmask, dxs, dae, ae_edge_order, dbias_partial, n, heads,

@@ -268,9 +268,278 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// backward: one 256-thread workgroup per graph, wave w owns heads w, w + 4.
+// Per head h (all in the wave's registers and its own LDS area):
+//   dZ_h[i][c] = act'(dy, y) (· 1/H for the head mean),
+//   G[j][i]    = Σ_c xs[j][h·C + c] · dZ_h[i][c]          (dP_dᵀ: lane i, rows j)
+//   dxs[j][h·C + c] = Σ_i P_d[i][j] · dZ_h[i][c]
+// over 32-column chunks of the head staged through the wave's LDS area (xs and
+// dZ rows, stride 33: conflict-free row and column operand reads); then the
+// dropout / softmax / leaky_relu backward of G in the MFMA output layout
+// (lane i holds rows j = crow(r, half) — the positions its saved probabilities
+// are loaded at) -> dl in sDL.  After a barrier: d ae in edge order (one
+// decode per edge), d a_src = column sums of dl, d a_dst, zero padding.
+// LDS: sP[H][32][PS] (P_d, the A operand of dxs) | per wave 2 x [32][33]
+//      chunk area | sDL[H][32][33] | sSh[H][32] (self-loop share of row i) |
+//      sDad[H][32]
+// ---------------------------------------------------------------------------
+constexpr int CS = 33;  // chunk / dl row stride (floats)
+
+template <int ACT, bool CONCAT, bool KEEP>
+__global__ __launch_bounds__(THREADS) void k_bwd(
+    const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ xs,
+    int ldx, const float* __restrict__ psave, const uint8_t* __restrict__ keep, float keep_scale,
+    float* __restrict__ dxs, float* __restrict__ dae, float* __restrict__ dbias_part, int n,
+    int H, int C, float slope) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sP = smem;
+  float* sArea = sP + H * 32 * PS;
+  float* sDL = sArea + 4 * 2 * 32 * CS;
+  float* sSh = sDL + H * 32 * CS;
+  float* sDad = sSh + H * 32;
+
+  const int g = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int l32 = lane & 31, half = lane >> 5;
+  const int HC = H * C, OC = CONCAT ? HC : C;
+  const int E0 = n * (n - 1);
+  const float invH = 1.f / (float)H;
+  const rsrc_t rx = make_rsrc(xs + (int64_t)g * n * ldx, (uint32_t)(n * ldx) * 4u);
+  const rsrc_t rdx = make_rsrc(dxs + (int64_t)g * n * ldx, (uint32_t)(n * ldx) * 4u);
+  const rsrc_t rdy = make_rsrc(dy + (int64_t)g * n * OC, (uint32_t)(n * OC) * 4u);
+  const rsrc_t ryy = make_rsrc(y + (int64_t)g * n * OC, (uint32_t)(n * OC) * 4u);
+  const rsrc_t rps = make_rsrc(psave + (int64_t)g * H * 1024, (uint32_t)H * 4096u);
+  const rsrc_t rdb = make_rsrc(dbias_part + (int64_t)g * OC, (uint32_t)OC * 4u);
+
+  float* sX = sArea + wave * 2 * 32 * CS;
+  float* sZ = sX + 32 * CS;
+  const int nch = (C + 31) >> 5;
+  const int cwb = (C + nch - 1) / nch;  // balanced chunk width (<= 32)
+  const int nhw = (H - wave + 3) / 4;  // heads of this wave
+  const int nseq = nhw * nch;          // (head, chunk) steps of this wave
+
+  // chunk step q: rows 2m + half, column l32 of the chunk (dword loads, the
+  // row stride in the scalar offset)
+  float rx_[16], rdy_[16], ry_[16];
+  auto load_chunk = [&](int q) {
+    const int hq = q / nch, ch = q - hq * nch, h = wave + 4 * hq;
+    const int c = cwb * ch + l32;
+    const bool cv = l32 < cwb && c < C;
+    const int xo = cv ? (half * ldx + h * C + c) * 4 : OOB;
+    const int zo = cv ? (half * OC + (CONCAT ? h * C : 0) + c) * 4 : OOB;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      rx_[m] = bld_s(rx, xo, 2 * m * ldx * 4);
+      rdy_[m] = bld_s(rdy, zo, 2 * m * OC * 4);
+      ry_[m] = bld_s(ryy, zo, 2 * m * OC * 4);
+    }
+  };
+  // saved probabilities / keep bytes of head h at lane i's output rows
+  // j = crow(r, half): four 16-B pieces of row i
+  f32x4 pr[4];
+  uint32_t kb[4];
+  auto load_p = [&](int h) {
+    const int base = ((h * 32 + l32) * 32 + 4 * half) * 4;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) pr[m] = bld4(rps, base + 32 * m);
+    if constexpr (KEEP) {
+      const rsrc_t rk = make_rsrc(keep + ((int64_t)g * H + h) * 1024, 1024u);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) kb[m] = bld_u32(rk, (l32 * 32 + 4 * half) + 8 * m);
+    }
+  };
+
+  if (nseq > 0) {
+    load_p(wave);
+    load_chunk(0);
+  }
+  floatx16 G;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) G[r] = 0.f;
+  const int i = l32;
+  const bool iv = i < n;
+
+  for (int q = 0; q < nseq; ++q) {
+    const int hq = q / nch, ch = q - hq * nch, h = wave + 4 * hq;
+    const int c0 = cwb * ch, cw = min(cwb, C - c0);
+    if (ch == 0) {
+      // P_d of head h -> sP rows (each lane: its 16 positions of row i)
+      float* prow = sP + (h * 32 + l32) * PS + 4 * half;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a = fabsf(pr[m][e]);
+          if constexpr (KEEP) a = ((kb[m] >> (8 * e)) & 0xffu) ? a * keep_scale : 0.f;
+          v[e] = iv ? a : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(prow + 8 * m) = v;
+      }
+    }
+    // stage the chunk: sX[row][c] = xs, sZ[row][c] = act'(dy, y)
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int row = 2 * m + half;
+      sX[row * CS + l32] = rx_[m];
+      sZ[row * CS + l32] = act_bwd<ACT>(rdy_[m], ry_[m]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes, in order
+    if (q + 1 < nseq) load_chunk(q + 1);
+    // bias partials: column sums of dz (concat: this head's columns; mean: once)
+    if (CONCAT || h == 0) {
+      float sb = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sb += sZ[(16 * half + r) * CS + l32];
+      sb += __shfl_xor(sb, 32, 64);
+      bst(rdb, (half == 0 && l32 < cw) ? ((CONCAT ? h * C : 0) + c0 + l32) * 4 : OOB, sb);
+    }
+    // G[j][i] += Σ_c xs[j][c] · dZ[i][c]    (k = 2kk + half)
+    const int nk = (cw + 1) >> 1;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      if (kk < nk) {  // wave-uniform
+        const float a = sX[l32 * CS + 2 * kk + half];
+        const float b = sZ[l32 * CS + 2 * kk + half];
+        G = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, G, 0, 0, 0);
+      }
+    }
+    // dxs[j][c] = Σ_i P_d[i][j] · dZ[i][c]    (k: i = 16·half + kk)
+    floatx16 D;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) D[r] = 0.f;
+    const float* pcol = sP + (h * 32 + 16 * half) * PS + l32;
+    const float* zcol = sZ + (16 * half) * CS + l32;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+      D = __builtin_amdgcn_mfma_f32_32x32x2f32(pcol[kk * PS], zcol[kk * CS], D, 0, 0, 0);
+    {
+      const int voff = l32 < cw ? (4 * half * ldx + h * C + c0 + l32) * 4 : OOB;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        bst_s(rdx, voff, ((r & 3) + 8 * (r >> 2)) * ldx * 4, CONCAT ? D[r] : D[r] * invH);
+    }
+    if (ch == nch - 1) {
+      // ---- softmax / leaky_relu backward of head h: lane (i, half), rows j = crow(r, half)
+      float ps[16], dp[16];
+      float tl = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int jr = crow(r, half);
+        ps[r] = pr[r >> 2][r & 3];
+        const bool valid = iv && jr < n;
+        float d = valid ? (CONCAT ? G[r] : G[r] * invH) : 0.f;
+        if constexpr (KEEP) d = ((kb[r >> 2] >> (8 * (r & 3))) & 0xffu) ? d * keep_scale : 0.f;
+        dp[r] = d;
+        tl += fabsf(ps[r]) * d;
+      }
+      tl += __shfl_xor(tl, 32, 64);
+      float dad = 0.f, mine = 0.f;
+      const int ri = (i & 3) + 4 * (i >> 3), hi = (i >> 2) & 1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int jr = crow(r, half);
+        const bool valid = iv && jr < n;
+        const float ds = fabsf(ps[r]) * (dp[r] - tl);
+        const float dl = valid ? (signbit(ps[r]) ? ds * slope : ds) : 0.f;
+        dad += dl;
+        mine = (r == ri) ? dl : mine;
+        sDL[(h * 32 + i) * CS + jr] = dl;
+      }
+      dad += __shfl_xor(dad, 32, 64);
+      const float other = __shfl_xor(mine, 32, 64);
+      const float dlii = (half == hi) ? mine : other;
+      if (half == 0) {
+        sDad[h * 32 + i] = iv ? dad : 0.f;
+        sSh[h * 32 + i] = (iv && n > 1) ? dlii / (float)(n - 1) : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) G[r] = 0.f;
+      if (hq + 1 < nhw) load_p(h + 4);
+    }
+  }
+  __syncthreads();
+
+  // ---- d ae in canonical edge order [E0][H] ----
+  if (dae) {
+    const int nae = E0 * H;
+    const rsrc_t rdae = make_rsrc(dae + (int64_t)g * nae, (uint32_t)nae * 4u);
+    for (int e = t; e < E0; e += THREADS) {
+      int ti, tj;
+      canon_decode(e, n, ti, tj);
+      if (H == 4) {
+        f32x4 v;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) v[h] = sDL[(h * 32 + ti) * CS + tj] + sSh[h * 32 + ti];
+        bst4(rdae, e * 16, v);
+      } else {
+        for (int h = 0; h < H; ++h)
+          bst(rdae, (e * H + h) * 4, sDL[(h * 32 + ti) * CS + tj] + sSh[h * 32 + ti]);
+      }
+    }
+  }
+  // ---- dxs columns [HC, ldx): d a_src (Σ_i dl[i][j]), d a_dst, zero padding ----
+  const int ntail = ldx - HC;
+  for (int e = t; e < n * ntail; e += THREADS) {
+    const int j = e / ntail, c2 = e - j * ntail;
+    float v = 0.f;
+    if (c2 < H) {
+      const float* col = sDL + c2 * 32 * CS + j;
+#pragma unroll 8
+      for (int ii = 0; ii < 32; ++ii) v += col[ii * CS];
+    } else if (c2 < 2 * H) {
+      v = sDad[(c2 - H) * 32 + j];
+    }
+    bst(rdx, (j * ldx + HC + c2) * 4, v);
+  }
+}
+
 }  // namespace canon
 
 // ---- launchers (called by the C-ABI entry points in sv2n_attn.hip) ---------
+size_t attn_canon_bwd_lds(int H) {
+  return sizeof(float) * ((size_t)H * 32 * canon::PS + 4 * 2 * 32 * canon::CS +
+                          (size_t)H * 32 * canon::CS + 2 * (size_t)H * 32);
+}
+
+template <int ACT, bool CONCAT, bool KEEP>
+static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y,
+                             const float* xs, int ldx, const float* psave, const uint8_t* keep,
+                             float keep_scale, float* dxs, float* dae, float* dbias, int n, int H,
+                             int C, float slope) {
+  const size_t lds = attn_canon_bwd_lds(H);
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)canon::k_bwd<ACT, CONCAT, KEEP>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL((canon::k_bwd<ACT, CONCAT, KEEP>), dim3((unsigned)B), dim3(canon::THREADS),
+                     lds, st, dy, y, xs, ldx, psave, keep, keep_scale, dxs, dae, dbias, n, H, C,
+                     slope);
+}
+
+void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, const float* xs,
+                    int ldx, const float* psave, const uint8_t* keep, float keep_scale,
+                    float* dxs, float* dae, float* dbias, int n, int H, int C, int concat,
+                    int act, float slope) {
+#define SV2N_CB(A, CC, K)                                                                 \
+  launch_canon_bwd<A, CC, K>(B, st, dy, y, xs, ldx, psave, keep, keep_scale, dxs, dae, dbias, n, \
+                             H, C, slope)
+#define SV2N_CB_ACT(CC, K)                 \
+  switch (act) {                           \
+    case 0: SV2N_CB(0, CC, K); break;      \
+    case 1: SV2N_CB(1, CC, K); break;      \
+    case 2: SV2N_CB(2, CC, K); break;      \
+    default: SV2N_CB(3, CC, K); break;     \
+  }
+  if (concat) {
+    if (keep) { SV2N_CB_ACT(true, true) } else { SV2N_CB_ACT(true, false) }
+  } else {
+    if (keep) { SV2N_CB_ACT(false, true) } else { SV2N_CB_ACT(false, false) }
+  }
+#undef SV2N_CB_ACT
+#undef SV2N_CB
+}
 size_t attn_canon_fwd_lds(int n, int H, bool has_ae) {
   const int nae = has_ae ? n * (n - 1) * H : 0;
   return sizeof(float) * ((size_t)H * 32 * canon::PS + 2 * (size_t)H * 32 + 32 +
