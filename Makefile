@@ -4,14 +4,18 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Wall -Wno-unused-result
+BUILD ?= build
+LIB ?= spotv2net_amd/libsv2n.so
+ifeq ($(STAMPS),1)
+HIPFLAGS += -DSV2N_STAMPS   # diagnostic phase stamps (tools/stamps.py)
+endif
 SRC := $(wildcard spotv2net_amd/csrc/*.hip)
-OBJ := $(patsubst spotv2net_amd/csrc/%.hip,build/%.o,$(SRC))
-LIB := spotv2net_amd/libsv2n.so
+OBJ := $(patsubst spotv2net_amd/csrc/%.hip,$(BUILD)/%.o,$(SRC))
 
 all: $(LIB)
 
-build/%.o: spotv2net_amd/csrc/%.hip $(wildcard spotv2net_amd/csrc/*.h) include/sv2n.h
-	@mkdir -p build
+$(BUILD)/%.o: spotv2net_amd/csrc/%.hip $(wildcard spotv2net_amd/csrc/*.h) include/sv2n.h
+	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(OBJ)

@@ -13,7 +13,9 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsv2n.so")
+# SV2N_LIB: an alternative build of the same library (diagnostic builds, e.g.
+# tools/stamps.py); default the in-tree one
+LIB_PATH = os.environ.get("SV2N_LIB") or os.path.join(_HERE, "libsv2n.so")
 ABI_VERSION = 5
 
 _c_f = ctypes.POINTER(ctypes.c_float)

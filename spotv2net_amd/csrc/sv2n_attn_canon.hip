@@ -24,6 +24,18 @@
 namespace sv2n {
 namespace canon {
 
+// Diagnostic builds only (make STAMPS=1): per-wave s_memtime / s_memrealtime
+// stamps of the kernel phases, read back by sv2n_diag_stamps.
+#ifdef SV2N_STAMPS
+__device__ unsigned long long g_stamps[4096 * 4 * 16];
+#define SV2N_STAMP(k, v) \
+  if ((threadIdx.x & 63) == 0) g_stamps[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + (k)] = (v)
+#define SV2N_T() __builtin_amdgcn_s_memtime()
+#define SV2N_RT() __builtin_amdgcn_s_memrealtime()
+#else
+#define SV2N_STAMP(k, v)
+#endif
+
 constexpr int THREADS = 256;
 constexpr int PS = SV2N_PSTR;  // LDS row stride of a probability row (floats)
 constexpr int AEV = 8;         // 16-B slots per thread covering E0·H <= 992·8
@@ -44,7 +56,7 @@ __device__ __forceinline__ void bst_s(rsrc_t r, int voff, int soff, float v) {
 // ---------------------------------------------------------------------------
 // forward: one 256-thread workgroup per graph.
 // LDS: sP[H][32][PS] (dropped-out probabilities, the MFMA A operand) |
-//      sAS[H][32] a_src | sAD[H][32] a_dst | sT[32] T(x) | sAE[E0·H]
+//      sAS[H][32] a_src | sAD[H][32] a_dst | sAE[E0·H]
 // Work items of a wave (after the softmax): concat — (head h, 32-column tile
 // tc) pairs w, w+4, ...; mean — tiles tc = w, w+4, ..., each summed over the
 // heads (sub-items h = 0..H-1 on one accumulator, in head order).
@@ -58,9 +70,10 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
   float* sP = smem;
   float* sAS = sP + H * 32 * PS;
   float* sAD = sAS + H * 32;
-  int* sT = reinterpret_cast<int*>(sAD + H * 32);
-  float* sAE = reinterpret_cast<float*>(sT + 32);
+  float* sAE = sAD + H * 32;
 
+  SV2N_STAMP(0, SV2N_RT());
+  SV2N_STAMP(1, SV2N_T());
   const int g = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int l32 = lane & 31, half = lane >> 5;
@@ -119,8 +132,11 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     const int idx = t + THREADS * s, k = idx >> 5, j = idx & 31;
     asd[s] = bld(rx, k < 2 * H ? (j * ldx + HC + k) * 4 : OOB);  // rows j >= n read 0
   }
-  float bA[16], bB[16];
-  if (nq > 0) load_b(0, bA);
+  // B operands of the wave's first four work items (C2: all of them)
+  float bq[4][16];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (u < nq) load_b(u, bq[u]);
 
 #pragma unroll
   for (int q = 0; q < AEV; ++q) {
@@ -132,13 +148,15 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     const int idx = t + THREADS * s;
     if (idx < 2 * H * 32) sAS[idx] = asd[s];
   }
-  if (t < 32) sT[t] = t * (2 * n - t - 1) / 2;
   __syncthreads();
+  SV2N_STAMP(2, SV2N_T());
 
   // ---- per-target softmax: lane (i, half) = target i, sources 16·half + kk ----
   const int i = l32;
   const bool iv = i < n;
-  const int Ti = iv ? sT[i] : 0;
+  // canonical edge ids of row i: e = Q(j) + i (j < i), e = Ehi + j (j > i), with
+  // Q(j) = T(j) - j - 1 and Ehi = P + T(i) - i - 1 — no table, no branch
+  const int Ehi = P + ((i * (2 * n - 1 - i)) >> 1) - i - 1;
   float pkeep[2][16];  // signed probabilities for psave, stored after the next loads
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
@@ -151,6 +169,10 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       kw[0] = w4[0]; kw[1] = w4[1]; kw[2] = w4[2]; kw[3] = w4[3];
     }
     const float ad = sAD[h * 32 + i];
+    const f32x4* asr = reinterpret_cast<const f32x4*>(sAS + h * 32 + 16 * half);
+    f32x4 as4[4];
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) as4[k4] = asr[k4];
     float lg[16];
     float esum = 0.f;
 #pragma unroll
@@ -159,12 +181,12 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       float a = 0.f;
       if (ae) {
         const bool ev = iv && j < n && j != i;
-        const int e = j < i ? sT[j] + i - j - 1 : P + Ti + j - i - 1;
+        const int e = j < i ? ((j * (2 * n - 1 - j)) >> 1) - j - 1 + i : Ehi + j;
         const float v = sAE[ev ? e * H + h : 0];
         a = ev ? v : 0.f;
       }
       esum += a;
-      lg[kk] = sAS[h * 32 + j] + ad + a;
+      lg[kk] = as4[kk >> 2][kk & 3] + ad + a;
     }
     esum += __shfl_xor(esum, 32, 64);
     const float loopv = (ae && n > 1) ? esum / (float)(n - 1) : 0.f;
@@ -207,7 +229,6 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       *reinterpret_cast<f32x4*>(prow + 4 * k4) = pd;
     }
   }
-  if (nq > 1) load_b(1, bB);  // issued before the psave stores (one in-order vmcnt)
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
     const int h = wave + 4 * s2;
@@ -219,7 +240,9 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
            f32x4{pkeep[s2][4 * k4], pkeep[s2][4 * k4 + 1], pkeep[s2][4 * k4 + 2],
                  pkeep[s2][4 * k4 + 3]});
   }
+  SV2N_STAMP(3, SV2N_T());
   __syncthreads();  // sP complete
+  SV2N_STAMP(4, SV2N_T());
 
   // ---- aggregation: out_h[i][c] = Σ_j P_h[i][j] · xs[j][h·C + c] ----
   floatx16 acc;
@@ -250,22 +273,18 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       }
     }
   };
-  for (int q = 0; q < nq; q += 2) {
-    if (q + 2 < nq) {
-      run(q, bA);
-      load_b(q + 2, bA);
-    } else {
-      run(q, bA);
-    }
-    if (q + 1 < nq) {
-      if (q + 3 < nq) {
-        run(q + 1, bB);
-        load_b(q + 3, bB);
-      } else {
-        run(q + 1, bB);
+  for (int q0 = 0; q0 < nq; q0 += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = q0 + u;
+      if (q < nq) {
+        run(q, bq[u]);
+        if (q + 4 < nq) load_b(q + 4, bq[u]);
       }
     }
   }
+  SV2N_STAMP(5, SV2N_T());
+  SV2N_STAMP(6, SV2N_RT());
 }
 
 
@@ -283,9 +302,10 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 // decode per edge), d a_src = column sums of dl, d a_dst, zero padding.
 // LDS: sP[H][32][PS] (P_d, the A operand of dxs) | per wave 2 x [32][33]
 //      chunk area | sDL[H][32][33] | sSh[H][32] (self-loop share of row i) |
-//      sDad[H][32]
+//      sDad[H][32] | sDec[P] (pair p -> (u, w), u < w)
 // ---------------------------------------------------------------------------
-constexpr int CS = 33;  // chunk / dl row stride (floats)
+constexpr int CS = 36;  // chunk row stride (floats): 16-B rows, conflict-free b128 row reads
+constexpr int DS = 33;  // dl row stride (floats): conflict-free column sums
 
 template <int ACT, bool CONCAT, bool KEEP>
 __global__ __launch_bounds__(THREADS) void k_bwd(
@@ -297,9 +317,12 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   float* sP = smem;
   float* sArea = sP + H * 32 * PS;
   float* sDL = sArea + 4 * 2 * 32 * CS;
-  float* sSh = sDL + H * 32 * CS;
+  float* sSh = sDL + H * 32 * DS;
   float* sDad = sSh + H * 32;
+  uint16_t* sDec = reinterpret_cast<uint16_t*>(sDad + H * 32);  // pair p -> (u << 8 | w)
 
+  SV2N_STAMP(0, SV2N_RT());
+  SV2N_STAMP(1, SV2N_T());
   const int g = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int l32 = lane & 31, half = lane >> 5;
@@ -355,6 +378,10 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     load_p(wave);
     load_chunk(0);
   }
+  if (dae && t < n) {  // row u of the pair table (read after the final barrier)
+    const int base = (t * (2 * n - 1 - t)) >> 1;
+    for (int w = t + 1; w < n; ++w) sDec[base + w - t - 1] = (uint16_t)((t << 8) | w);
+  }
   floatx16 G;
 #pragma unroll
   for (int r = 0; r < 16; ++r) G[r] = 0.f;
@@ -380,6 +407,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       }
     }
     // stage the chunk: sX[row][c] = xs, sZ[row][c] = act'(dy, y)
+    SV2N_STAMP(2 + 2 * min(q, 3), SV2N_T());
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const int row = 2 * m + half;
@@ -387,6 +415,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       sZ[row * CS + l32] = act_bwd<ACT>(rdy_[m], ry_[m]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes, in order
+    SV2N_STAMP(3 + 2 * min(q, 3), SV2N_T());
     if (q + 1 < nseq) load_chunk(q + 1);
     // bias partials: column sums of dz (concat: this head's columns; mean: once)
     if (CONCAT || h == 0) {
@@ -396,15 +425,21 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       sb += __shfl_xor(sb, 32, 64);
       bst(rdb, (half == 0 && l32 < cw) ? ((CONCAT ? h * C : 0) + c0 + l32) * 4 : OOB, sb);
     }
-    // G[j][i] += Σ_c xs[j][c] · dZ[i][c]    (k = 2kk + half)
-    const int nk = (cw + 1) >> 1;
+    // G[j][i] += Σ_c xs[j][c] · dZ[i][c]    (step kk pairs columns kk and 16 + kk;
+    // the chunk's columns past cw are staged zeros)
+    {
+      const f32x4* xa = reinterpret_cast<const f32x4*>(sX + l32 * CS + 16 * half);
+      const f32x4* zb = reinterpret_cast<const f32x4*>(sZ + l32 * CS + 16 * half);
+      f32x4 a4[4], b4[4];
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      if (kk < nk) {  // wave-uniform
-        const float a = sX[l32 * CS + 2 * kk + half];
-        const float b = sZ[l32 * CS + 2 * kk + half];
-        G = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, G, 0, 0, 0);
+      for (int m = 0; m < 4; ++m) {
+        a4[m] = xa[m];
+        b4[m] = zb[m];
       }
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk)
+        G = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[kk >> 2][kk & 3], b4[kk >> 2][kk & 3], G, 0, 0,
+                                                 0);
     }
     // dxs[j][c] = Σ_i P_d[i][j] · dZ[i][c]    (k: i = 16·half + kk)
     floatx16 D;
@@ -446,7 +481,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
         const float dl = valid ? (signbit(ps[r]) ? ds * slope : ds) : 0.f;
         dad += dl;
         mine = (r == ri) ? dl : mine;
-        sDL[(h * 32 + i) * CS + jr] = dl;
+        sDL[(h * 32 + i) * DS + jr] = dl;
       }
       dad += __shfl_xor(dad, 32, 64);
       const float other = __shfl_xor(mine, 32, 64);
@@ -460,48 +495,68 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       if (hq + 1 < nhw) load_p(h + 4);
     }
   }
+  SV2N_STAMP(10, SV2N_T());
   __syncthreads();
+  SV2N_STAMP(11, SV2N_T());
 
-  // ---- d ae in canonical edge order [E0][H] ----
+  // ---- d ae in canonical edge order [E0][H]: pair p = (u, w), u < w, is edge
+  //      p (target w, source u) and edge P + p (target u, source w) ----
   if (dae) {
-    const int nae = E0 * H;
+    const int P = E0 / 2, nae = E0 * H;
     const rsrc_t rdae = make_rsrc(dae + (int64_t)g * nae, (uint32_t)nae * 4u);
-    for (int e = t; e < E0; e += THREADS) {
-      int ti, tj;
-      canon_decode(e, n, ti, tj);
-      if (H == 4) {
-        f32x4 v;
+    for (int p = t; p < P; p += THREADS) {
+      const uint32_t uw = sDec[p];
+      const int u = uw >> 8, w = uw & 0xff;
 #pragma unroll
-        for (int h = 0; h < 4; ++h) v[h] = sDL[(h * 32 + ti) * CS + tj] + sSh[h * 32 + ti];
-        bst4(rdae, e * 16, v);
-      } else {
-        for (int h = 0; h < H; ++h)
-          bst(rdae, (e * H + h) * 4, sDL[(h * 32 + ti) * CS + tj] + sSh[h * 32 + ti]);
+      for (int side = 0; side < 2; ++side) {
+        const int ti = side ? u : w, tj = side ? w : u, e = side ? P + p : p;
+        if (H == 4) {
+          f32x4 v;
+#pragma unroll
+          for (int h = 0; h < 4; ++h) v[h] = sDL[(h * 32 + ti) * DS + tj] + sSh[h * 32 + ti];
+          bst4(rdae, e * 16, v);
+        } else {
+          for (int h = 0; h < H; ++h)
+            bst(rdae, (e * H + h) * 4, sDL[(h * 32 + ti) * DS + tj] + sSh[h * 32 + ti]);
+        }
       }
     }
   }
-  // ---- dxs columns [HC, ldx): d a_src (Σ_i dl[i][j]), d a_dst, zero padding ----
-  const int ntail = ldx - HC;
-  for (int e = t; e < n * ntail; e += THREADS) {
-    const int j = e / ntail, c2 = e - j * ntail;
+  // ---- dxs columns [HC, ldx): d a_src[h][j] = Σ_i dl[h][i][j] (two lanes per
+  //      column, 16 rows each), d a_dst, zero padding ----
+  for (int q = t; q < 2 * 32 * H; q += THREADS) {
+    const int h = q >> 6, j = (q >> 1) & 31, part = q & 1;
+    const float* col = sDL + (h * 32 + 16 * part) * DS + j;
     float v = 0.f;
-    if (c2 < H) {
-      const float* col = sDL + c2 * 32 * CS + j;
-#pragma unroll 8
-      for (int ii = 0; ii < 32; ++ii) v += col[ii * CS];
-    } else if (c2 < 2 * H) {
-      v = sDad[(c2 - H) * 32 + j];
-    }
-    bst(rdx, (j * ldx + HC + c2) * 4, v);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v += col[r * DS];
+    v += __shfl_xor(v, 1, 64);
+    bst(rdx, (part == 0 && j < n) ? (j * ldx + HC + h) * 4 : OOB, v);
   }
+  const int ntail = ldx - HC - H;  // d a_dst columns, then zero padding
+  for (int q = t; q < 32 * ntail; q += THREADS) {
+    const int j = q & 31, c2 = q >> 5;
+    const float v = c2 < H ? sDad[c2 * 32 + j] : 0.f;
+    bst(rdx, j < n ? (j * ldx + HC + H + c2) * 4 : OOB, v);
+  }
+  SV2N_STAMP(12, SV2N_T());
+  SV2N_STAMP(13, SV2N_RT());
 }
 
 }  // namespace canon
 
+#ifdef SV2N_STAMPS
+extern "C" int sv2n_diag_stamps(unsigned long long* out, int64_t count) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(canon::g_stamps),
+                                  sizeof(unsigned long long) * (size_t)count);
+}
+#endif
+
 // ---- launchers (called by the C-ABI entry points in sv2n_attn.hip) ---------
 size_t attn_canon_bwd_lds(int H) {
   return sizeof(float) * ((size_t)H * 32 * canon::PS + 4 * 2 * 32 * canon::CS +
-                          (size_t)H * 32 * canon::CS + 2 * (size_t)H * 32);
+                          (size_t)H * 32 * canon::DS + 2 * (size_t)H * 32) +
+         sizeof(uint16_t) * 32 * 31 / 2;
 }
 
 template <int ACT, bool CONCAT, bool KEEP>
@@ -542,7 +597,7 @@ void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, 
 }
 size_t attn_canon_fwd_lds(int n, int H, bool has_ae) {
   const int nae = has_ae ? n * (n - 1) * H : 0;
-  return sizeof(float) * ((size_t)H * 32 * canon::PS + 2 * (size_t)H * 32 + 32 +
+  return sizeof(float) * ((size_t)H * 32 * canon::PS + 2 * (size_t)H * 32 +
                           (size_t)((nae + 3) & ~3));
 }
 
