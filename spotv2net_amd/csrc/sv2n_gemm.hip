@@ -27,6 +27,16 @@ struct GemmPlan {
   int64_t kslice;
 };
 
+// f32 weight gradient on the bf16x3 kernel k_gemm_tt3w (SV2N_WGRAD3=0: the
+// exact-f32 MFMA kernel)
+static bool wgrad3_on() {
+  static const bool on = [] {
+    const char* e = getenv("SV2N_WGRAD3");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t K) {
   constexpr int BM = 128;
   GemmPlan p{};
@@ -405,7 +415,23 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
     // K slices grouped per XCD (sv2n_gemm_kernel.h, XR): every tile of a slice
     // shares that XCD's L2 (C2 L0: HBM fetch 374 -> 122 MB, 178 -> 174 us;
     // tools/gemm_tt_tune.hip)
-    if (p.nt == 13)
+    if (p.nt == 13 && wgrad3_on() && avec && bvec && p.splitk > 1 && (F % 4) == 0 &&
+        num_nodes * std::max<int64_t>(ld_x, ldx) * 4 <= 0x7fffffff) {
+      // f32-accurate bf16x3 form (k_gemm_tt3w): same slabs, same fixed-order reduce
+      using Cfg = GemmTT3WCfg<13>;
+      static bool attr = [] {
+        (void)hipFuncSetAttribute((const void*)k_gemm_tt3w<13>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
+        return true;
+      }();
+      (void)attr;
+      const dim3 grid((unsigned)((F + Cfg::BM - 1) / Cfg::BM),
+                      (unsigned)((ldx + Cfg::BN - 1) / Cfg::BN),
+                      (unsigned)((p.splitk + 7) / 8 * 8));
+      hipLaunchKernelGGL(k_gemm_tt3w<13>, grid, dim3(Cfg::THREADS), Cfg::LDS, stream, x, ld_x,
+                         dxs, (int64_t)ldx, out, (int64_t)F, (int64_t)ldx, num_nodes, p.kslice,
+                         p.splitk);
+    } else if (p.nt == 13)
       launch_gemm_slabs<8, 1, 13, 16, false, false, 2, 0, true>(
           p.splitk, p.kslice, stream, x, ld_x, dxs, ldx, F, ldx, num_nodes, avec, bvec, out);
     else

@@ -187,3 +187,159 @@ __global__ __launch_bounds__(256) void k_gemm_tt(const float* __restrict__ A, in
 }
 
 }  // namespace sv2n
+
+namespace sv2n {
+
+// ---------------------------------------------------------------------------
+// k_gemm_tt3w: the f32-accurate (bf16x3, six products) weight-gradient GEMM,
+//   C[m][n] = Σ_k A[k][m] · B[k][n]      (A = x [K][lda], B = dxs [K][ldb])
+// shaped like the f32 kernel it replaces (k_gemm_f32<8, 1, NT, ...>): eight
+// waves stacked along M (16 rows each, BM = 128) x all BN = 16·NT columns, so
+// two waves share each SIMD — one wave's split VALU and LDS stores issue in
+// the other's MFMA shadow (an MFMA 16x16x32 holds the SIMD's issue for 8 of
+// its 16 cycles).  K steps of 32; the f32 operands of step s+1 are loaded
+// into registers while step s computes, split into three bf16 planes
+// (split3_pk) and stored to the other of two LDS stages ([plane][k][row]
+// images) after step s's MFMAs are issued; one barrier per step.  Fragments
+// come from ds_read_b64_tr_b16 exactly as in k_gemm_tt.  Split-K slices
+// write slabs part[z][M][N] with the XCD-grouped slice order of
+// k_gemm_f32<..., XR = true> (every tile of a slice on one XCD's L2).
+// ---------------------------------------------------------------------------
+template <int NT>
+struct GemmTT3WCfg {
+  static constexpr int NW = 8, THREADS = 512, BK = 32, BM = 128, BN = 16 * NT;
+  // bf16 per LDS row: the 8 rows a 32-lane half reads by ds_read_b64_tr_b16
+  // must start in 8 distinct 8-bank windows: row dwords ≡ 8 (mod 16)
+  static constexpr int pad(int w) {
+    int p = 16;
+    while (((w + p) / 2) % 16 != 8) p += 16;
+    return p;
+  }
+  static constexpr int SA = BM + pad(BM), SB = BN + pad(BN);
+  static constexpr int PA = BK * SA, PB = BK * SB;   // bf16 per plane image
+  static constexpr int STAGE = 3 * (PA + PB);        // bf16 per stage
+  static constexpr size_t LDS = sizeof(unsigned short) * 2 * STAGE;
+  static constexpr int AV = BK * BM / 4 / THREADS;                   // float4 per thread (2)
+  static constexpr int BVN = BK * BN / 4, BV = (BVN + THREADS - 1) / THREADS;
+  static_assert(BK * BM / 4 % THREADS == 0, "A staging tiles the threads");
+};
+
+template <int NT>
+__global__ __launch_bounds__(512) void k_gemm_tt3w(const float* __restrict__ A, int64_t lda,
+                                                   const float* __restrict__ B, int64_t ldb,
+                                                   float* __restrict__ part, int64_t M, int64_t N,
+                                                   int64_t K, int64_t kslice, int nz) {
+  using Cfg = GemmTT3WCfg<NT>;
+  constexpr int BK = Cfg::BK, BM = Cfg::BM, BN = Cfg::BN, SA = Cfg::SA, SB = Cfg::SB;
+  constexpr int PA = Cfg::PA, PB = Cfg::PB, STAGE = Cfg::STAGE, AV = Cfg::AV, BV = Cfg::BV;
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  // XCD-grouped K slices (k_gemm_f32 XR): block b = xcd + 8 * slot
+  const int tiles = gridDim.x * gridDim.y;
+  const int id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int xcd = id & 7, slot = id >> 3;
+  const int bz = xcd + 8 * (slot / tiles);
+  const int tile = slot - (slot / tiles) * tiles;
+  const int by = tile / gridDim.x, bx = tile - by * gridDim.x;
+  if (bz >= nz) return;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int64_t m0 = (int64_t)bx * BM, n0 = (int64_t)by * BN;
+  const int64_t kbeg = (int64_t)bz * kslice, kend = min(K, kbeg + kslice);
+  float* C = part + (int64_t)bz * M * N;
+  const rsrc_t ra = make_rsrc(A, (uint32_t)min<int64_t>(K * lda * 4, 0x7fffffff));
+  const rsrc_t rb = make_rsrc(B, (uint32_t)min<int64_t>(K * ldb * 4, 0x7fffffff));
+
+  f32x4 va[AV], vb[BV];
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int s = 0; s < AV; ++s) {
+      const int idx = t + 512 * s;
+      const int r = idx / (BM / 4), c4 = idx - r * (BM / 4);
+      const int64_t k = k0 + r, m = m0 + 4 * c4;
+      va[s] = bld4(ra, (k < kend && m < M) ? (int)((k * lda + m) * 4) : OOB);
+    }
+#pragma unroll
+    for (int s = 0; s < BV; ++s) {
+      const int idx = t + 512 * s;
+      const int r = idx / (BN / 4), c4 = idx - r * (BN / 4);
+      const int64_t k = k0 + r, n = n0 + 4 * c4;
+      vb[s] = bld4(rb, (idx < Cfg::BVN && k < kend && n < N) ? (int)((k * ldb + n) * 4) : OOB);
+    }
+  };
+  auto put = [&](unsigned short* dst, int plane, int stride, int r, int c, const f32x4& v) {
+    uint2 w[3];
+    split3_pk(v[0], v[1], w[0].x, w[1].x, w[2].x);
+    split3_pk(v[2], v[3], w[0].y, w[1].y, w[2].y);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(dst + p * plane + r * stride + c) = w[p];
+  };
+  auto store = [&](unsigned short* st) {
+#pragma unroll
+    for (int s = 0; s < AV; ++s) {
+      const int idx = t + 512 * s;
+      const int r = idx / (BM / 4), c4 = idx - r * (BM / 4);
+      put(st, PA, SA, r, 4 * c4, va[s]);
+    }
+    unsigned short* sb = st + 3 * PA;
+#pragma unroll
+    for (int s = 0; s < BV; ++s) {
+      const int idx = t + 512 * s;
+      if (idx < Cfg::BVN) {
+        const int r = idx / (BN / 4), c4 = idx - r * (BN / 4);
+        put(sb, PB, SB, r, 4 * c4, vb[s]);
+      }
+    }
+  };
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int b = 0; b < NT; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // transposed-read addresses (k_gemm_tt): lane 4q+p of its 16-lane group ->
+  // k row q (+4lg, +16), columns 4p..4p+3
+  const int q = li >> 2, p4 = 4 * (li & 3);
+  const int kA0 = (4 * lg + q) * SA, kA1 = (16 + 4 * lg + q) * SA;
+  const int kB0 = (4 * lg + q) * SB, kB1 = (16 + 4 * lg + q) * SB;
+  auto compute = [&](const unsigned short* st) {
+    const unsigned short* sa = st;
+    const unsigned short* sb = st + 3 * PA;
+    bf16x8 af[3];
+    const int ca = 16 * wave + p4;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) af[pl] = tr_frag(sa + pl * PA + kA0 + ca, sa + pl * PA + kA1 + ca);
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int cb = 16 * b + p4;
+      bf16x8 bf[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        bf[pl] = tr_frag(sb + pl * PB + kB0 + cb, sb + pl * PB + kB1 + cb);
+      acc[b] = mfma_planes<3>(af, bf, acc[b]);
+    }
+  };
+
+  const int nsteps = (int)((kend - kbeg + BK - 1) / BK);
+  if (nsteps > 0) {
+    load(kbeg);
+    store(lds);
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+      if (s + 1 < nsteps) load(kbeg + (int64_t)(s + 1) * BK);
+      compute(lds + (s & 1) * STAGE);
+      if (s + 1 < nsteps) store(lds + ((s + 1) & 1) * STAGE);
+      __syncthreads();
+    }
+  }
+  // acc[b][r] = C[row 16·wave + 4lg + r][col 16b + li] of the block tile
+#pragma unroll
+  for (int b = 0; b < NT; ++b) {
+    const int64_t gn = n0 + 16 * b + li;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t gm = m0 + 16 * wave + 4 * lg + r;
+      if (gm < M && gn < N) C[gm * N + gn] = acc[b][r];
+    }
+  }
+}
+
+}  // namespace sv2n
