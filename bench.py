@@ -159,8 +159,8 @@ def kernel_table(model, data, reps=50):
         lib.sv2n_gemm_f32x3(x0.data_ptr(), x0.stride(0), planes0.data_ptr(), out0.data_ptr(),
                             out0.stride(0), N0, W[0].shape[0], x0.shape[1], sh)
 
-    # the layer-0 weight-gradient GEMM (split-K f32 MFMA; its slab reduce and
-    # epilogue are separate launches of sv2n_gat_wgrad_node)
+    # the layer-0 weight-gradient GEMM (split-K, bf16x3 on MFMA; its slab reduce
+    # and epilogue are separate launches of sv2n_gat_wgrad_node)
     Fd, Nd = x0.shape[1], W[0].shape[0]
     nslab = lib.sv2n_gemm_f32_slabs_count(Fd, Nd, N0)
     slabs = torch.empty(nslab * Fd * Nd, device=dev)
@@ -174,8 +174,11 @@ def kernel_table(model, data, reps=50):
     rows = {
         "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * N0c * K0,
                         4.0 * (M0 * K0 + N0c * K0 + M0 * N0c), BF16X3_PEAK_TFLOPS),
+        # bf16x3 weight-gradient kernel (k_gemm_tt3w) unless SV2N_WGRAD3=0
         "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * N0c * K0,
-                        4.0 * (M0 * K0 + M0 * N0c + N0c * K0), F32_MFMA_PEAK_TFLOPS),
+                        4.0 * (M0 * K0 + M0 * N0c + N0c * K0),
+                        F32_MFMA_PEAK_TFLOPS if os.environ.get("SV2N_WGRAD3", "1") == "0"
+                        else BF16X3_PEAK_TFLOPS),
         "edge_logits_fwd": (edge_fwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS),
                             None),
         "edge_logits_bwd": (edge_bwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS),

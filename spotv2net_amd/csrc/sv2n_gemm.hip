@@ -46,7 +46,11 @@ static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + bn - 1) / bn);
   int64_t sk = 1;
   if (tiles < 240 && K >= 2048) {
-    sk = std::min<int64_t>(32, (480 + tiles - 1) / tiles);
+    static const int64_t target = [] {  // tuning override: workgroups aimed at
+      const char* e = getenv("SV2N_SPLITK_TARGET");
+      return e ? (int64_t)atoll(e) : (int64_t)480;
+    }();
+    sk = std::min<int64_t>(32, (target + tiles - 1) / tiles);
     sk = std::min<int64_t>(sk, std::max<int64_t>(1, K / 256));
   }
   int64_t ks = (K + sk - 1) / sk;
@@ -251,12 +255,88 @@ extern "C" int sv2n_gemm_f32(int a_kmajor, int b_kmajor, const float* A, int64_t
   return (int)hipGetLastError();
 }
 
+// rows-tiles per wave of k_gemm_tt3w (SV2N_WGRAD3_MT = 1 / 2 forces; 0 auto)
+static int wgrad3_mt() {
+  static const int v = [] {
+    const char* e = getenv("SV2N_WGRAD3_MT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+// How the slab GEMM of a weight gradient runs.  kind 0: exact-f32 kernel
+// (k_gemm_f32, XR slices); kind 1 / 2: bf16x3 k_gemm_tt3w<13, kind>.  For the
+// 208-column tiling the split count follows the bf16x3 kernel's rule — one
+// round of 144 KiB / 98 KiB workgroups balanced over the 8 XCDs (a multiple
+// of 8 slices, tiles x slices <= 256; MI355X, C2 L0 dWᵀ 1260 x 408 x 15360:
+// 24 slices 92 us, 16: 126 us, 32: 130 us), at most 64 slices of >= 256 rows
+// (sv2n_gat_wgrad_node_workspace covers both plans); unaligned operands run
+// the f32 kernel on the same slices.
+struct SlabPlan {
+  int kind, nt, splitk;
+  int64_t kslice;
+};
+static SlabPlan slab_plan(int64_t F, int64_t N, int64_t K, bool vec, int64_t lda, int64_t ldb) {
+  const GemmPlan p = plan_gemm(F, N, K);
+  SlabPlan sp{0, p.nt, p.splitk, p.kslice};
+  // 208-column tiles: N = 408 (C2 L0, two tiles) and N = 208 (C2 L1, one)
+  const bool cols208 = (N + 207) / 208 * 208 * 4 <= 5 * N;
+  if (!(cols208 && wgrad3_on() && p.splitk > 1)) return sp;
+  sp.nt = 13;
+  int mt = wgrad3_mt();
+  if (mt != 1 && mt != 2) mt = ((F + 255) / 256) * ((N + 207) / 208) >= 8 ? 2 : 1;
+  const int64_t tiles = ((F + 128 * mt - 1) / (128 * mt)) * ((N + 207) / 208);
+  int64_t sk = 8 * std::max<int64_t>(1, 256 / (8 * tiles));
+  sk = std::min<int64_t>(sk, std::min<int64_t>(64, std::max<int64_t>(8, K / 256 / 8 * 8)));
+  int64_t ks = (K + sk - 1) / sk;
+  ks = (ks + 31) / 32 * 32;
+  sp.splitk = (int)((K + ks - 1) / ks);
+  sp.kslice = ks;
+  const bool ok = vec && (F % 4) == 0 && K * std::max(lda, ldb) * 4 <= 0x7fffffff;
+  sp.kind = ok ? mt : 0;
+  return sp;
+}
+
+template <int NT, int MT>
+static void launch_tt3w(const SlabPlan& p, hipStream_t stream, const float* x, int64_t ld_x,
+                        const float* dxs, int64_t ldx, int64_t F, int64_t N, int64_t K,
+                        float* out) {
+  using Cfg = GemmTT3WCfg<NT, MT>;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)k_gemm_tt3w<NT, MT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
+    return true;
+  }();
+  (void)attr;
+  const dim3 grid((unsigned)((F + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN),
+                  (unsigned)((p.splitk + 7) / 8 * 8));
+  hipLaunchKernelGGL((k_gemm_tt3w<NT, MT>), grid, dim3(Cfg::THREADS), Cfg::LDS, stream, x, ld_x,
+                     dxs, ldx, out, F, N, K, p.kslice, p.splitk);
+}
+
+static void launch_wgrad_slabs(const SlabPlan& p, hipStream_t stream, const float* x,
+                               int64_t ld_x, const float* dxs, int64_t ldx, int64_t F, int64_t N,
+                               int64_t K, bool avec, bool bvec, float* out) {
+  if (p.kind == 2) {
+    launch_tt3w<13, 2>(p, stream, x, ld_x, dxs, ldx, F, N, K, out);
+  } else if (p.kind == 1) {
+    launch_tt3w<13, 1>(p, stream, x, ld_x, dxs, ldx, F, N, K, out);
+  } else if (p.nt == 13) {
+    launch_gemm_slabs<8, 1, 13, 16, false, false, 2, 0, true>(p.splitk, p.kslice, stream, x, ld_x,
+                                                              dxs, ldx, F, N, K, avec, bvec, out);
+  } else {
+    launch_gemm_slabs<8, 1, 8, 16, false, false, 2, 0, true>(p.splitk, p.kslice, stream, x, ld_x,
+                                                             dxs, ldx, F, N, K, avec, bvec, out);
+  }
+}
+
 // ---- the split-K GEMM alone: C's K slices left as slabs [nsplit][M][N] ------
 // (what sv2n_gat_wgrad_node runs before its reduce; exposed for consumers that
 // fuse the reduction, and so the kernel can be timed by itself)
 extern "C" int sv2n_gemm_f32_slabs_count(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
-  return plan_gemm(M, N, K).splitk;
+  // enough for either plan (the non-k-major weight-gradient case follows slab_plan)
+  return std::max(plan_gemm(M, N, K).splitk, slab_plan(M, N, K, true, M, N).splitk);
 }
 
 extern "C" int sv2n_gemm_f32_slabs(int a_kmajor, int b_kmajor, const float* A, int64_t lda,
@@ -272,6 +352,12 @@ extern "C" int sv2n_gemm_f32_slabs(int a_kmajor, int b_kmajor, const float* A, i
   launch_gemm_slabs<8, 1, NT, 16, AK, BK, 2, 0, true>(p.splitk, p.kslice, stream, A, lda, B, ldb, \
                                                     M, N, K, \
                                              avec, bvec, slabs)
+  if (!a_kmajor && !b_kmajor) {
+    const SlabPlan sp = slab_plan(M, N, K, avec && bvec, lda, ldb);
+    if (slab_floats < (int64_t)sp.splitk * M * N) return SV2N_ERR_WORKSPACE;
+    launch_wgrad_slabs(sp, stream, A, lda, B, ldb, M, N, K, avec, bvec, slabs);
+    return (int)hipGetLastError();
+  }
   if (p.nt == 13) {
     if (a_kmajor && b_kmajor) SV2N_SLABS(13, true, true);
     else if (a_kmajor) SV2N_SLABS(13, true, false);
@@ -288,9 +374,15 @@ extern "C" int sv2n_gemm_f32_slabs(int a_kmajor, int b_kmajor, const float* A, i
 }
 
 // ---- weight gradients of one layer: split-K GEMM + fused epilogue ----------
+// The slab GEMM of a weight gradient, T[f][o] = Σ_k x[k][f] · dxs[k][o] (both
+// operands k-strided): the bf16x3 kernel k_gemm_tt3w where it applies (208-
+// column tiles, split-K, 16-B aligned operands), else the exact-f32 kernel; K
+// slices grouped per XCD either way (C2 L0: HBM fetch 374 -> 122 MB).
 static int64_t wgrad_slab_floats(int64_t n_nodes, int F, int ldt) {
   const GemmPlan p = plan_gemm(F, ldt, n_nodes);
-  return p.splitk > 1 ? (int64_t)p.splitk * F * ldt : 0;
+  const SlabPlan sp = slab_plan(F, ldt, n_nodes, true, F, ldt);
+  const int sk = std::max(p.splitk, sp.splitk);
+  return sk > 1 ? (int64_t)sk * F * ldt : 0;
 }
 
 extern "C" int64_t sv2n_gat_wgrad_node_workspace(int64_t num_nodes, int in_features, int ldx,
@@ -408,35 +500,11 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
     }
   } else if (weights) {
     // T[f][o] = Σ_k x[k][f] · dxs[k][o]   (both operands k-strided)
-    const GemmPlan p = plan_gemm(F, ldx, num_nodes);
     const bool avec = ((uintptr_t)x % 16 == 0) && (ld_x % 4 == 0);
     const bool bvec = ((uintptr_t)dxs % 16 == 0) && (ldx % 4 == 0);
+    const SlabPlan p = slab_plan(F, ldx, num_nodes, avec && bvec, ld_x, ldx);
     float* out = p.splitk > 1 ? slabs : T;
-    // K slices grouped per XCD (sv2n_gemm_kernel.h, XR): every tile of a slice
-    // shares that XCD's L2 (C2 L0: HBM fetch 374 -> 122 MB, 178 -> 174 us;
-    // tools/gemm_tt_tune.hip)
-    if (p.nt == 13 && wgrad3_on() && avec && bvec && p.splitk > 1 && (F % 4) == 0 &&
-        num_nodes * std::max<int64_t>(ld_x, ldx) * 4 <= 0x7fffffff) {
-      // f32-accurate bf16x3 form (k_gemm_tt3w): same slabs, same fixed-order reduce
-      using Cfg = GemmTT3WCfg<13>;
-      static bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)k_gemm_tt3w<13>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
-        return true;
-      }();
-      (void)attr;
-      const dim3 grid((unsigned)((F + Cfg::BM - 1) / Cfg::BM),
-                      (unsigned)((ldx + Cfg::BN - 1) / Cfg::BN),
-                      (unsigned)((p.splitk + 7) / 8 * 8));
-      hipLaunchKernelGGL(k_gemm_tt3w<13>, grid, dim3(Cfg::THREADS), Cfg::LDS, stream, x, ld_x,
-                         dxs, (int64_t)ldx, out, (int64_t)F, (int64_t)ldx, num_nodes, p.kslice,
-                         p.splitk);
-    } else if (p.nt == 13)
-      launch_gemm_slabs<8, 1, 13, 16, false, false, 2, 0, true>(
-          p.splitk, p.kslice, stream, x, ld_x, dxs, ldx, F, ldx, num_nodes, avec, bvec, out);
-    else
-      launch_gemm_slabs<8, 1, 8, 16, false, false, 2, 0, true>(
-          p.splitk, p.kslice, stream, x, ld_x, dxs, ldx, F, ldx, num_nodes, avec, bvec, out);
+    launch_wgrad_slabs(p, stream, x, ld_x, dxs, ldx, F, ldx, num_nodes, avec, bvec, out);
     if (p.splitk > 1) {
       const int64_t tot = (int64_t)F * ldx;
       hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,

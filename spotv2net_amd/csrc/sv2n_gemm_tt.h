@@ -205,9 +205,9 @@ namespace sv2n {
 // write slabs part[z][M][N] with the XCD-grouped slice order of
 // k_gemm_f32<..., XR = true> (every tile of a slice on one XCD's L2).
 // ---------------------------------------------------------------------------
-template <int NT>
+template <int NT, int MT>
 struct GemmTT3WCfg {
-  static constexpr int NW = 8, THREADS = 512, BK = 32, BM = 128, BN = 16 * NT;
+  static constexpr int NW = 8, THREADS = 512, BK = 32, BM = 16 * MT * NW, BN = 16 * NT;
   // bf16 per LDS row: the 8 rows a 32-lane half reads by ds_read_b64_tr_b16
   // must start in 8 distinct 8-bank windows: row dwords ≡ 8 (mod 16)
   static constexpr int pad(int w) {
@@ -218,18 +218,20 @@ struct GemmTT3WCfg {
   static constexpr int SA = BM + pad(BM), SB = BN + pad(BN);
   static constexpr int PA = BK * SA, PB = BK * SB;   // bf16 per plane image
   static constexpr int STAGE = 3 * (PA + PB);        // bf16 per stage
-  static constexpr size_t LDS = sizeof(unsigned short) * 2 * STAGE;
-  static constexpr int AV = BK * BM / 4 / THREADS;                   // float4 per thread (2)
+  // two stages (one barrier per step) when they fit the 160 KiB LDS, else one
+  static constexpr int NSTAGE = sizeof(unsigned short) * 2 * STAGE <= 160 * 1024 ? 2 : 1;
+  static constexpr size_t LDS = sizeof(unsigned short) * NSTAGE * STAGE;
+  static constexpr int AV = BK * BM / 4 / THREADS;                   // float4 per thread
   static constexpr int BVN = BK * BN / 4, BV = (BVN + THREADS - 1) / THREADS;
   static_assert(BK * BM / 4 % THREADS == 0, "A staging tiles the threads");
 };
 
-template <int NT>
+template <int NT, int MT>
 __global__ __launch_bounds__(512) void k_gemm_tt3w(const float* __restrict__ A, int64_t lda,
                                                    const float* __restrict__ B, int64_t ldb,
                                                    float* __restrict__ part, int64_t M, int64_t N,
                                                    int64_t K, int64_t kslice, int nz) {
-  using Cfg = GemmTT3WCfg<NT>;
+  using Cfg = GemmTT3WCfg<NT, MT>;
   constexpr int BK = Cfg::BK, BM = Cfg::BM, BN = Cfg::BN, SA = Cfg::SA, SB = Cfg::SB;
   constexpr int PA = Cfg::PA, PB = Cfg::PB, STAGE = Cfg::STAGE, AV = Cfg::AV, BV = Cfg::BV;
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
@@ -292,9 +294,11 @@ __global__ __launch_bounds__(512) void k_gemm_tt3w(const float* __restrict__ A, 
     }
   };
 
-  f32x4 acc[NT];
+  f32x4 acc[MT][NT];
 #pragma unroll
-  for (int b = 0; b < NT; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   // transposed-read addresses (k_gemm_tt): lane 4q+p of its 16-lane group ->
   // k row q (+4lg, +16), columns 4p..4p+3
   const int q = li >> 2, p4 = 4 * (li & 3);
@@ -303,10 +307,14 @@ __global__ __launch_bounds__(512) void k_gemm_tt3w(const float* __restrict__ A, 
   auto compute = [&](const unsigned short* st) {
     const unsigned short* sa = st;
     const unsigned short* sb = st + 3 * PA;
-    bf16x8 af[3];
-    const int ca = 16 * wave + p4;
+    bf16x8 af[MT][3];
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) af[pl] = tr_frag(sa + pl * PA + kA0 + ca, sa + pl * PA + kA1 + ca);
+    for (int a = 0; a < MT; ++a) {
+      const int ca = 16 * (MT * wave + a) + p4;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        af[a][pl] = tr_frag(sa + pl * PA + kA0 + ca, sa + pl * PA + kA1 + ca);
+    }
 #pragma unroll
     for (int b = 0; b < NT; ++b) {
       const int cb = 16 * b + p4;
@@ -314,7 +322,8 @@ __global__ __launch_bounds__(512) void k_gemm_tt3w(const float* __restrict__ A, 
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
         bf[pl] = tr_frag(sb + pl * PB + kB0 + cb, sb + pl * PB + kB1 + cb);
-      acc[b] = mfma_planes<3>(af, bf, acc[b]);
+#pragma unroll
+      for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<3>(af[a], bf, acc[a][b]);
     }
   };
 
@@ -325,21 +334,29 @@ __global__ __launch_bounds__(512) void k_gemm_tt3w(const float* __restrict__ A, 
     __syncthreads();
     for (int s = 0; s < nsteps; ++s) {
       if (s + 1 < nsteps) load(kbeg + (int64_t)(s + 1) * BK);
-      compute(lds + (s & 1) * STAGE);
-      if (s + 1 < nsteps) store(lds + ((s + 1) & 1) * STAGE);
+      if constexpr (Cfg::NSTAGE == 2) {
+        compute(lds + (s & 1) * STAGE);
+        if (s + 1 < nsteps) store(lds + ((s + 1) & 1) * STAGE);
+      } else {
+        compute(lds);
+        __syncthreads();  // every wave is done reading the stage
+        if (s + 1 < nsteps) store(lds);
+      }
       __syncthreads();
     }
   }
-  // acc[b][r] = C[row 16·wave + 4lg + r][col 16b + li] of the block tile
+  // acc[a][b][r] = C[row 16(MT·wave + a) + 4lg + r][col 16b + li] of the block tile
 #pragma unroll
-  for (int b = 0; b < NT; ++b) {
-    const int64_t gn = n0 + 16 * b + li;
+  for (int a = 0; a < MT; ++a)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t gm = m0 + 16 * wave + 4 * lg + r;
-      if (gm < M && gn < N) C[gm * N + gn] = acc[b][r];
+    for (int b = 0; b < NT; ++b) {
+      const int64_t gn = n0 + 16 * b + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t gm = m0 + 16 * (MT * wave + a) + 4 * lg + r;
+        if (gm < M && gn < N) C[gm * N + gn] = acc[a][b][r];
+      }
     }
-  }
 }
 
 }  // namespace sv2n
