@@ -24,11 +24,11 @@ from collections import defaultdict
 # bench.py kernel_table name -> rocprof kernel name prefix (the C2 instantiation)
 KERNELS = {
     "gemm_l0_fwd": "sv2n::k_gemm3<8, 1, 13, 64, 1, 3>",
-    "gemm_l0_dwT": "sv2n::k_gemm_f32<8, 1, 13, 16, false, false, 2, 0, true, true, true>",
+    "gemm_l0_dwT": "sv2n::k_gemm_tt3w<13, 2>",
     "edge_logits_fwd": "sv2n::k_edge_fwd<8, 8, false>",
     "edge_logits_bwd": "sv2n::k_edge_bwd<8, 8, false>",
-    "gat_attn_fwd_l0": "sv2n::k_attn_fwd<1, true>",
-    "gat_attn_bwd_l0": "sv2n::k_attn_bwd<1, true>",
+    "gat_attn_fwd_l0": "sv2n::canon::k_fwd<1, true, false>",
+    "gat_attn_bwd_l0": "sv2n::canon::k_bwd<1, true, false>",
 }
 
 
