@@ -898,22 +898,24 @@ using namespace sv2n;
 namespace sv2n {
 // sv2n_attn_canon.hip: complete graphs in canonical edge order
 void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
-                    const float* bias, const uint8_t* keep, float keep_scale, float* y,
-                    float* psave, int n, int H, int C, int concat, int act, float slope);
+                    int ae_edge_order, const uint32_t* rowmask, const float* bias,
+                    const uint8_t* keep, float keep_scale, float* y, float* psave, int n, int H,
+                    int C, int concat, int act, float slope);
 void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, const float* xs,
                     int ldx, const float* psave, const uint8_t* keep, float keep_scale,
-                    float* dxs, float* dae, float* dbias, int n, int H, int C, int concat,
-                    int act, float slope);
+                    const uint32_t* rowmask, float* dxs, float* dae, int ae_edge_order,
+                    float* dbias, int n, int H, int C, int concat, int act, float slope);
 }  // namespace sv2n
 
-// The lean complete-graph kernels take every canonical batch (edge logits in
-// edge order, or no edge features) unless SV2N_ATTN_CANON=0 (A/B switch).
-static bool canon_path(const float* ae, int ae_edge_order, const uint32_t* rowmask, int n, int H) {
+// The lean kernels (sv2n_attn_canon.hip) take every n <= 32 launch — canonical
+// batches (edge logits in edge order) and block layouts (row masks, dense
+// [n][n][H] logits) — unless SV2N_ATTN_CANON=0 (A/B switch: the kernels below).
+static bool canon_path(int n, int H) {
   static const bool on = [] {
     const char* e = getenv("SV2N_ATTN_CANON");
     return !(e && e[0] == '0');
   }();
-  return on && !rowmask && (!ae || ae_edge_order) && n >= 2 && n <= 32 && H <= 8;
+  return on && n >= 1 && n <= 32 && H <= 8;
 }
 
 static size_t fwd_lds(int H, FwdChunking ck) {
@@ -1037,9 +1039,9 @@ extern "C" int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, int 
   if (!xs || !y || !psave) return SV2N_ERR_ARG;
   if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
   if (ae_edge_order && (rowmask || n < 2)) return SV2N_ERR_ARG;  // complete graphs only
-  if (canon_path(ae, ae_edge_order, rowmask, n, heads)) {
-    attn_canon_fwd(num_graphs, stream, xs, ldx, ae, bias, keep, keep_scale, y, psave, n, heads,
-                   channels, concat, act, negative_slope);
+  if (canon_path(n, heads)) {
+    attn_canon_fwd(num_graphs, stream, xs, ldx, ae, ae_edge_order, rowmask, bias, keep,
+                   keep_scale, y, psave, n, heads, channels, concat, act, negative_slope);
     return (int)hipGetLastError();
   }
   if (concat) {
@@ -1061,9 +1063,10 @@ extern "C" int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* x
   if (!dy || !y || !xs || !psave || !dxs || !dbias_partial) return SV2N_ERR_ARG;
   if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
   if (ae_edge_order && (rowmask || n < 2)) return SV2N_ERR_ARG;  // complete graphs only
-  if (canon_path(dae, ae_edge_order, rowmask, n, heads)) {
-    attn_canon_bwd(num_graphs, stream, dy, y, xs, ldx, psave, keep, keep_scale, dxs, dae,
-                   dbias_partial, n, heads, channels, concat, act, negative_slope);
+  if (canon_path(n, heads)) {
+    attn_canon_bwd(num_graphs, stream, dy, y, xs, ldx, psave, keep, keep_scale, rowmask, dxs,
+                   dae, ae_edge_order, dbias_partial, n, heads, channels, concat, act,
+                   negative_slope);
     return (int)hipGetLastError();
   }
   if (concat) {

@@ -63,8 +63,8 @@ __device__ __forceinline__ void bst_s(rsrc_t r, int voff, int soff, float v) {
 // ---------------------------------------------------------------------------
 template <int ACT, bool CONCAT, bool KEEP>
 __global__ __launch_bounds__(THREADS) void k_fwd(
-    const float* __restrict__ xs, int ldx, const float* __restrict__ ae,
-    const float* __restrict__ bias, const uint8_t* __restrict__ keep, float keep_scale,
+    const float* __restrict__ xs, int ldx, const float* __restrict__ ae, int ae_edge_order,
+    const uint32_t* __restrict__ rowmask, const float* __restrict__ bias, const uint8_t* __restrict__ keep, float keep_scale,
     float* __restrict__ y, float* __restrict__ psave, int n, int H, int C, float slope) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sP = smem;
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
   const int l32 = lane & 31, half = lane >> 5;
   const int HC = H * C, OC = CONCAT ? HC : C;
   const int E0 = n * (n - 1), P = E0 / 2;
-  const int nae = ae ? E0 * H : 0;
+  const int nae = ae ? (ae_edge_order ? E0 : n * n) * H : 0;
   const int ntc = (C + 31) >> 5;
   const rsrc_t rx = make_rsrc(xs + (int64_t)g * n * ldx, (uint32_t)(n * ldx) * 4u);
   const rsrc_t ry = make_rsrc(y + (int64_t)g * n * OC, (uint32_t)(n * OC) * 4u);
@@ -137,6 +137,11 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 #pragma unroll
   for (int u = 0; u < 4; ++u)
     if (u < nq) load_b(u, bq[u]);
+  // sources of target row l32 (block layouts: the row mask; else all n)
+  const uint32_t allm = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
+  const uint32_t rbits =
+      (rowmask ? bld_u32(make_rsrc(rowmask + (int64_t)g * n, (uint32_t)n * 4u), l32 * 4) : allm) &
+      ~(1u << l32);
 
 #pragma unroll
   for (int q = 0; q < AEV; ++q) {
@@ -180,8 +185,10 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       const int j = 16 * half + kk;
       float a = 0.f;
       if (ae) {
-        const bool ev = iv && j < n && j != i;
-        const int e = j < i ? ((j * (2 * n - 1 - j)) >> 1) - j - 1 + i : Ehi + j;
+        const bool ev = iv && ((rbits >> j) & 1u);
+        const int e = !ae_edge_order ? i * n + j
+                      : j < i        ? ((j * (2 * n - 1 - j)) >> 1) - j - 1 + i
+                                     : Ehi + j;
         const float v = sAE[ev ? e * H + h : 0];
         a = ev ? v : 0.f;
       }
@@ -189,7 +196,8 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       lg[kk] = as4[kk >> 2][kk & 3] + ad + a;
     }
     esum += __shfl_xor(esum, 32, 64);
-    const float loopv = (ae && n > 1) ? esum / (float)(n - 1) : 0.f;
+    const int cnt = __popc(rbits);
+    const float loopv = (ae && cnt > 0) ? esum / (float)cnt : 0.f;
     float mx = -INFINITY;
     uint32_t negm = 0u;
 #pragma unroll
@@ -200,14 +208,14 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       negm |= neg ? (1u << kk) : 0u;
       v = neg ? v * slope : v;
       lg[kk] = v;
-      if (iv && j < n) mx = fmaxf(mx, v);
+      if (iv && (j == i || ((rbits >> j) & 1u))) mx = fmaxf(mx, v);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     float den = 0.f;
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       const int j = 16 * half + kk;
-      lg[kk] = (iv && j < n) ? __expf(lg[kk] - mx) : 0.f;
+      lg[kk] = (iv && (j == i || ((rbits >> j) & 1u))) ? __expf(lg[kk] - mx) : 0.f;
       den += lg[kk];
     }
     den += __shfl_xor(den, 32, 64);
@@ -220,7 +228,8 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       for (int c = 0; c < 4; ++c) {
         const int kk = 4 * k4 + c;
         const float p = lg[kk] * inv;
-        const bool valid = iv && 16 * half + kk < n;
+        const int jv = 16 * half + kk;
+        const bool valid = iv && (jv == i || ((rbits >> jv) & 1u));
         pkeep[s2][kk] = valid ? (((negm >> kk) & 1u) ? -p : p) : 0.f;
         float d = p;
         if constexpr (KEEP) d = ((kw[k4] >> (8 * c)) & 0xffu) ? d * keep_scale : 0.f;
@@ -311,15 +320,16 @@ template <int ACT, bool CONCAT, bool KEEP>
 __global__ __launch_bounds__(THREADS) void k_bwd(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ xs,
     int ldx, const float* __restrict__ psave, const uint8_t* __restrict__ keep, float keep_scale,
-    float* __restrict__ dxs, float* __restrict__ dae, float* __restrict__ dbias_part, int n,
-    int H, int C, float slope) {
+    const uint32_t* __restrict__ rowmask, float* __restrict__ dxs, float* __restrict__ dae,
+    int ae_edge_order, float* __restrict__ dbias_part, int n, int H, int C, float slope) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sP = smem;
   float* sArea = sP + H * 32 * PS;
   float* sDL = sArea + 4 * 2 * 32 * CS;
   float* sSh = sDL + H * 32 * DS;
   float* sDad = sSh + H * 32;
-  uint16_t* sDec = reinterpret_cast<uint16_t*>(sDad + H * 32);  // pair p -> (u << 8 | w)
+  uint32_t* sRB = reinterpret_cast<uint32_t*>(sDad + H * 32);  // source bits of row i
+  uint16_t* sDec = reinterpret_cast<uint16_t*>(sRB + 32);       // pair p -> (u << 8 | w)
 
   SV2N_STAMP(0, SV2N_RT());
   SV2N_STAMP(1, SV2N_T());
@@ -378,7 +388,13 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     load_p(wave);
     load_chunk(0);
   }
-  if (dae && t < n) {  // row u of the pair table (read after the final barrier)
+  // sources of target row l32 (block layouts: the row mask; else all n)
+  const uint32_t allm = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
+  const uint32_t rbits =
+      (rowmask ? bld_u32(make_rsrc(rowmask + (int64_t)g * n, (uint32_t)n * 4u), l32 * 4) : allm) &
+      ~(1u << l32);
+  if (t < 32) sRB[t] = rbits;
+  if (dae && ae_edge_order && t < n) {  // row u of the pair table (read after the final barrier)
     const int base = (t * (2 * n - 1 - t)) >> 1;
     for (int w = t + 1; w < n; ++w) sDec[base + w - t - 1] = (uint16_t)((t << 8) | w);
   }
@@ -464,7 +480,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       for (int r = 0; r < 16; ++r) {
         const int jr = crow(r, half);
         ps[r] = pr[r >> 2][r & 3];
-        const bool valid = iv && jr < n;
+        const bool valid = iv && (jr == i || ((rbits >> jr) & 1u));
         float d = valid ? (CONCAT ? G[r] : G[r] * invH) : 0.f;
         if constexpr (KEEP) d = ((kb[r >> 2] >> (8 * (r & 3))) & 0xffu) ? d * keep_scale : 0.f;
         dp[r] = d;
@@ -476,7 +492,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int jr = crow(r, half);
-        const bool valid = iv && jr < n;
+        const bool valid = iv && (jr == i || ((rbits >> jr) & 1u));
         const float ds = fabsf(ps[r]) * (dp[r] - tl);
         const float dl = valid ? (signbit(ps[r]) ? ds * slope : ds) : 0.f;
         dad += dl;
@@ -488,7 +504,8 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       const float dlii = (half == hi) ? mine : other;
       if (half == 0) {
         sDad[h * 32 + i] = iv ? dad : 0.f;
-        sSh[h * 32 + i] = (iv && n > 1) ? dlii / (float)(n - 1) : 0.f;
+        const int cnt = __popc(rbits);
+        sSh[h * 32 + i] = (iv && cnt > 0) ? dlii / (float)cnt : 0.f;
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) G[r] = 0.f;
@@ -501,7 +518,24 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 
   // ---- d ae in canonical edge order [E0][H]: pair p = (u, w), u < w, is edge
   //      p (target w, source u) and edge P + p (target u, source w) ----
-  if (dae) {
+  if (dae && !ae_edge_order) {
+    // ---- dense [n][n][H] block (block layouts): zeros off the edge set ----
+    const int nae = n * n * H;
+    const rsrc_t rdae = make_rsrc(dae + (int64_t)g * nae, (uint32_t)nae * 4u);
+    for (int k = t; k < n * n; k += THREADS) {
+      const int ti = k / n, tj = k - ti * n;
+      const bool e = tj != ti && ((sRB[ti] >> tj) & 1u);
+      if (H == 4) {
+        f32x4 v;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) v[h] = e ? sDL[(h * 32 + ti) * DS + tj] + sSh[h * 32 + ti] : 0.f;
+        bst4(rdae, k * 16, v);
+      } else {
+        for (int h = 0; h < H; ++h)
+          bst(rdae, (k * H + h) * 4, e ? sDL[(h * 32 + ti) * DS + tj] + sSh[h * 32 + ti] : 0.f);
+      }
+    }
+  } else if (dae) {
     const int P = E0 / 2, nae = E0 * H;
     const rsrc_t rdae = make_rsrc(dae + (int64_t)g * nae, (uint32_t)nae * 4u);
     for (int p = t; p < P; p += THREADS) {
@@ -555,31 +589,31 @@ extern "C" int sv2n_diag_stamps(unsigned long long* out, int64_t count) {
 // ---- launchers (called by the C-ABI entry points in sv2n_attn.hip) ---------
 size_t attn_canon_bwd_lds(int H) {
   return sizeof(float) * ((size_t)H * 32 * canon::PS + 4 * 2 * 32 * canon::CS +
-                          (size_t)H * 32 * canon::DS + 2 * (size_t)H * 32) +
+                          (size_t)H * 32 * canon::DS + 2 * (size_t)H * 32 + 32) +
          sizeof(uint16_t) * 32 * 31 / 2;
 }
 
 template <int ACT, bool CONCAT, bool KEEP>
 static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y,
                              const float* xs, int ldx, const float* psave, const uint8_t* keep,
-                             float keep_scale, float* dxs, float* dae, float* dbias, int n, int H,
-                             int C, float slope) {
+                             float keep_scale, const uint32_t* rowmask, float* dxs, float* dae,
+                             int ae_edge_order, float* dbias, int n, int H, int C, float slope) {
   const size_t lds = attn_canon_bwd_lds(H);
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)canon::k_bwd<ACT, CONCAT, KEEP>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipLaunchKernelGGL((canon::k_bwd<ACT, CONCAT, KEEP>), dim3((unsigned)B), dim3(canon::THREADS),
-                     lds, st, dy, y, xs, ldx, psave, keep, keep_scale, dxs, dae, dbias, n, H, C,
-                     slope);
+                     lds, st, dy, y, xs, ldx, psave, keep, keep_scale, rowmask, dxs, dae,
+                     ae_edge_order, dbias, n, H, C, slope);
 }
 
 void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, const float* xs,
                     int ldx, const float* psave, const uint8_t* keep, float keep_scale,
-                    float* dxs, float* dae, float* dbias, int n, int H, int C, int concat,
-                    int act, float slope) {
-#define SV2N_CB(A, CC, K)                                                                 \
-  launch_canon_bwd<A, CC, K>(B, st, dy, y, xs, ldx, psave, keep, keep_scale, dxs, dae, dbias, n, \
-                             H, C, slope)
+                    const uint32_t* rowmask, float* dxs, float* dae, int ae_edge_order,
+                    float* dbias, int n, int H, int C, int concat, int act, float slope) {
+#define SV2N_CB(A, CC, K)                                                                  \
+  launch_canon_bwd<A, CC, K>(B, st, dy, y, xs, ldx, psave, keep, keep_scale, rowmask, dxs, dae, \
+                             ae_edge_order, dbias, n, H, C, slope)
 #define SV2N_CB_ACT(CC, K)                 \
   switch (act) {                           \
     case 0: SV2N_CB(0, CC, K); break;      \
@@ -595,29 +629,34 @@ void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, 
 #undef SV2N_CB_ACT
 #undef SV2N_CB
 }
-size_t attn_canon_fwd_lds(int n, int H, bool has_ae) {
-  const int nae = has_ae ? n * (n - 1) * H : 0;
+
+size_t attn_canon_fwd_lds(int n, int H, bool has_ae, bool edge_order) {
+  const int nae = has_ae ? (edge_order ? n * (n - 1) : n * n) * H : 0;
   return sizeof(float) * ((size_t)H * 32 * canon::PS + 2 * (size_t)H * 32 +
                           (size_t)((nae + 3) & ~3));
 }
 
 template <int ACT, bool CONCAT, bool KEEP>
 static void launch_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
-                             const float* bias, const uint8_t* keep, float keep_scale, float* y,
-                             float* psave, int n, int H, int C, float slope) {
-  const size_t lds = attn_canon_fwd_lds(n, H, ae != nullptr);
+                             int ae_edge_order, const uint32_t* rowmask, const float* bias,
+                             const uint8_t* keep, float keep_scale, float* y, float* psave, int n,
+                             int H, int C, float slope) {
+  const size_t lds = attn_canon_fwd_lds(n, H, ae != nullptr, ae_edge_order != 0);
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)canon::k_fwd<ACT, CONCAT, KEEP>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipLaunchKernelGGL((canon::k_fwd<ACT, CONCAT, KEEP>), dim3((unsigned)B), dim3(canon::THREADS),
-                     lds, st, xs, ldx, ae, bias, keep, keep_scale, y, psave, n, H, C, slope);
+                     lds, st, xs, ldx, ae, ae_edge_order, rowmask, bias, keep, keep_scale, y,
+                     psave, n, H, C, slope);
 }
 
 void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
-                    const float* bias, const uint8_t* keep, float keep_scale, float* y,
-                    float* psave, int n, int H, int C, int concat, int act, float slope) {
-#define SV2N_CF(A, CC, K) \
-  launch_canon_fwd<A, CC, K>(B, st, xs, ldx, ae, bias, keep, keep_scale, y, psave, n, H, C, slope)
+                    int ae_edge_order, const uint32_t* rowmask, const float* bias,
+                    const uint8_t* keep, float keep_scale, float* y, float* psave, int n, int H,
+                    int C, int concat, int act, float slope) {
+#define SV2N_CF(A, CC, K)                                                                     \
+  launch_canon_fwd<A, CC, K>(B, st, xs, ldx, ae, ae_edge_order, rowmask, bias, keep, keep_scale, \
+                             y, psave, n, H, C, slope)
 #define SV2N_CF_ACT(CC, K)                 \
   switch (act) {                           \
     case 0: SV2N_CF(0, CC, K); break;      \
