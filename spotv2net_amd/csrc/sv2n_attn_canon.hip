@@ -1,24 +1,25 @@
-// GAT attention for COMPLETE graphs of n <= 32 nodes in the reference's
-// canonical edge order — the 30-asset volatility-spillover graphs of every
-// SpotV2Net configuration (utils/dataset.py:216-226; PyG 2.3.0 GATConv inside
-// utils/models.py:146).  Same contract and saved
-// state as k_attn_fwd / k_attn_bwd (sv2n_attn.hip), which keep the general
-// block layouts (row masks, dense [n][n][H] logits, column chunking); these
-// kernels are the lean form of the common case:
+// GAT attention for graphs of n <= 32 nodes — the 30-asset volatility-
+// spillover graphs of every SpotV2Net configuration (utils/dataset.py:216-226;
+// PyG 2.3.0 GATConv inside utils/models.py:146).
+// Same contract and saved state as k_attn_fwd / k_attn_bwd (sv2n_attn.hip, the
+// round-1 kernels, kept behind SV2N_ATTN_CANON=0), with far fewer instructions
+// per wave:
 //
-//  * the edge logits of a graph arrive as one contiguous [E0][H] block and are
-//    copied into LDS as they lie (16-B loads and stores, no per-element
-//    decode); the softmax lane of target i and source j finds its edge by the
-//    closed form of the canonical order,
+//  * the edge logits of a graph arrive as one contiguous block — [E0][H] in
+//    the canonical edge order, or the dense [n][n][H] block of a row-mask
+//    layout — and are copied into LDS as they lie (16-B loads and stores, no
+//    per-element decode); the softmax lane of target i and source j finds a
+//    canonical edge by the closed form of the order,
 //      e(i, j) = T(j) + i - j - 1              (j < i: the upper pair (j, i))
 //              = P + T(i) + j - i - 1          (j > i: the swapped pair),
 //    T(x) = x(2n - x - 1)/2, P = n(n - 1)/2;
-//  * lane (i, half) of a wave owns target row i and sources 16·half .. +15, so
-//    its 16 probabilities are exactly the A operand it feeds to the 16 steps of
-//    v_mfma_f32_32x32x2f32 (step kk pairs source kk with source 16 + kk);
+//  * lane (i, half) of a wave owns target row i and sources 16·half .. +15:
+//    its 16 probabilities are the A operand of the 16 steps of
+//    v_mfma_f32_32x32x2f32 (step kk pairs source kk with source 16 + kk), read
+//    back from LDS with four ds_read_b128 by whichever wave aggregates the head;
 //  * the xs / dy / y operands are read straight from HBM in the MFMA operand
 //    layouts (dword buffer loads, 128 B per half-wave, the row stride in a
-//    scalar offset register), one work item ahead of the MFMAs that use them.
+//    scalar offset register), ahead of the MFMAs that use them.
 #include "sv2n_common.h"
 
 namespace sv2n {
