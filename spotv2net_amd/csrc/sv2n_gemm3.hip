@@ -39,19 +39,35 @@ __global__ void k_split3_t(const float* __restrict__ x, int64_t rows, int64_t K,
   }
 }
 
-template <int NW, int MT, int NT, int BK>
-static int launch_gemm3(hipStream_t st, const float* A, int64_t lda, const unsigned short* Bp,
-                        int64_t Kp, int64_t N, float* C, int64_t ldc, int64_t M, int64_t K) {
+// SV2N_GEMM3_PIPE=0: the compiler-scheduled fragment reads (A/B switch)
+static bool gemm3_pipe() {
+  static const bool on = [] {
+    const char* e = getenv("SV2N_GEMM3_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <int NW, int MT, int NT, int BK, int PIPE>
+static int launch_gemm3_p(hipStream_t st, const float* A, int64_t lda, const unsigned short* Bp,
+                          int64_t Kp, int64_t N, float* C, int64_t ldc, int64_t M, int64_t K) {
   using Cfg = Gemm3Cfg<NW, MT, NT, BK>;
   constexpr size_t lds = Cfg::LDS;
   static_assert(lds <= 160 * 1024, "LDS budget");
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)k_gemm3<NW, MT, NT, BK, 1>,
+    (void)hipFuncSetAttribute((const void*)k_gemm3<NW, MT, NT, BK, 1, 3, PIPE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   const dim3 grid((unsigned)((M + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN));
-  hipLaunchKernelGGL((k_gemm3<NW, MT, NT, BK, 1>), grid, dim3(Cfg::THREADS), lds, st, A, lda, Bp,
-                     Kp, N * Kp, C, ldc, M, N, K);
+  hipLaunchKernelGGL((k_gemm3<NW, MT, NT, BK, 1, 3, PIPE>), grid, dim3(Cfg::THREADS), lds, st, A,
+                     lda, Bp, Kp, N * Kp, C, ldc, M, N, K);
   return (int)hipGetLastError();
+}
+
+template <int NW, int MT, int NT, int BK>
+static int launch_gemm3(hipStream_t st, const float* A, int64_t lda, const unsigned short* Bp,
+                        int64_t Kp, int64_t N, float* C, int64_t ldc, int64_t M, int64_t K) {
+  return gemm3_pipe() ? launch_gemm3_p<NW, MT, NT, BK, 1>(st, A, lda, Bp, Kp, N, C, ldc, M, K)
+                      : launch_gemm3_p<NW, MT, NT, BK, 0>(st, A, lda, Bp, Kp, N, C, ldc, M, K);
 }
 
 // bf16 operands (one plane), fp32 accumulation: the bf16 execution mode

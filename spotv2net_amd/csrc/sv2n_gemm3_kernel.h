@@ -115,7 +115,12 @@ __device__ __forceinline__ f32x4 mfma_planes(const bf16x8 (&a)[NP], const bf16x8
 // Workgroup = NW waves stacked along M (wave tile MT x NT 16x16 tiles), K
 // blocks of BK, PF register sets of staged operands in flight (the loads for
 // block kb+PF are issued while block kb is computed from LDS).
-template <int NW, int MT, int NT, int BK, int PF, int NP = 3>
+// PIPE = 1: the B fragments of column tile b+1 are read while tile b's MFMAs
+// run (an explicit register double buffer, with scheduling-group barriers
+// holding the compiler to "NP reads, then the tile's MFMAs"); PIPE = 0 lets
+// the compiler place the reads (it issued each one a single MFMA ahead of its
+// use and waited on lgkmcnt(0) between the MFMAs of one tile).
+template <int NW, int MT, int NT, int BK, int PF, int NP = 3, int PIPE = 0>
 __global__ __launch_bounds__(64 * NW) void k_gemm3(const float* __restrict__ A, int64_t lda,
                                                    const unsigned short* __restrict__ Bp,
                                                    int64_t ldb, int64_t bplane,
@@ -198,7 +203,41 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3(const float* __restrict__ A, 
       }
     }
   };
+  auto compute_pipe = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[MT][NP];
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          af[a][p] = *reinterpret_cast<const bf16x8*>(
+              sA + (p * BM + wave * 16 * MT + 16 * a + li) * ROW + kk + 8 * lg);
+      bf16x8 bq[2][NP];
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        bq[0][p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + li) * ROW + kk + 8 * lg);
+      __builtin_amdgcn_sched_group_barrier(0x100, NP * (MT + 1), 0);  // DS reads: A, B tile 0
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        if (b + 1 < NT) {
+#pragma unroll
+          for (int p = 0; p < NP; ++p)
+            bq[(b + 1) & 1][p] = *reinterpret_cast<const bf16x8*>(
+                sB + (p * BN + 16 * (b + 1) + li) * ROW + kk + 8 * lg);
+          __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);  // DS reads: B tile b+1
+        }
+#pragma unroll
+        for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<NP>(af[a], bq[b & 1], acc[a][b]);
+        __builtin_amdgcn_sched_group_barrier(0x008, (NP == 3 ? 6 : 1) * MT, 0);  // MFMAs of tile b
+      }
+    }
+  };
   auto compute = [&]() {
+    if constexpr (PIPE) {
+      compute_pipe();
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 af[MT][NP];
