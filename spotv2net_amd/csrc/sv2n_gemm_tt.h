@@ -315,15 +315,25 @@ __global__ __launch_bounds__(512) void k_gemm_tt3w(const float* __restrict__ A, 
       for (int pl = 0; pl < 3; ++pl)
         af[a][pl] = tr_frag(sa + pl * PA + kA0 + ca, sa + pl * PA + kA1 + ca);
     }
+    // B fragments of column tile b+1 read while tile b's MFMAs run (as in
+    // k_gemm3<..., PIPE = 1>)
+    bf16x8 bq[2][3];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      bq[0][pl] = tr_frag(sb + pl * PB + kB0 + p4, sb + pl * PB + kB1 + p4);
+    __builtin_amdgcn_sched_group_barrier(0x100, 6 * (MT + 1), 0);
 #pragma unroll
     for (int b = 0; b < NT; ++b) {
-      const int cb = 16 * b + p4;
-      bf16x8 bf[3];
+      if (b + 1 < NT) {
+        const int cb = 16 * (b + 1) + p4;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        bf[pl] = tr_frag(sb + pl * PB + kB0 + cb, sb + pl * PB + kB1 + cb);
+        for (int pl = 0; pl < 3; ++pl)
+          bq[(b + 1) & 1][pl] = tr_frag(sb + pl * PB + kB0 + cb, sb + pl * PB + kB1 + cb);
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+      }
 #pragma unroll
-      for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<3>(af[a], bf, acc[a][b]);
+      for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<3>(af[a], bq[b & 1], acc[a][b]);
+      __builtin_amdgcn_sched_group_barrier(0x008, 6 * MT, 0);
     }
   };
 
