@@ -269,31 +269,37 @@ static int wgrad3_mt() {
 // 208-column tiling the split count follows the bf16x3 kernel's rule — one
 // round of 144 KiB / 98 KiB workgroups balanced over the 8 XCDs (a multiple
 // of 8 slices, tiles x slices <= 256; MI355X, C2 L0 dWᵀ 1260 x 408 x 15360:
-// 24 slices 92 us, 16: 126 us, 32: 130 us), at most 64 slices of >= 256 rows
+// 24 slices 92 us, 16: 126 us, 32: 130 us), at most 256 slices of >= 256 rows
 // (sv2n_gat_wgrad_node_workspace covers both plans); unaligned operands run
 // the f32 kernel on the same slices.
 struct SlabPlan {
-  int kind, nt, splitk;
+  int kind, nt, splitk;  // kind: 0 f32 kernel; 1 / 2: tt3w<13, MT>; 3 / 4: tt3w<9, MT>
   int64_t kslice;
 };
 static SlabPlan slab_plan(int64_t F, int64_t N, int64_t K, bool vec, int64_t lda, int64_t ldb) {
   const GemmPlan p = plan_gemm(F, N, K);
   SlabPlan sp{0, p.nt, p.splitk, p.kslice};
-  // 208-column tiles: N = 408 (C2 L0, two tiles) and N = 208 (C2 L1, one)
-  const bool cols208 = (N + 207) / 208 * 208 * 4 <= 5 * N;
-  if (!(cols208 && wgrad3_on() && p.splitk > 1)) return sp;
-  sp.nt = 13;
+  if (!(wgrad3_on() && p.splitk > 1)) return sp;
+  // column tiles of 208 (C2: N = 408, 208) or 144 (C5: N = 144), at most 25 % padding
+  int bn = 0;
+  for (const int w : {208, 144})
+    if ((N + w - 1) / w * w * 4 <= 5 * N) {
+      bn = w;
+      break;
+    }
+  if (bn == 0) return sp;
+  const int64_t ntile = (N + bn - 1) / bn;
   int mt = wgrad3_mt();
-  if (mt != 1 && mt != 2) mt = ((F + 255) / 256) * ((N + 207) / 208) >= 8 ? 2 : 1;
-  const int64_t tiles = ((F + 128 * mt - 1) / (128 * mt)) * ((N + 207) / 208);
+  if (mt != 1 && mt != 2) mt = ((F + 255) / 256) * ntile >= 8 ? 2 : 1;
+  const int64_t tiles = ((F + 128 * mt - 1) / (128 * mt)) * ntile;
   int64_t sk = 8 * std::max<int64_t>(1, 256 / (8 * tiles));
-  sk = std::min<int64_t>(sk, std::min<int64_t>(64, std::max<int64_t>(8, K / 256 / 8 * 8)));
+  sk = std::min<int64_t>(sk, std::min<int64_t>(256, std::max<int64_t>(8, K / 256 / 8 * 8)));
   int64_t ks = (K + sk - 1) / sk;
   ks = (ks + 31) / 32 * 32;
   sp.splitk = (int)((K + ks - 1) / ks);
   sp.kslice = ks;
   const bool ok = vec && (F % 4) == 0 && K * std::max(lda, ldb) * 4 <= 0x7fffffff;
-  sp.kind = ok ? mt : 0;
+  sp.kind = ok ? (bn == 208 ? 0 : 2) + mt : 0;
   return sp;
 }
 
@@ -321,6 +327,10 @@ static void launch_wgrad_slabs(const SlabPlan& p, hipStream_t stream, const floa
     launch_tt3w<13, 2>(p, stream, x, ld_x, dxs, ldx, F, N, K, out);
   } else if (p.kind == 1) {
     launch_tt3w<13, 1>(p, stream, x, ld_x, dxs, ldx, F, N, K, out);
+  } else if (p.kind == 4) {
+    launch_tt3w<9, 2>(p, stream, x, ld_x, dxs, ldx, F, N, K, out);
+  } else if (p.kind == 3) {
+    launch_tt3w<9, 1>(p, stream, x, ld_x, dxs, ldx, F, N, K, out);
   } else if (p.nt == 13) {
     launch_gemm_slabs<8, 1, 13, 16, false, false, 2, 0, true>(p.splitk, p.kslice, stream, x, ld_x,
                                                               dxs, ldx, F, N, K, avec, bvec, out);
