@@ -133,6 +133,11 @@ extern "C" int sv2n_gemm_f32x3(const float* A, int64_t lda, const uint16_t* Bp, 
   const int64_t mb = (M + 127) / 128;
   const bool wide = mb * ((N + 207) / 208) >= 240;  // else narrower tiles for more workgroups
   const bool longk = K > 256;
+  // 144-column tiles when they pad N less than 208-column ones (C5: N = 144)
+  const bool t144 = (N + 143) / 144 * 144 < (N + 207) / 208 * 208 && mb * ((N + 143) / 144) >= 240;
+  if (t144)
+    return longk ? launch_gemm3<8, 1, 9, 64>(stream, A, lda, B, Kp, N, C, ldc, M, K)
+                 : launch_gemm3<8, 1, 9, 32>(stream, A, lda, B, Kp, N, C, ldc, M, K);
   if (wide)
     return longk ? launch_gemm3<8, 1, 13, 64>(stream, A, lda, B, Kp, N, C, ldc, M, K)
                  : launch_gemm3<8, 1, 13, 32>(stream, A, lda, B, Kp, N, C, ldc, M, K);
