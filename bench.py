@@ -282,7 +282,8 @@ def kernel_table_tiled(model, data, cfg, reps=10):
         "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * Nc * K0, 4.0 * (M0 * K0 + Nc * K0 + M0 * Nc),
                         BF16X3_PEAK_TFLOPS),
         "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * Nd * K0, 4.0 * (M0 * K0 + M0 * Nd + Nd * K0),
-                        F32_MFMA_PEAK_TFLOPS),
+                        F32_MFMA_PEAK_TFLOPS if os.environ.get("SV2N_WGRAD3", "1") == "0"
+                        else BF16X3_PEAK_TFLOPS),
     }
     res = {}
     for name, (fn, bound, flops, nbytes, peak) in rows.items():
