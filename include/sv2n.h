@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 5
+#define SV2N_ABI_VERSION 6
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -329,6 +329,18 @@ int sv2n_head_mse_bwd(const float* x, int64_t num_rows, int in_features, const f
                       int out_features, const float* diff, const float* grad_loss, float* dx,
                       float* g_weight, float* g_bias, float* workspace,
                       int64_t workspace_floats, hipStream_t stream);
+
+/* Head + MSE forward and backward in ONE launch for a training step whose
+ * upstream loss gradient is 1 (loss.backward()): loss[0] = mean(diff²), dx =
+ * 2/(rows·out)·diff·weight, and g_weight / g_bias ACCUMULATE Σ 2/(rows·out)·
+ * diff ⊗ [x, 1] (either may be NULL).  Equals sv2n_head_mse_fwd followed by
+ * sv2n_head_mse_bwd with grad_loss = 1.  workspace:
+ * sv2n_head_mse_train_workspace(...) floats, same counter rule. */
+int64_t sv2n_head_mse_train_workspace(int64_t num_rows, int in_features, int out_features);
+int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_features, const float* weight,
+                        const float* bias, int out_features, const float* target, float* loss,
+                        float* dx, float* g_weight, float* g_bias, float* workspace,
+                        int64_t workspace_floats, hipStream_t stream);
 
 /* Fused attention for dense-block graphs of 32 < n <= 256 nodes (any n <= 256
  * works; n <= 32 is faster on sv2n_gat_attn_fwd/bwd).  Same semantics and

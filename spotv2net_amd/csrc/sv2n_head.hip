@@ -320,6 +320,137 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ x, i
   }
 }
 
+// Head + MSE forward AND backward in one launch, for a training step whose
+// upstream loss gradient is 1 (train.TrainStep: loss.backward()): per block
+// the rows' outputs, diff = out - target, the squared-error partial, dout =
+// diff · 2/(rows·out), dx rows and the [OUT][C+1] weight/bias partial; the
+// last-arriving block sums the loss partials and the weight / bias partials
+// in a fixed order.  Replaces k_head_mse_fwd + k_head_bwd (x read once, one
+// launch, one ticket).
+template <int OUT>
+__global__ __launch_bounds__(256) void k_head_mse_train(
+    const float* __restrict__ x, int64_t N, int C, const float* __restrict__ W,
+    const float* __restrict__ b, const float* __restrict__ target, float* __restrict__ dx,
+    float* __restrict__ ws, float* __restrict__ gW, float* __restrict__ gb,
+    float* __restrict__ loss, float inv_count, float scale, int R) {
+  extern __shared__ __attribute__((aligned(16))) float sx[];  // [R][C+1] | sw [OUT][C]
+  __shared__ float s_part[256 * OUT];
+  __shared__ float sd[HEAD_ROWS][HEAD_MAX_OUT];
+  __shared__ float s_grp[256];
+  float* sw = sx + R * (C + 1);
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int nr = (int)min((int64_t)R, N - r0);
+  const int CP = C + 1;
+  const int tot = OUT * CP;
+  head_rows<OUT>(x, r0, nr, C, sx, W, sw, t);
+  for (int k = t; k < R * OUT; k += 256) sd[k / OUT][k - (k / OUT) * OUT] = 0.f;
+  __syncthreads();
+  float sq = 0.f;
+  float acc[OUT];
+  if (head_dot<OUT>(sx, sw, C, R, nr, t, acc, s_part)) {
+    const int r = t % R;
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) {
+      const int64_t k = (r0 + r) * OUT + o;
+      const float d = acc[o] + (b ? b[o] : 0.f) - target[k];
+      sq = fmaf(d, d, sq);
+      sd[r][o] = d * scale;
+    }
+  }
+  // block loss partial: wave sums, then the 4 waves in order
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) sq += __shfl_xor(sq, m, 64);
+  if ((t & 63) == 0) s_grp[t >> 6] = sq;
+  __syncthreads();
+  float* part = ws + HEAD_WS_HDR;
+  float* pb = part + (int64_t)blockIdx.x * (tot + 1);
+  if (t == 0) st_sc1(pb + tot, (s_grp[0] + s_grp[1]) + (s_grp[2] + s_grp[3]));
+  __syncthreads();
+  // weight / bias partial: column oc = t % tot over rows r = g (mod RG)
+  const int RG = tot <= 256 ? 256 / tot : 1;
+  if (RG > 1) {
+    if (t < RG * tot) {
+      const int oc = t % tot, g = t / tot;
+      const int o = oc / CP, c = oc - o * CP;
+      float s = 0.f;
+      if (c < C) {
+        for (int r = g; r < nr; r += RG) s = fmaf(sd[r][o], sx[r * CP + c], s);
+      } else {
+        for (int r = g; r < nr; r += RG) s += sd[r][o];
+      }
+      s_grp[t] = s;
+    }
+    __syncthreads();
+    if (t < tot) {
+      float s = 0.f;
+      for (int g = 0; g < RG; ++g) s += s_grp[g * tot + t];
+      st_sc1(pb + t, s);
+    }
+  } else {
+    for (int oc = t; oc < tot; oc += 256) {
+      const int o = oc / CP, c = oc - o * CP;
+      float s = 0.f;
+      if (c < C) {
+        for (int r = 0; r < nr; ++r) s = fmaf(sd[r][o], sx[r * CP + c], s);
+      } else {
+        for (int r = 0; r < nr; ++r) s += sd[r][o];
+      }
+      st_sc1(pb + oc, s);
+    }
+  }
+  // dx rows
+  for (int k = t; k < nr * C; k += 256) {
+    const int r = k / C, c = k - r * C;
+    float s = 0.f;
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) s = fmaf(sd[r][o], sw[o * C + c], s);
+    dx[r0 * C + k] = s;
+  }
+  int* s_flag = reinterpret_cast<int*>(s_part);
+  __syncthreads();  // s_part free: one word as the flag
+  if (last_block_sc1_2(reinterpret_cast<unsigned*>(ws), gridDim.x, s_flag)) {
+    const int nparts = gridDim.x;
+    const int stride = tot + 1;
+    for (int base = 0; base < stride; base += 256) {
+      const int cols = min(256, stride - base);
+      const int PG = 256 / cols;  // part groups
+      if (t < PG * cols) {
+        const int oc = base + t % cols, g = t / cols;
+        float s = 0.f;
+        for (int b0 = g; b0 < nparts; b0 += 16 * PG) {
+          float v[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const int bb = b0 + u * PG;
+            v[u] = bb < nparts ? ld_sc1(part + (int64_t)bb * stride + oc) : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < 16; ++u) s += v[u];
+        }
+        s_grp[t] = s;
+      }
+      __syncthreads();
+      if (t < cols) {
+        float s = 0.f;
+        for (int g = 0; g < PG; ++g) s += s_grp[g * cols + t];
+        const int oc = base + t;
+        if (oc == tot) {
+          loss[0] = s * inv_count;
+        } else {
+          const int o = oc / CP, c = oc - o * CP;
+          if (c < C) {
+            if (gW) gW[o * C + c] += s;
+          } else if (gb) {
+            gb[o] += s;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 }  // namespace sv2n
 
 using namespace sv2n;
@@ -435,4 +566,32 @@ extern "C" int sv2n_head_mse_bwd(const float* x, int64_t num_rows, int in_featur
   const float scale = 2.f / (float)(num_rows * (int64_t)out_features);
   return head_bwd_launch(x, num_rows, in_features, weight, out_features, diff, scale, grad_loss,
                          dx, g_weight, g_bias, workspace, workspace_floats, stream);
+}
+
+extern "C" int64_t sv2n_head_mse_train_workspace(int64_t num_rows, int in_features,
+                                                 int out_features) {
+  return HEAD_WS_HDR + head_bwd_blocks(num_rows, in_features, out_features) *
+                           ((int64_t)out_features * (in_features + 1) + 1);
+}
+
+extern "C" int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_features,
+                                   const float* weight, const float* bias, int out_features,
+                                   const float* target, float* loss, float* dx, float* g_weight,
+                                   float* g_bias, float* workspace, int64_t workspace_floats,
+                                   hipStream_t stream) {
+  const int out_ch = out_features;
+  if (!x || !weight || !target || !loss || !dx || !workspace) return SV2N_ERR_ARG;
+  if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
+  if (workspace_floats < sv2n_head_mse_train_workspace(num_rows, in_features, out_ch))
+    return SV2N_ERR_WORKSPACE;
+  if ((uintptr_t)workspace & 15) return SV2N_ERR_ALIGN;
+  const int R = head_rows_per_block(in_features, out_ch, num_rows);
+  const unsigned grid = (unsigned)((num_rows + R - 1) / R);
+  const size_t lds = head_lds_bytes(in_features, out_ch, num_rows);
+  const float inv_count = 1.f / (float)(num_rows * out_ch);
+  const float scale = 2.f / (float)(num_rows * (int64_t)out_ch);
+  SV2N_HEAD_DISPATCH(k_head_mse_train, dim3(grid), dim3(256), lds, stream, x, num_rows,
+                     in_features, weight, bias, target, dx, workspace, g_weight, g_bias, loss,
+                     inv_count, scale, R)
+  return (int)hipGetLastError();
 }

@@ -69,6 +69,8 @@ _SCHEMAS = {
     "head_bwd": "(Tensor x, Tensor weight, Tensor dout, Tensor(a!)? g_weight, "
                 "Tensor(b!)? g_bias) -> Tensor",
     "head_mse_fwd": "(Tensor x, Tensor weight, Tensor? bias, Tensor target) -> (Tensor, Tensor)",
+    "head_mse_train": "(Tensor x, Tensor weight, Tensor? bias, Tensor target, "
+                      "Tensor(a!)? g_weight, Tensor(b!)? g_bias) -> (Tensor, Tensor)",
     "head_mse_bwd": "(Tensor x, Tensor weight, Tensor diff, Tensor grad_loss, "
                     "Tensor(a!)? g_weight, Tensor(b!)? g_bias) -> Tensor",
     "adam_step": "(Tensor(a!) param, Tensor(b!) grad, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "
@@ -656,6 +658,33 @@ def _head_mse_bwd(x, weight, diff, grad_loss, g_weight, g_bias):
 @_fake("head_mse_bwd")
 def _head_mse_bwd_fake(x, weight, diff, grad_loss, g_weight, g_bias):
     return torch.empty_like(x)
+
+
+@_impl("head_mse_train")
+def _head_mse_train(x, weight, bias, target, g_weight, g_bias):
+    """Head + MSE forward and backward in one launch (upstream loss gradient
+    1): returns (loss, dx) and accumulates the head's parameter gradients."""
+    lib = _lib.load()
+    _f32(x, weight, bias, target)
+    _dense(x, weight, bias, g_weight, g_bias)
+    N, C = x.shape
+    O = weight.shape[0]
+    target = target.reshape(-1).contiguous()
+    _need(target.numel() == N * O, f"target has {target.numel()} elements, expected {N * O}")
+    loss = torch.empty((), device=x.device)
+    dx = torch.empty_like(x)
+    ws_n = lib.sv2n_head_mse_train_workspace(N, C, O)
+    ws = _lib.persistent_zeros("head", ws_n, x.device)
+    _lib.check(lib.sv2n_head_mse_train(x.data_ptr(), N, C, weight.data_ptr(), _p(bias), O,
+                                       target.data_ptr(), loss.data_ptr(), dx.data_ptr(),
+                                       _p(g_weight), _p(g_bias), ws.data_ptr(), ws_n, _st(x)),
+               "sv2n_head_mse_train")
+    return loss, dx
+
+
+@_fake("head_mse_train")
+def _head_mse_train_fake(x, weight, bias, target, g_weight, g_bias):
+    return x.new_empty(()), torch.empty_like(x)
 
 
 # --------------------------------------------------------------------------

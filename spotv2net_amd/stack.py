@@ -462,6 +462,24 @@ def head_mse_loss(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tensor
     return _HeadMSE.apply(x, target, linear, linear.weight, linear.bias)
 
 
+def head_mse_train(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tensor):
+    """Training step's head + loss with the upstream loss gradient 1 (what
+    ``loss.backward()`` gives): ONE launch returns ``(loss, dx)`` and
+    accumulates ``linear``'s parameter gradients into their ``.grad`` — the
+    caller continues the backward with ``torch.autograd.backward(x, dx)``.
+    Outside autograd; ``train.TrainStep`` uses it (``None`` when the head does
+    not fit the kernels)."""
+    _require_params((linear.weight, linear.bias))
+    _require_device(x, target)
+    if not head_fits(linear.in_features, linear.out_features):
+        return None
+    gw = _grad_buf(linear.weight)
+    gb = _grad_buf(linear.bias) if linear.bias is not None else None
+    return torch.ops.sv2n.head_mse_train(_aligned(x.detach()), linear.weight.detach(),
+                                         None if linear.bias is None else linear.bias.detach(),
+                                         target, gw, gb)
+
+
 def linear_head(x: torch.Tensor, linear: torch.nn.Linear) -> torch.Tensor:
     """``linear(x)`` for GATModel's output layer on the sv2n head kernels
     (in_features <= 1024, out_features <= 16; otherwise the nn.Linear itself)."""

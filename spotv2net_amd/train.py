@@ -142,8 +142,9 @@ class TrainStep:
         self.use_graph = use_graph
         self.loss = torch.zeros((), device=self.flat.device)
         self._one = torch.ones((), device=self.flat.device)
-        # fused head + MSE (two launches) when the model offers it
-        self._fused_mse = loss_fn is torch.nn.functional.mse_loss and hasattr(model, "mse_loss")
+        # fused head + MSE (one launch, forward and backward) when the model offers it
+        self._fused_mse = loss_fn is torch.nn.functional.mse_loss and hasattr(model, "mse_loss") \
+            and hasattr(model, "_hidden") and hasattr(model, "linear")
         self._shapes = []
         self.add_shape(data, prepare)
 
@@ -162,7 +163,7 @@ class TrainStep:
 
     # -- eager pieces -------------------------------------------------------
     def _fwd_bwd(self, sh: _Shape) -> None:
-        from .stack import direct_grad_accumulation
+        from .stack import direct_grad_accumulation, head_mse_train
         if sh.prepare is not None:
             sh.prepare()
         if not getattr(self.opt, "zeroes_grads", False):
@@ -171,6 +172,15 @@ class TrainStep:
         # it directly (no per-parameter AccumulateGrad launches)
         with direct_grad_accumulation():
             if self._fused_mse:
+                # head + loss forward AND backward in one launch (the upstream
+                # gradient of the loss is 1), then the GAT stack's backward
+                h = self.model._hidden(sh.data)
+                res = head_mse_train(h, self.model.linear, sh.data.y_x)
+                if res is not None:
+                    loss, dh = res
+                    torch.autograd.backward(h, dh)
+                    sh.loss = loss.detach()
+                    return
                 loss = self.model.mse_loss(sh.data)
             else:
                 loss = self.loss_fn(self.model(sh.data), sh.data.y_x)

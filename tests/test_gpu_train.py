@@ -104,6 +104,56 @@ def test_fused_head_mse_matches_unfused(dev, out_ch):
         assert_close(p.grad, q.grad, tol=1e-6, what=n)
 
 
+@pytest.mark.parametrize("out_ch,rows", [(1, 15360), (3, 180), (14, 1000)])
+def test_head_mse_train_matches_fwd_bwd(dev, out_ch, rows):
+    """sv2n_head_mse_train (one launch: loss, dx, accumulated head grads) ==
+    sv2n_head_mse_fwd + sv2n_head_mse_bwd with grad_loss = 1: dx bit for bit
+    (same products and order), the parameter gradients and the loss within
+    float rounding (the last-block combine groups the per-block partials
+    differently: both orders fixed); the C2 head shape (15,360 x 50) included."""
+    ops = torch.ops.sv2n
+    torch.manual_seed(3)
+    C = 50
+    x = torch.randn(rows, C, device=dev)
+    W = torch.randn(out_ch, C, device=dev) * 0.1
+    b = torch.randn(out_ch, device=dev)
+    y = torch.randn(rows * out_ch, device=dev)
+    gw1, gb1 = torch.full_like(W, 0.5), torch.full_like(b, 0.25)
+    gw2, gb2 = gw1.clone(), gb1.clone()
+    loss1, dx1 = ops.head_mse_train(x, W, b, y, gw1, gb1)
+    loss2, diff = ops.head_mse_fwd(x, W, b, y)
+    dx2 = ops.head_mse_bwd(x, W, diff, torch.ones((), device=dev), gw2, gb2)
+    assert_close(loss1, loss2, tol=1e-6, what="loss")
+    assert torch.equal(dx1, dx2)
+    assert_close(gw1, gw2, tol=1e-6, what="g_weight")
+    assert_close(gb1, gb2, tol=1e-6, what="g_bias")
+    gw3, gb3 = torch.full_like(W, 0.5), torch.full_like(b, 0.25)
+    ops.head_mse_train(x, W, b, y, gw3, gb3)
+    assert torch.equal(gw1, gw3) and torch.equal(gb1, gb3)  # deterministic
+
+
+def test_trainstep_fused_head_matches_reference_steps(dev):
+    """TrainStep's captured step (fused head+loss launch, then the GAT stack's
+    backward) == k eager steps of nn.MSELoss + backward + torch.optim.Adam
+    (reference 5_train_SpotV2Net.py:150-159) from the same init."""
+    from spotv2net_amd import synthetic_batch
+    from spotv2net_amd.train import TrainStep
+    m1 = _model(dev, seed=11)
+    m2 = copy.deepcopy(m1)
+    data = synthetic_batch(8, 4, seed=2, device=dev)
+    step = TrainStep(m1, data, lr=1e-3, use_graph=True)
+    opt = torch.optim.Adam(m2.parameters(), lr=1e-3)
+    for _ in range(3):
+        step()
+        opt.zero_grad()
+        l2 = torch.nn.functional.mse_loss(m2(data), data.y_x)
+        l2.backward()
+        opt.step()
+        assert_close(step.loss, l2.detach(), tol=1e-5, what="loss")
+    for (n, p), (_, q) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert_close(p.detach(), q.detach(), tol=1e-5, what=n)
+
+
 def test_flat_adam_advances_step_and_zeroes_grads(dev):
     from spotv2net_amd import synthetic_batch
     from spotv2net_amd.train import TrainStep
