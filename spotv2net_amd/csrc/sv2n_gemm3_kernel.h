@@ -23,6 +23,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "sv2n_common.h"
 
 namespace sv2n {
@@ -586,6 +587,151 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3b(const float* __restrict__ A,
       if (s + 2 < nk) load_b((int64_t)(s + 2) * BK);
     }
     __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int64_t gn = n0 + 16 * b + li;
+      if (gn < N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t gm = arow0 + 16 * a + 4 * lg + r;
+          if (gm < M) C[gm * ldc + gn] = acc[a][b][r];
+        }
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_gemm3c: k_gemm3b's operand flow (A straight to registers, split there; B
+// planes double-buffered in LDS, one barrier per K-step) with the step
+// reordered so no phase of the workgroup runs without MFMAs:
+//   top of step s   store the B planes of step s+1 (loaded during step s-1)
+//                   into the other stage, issue the loads of step s+2's B;
+//   body            the MFMAs of step s, B fragments of column tile b+1 read
+//                   while tile b's MFMAs run (scheduling-group barriers);
+//   end             A loads of step s+AP, barrier.
+// The stage written at the top of step s was last read in step s-1, which
+// every wave finished before the barrier that closed it.
+// ---------------------------------------------------------------------------
+template <int NW, int MT, int NT, int BK, int AP>
+__global__ __launch_bounds__(64 * NW) void k_gemm3c(const float* __restrict__ A, int64_t lda,
+                                                    const unsigned short* __restrict__ Bp,
+                                                    int64_t ldb, int64_t bplane,
+                                                    float* __restrict__ C, int64_t ldc, int64_t M,
+                                                    int64_t N, int64_t K, int nm, int nn) {
+  using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
+  constexpr int TH = Cfg::THREADS, BN = Cfg::BN, ROW = Cfg::ROW, BV = Cfg::BV;
+  constexpr int STAGE = Cfg::STAGE, BC = BK / 8, KS = BK / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int id = blockIdx.x;
+  const int q = id / (8 * nn), rem = id - q * 8 * nn;
+  const int nb = rem >> 3, mb = q * 8 + (rem & 7);
+  if (mb >= nm) return;
+  const int64_t m0 = (int64_t)mb * Cfg::BM, n0 = (int64_t)nb * BN;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t arow0 = m0 + (int64_t)wave * 16 * MT;
+  const int64_t arows = M - arow0;
+  const rsrc_t ra_src = make_rsrc(A + (arow0 > M ? 0 : arow0 * lda),
+                                  arows > 0 ? (uint32_t)(min(arows, (int64_t)16 * MT) * lda * 4) : 0u);
+  f32x4 ra[AP][MT][KS][2];
+  auto load_a = [&](int set, int64_t k0) {
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int hv = 0; hv < 2; ++hv) {
+          const int64_t k = k0 + 32 * ks + 8 * lg + 4 * hv;
+          const int off = k < K ? (int)(((16 * a + li) * lda + k) * 4) : OOB;
+          ra[set][a][ks][hv] = bld4(ra_src, off);
+        }
+  };
+  uint4 rb[BV];
+  auto load_b = [&](int64_t k0) {
+#pragma unroll
+    for (int sv = 0; sv < BV; ++sv) {
+      const int idx = t + TH * sv;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (idx < 3 * BN * BC) {
+        const int p = idx / (BN * BC), r2 = idx - p * BN * BC;
+        const int r = r2 / BC, c = r2 - r * BC;
+        const int64_t gn = min(n0 + r, N - 1);
+        v = *reinterpret_cast<const uint4*>(Bp + p * bplane + gn * ldb + k0 + 8 * c);
+      }
+      rb[sv] = v;
+    }
+  };
+  auto store_b = [&](unsigned short* sB) {
+#pragma unroll
+    for (int sv = 0; sv < BV; ++sv) {
+      const int idx = t + TH * sv;
+      if (idx < 3 * BN * BC) {
+        const int p = idx / (BN * BC), r2 = idx - p * BN * BC;
+        const int r = r2 / BC, c = r2 - r * BC;
+        *reinterpret_cast<uint4*>(sB + (p * BN + r) * ROW + 8 * c) = rb[sv];
+      }
+    }
+  };
+
+  const int nk = (int)((K + BK - 1) / BK);
+#pragma unroll
+  for (int s = 0; s < AP; ++s)
+    if (s < nk) load_a(s, (int64_t)s * BK);
+  load_b(0);
+  store_b(lds);
+  if (nk > 1) load_b(BK);
+  __syncthreads();
+  // one step; `set` (the A register set) is a compile-time index
+  auto step = [&](int s, auto set_c) {
+    constexpr int set = decltype(set_c)::value;
+    const unsigned short* sB = lds + (s & 1) * STAGE;
+    if (s + 1 < nk) {
+      store_b(lds + ((s + 1) & 1) * STAGE);
+      if (s + 2 < nk) load_b((int64_t)(s + 2) * BK);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 af[MT][3];
+#pragma unroll
+      for (int a = 0; a < MT; ++a) split3_frag(ra[set][a][ks][0], ra[set][a][ks][1], af[a]);
+      bf16x8 bq[2][3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        bq[0][p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + li) * ROW + 32 * ks + 8 * lg);
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        if (b + 1 < NT) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            bq[(b + 1) & 1][p] = *reinterpret_cast<const bf16x8*>(
+                sB + (p * BN + 16 * (b + 1) + li) * ROW + 32 * ks + 8 * lg);
+          __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        }
+#pragma unroll
+        for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<3>(af[a], bq[b & 1], acc[a][b]);
+        __builtin_amdgcn_sched_group_barrier(0x008, 6 * MT, 0);
+      }
+    }
+    if (s + AP < nk) load_a(set, (int64_t)(s + AP) * BK);
+    __syncthreads();
+  };
+  static_assert(AP == 2 || AP == 3, "A register sets");
+  for (int s = 0; s < nk; s += AP) {
+    step(s, std::integral_constant<int, 0>{});
+    if (s + 1 < nk) step(s + 1, std::integral_constant<int, 1>{});
+    if constexpr (AP == 3)
+      if (s + 2 < nk) step(s + 2, std::integral_constant<int, 2>{});
   }
 #pragma unroll
   for (int a = 0; a < MT; ++a)

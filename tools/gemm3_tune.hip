@@ -49,17 +49,17 @@ __global__ void k_fill(float* p, int64_t n, uint32_t seed, float scale) {
 
 struct Shape { const char* name; int64_t M, N, K; };
 
-template <int NW, int MT, int NT, int BK, int PF>
+template <int NW, int MT, int NT, int BK, int PF, int PIPE = 1>
 void run3(const Shape& sh, hipStream_t st, const float* A, const unsigned short* Bp, int64_t Kp,
           float* C, const std::vector<double>& ref, const std::vector<double>& absr) {
   using Cfg = Gemm3Cfg<NW, MT, NT, BK>;
   const size_t lds = Cfg::LDS;
   if (lds > 160 * 1024) return;
   if (lds > 65536)
-    CK(hipFuncSetAttribute((const void*)k_gemm3<NW, MT, NT, BK, PF>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CK(hipFuncSetAttribute((const void*)k_gemm3<NW, MT, NT, BK, PF, 3, PIPE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   dim3 grid((unsigned)((sh.M + Cfg::BM - 1) / Cfg::BM), (unsigned)((sh.N + Cfg::BN - 1) / Cfg::BN));
   auto f = [&]() {
-    hipLaunchKernelGGL((k_gemm3<NW, MT, NT, BK, PF>), grid, dim3(Cfg::THREADS), lds, st, A, sh.K, Bp, Kp,
+    hipLaunchKernelGGL((k_gemm3<NW, MT, NT, BK, PF, 3, PIPE>), grid, dim3(Cfg::THREADS), lds, st, A, sh.K, Bp, Kp,
                        sh.N * Kp, C, sh.N, sh.M, sh.N, sh.K);
   };
   f();
@@ -84,18 +84,18 @@ void run3(const Shape& sh, hipStream_t st, const float* A, const unsigned short*
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
   const double us = ms * 1e3 / reps;
-  printf("  gemm3 NW%d MT%d NT%-2d BK%d PF%d %8.1f us %7.1f TF(f32-eq)  max|err| %.2e  max err/S|ab| %.2e\n",
-         NW, MT, NT, BK, PF, us, 2.0 * sh.M * sh.N * sh.K / us / 1e6, maxabs, maxrel);
+  printf("  gemm3 NW%d MT%d NT%-2d BK%d PF%d P%d %8.1f us %7.1f TF(f32-eq)  max|err| %.2e  max err/S|ab| %.2e\n",
+         NW, MT, NT, BK, PF, PIPE, us, 2.0 * sh.M * sh.N * sh.K / us / 1e6, maxabs, maxrel);
   fflush(stdout);
 }
 
-template <int NW, int MT, int NT, int BK, int AP>
+template <int NW, int MT, int NT, int BK, int AP, bool CV = false>
 void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short* Bp, int64_t Kp,
            float* C, const std::vector<double>& ref, const std::vector<double>& absr) {
   using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
   const size_t lds = Cfg::LDS;
   if (lds > 160 * 1024) return;
-  auto kern = k_gemm3b<NW, MT, NT, BK, AP>;
+  auto kern = CV ? k_gemm3c<NW, MT, NT, BK, AP> : k_gemm3b<NW, MT, NT, BK, AP>;
   if (lds > 65536)
     CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   const int nm = (int)((sh.M + Cfg::BM - 1) / Cfg::BM), nn = (int)((sh.N + Cfg::BN - 1) / Cfg::BN);
@@ -127,8 +127,8 @@ void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
   const double us = ms * 1e3 / reps;
-  printf("  gemm3b NW%d MT%d NT%-2d BK%d AP%d %8.1f us %7.1f TF(f32-eq)  max|err| %.2e  max err/S|ab| %.2e\n",
-         NW, MT, NT, BK, AP, us, 2.0 * sh.M * sh.N * sh.K / us / 1e6, maxabs, maxrel);
+  printf("  gemm3%s NW%d MT%d NT%-2d BK%d AP%d %8.1f us %7.1f TF(f32-eq)  max|err| %.2e  max err/S|ab| %.2e\n",
+         CV ? "c" : "b", NW, MT, NT, BK, AP, us, 2.0 * sh.M * sh.N * sh.K / us / 1e6, maxabs, maxrel);
   fflush(stdout);
 }
 
@@ -190,11 +190,14 @@ int main() {
     run3<8, 1, 13, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
     run3<8, 1, 7, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<8, 1, 13, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 13, 32, 3>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<4, 2, 13, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<8, 1, 7, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 2, 7, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<4, 1, 13, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 13, 32, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 13, 32, 3, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 7, 32, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 7, 64, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 2, 7, 32, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<4, 2, 13, 32, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 9, 32, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(S)); CK(hipFree(Bp));
   }
   return 0;
