@@ -70,35 +70,37 @@ static int launch_gemm3(hipStream_t st, const float* A, int64_t lda, const unsig
                       : launch_gemm3_p<NW, MT, NT, BK, 0>(st, A, lda, Bp, Kp, N, C, ldc, M, K);
 }
 
-// SV2N_GEMM3C=0: the LDS-staged kernel for every shape (A/B switch)
-static bool gemm3c_on() {
+// SV2N_GEMM3D=0: the LDS-staged kernel for every shape (A/B switch)
+static bool gemm3d_on() {
   static const bool on = [] {
-    const char* e = getenv("SV2N_GEMM3C");
+    const char* e = getenv("SV2N_GEMM3D");
     return !(e && e[0] == '0');
   }();
   return on;
 }
 
-// k_gemm3c: A straight to registers, B planes double-buffered, XCD-grouped
-// block order (MI355X, tools/gemm3_tune.hip: C2 L0 fwd 15360 x 408 x 1260
-// 103.6 -> 101.7 us, L1 fwd x 208 x 400 26.1 -> 24.7, L1 dX x 400 x 208
-// 26.8 -> 24.7).  Needs K % 4 == 0 (whole 16-B A chunks per row).
-template <int NW, int MT, int NT, int BK, int AP>
-static int launch_gemm3c(hipStream_t st, const float* A, int64_t lda, const unsigned short* Bp,
+// k_gemm3d: A straight to registers, B planes double-buffered, the next
+// step's split and B staging spread under the current step's MFMAs,
+// XCD-grouped block order (MI355X, tools/gemm3_tune.hip, LDS-staged k_gemm3
+// -> k_gemm3d: C2 L0 fwd 15360 x 408 x 1260 104.3 -> 89.8 us, L1 fwd x 208 x
+// 400 25.9 -> 22.1, L1 dX x 400 x 208 27.0 -> 22.6, C5 L0 fwd 262144 x 144 x
+// 1024 596 -> 567).  Needs K % 4 == 0 (whole 16-B A chunks per row).
+template <int NW, int MT, int NT, int AP>
+static int launch_gemm3d(hipStream_t st, const float* A, int64_t lda, const unsigned short* Bp,
                          int64_t Kp, int64_t N, float* C, int64_t ldc, int64_t M, int64_t K) {
-  using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
+  using Cfg = Gemm3bCfg<NW, MT, NT, 32>;
   constexpr size_t lds = Cfg::LDS;
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)k_gemm3c<NW, MT, NT, BK, AP>,
+    (void)hipFuncSetAttribute((const void*)k_gemm3d<NW, MT, NT, AP>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     return true;
   }();
   (void)attr;
   const int nm = (int)((M + Cfg::BM - 1) / Cfg::BM), nn = (int)((N + Cfg::BN - 1) / Cfg::BN);
   const unsigned grid = (unsigned)(((nm + 7) / 8) * 8 * nn);
-  hipLaunchKernelGGL((k_gemm3c<NW, MT, NT, BK, AP>), dim3(grid), dim3(Cfg::THREADS), lds, st, A,
-                     lda, Bp, Kp, N * Kp, C, ldc, M, N, K, nm, nn);
+  hipLaunchKernelGGL((k_gemm3d<NW, MT, NT, AP>), dim3(grid), dim3(Cfg::THREADS), lds, st, A, lda,
+                     Bp, Kp, N * Kp, C, ldc, M, N, K, nm, nn);
   return (int)hipGetLastError();
 }
 
@@ -167,14 +169,14 @@ extern "C" int sv2n_gemm_f32x3(const float* A, int64_t lda, const uint16_t* Bp, 
   const bool longk = K > 256;
   // 144-column tiles when they pad N less than 208-column ones (C5: N = 144)
   const bool t144 = (N + 143) / 144 * 144 < (N + 207) / 208 * 208 && mb * ((N + 143) / 144) >= 240;
+  if (gemm3d_on() && K % 4 == 0) {
+    if (t144) return launch_gemm3d<8, 1, 9, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+    if (wide) return launch_gemm3d<8, 1, 13, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+    return launch_gemm3d<8, 1, 7, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+  }
   if (t144)
     return longk ? launch_gemm3<8, 1, 9, 64>(stream, A, lda, B, Kp, N, C, ldc, M, K)
                  : launch_gemm3<8, 1, 9, 32>(stream, A, lda, B, Kp, N, C, ldc, M, K);
-  if (gemm3c_on() && K % 4 == 0 && M * std::max(lda, K) * 4 <= 0x7fffffff) {
-    if (wide) return launch_gemm3c<8, 1, 13, 32, 3>(stream, A, lda, B, Kp, N, C, ldc, M, K);
-    return longk ? launch_gemm3c<8, 1, 7, 64, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K)
-                 : launch_gemm3c<8, 1, 7, 32, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
-  }
   if (wide)
     return longk ? launch_gemm3<8, 1, 13, 64>(stream, A, lda, B, Kp, N, C, ldc, M, K)
                  : launch_gemm3<8, 1, 13, 32>(stream, A, lda, B, Kp, N, C, ldc, M, K);

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
+#include <utility>
 #include "sv2n_common.h"
 
 namespace sv2n {
@@ -615,7 +616,15 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3b(const float* __restrict__ A,
 // The stage written at the top of step s was last read in step s-1, which
 // every wave finished before the barrier that closed it.
 // ---------------------------------------------------------------------------
-template <int NW, int MT, int NT, int BK, int AP>
+#ifdef SV2N_GEMM_CLOCK
+// diagnostic build of tools/gemm3_tune.hip only: per workgroup (shader clock
+// ticks, 100 MHz real-time ticks) between the first and the last instruction
+// of wave 0, written to a buffer nothing else reads
+__device__ unsigned long long g_gemm_clock[2 * 4096];
+#endif
+// ABL (tools/gemm3_tune.hip timing ablations only; results are wrong when
+// set): 1 no A split, 2 no B staging, 3 no barrier in the loop, 4 no A loads
+template <int NW, int MT, int NT, int BK, int AP, int ABL = 0, int PD = 1>
 __global__ __launch_bounds__(64 * NW) void k_gemm3c(const float* __restrict__ A, int64_t lda,
                                                     const unsigned short* __restrict__ Bp,
                                                     int64_t ldb, int64_t bplane,
@@ -625,6 +634,9 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3c(const float* __restrict__ A,
   constexpr int TH = Cfg::THREADS, BN = Cfg::BN, ROW = Cfg::ROW, BV = Cfg::BV;
   constexpr int STAGE = Cfg::STAGE, BC = BK / 8, KS = BK / 32;
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+#ifdef SV2N_GEMM_CLOCK
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int id = blockIdx.x;
@@ -653,7 +665,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3c(const float* __restrict__ A,
         for (int hv = 0; hv < 2; ++hv) {
           const int64_t k = k0 + 32 * ks + 8 * lg + 4 * hv;
           const int off = k < K ? (int)(((16 * a + li) * lda + k) * 4) : OOB;
-          ra[set][a][ks][hv] = bld4(ra_src, off);
+          ra[set][a][ks][hv] = ABL == 4 ? f32x4{1.f, 2.f, 3.f, (float)off} : bld4(ra_src, off);
         }
   };
   uint4 rb[BV];
@@ -695,7 +707,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3c(const float* __restrict__ A,
   auto step = [&](int s, auto set_c) {
     constexpr int set = decltype(set_c)::value;
     const unsigned short* sB = lds + (s & 1) * STAGE;
-    if (s + 1 < nk) {
+    if (ABL != 2 && s + 1 < nk) {
       store_b(lds + ((s + 1) & 1) * STAGE);
       if (s + 2 < nk) load_b((int64_t)(s + 2) * BK);
     }
@@ -703,30 +715,235 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3c(const float* __restrict__ A,
     for (int ks = 0; ks < KS; ++ks) {
       bf16x8 af[MT][3];
 #pragma unroll
-      for (int a = 0; a < MT; ++a) split3_frag(ra[set][a][ks][0], ra[set][a][ks][1], af[a]);
-      bf16x8 bq[2][3];
+      for (int a = 0; a < MT; ++a) {
+        if constexpr (ABL == 1) {
+          af[a][0] = __builtin_bit_cast(bf16x8, ra[set][a][ks][0]);
+          af[a][1] = __builtin_bit_cast(bf16x8, ra[set][a][ks][1]);
+          af[a][2] = af[a][0];
+        } else {
+          split3_frag(ra[set][a][ks][0], ra[set][a][ks][1], af[a]);
+        }
+      }
+      // B fragments PD column tiles ahead, in a ring of PD + 1 register sets
+      bf16x8 bq[PD + 1][3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
-        bq[0][p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + li) * ROW + 32 * ks + 8 * lg);
-      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+      for (int b = 0; b < PD && b < NT; ++b)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bq[b][p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + 16 * b + li) * ROW + 32 * ks +
+                                                      8 * lg);
+      __builtin_amdgcn_sched_group_barrier(0x100, 3 * (PD < NT ? PD : NT), 0);
 #pragma unroll
       for (int b = 0; b < NT; ++b) {
-        if (b + 1 < NT) {
+        if (b + PD < NT) {
 #pragma unroll
           for (int p = 0; p < 3; ++p)
-            bq[(b + 1) & 1][p] = *reinterpret_cast<const bf16x8*>(
-                sB + (p * BN + 16 * (b + 1) + li) * ROW + 32 * ks + 8 * lg);
+            bq[(b + PD) % (PD + 1)][p] = *reinterpret_cast<const bf16x8*>(
+                sB + (p * BN + 16 * (b + PD) + li) * ROW + 32 * ks + 8 * lg);
           __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
         }
 #pragma unroll
-        for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<3>(af[a], bq[b & 1], acc[a][b]);
+        for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<3>(af[a], bq[b % (PD + 1)], acc[a][b]);
         __builtin_amdgcn_sched_group_barrier(0x008, 6 * MT, 0);
       }
     }
     if (s + AP < nk) load_a(set, (int64_t)(s + AP) * BK);
-    __syncthreads();
+    if constexpr (ABL != 3) __syncthreads();
   };
   static_assert(AP == 2 || AP == 3, "A register sets");
+  for (int s = 0; s < nk; s += AP) {
+    step(s, std::integral_constant<int, 0>{});
+    if (s + 1 < nk) step(s + 1, std::integral_constant<int, 1>{});
+    if constexpr (AP == 3)
+      if (s + 2 < nk) step(s + 2, std::integral_constant<int, 2>{});
+  }
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int64_t gn = n0 + 16 * b + li;
+      if (gn < N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t gm = arow0 + 16 * a + 4 * lg + r;
+          if (gm < M) C[gm * ldc + gn] = acc[a][b][r];
+        }
+      }
+    }
+#ifdef SV2N_GEMM_CLOCK
+  if (t == 0 && blockIdx.x < 4096) {
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    g_gemm_clock[2 * blockIdx.x] = c1 - c0;
+    g_gemm_clock[2 * blockIdx.x + 1] = r1 - r0;
+  }
+#endif
+}
+
+// compile-time loop: f(std::integral_constant<int, 0>{}) ... f(<N-1>)
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// ---------------------------------------------------------------------------
+// k_gemm3d: k_gemm3c with the work between two barriers spread under the
+// step's MFMAs instead of run ahead of them (BK = 32: one K-step per barrier):
+//   * the bf16x3 split of step s+1's A fragments runs during step s, a pair
+//     of elements per column tile (split3_pk: ~11 VALU) beside its MFMAs
+//     (splitting in the last tiles instead: 91.8 vs 88.8 us at C2 L0);
+//   * the B planes of step s+1 go to the other LDS stage one ds_write per
+//     column tile, and step s+2's loads follow the last write;
+// so after the barrier a wave only waits for its first B fragments.
+// Scheduling-group barriers hold the compiler to that interleave.
+// ---------------------------------------------------------------------------
+template <int NW, int MT, int NT, int AP>
+__global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A, int64_t lda,
+                                                    const unsigned short* __restrict__ Bp,
+                                                    int64_t ldb, int64_t bplane,
+                                                    float* __restrict__ C, int64_t ldc, int64_t M,
+                                                    int64_t N, int64_t K, int nm, int nn) {
+  constexpr int BK = 32;
+  using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
+  constexpr int TH = Cfg::THREADS, BN = Cfg::BN, ROW = Cfg::ROW, BV = Cfg::BV;
+  constexpr int STAGE = Cfg::STAGE, BC = BK / 8;
+  constexpr int NPAIR = 4 * MT;  // split3_pk pairs per step (8 floats per fragment)
+  constexpr int PPT = (NPAIR + NT - 1) / NT;  // pairs split per column tile
+  static_assert(BV + 1 < NT, "interleave needs enough column tiles");
+  static_assert(AP >= 2 && AP <= 3, "A register sets");
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int id = blockIdx.x;
+  const int q = id / (8 * nn), rem = id - q * 8 * nn;
+  const int nb = rem >> 3, mb = q * 8 + (rem & 7);
+  if (mb >= nm) return;
+  const int64_t m0 = (int64_t)mb * Cfg::BM, n0 = (int64_t)nb * BN;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t arow0 = m0 + (int64_t)wave * 16 * MT;
+  const int64_t arows = M - arow0;
+  const rsrc_t ra_src = make_rsrc(A + (arow0 > M ? 0 : arow0 * lda),
+                                  arows > 0 ? (uint32_t)(min(arows, (int64_t)16 * MT) * lda * 4) : 0u);
+  f32x4 ra[AP][MT][2];
+  auto load_a = [&](int set, int64_t k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int hv = 0; hv < 2; ++hv) {
+        const int64_t k = k0 + 8 * lg + 4 * hv;
+        const int off = k < K ? (int)(((16 * a + li) * lda + k) * 4) : OOB;
+        ra[set][a][hv] = bld4(ra_src, off);
+      }
+  };
+  u32x4_t rb[BV];
+  // branch-free staging (branches would split the interleaved block): slots
+  // past the image repeat the last one (same value, same address)
+  auto b_slot = [&](int sv, int& p, int& r, int& c) __attribute__((always_inline)) {
+    const int idx = min(t + TH * sv, 3 * BN * BC - 1);
+    p = idx / (BN * BC);
+    const int r2 = idx - p * BN * BC;
+    r = r2 / BC;
+    c = r2 - r * BC;
+  };
+  auto load_b1 = [&](int sv, int64_t k0) __attribute__((always_inline)) {
+    int p, r, c;
+    b_slot(sv, p, r, c);
+    const int64_t gn = min(n0 + r, N - 1);
+    rb[sv] = *reinterpret_cast<const u32x4_t*>(Bp + p * bplane + gn * ldb + k0 + 8 * c);
+  };
+  auto store_b1 = [&](int sv, unsigned short* sB) __attribute__((always_inline)) {
+    int p, r, c;
+    b_slot(sv, p, r, c);
+    *reinterpret_cast<u32x4_t*>(sB + (p * BN + r) * ROW + 8 * c) = rb[sv];
+  };
+  // packed bf16 planes of the current step's A fragments, and the next step's
+  u32x4_t afc[MT][3], afn[MT][3];
+  auto split_pair = [&](u32x4_t (&dst)[MT][3], const f32x4 (&src)[MT][2], int pr) {
+    const int a = pr >> 2, qd = pr & 3;  // fragment a, word qd (elements 2qd, 2qd+1)
+    const f32x4& v = src[a][qd >> 1];
+    unsigned w0, w1, w2;
+    split3_pk(v[2 * (qd & 1)], v[2 * (qd & 1) + 1], w0, w1, w2);
+    dst[a][0][qd] = w0;
+    dst[a][1][qd] = w1;
+    dst[a][2][qd] = w2;
+  };
+
+  const int nk = (int)((K + BK - 1) / BK);
+#pragma unroll
+  for (int s = 0; s < AP; ++s)
+    if (s < nk) load_a(s, (int64_t)s * BK);
+#pragma unroll
+  for (int sv = 0; sv < BV; ++sv) load_b1(sv, 0);
+#pragma unroll
+  for (int sv = 0; sv < BV; ++sv) store_b1(sv, lds);
+  if (nk > 1)
+#pragma unroll
+    for (int sv = 0; sv < BV; ++sv) load_b1(sv, BK);
+#pragma unroll
+  for (int pr = 0; pr < NPAIR; ++pr) split_pair(afc, ra[0], pr);
+  __syncthreads();
+
+  auto step = [&](int s, auto set_c) __attribute__((always_inline)) {
+    constexpr int set = decltype(set_c)::value, nset = (set + 1) % AP;
+    const unsigned short* sB = lds + (s & 1) * STAGE;
+    unsigned short* sW = lds + ((s + 1) & 1) * STAGE;
+    // the last steps stage a copy nobody reads (the other stage is free after
+    // the barrier) and reload the last K-step: no branch in the block
+    const int64_t kb2 = (int64_t)min(s + 2, nk - 1) * BK;
+    bf16x8 af[MT][3];
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) af[a][p] = __builtin_bit_cast(bf16x8, afc[a][p]);
+    bf16x8 bq[2][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bq[0][p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + li) * ROW + 8 * lg);
+    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+    static_for<NT>([&](auto bc) __attribute__((always_inline)) {
+      constexpr int b = decltype(bc)::value;
+      if constexpr (b + 1 < NT) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bq[(b + 1) & 1][p] = *reinterpret_cast<const bf16x8*>(
+              sB + (p * BN + 16 * (b + 1) + li) * ROW + 8 * lg);
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+      }
+      if constexpr (b < BV) {
+        store_b1(b, sW);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      } else if constexpr (b == BV) {
+#pragma unroll
+        for (int sv = 0; sv < BV; ++sv) load_b1(sv, kb2);
+        __builtin_amdgcn_sched_group_barrier(0x020, BV, 0);
+      }
+      if constexpr (b * PPT < NPAIR) {
+        static_for<PPT>([&](auto pc) __attribute__((always_inline)) {
+          constexpr int pr = b * PPT + decltype(pc)::value;
+          if constexpr (pr < NPAIR) split_pair(afn, ra[nset], pr);
+        });
+        __builtin_amdgcn_sched_group_barrier(0x002, 11 * PPT, 0);
+      }
+#pragma unroll
+      for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<3>(af[a], bq[b & 1], acc[a][b]);
+      __builtin_amdgcn_sched_group_barrier(0x008, 6 * MT, 0);
+    });
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) afc[a][p] = afn[a][p];
+    if (s + AP < nk) load_a(set, (int64_t)(s + AP) * BK);
+    __syncthreads();
+  };
   for (int s = 0; s < nk; s += AP) {
     step(s, std::integral_constant<int, 0>{});
     if (s + 1 < nk) step(s + 1, std::integral_constant<int, 1>{});

@@ -9,6 +9,7 @@
 #include <functional>
 #include <string>
 #include <vector>
+#include <algorithm>
 
 #include "../spotv2net_amd/csrc/sv2n_common.h"
 #include "../spotv2net_amd/csrc/sv2n_gemm3_kernel.h"
@@ -89,13 +90,13 @@ void run3(const Shape& sh, hipStream_t st, const float* A, const unsigned short*
   fflush(stdout);
 }
 
-template <int NW, int MT, int NT, int BK, int AP, bool CV = false>
+template <int NW, int MT, int NT, int BK, int AP, bool CV = false, int ABL = 0, int PD = 1, bool DV = false>
 void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short* Bp, int64_t Kp,
            float* C, const std::vector<double>& ref, const std::vector<double>& absr) {
   using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
   const size_t lds = Cfg::LDS;
   if (lds > 160 * 1024) return;
-  auto kern = CV ? k_gemm3c<NW, MT, NT, BK, AP> : k_gemm3b<NW, MT, NT, BK, AP>;
+  auto kern = DV ? k_gemm3d<NW, MT, NT, AP> : CV ? k_gemm3c<NW, MT, NT, BK, AP, ABL, PD> : k_gemm3b<NW, MT, NT, BK, AP>;
   if (lds > 65536)
     CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   const int nm = (int)((sh.M + Cfg::BM - 1) / Cfg::BM), nn = (int)((sh.N + Cfg::BN - 1) / Cfg::BN);
@@ -127,6 +128,21 @@ void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
   const double us = ms * 1e3 / reps;
+#ifdef SV2N_GEMM_CLOCK
+  if (CV) {
+    std::vector<unsigned long long> ck(2 * 4096);
+    CK(hipMemcpyFromSymbol(ck.data(), HIP_SYMBOL(g_gemm_clock), sizeof(unsigned long long) * ck.size()));
+    std::vector<double> ghz;
+    for (unsigned b = 0; b < std::min<unsigned>(grid, 4096); ++b)
+      if (ck[2 * b + 1] > 0) ghz.push_back(ck[2 * b] / (ck[2 * b + 1] * 10.0));
+    std::sort(ghz.begin(), ghz.end());
+    if (!ghz.empty())
+      printf("    in-kernel clock (last launch, median over workgroups): %.3f GHz\n", ghz[ghz.size() / 2]);
+  }
+#endif
+  if (ABL) printf("  [ablation %d]", ABL);
+  if (PD != 1) printf("  [PD %d]", PD);
+  if (DV) printf("  [3d]");
   printf("  gemm3%s NW%d MT%d NT%-2d BK%d AP%d %8.1f us %7.1f TF(f32-eq)  max|err| %.2e  max err/S|ab| %.2e\n",
          CV ? "c" : "b", NW, MT, NT, BK, AP, us, 2.0 * sh.M * sh.N * sh.K / us / 1e6, maxabs, maxrel);
   fflush(stdout);
@@ -134,7 +150,7 @@ void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short
 
 int main() {
   std::vector<Shape> shapes = {{"fwd L0", 15360, 408, 1260}, {"fwd L1", 15360, 208, 400},
-                               {"dX L1", 15360, 400, 208}};
+                               {"dX L1", 15360, 400, 208}, {"C5 fwd L0", 262144, 144, 1024}};
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (auto& sh : shapes) {
@@ -189,15 +205,13 @@ int main() {
     }
     run3<8, 1, 13, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
     run3<8, 1, 7, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 13, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 7, 32, 2>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 13, 32, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3<8, 1, 9, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<8, 1, 13, 32, 3, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 7, 32, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<8, 1, 7, 64, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 2, 7, 32, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<4, 2, 13, 32, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 9, 32, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 2, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 9, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(S)); CK(hipFree(Bp));
   }
   return 0;
