@@ -671,7 +671,9 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
   __shared__ __attribute__((aligned(16))) float sM[MH * BT], sInv[MH * BT], sR[MH * BT],
       sAd[MH * BT], sSh[MH * BT];
   __shared__ uint32_t sPres[2][BT];
-  __shared__ __attribute__((aligned(16))) float sW[D * MH];
+  // W̃ in four head orders: variant q holds head p ^ q at position p, so the
+  // quad's reduce-scatter of the partial logits needs no selects
+  __shared__ __attribute__((aligned(16))) float sW[4 * D * MH];
 
   const int NS = (n + BS - 1) / BS;
   int64_t g;
@@ -692,7 +694,10 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
   const float slope2 = slope * L2E;
   const bool hv = hh < H;
 
-  if (t < D * MH) sW[t] = (t % MH) < H ? wf[(t / MH) * hl_pad + col0 + t % MH] : 0.f;
+  for (int k = t; k < 4 * D * MH; k += WT) {
+    const int qv = k / (D * MH), rem = k - qv * D * MH, d = rem / MH, hq = (rem % MH) ^ qv;
+    sW[k] = hq < H ? wf[d * hl_pad + col0 + hq] : 0.f;
+  }
   if (eidm && t < 2 * BT) sPres[t >> 4][t & 15] = 0u;
   // source rows of the tile (constant): xs_h padded to 16 columns per head
   for (int idx = t; idx < BS * MH * 16; idx += WT) {
@@ -712,6 +717,7 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
   // edge slots: 512 per block, each split over 4 lanes (quarter = lane & 3)
   constexpr int DQ = (D + 3) / 4;
   const int qtr = t & 3, d0 = qtr * DQ;
+  const float* sWq = sW + qtr * D * MH;
   float wacc[DQ][MH];
 #pragma unroll
   for (int d = 0; d < DQ; ++d)
@@ -782,29 +788,32 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
     for (int k = 0; k < 4; ++k) {
       // partial logits over this lane's quarter of the row (scalar FMAs: no
       // packed copies of the prefetched values), completed over the quad
+      // position p holds head p ^ qtr (this lane's W̃ variant)
       float lf[MH];
 #pragma unroll
       for (int h = 0; h < MH; ++h) lf[h] = 0.f;
 #pragma unroll
       for (int dd = 0; dd < DQ; ++dd) {
-        const float* wr = sW + min(d0 + dd, D - 1) * MH;
+        const float* wr = sWq + min(d0 + dd, D - 1) * MH;
         const f4 wa = *reinterpret_cast<const f4*>(wr);
         const f4 wb = *reinterpret_cast<const f4*>(wr + 4);
         const float wv[MH] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
         for (int h = 0; h < MH; ++h) lf[h] = fmaf(evc[k][dd], wv[h], lf[h]);
       }
+      // quad reduce-scatter: partner q^1's position p^1 holds this lane's
+      // head p^q, then partner q^2's s1[i^1] holds s1[i]'s head; lane q ends
+      // with heads q (position 0) and q + 4 (position 4)
+      float s1[4];
 #pragma unroll
-      for (int h = 0; h < MH; ++h) {
-        lf[h] += dpp_xor1(lf[h]);
-        lf[h] += dpp_xor2(lf[h]);
-      }
+      for (int i = 0; i < 4; ++i) s1[i] = lf[2 * i] + dpp_xor1(lf[2 * i + 1]);
+      const float hq0 = s1[0] + dpp_xor2(s1[1]);
+      const float hq4 = s1[2] + dpp_xor2(s1[3]);
       int il, jl;
       slot(k, i0, il, jl);
       float* dst = sE + il * RS + jl;
-      // lane quarter q stores heads q and q + 4
-      dst[qtr * BHS] = qtr == 0 ? lf[0] : qtr == 1 ? lf[1] : qtr == 2 ? lf[2] : lf[3];
-      dst[(qtr + 4) * BHS] = qtr == 0 ? lf[4] : qtr == 1 ? lf[5] : qtr == 2 ? lf[6] : lf[7];
+      dst[qtr * BHS] = hq0;
+      dst[(qtr + 4) * BHS] = hq4;
       if (eidm && qtr == 0) {
         const int i = i0 + il, j = j0 + jl;
         const bool pres = i < n && j < n && i != j && eid[(row0 + i) * n + j] >= 0;
