@@ -68,13 +68,14 @@ constexpr int XCHUNKS = 3;  // forward xs prefetch: ceil(32 rows x 34 chunks / 5
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ int tri_off(int n, int u) { return u * (2 * n - u - 1) / 2; }
+// 24-bit multiplies (full rate; the 32-bit v_mul_lo_u32 is quarter rate): u, n < 2^12
+__device__ __forceinline__ int tri_off(int n, int u) { return __mul24(u, 2 * n - u - 1) >> 1; }
 
 // canonical in-graph edge id of (target i <- source j) (reference
 // utils/dataset.py:216-226: upper pairs u->w row-major, then swapped), -1 if
 // (i, j) is not an edge
 __device__ __forceinline__ int canon_id(int i, int j, int n) {
-  const int U = n * (n - 1) / 2;
+  const int U = __mul24(n, n - 1) >> 1;
   const int id = j > i ? U + tri_off(n, i) + (j - i - 1) : tri_off(n, j) + (i - j - 1);
   return (i < n && j < n && i != j) ? id : -1;
 }
@@ -690,9 +691,13 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
   const rsrc_t rea = eidm ? make_rsrc(nullptr, 0u)
                           : make_rsrc(ea + g * (int64_t)E0 * D, (uint32_t)(4 * E0 * D));
   const rsrc_t rdo = make_rsrc(dout + row0 * HC, (uint32_t)(4 * n * HC));
+  const rsrc_t rst = make_rsrc(stats + row0 * 4 * H, (uint32_t)(16 * n * H));
+  const rsrc_t rrs = make_rsrc(rs + row0 * 4 * H, (uint32_t)(16 * n * H));
+  const rsrc_t rxs = make_rsrc(xs + row0 * ldx, (uint32_t)(4 * n * ldx));
   const int HQ = HC >> 2;  // 16-B chunks per dOut row
   const float slope2 = slope * L2E;
   const bool hv = hh < H;
+  float* const adst_row = adst_part + ((int64_t)js * Ntot + row0) * H + hh;  // + i*H
 
   for (int k = t; k < 4 * D * MH; k += WT) {
     const int qv = k / (D * MH), rem = k - qv * D * MH, d = rem / MH, hq = (rem % MH) ^ qv;
@@ -757,7 +762,7 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
       } else {
 #pragma unroll
         for (int dd = 0; dd < DQ; ++dd)
-          evn[k][dd] = (d0 + dd < D) ? bld(rea, cid >= 0 ? 4 * (cid * D + d0 + dd) : OOB) : 0.f;
+          evn[k][dd] = (d0 + dd < D) ? bld(rea, cid >= 0 ? 4 * (__mul24(cid, D) + d0 + dd) : OOB) : 0.f;
       }
     }
     {
@@ -765,14 +770,16 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
       don = bld4(rdo, (r < BT && i < n) ? 4 * (i * HC + 4 * cq) : OOB);
     }
     if (t < MH * BT) {
+      // graph-local buffer offsets (a miss reads 0)
       const int h = t >> 4, il = t & 15, i = i0 + il;
       const bool ok = h < H && i < n;
-      const int64_t row = row0 + (ok ? i : 0);
-      vecn[0] = ok ? stats[row * 4 * H + h] : 0.f;
-      vecn[1] = ok ? stats[row * 4 * H + H + h] : 0.f;
-      vecn[2] = ok ? rs[row * 4 * H + h] : 0.f;
-      vecn[3] = ok ? xs[row * ldx + HC + H + h] : 0.f;
-      vecn[4] = ok ? rs[row * 4 * H + 3 * H + h] : 0.f;
+      const int o4 = ok ? 4 * (__mul24(i, 4 * H) + h) : OOB;
+      const int ox = ok ? 4 * (__mul24(i, ldx) + HC + H + h) : OOB;
+      vecn[0] = bld(rst, o4);
+      vecn[1] = bld(rst, ok ? o4 + 4 * H : OOB);
+      vecn[2] = bld(rrs, o4);
+      vecn[3] = bld(rxs, ox);
+      vecn[4] = bld(rrs, ok ? o4 + 12 * H : OOB);
     }
   };
 
@@ -898,7 +905,7 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
       for (int r = 0; r < 4; ++r) {
         const float s = row16_sum(rowacc[r]);
         const int i = i0 + 4 * lk + r;
-        if (li == 0 && i < n) adst_part[((int64_t)js * Ntot + row0 + i) * H + hh] = s;
+        if (li == 0 && i < n) adst_row[__mul24(i, H)] = s;
       }
       // dxs_h[j][c] += Σ_i P[i][j] dOut_h[i][c]: A = P from registers (k = 4lk + s)
 #pragma unroll
