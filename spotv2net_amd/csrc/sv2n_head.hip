@@ -418,15 +418,16 @@ __global__ __launch_bounds__(256) void k_head_mse_train(
       if (t < PG * cols) {
         const int oc = base + t % cols, g = t / cols;
         float s = 0.f;
-        for (int b0 = g; b0 < nparts; b0 += 16 * PG) {
-          float v[16];
+        // 64 loads in flight: one round trip for up to 64·PG partials (C2: 240)
+        for (int b0 = g; b0 < nparts; b0 += 64 * PG) {
+          float v[64];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) {
+          for (int u = 0; u < 64; ++u) {
             const int bb = b0 + u * PG;
             v[u] = bb < nparts ? ld_sc1(part + (int64_t)bb * stride + oc) : 0.f;
           }
 #pragma unroll
-          for (int u = 0; u < 16; ++u) s += v[u];
+          for (int u = 0; u < 64; ++u) s += v[u];
         }
         s_grp[t] = s;
       }
