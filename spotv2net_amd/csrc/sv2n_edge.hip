@@ -11,6 +11,7 @@
 //
 // HBM layout: edge_attr [E][D] fp32 row-major (D = 3*seq_length), read once
 // per pass with 16-B loads into an LDS chunk of 64 edges.
+#include <cstdlib>
 #include "sv2n_common.h"
 
 namespace sv2n {
@@ -585,6 +586,13 @@ using namespace sv2n;
 
 static constexpr int EDGE_BWD_GRID = 768;
 static constexpr int EDGE_FWD_GRID = 1024;
+// SV2N_EDGE_FWD_GRID / SV2N_EDGE_BWD_GRID: workgroup-count overrides for
+// tuning sweeps (the backward's is capped at EDGE_BWD_GRID: workspace size)
+static int edge_grid_env(const char* name, int dflt, int cap) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? std::min(v, cap) : dflt;
+}
 static constexpr int EDGE_SMALL_FWD_GRID = 4096;
 static constexpr int EDGE_SMALL_BWD_GRID = 1024;
 
@@ -700,7 +708,8 @@ static int edge_fwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
                                           wfold, hl_pad, lp, num_layers, heads, num_graphs, n,
                                           stream);
   const int64_t nchunks = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
-  const unsigned grid = (unsigned)std::min<int64_t>(nchunks, EDGE_FWD_GRID);
+  static const int fwd_grid = edge_grid_env("SV2N_EDGE_FWD_GRID", EDGE_FWD_GRID, 1 << 20);
+  const unsigned grid = (unsigned)std::min<int64_t>(nchunks, fwd_grid);
   const int rf = (EDGE_CHUNK * edge_dim / 4 + EDGE_THREADS - 1) / EDGE_THREADS;
   if (rf > EDGE_RF_MAX) return SV2N_ERR_SHAPE;
   const int rfi = rf <= 2 ? 2 : rf <= 8 ? 8 : rf <= 16 ? 16 : 24;  // instantiated RF
@@ -775,7 +784,8 @@ static int edge_bwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
                                           lp, num_layers, heads, num_graphs, n, workspace,
                                           workspace_floats, dwfold, hl_pad, stream);
   const int64_t nchunks = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(EDGE_BWD_GRID, nchunks));
+  static const int bwd_grid = edge_grid_env("SV2N_EDGE_BWD_GRID", EDGE_BWD_GRID, EDGE_BWD_GRID);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(bwd_grid, nchunks));
   if (workspace_floats < (int64_t)grid * O) return SV2N_ERR_WORKSPACE;
   const int rf = (EDGE_CHUNK * edge_dim / 4 + EDGE_THREADS - 1) / EDGE_THREADS;
   if (rf > EDGE_RF_MAX) return SV2N_ERR_SHAPE;

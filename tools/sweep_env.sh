@@ -9,5 +9,5 @@ for v in $vals; do
 import json
 d = json.loads(open('$out/sw_$v.json').read().strip().splitlines()[-1])
 k = d.get('kernels', {})
-print('$var=$v', d['value'], d['ms_per_step'], {n: round(x['avg_us'], 1) for n, x in k.items() if 'gemm' in n})"
+print('$var=$v', d['value'], d['ms_per_step'], {n: round(x['avg_us'], 1) for n, x in k.items()})"
 done
