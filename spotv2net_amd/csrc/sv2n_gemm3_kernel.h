@@ -847,12 +847,16 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
   u32x4_t rb[BV];
   // branch-free staging (branches would split the interleaved block): slots
   // past the image repeat the last one (same value, same address)
+  // 16 consecutive slots = 4 rows x 4 chunks, row-minor: each 8-lane group of
+  // a ds_write_b128 then covers 8 distinct 4-dword bank windows (96-B rows;
+  // row-major slots put lanes 6-7 on lanes 0-1's banks)
+  static_assert(BC == 4 && BN % 4 == 0, "slot order assumes 4 chunks per row");
   auto b_slot = [&](int sv, int& p, int& r, int& c) __attribute__((always_inline)) {
     const int idx = min(t + TH * sv, 3 * BN * BC - 1);
     p = idx / (BN * BC);
     const int r2 = idx - p * BN * BC;
-    r = r2 / BC;
-    c = r2 - r * BC;
+    r = ((r2 >> 4) << 2) + (r2 & 3);
+    c = (r2 >> 2) & 3;
   };
   auto load_b1 = [&](int sv, int64_t k0) __attribute__((always_inline)) {
     int p, r, c;
