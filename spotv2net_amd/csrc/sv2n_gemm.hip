@@ -303,11 +303,39 @@ static SlabPlan slab_plan(int64_t F, int64_t N, int64_t K, bool vec, int64_t lda
   return sp;
 }
 
+// SV2N_WGRAD3Y=0: k_gemm_tt3w (staging between two barriers) instead of
+// k_gemm_tt3y (staging under the MFMAs)
+static bool wgrad3y_on() {
+  static const bool on = [] {
+    const char* e = getenv("SV2N_WGRAD3Y");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int NT, int MT>
 static void launch_tt3w(const SlabPlan& p, hipStream_t stream, const float* x, int64_t ld_x,
                         const float* dxs, int64_t ldx, int64_t F, int64_t N, int64_t K,
                         float* out) {
   using Cfg = GemmTT3WCfg<NT, MT>;
+  using CfgY = GemmTT3YCfg<NT, MT>;
+  // tt3y where it measured faster: the 208-column tilings (C2 L0 dWᵀ 92.9 ->
+  // 91.0 us, step 0.5476 -> 0.5424 ms); C5's 144-column one: 524 vs 530 us
+  if constexpr (NT == 13 && CfgY::LDS <= 160 * 1024) {
+    if (wgrad3y_on()) {
+      static bool attr_y = [] {
+        (void)hipFuncSetAttribute((const void*)k_gemm_tt3y<NT, MT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)CfgY::LDS);
+        return true;
+      }();
+      (void)attr_y;
+      const dim3 gy((unsigned)((F + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN),
+                    (unsigned)((p.splitk + 7) / 8 * 8));
+      hipLaunchKernelGGL((k_gemm_tt3y<NT, MT>), gy, dim3(Cfg::THREADS), CfgY::LDS, stream, x,
+                         ld_x, dxs, ldx, out, F, N, K, p.kslice, p.splitk);
+      return;
+    }
+  }
   static bool attr = [] {
     (void)hipFuncSetAttribute((const void*)k_gemm_tt3w<NT, MT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);

@@ -369,4 +369,178 @@ __global__ __launch_bounds__(512) void k_gemm_tt3w(const float* __restrict__ A, 
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_gemm_tt3y: k_gemm_tt3w<NT, MT> with the next step's staging under the
+// current step's MFMAs, in the LDS of one A image and two B stages.
+//   * A (x, k-strided) is staged per wave: wave w loads, splits and writes the
+//     16·MT rows it alone reads.  Its fragments are read into registers at the
+//     top of the step, so once those reads land the wave rewrites its rows
+//     with step s+1 while its MFMAs run — no second A image, no barrier.
+//   * B (dxs) is shared: step s+1 goes to the other of two stages, one
+//     staging piece per column tile, published by the step's barrier.
+//   * step s+1's operands are loaded at the top of step s and staged, one
+//     piece per column tile, in its last tiles (registers: the two-tile
+//     tiling is at 240 VGPRs without them); staging is branch-free (slots past the B image repeat the last one; the
+//     last steps reload the last K-step and write what nobody reads).
+// Same products in the same order as k_gemm_tt3w.  C2 L0 dWᵀ: 98 KiB of
+// stage for tt3w's single stage, 144 KiB here.
+// ---------------------------------------------------------------------------
+template <int NT, int MT>
+struct GemmTT3YCfg {
+  using W = GemmTT3WCfg<NT, MT>;
+  static constexpr int AVW = 16 * MT * W::BK / 4 / 64;  // float4 per lane: the wave's A rows
+  static constexpr size_t LDS = sizeof(unsigned short) * (3 * W::PA + 2 * 3 * W::PB);
+  static_assert(16 * MT * W::BK / 4 % 64 == 0, "wave A staging tiles the lanes");
+};
+
+template <int NT, int MT>
+__global__ __launch_bounds__(512) void k_gemm_tt3y(const float* __restrict__ A, int64_t lda,
+                                                   const float* __restrict__ B, int64_t ldb,
+                                                   float* __restrict__ part, int64_t M, int64_t N,
+                                                   int64_t K, int64_t kslice, int nz) {
+  using Cfg = GemmTT3WCfg<NT, MT>;
+  constexpr int BK = Cfg::BK, BN = Cfg::BN, SA = Cfg::SA, SB = Cfg::SB;
+  constexpr int PA = Cfg::PA, PB = Cfg::PB, BV = Cfg::BV, BVN = Cfg::BVN;
+  constexpr int AVW = GemmTT3YCfg<NT, MT>::AVW;
+  constexpr int NPUT = AVW + BV;
+  static_assert(AVW + BV <= NT, "one staging piece per column tile");
+  constexpr int WR = 16 * MT;  // A rows of one wave
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  unsigned short* const sA = lds;            // [3][BK][SA], rows of wave w at 16·MT·w
+  unsigned short* const sB0 = lds + 3 * PA;  // two stages of [3][BK][SB]
+  const int tiles = gridDim.x * gridDim.y;
+  const int id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int xcd = id & 7, slot = id >> 3;
+  const int bz = xcd + 8 * (slot / tiles);
+  const int tile = slot - (slot / tiles) * tiles;
+  const int by = tile / gridDim.x, bx = tile - by * gridDim.x;
+  if (bz >= nz) return;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int64_t m0 = (int64_t)bx * Cfg::BM, n0 = (int64_t)by * BN;
+  const int64_t kbeg = (int64_t)bz * kslice, kend = min(K, kbeg + kslice);
+  float* C = part + (int64_t)bz * M * N;
+  const rsrc_t ra = make_rsrc(A, (uint32_t)min<int64_t>(K * lda * 4, 0x7fffffff));
+  const rsrc_t rb = make_rsrc(B, (uint32_t)min<int64_t>(K * ldb * 4, 0x7fffffff));
+  const int wrow = WR * wave;  // first A row (in the block) of this wave
+
+  f32x4 va[AVW], vb[BV];
+  auto load_a = [&](int64_t k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < AVW; ++s) {
+      const int idx = lane + 64 * s;
+      const int r = idx / (WR / 4), c4 = idx - r * (WR / 4);
+      const int64_t k = k0 + r, m = m0 + wrow + 4 * c4;
+      va[s] = bld4(ra, (k < kend && m < M) ? (int)((k * lda + m) * 4) : OOB);
+    }
+  };
+  auto load_b = [&](int64_t k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < BV; ++s) {
+      const int idx = min(t + 512 * s, BVN - 1);
+      const int r = idx / (BN / 4), c4 = idx - r * (BN / 4);
+      const int64_t k = k0 + r, n = n0 + 4 * c4;
+      vb[s] = bld4(rb, (k < kend && n < N) ? (int)((k * ldb + n) * 4) : OOB);
+    }
+  };
+  auto put = [&](unsigned short* dst, int plane, int stride, int r, int c, const f32x4& v)
+      __attribute__((always_inline)) {
+    uint2 w[3];
+    split3_pk(v[0], v[1], w[0].x, w[1].x, w[2].x);
+    split3_pk(v[2], v[3], w[0].y, w[1].y, w[2].y);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(dst + p * plane + r * stride + c) = w[p];
+  };
+  // piece i < AVW: the wave's A rows; else a B slot into stage sb
+  auto put_piece = [&](auto i_c, unsigned short* sb) __attribute__((always_inline)) {
+    constexpr int i = decltype(i_c)::value;
+    if constexpr (i < AVW) {
+      const int idx = lane + 64 * i;
+      const int r = idx / (WR / 4), c4 = idx - r * (WR / 4);
+      put(sA, PA, SA, r, wrow + 4 * c4, va[i]);
+    } else {
+      const int idx = min(t + 512 * (i - AVW), BVN - 1);
+      const int r = idx / (BN / 4), c4 = idx - r * (BN / 4);
+      put(sb, PB, SB, r, 4 * c4, vb[i - AVW]);
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int q = li >> 2, p4 = 4 * (li & 3);
+  const int kA0 = (4 * lg + q) * SA, kA1 = (16 + 4 * lg + q) * SA;
+  const int kB0 = (4 * lg + q) * SB, kB1 = (16 + 4 * lg + q) * SB;
+
+  const int nsteps = (int)((kend - kbeg + BK - 1) / BK);
+  auto step = [&](int s, auto cur_c) __attribute__((always_inline)) {
+    constexpr int cur = decltype(cur_c)::value, nxt = 1 - cur;
+    const unsigned short* sb = sB0 + cur * 3 * PB;
+    unsigned short* sw = sB0 + nxt * 3 * PB;
+    // step s+1's operands, staged in this step's last column tiles
+    load_a(kbeg + (int64_t)min(s + 1, nsteps - 1) * BK);
+    load_b(kbeg + (int64_t)min(s + 1, nsteps - 1) * BK);
+    bf16x8 af[MT][3];
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+      const int ca = 16 * (MT * wave + a) + p4;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        af[a][pl] = tr_frag(sA + pl * PA + kA0 + ca, sA + pl * PA + kA1 + ca);
+    }
+    bf16x8 bq[2][3];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      bq[0][pl] = tr_frag(sb + pl * PB + kB0 + p4, sb + pl * PB + kB1 + p4);
+    __builtin_amdgcn_sched_group_barrier(0x100, 6 * (MT + 1), 0);
+    // a wave's LDS operations execute in issue order: its A rows can be
+    // rewritten right behind these reads
+    static_for<NT>([&](auto bc) __attribute__((always_inline)) {
+      constexpr int b = decltype(bc)::value;
+      if constexpr (b + 1 < NT) {
+        const int cb = 16 * (b + 1) + p4;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          bq[(b + 1) & 1][pl] = tr_frag(sb + pl * PB + kB0 + cb, sb + pl * PB + kB1 + cb);
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+      }
+      // one staging piece per tile in the last NPUT tiles (loads issued at the
+      // top of this step)
+      constexpr int i = b - (NT - NPUT);
+      if constexpr (i >= 0) {
+        put_piece(std::integral_constant<int, i>{}, sw);
+        __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
+      }
+#pragma unroll
+      for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<3>(af[a], bq[b & 1], acc[a][b]);
+      __builtin_amdgcn_sched_group_barrier(0x008, 6 * MT, 0);
+    });
+    __syncthreads();
+  };
+  if (nsteps > 0) {
+    load_a(kbeg);
+    load_b(kbeg);
+    static_for<NPUT>([&](auto ic) __attribute__((always_inline)) { put_piece(ic, sB0); });
+    __syncthreads();
+    for (int s = 0; s < nsteps; s += 2) {
+      step(s, std::integral_constant<int, 0>{});
+      if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>{});
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int64_t gn = n0 + 16 * b + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t gm = m0 + 16 * (MT * wave + a) + 4 * lg + r;
+        if (gm < M && gn < N) C[gm * N + gn] = acc[a][b][r];
+      }
+    }
+}
+
 }  // namespace sv2n
