@@ -44,7 +44,9 @@ def test_linear_autograd(dev):
 @pytest.mark.parametrize("M,N,K,transpose", [(15360, 408, 1260, False), (300, 17, 5, False),
                                              (257, 400, 208, True), (64, 1, 70, True),
                                              (1000, 130, 64, False), (15360, 400, 208, False),
-                                             (15360, 208, 400, False), (4000, 208, 1260, True)])
+                                             (15360, 208, 400, False), (4000, 208, 1260, True),
+                                             (100, 50, 4, False), (129, 208, 36, False),
+                                             (300, 144, 1024, False)])
 def test_split3_gemm_matches_f32_accuracy(dev, M, N, K, transpose):
     """sv2n_gemm_f32x3 (three bf16 planes, six MFMA products) is as close to
     the float64 product as the exact-f32 MFMA GEMM: max error relative to
