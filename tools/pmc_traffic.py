@@ -24,7 +24,7 @@ from collections import defaultdict
 # bench.py kernel_table name -> rocprof kernel name prefix (the C2 instantiation)
 KERNELS = {
     "gemm_l0_fwd": "sv2n::k_gemm3d<8, 1, 13, 2>",
-    "gemm_l0_dwT": "sv2n::k_gemm_tt3w<13, 2>",
+    "gemm_l0_dwT": "sv2n::k_gemm_tt3y<13, 2>",
     "edge_logits_fwd": "sv2n::k_edge_fwd<8, 8, false>",
     "edge_logits_bwd": "sv2n::k_edge_bwd<8, 8, false>",
     "gat_attn_fwd_l0": "sv2n::canon::k_fwd<1, true, false>",
