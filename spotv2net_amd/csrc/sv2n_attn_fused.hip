@@ -723,11 +723,13 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
   constexpr int DQ = (D + 3) / 4;
   const int qtr = t & 3, d0 = qtr * DQ;
   const float* sWq = sW + qtr * D * MH;
-  float wacc[DQ][MH];
+  // dW̃ accumulators as (head 2p, head 2p+1) pairs: packed FMAs (the kernel
+  // is VALU-issue-bound)
+  f2 wacc[DQ][MH / 2];
 #pragma unroll
   for (int d = 0; d < DQ; ++d)
 #pragma unroll
-    for (int h = 0; h < MH; ++h) wacc[d][h] = 0.f;
+    for (int h2 = 0; h2 < MH / 2; ++h2) wacc[d][h2] = f2{0.f, 0.f};
   f4 dacc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
   float das[2] = {0.f, 0.f};
 
@@ -799,15 +801,20 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
       float lf[MH];
 #pragma unroll
       for (int h = 0; h < MH; ++h) lf[h] = 0.f;
+      f2 lf2[MH / 2] = {f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}};
 #pragma unroll
       for (int dd = 0; dd < DQ; ++dd) {
         const float* wr = sWq + min(d0 + dd, D - 1) * MH;
         const f4 wa = *reinterpret_cast<const f4*>(wr);
         const f4 wb = *reinterpret_cast<const f4*>(wr + 4);
-        const float wv[MH] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-        for (int h = 0; h < MH; ++h) lf[h] = fmaf(evc[k][dd], wv[h], lf[h]);
+        const f2 e2 = f2{evc[k][dd], evc[k][dd]};
+        lf2[0] = __builtin_elementwise_fma(e2, f2{wa.x, wa.y}, lf2[0]);
+        lf2[1] = __builtin_elementwise_fma(e2, f2{wa.z, wa.w}, lf2[1]);
+        lf2[2] = __builtin_elementwise_fma(e2, f2{wb.x, wb.y}, lf2[2]);
+        lf2[3] = __builtin_elementwise_fma(e2, f2{wb.z, wb.w}, lf2[3]);
       }
+#pragma unroll
+      for (int h = 0; h < MH; ++h) lf[h] = lf2[h >> 1][h & 1];
       // quad reduce-scatter: partner q^1's position p^1 holds this lane's
       // head p^q, then partner q^2's s1[i^1] holds s1[i]'s head; lane q ends
       // with heads q (position 0) and q + 4 (position 4)
@@ -929,10 +936,11 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
       slot(k, i0, il, jl);
       const float* dr = sD + il * RS + jl;
 #pragma unroll
-      for (int h = 0; h < MH; ++h) {
-        const float dlw = dr[h * BHS];
+      for (int h2 = 0; h2 < MH / 2; ++h2) {
+        const f2 dlw = f2{dr[(2 * h2) * BHS], dr[(2 * h2 + 1) * BHS]};
 #pragma unroll
-        for (int d = 0; d < DQ; ++d) wacc[d][h] = fmaf(evc[k][d], dlw, wacc[d][h]);
+        for (int d = 0; d < DQ; ++d)
+          wacc[d][h2] = __builtin_elementwise_fma(f2{evc[k][d], evc[k][d]}, dlw, wacc[d][h2]);
       }
     }
   }
@@ -978,7 +986,7 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
   for (int d = 0; d < DQ; ++d)
 #pragma unroll
     for (int h = 0; h < MH; ++h) {
-      float v = wacc[d][h];
+      float v = wacc[d][h >> 1][h & 1];
       v += dppf<0x124>(v);
       v += dppf<0x128>(v);
       if (li < 4 && d0 + d < D) sRed[(hh * 4 + lk) * (D * MH) + (d0 + d) * MH + h] = v;
