@@ -532,9 +532,7 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
     float* out = p.splitk > 1 ? slabs : T;
     launch_wgrad_bf16(p, stream, x, ld_x, dxs, ldx, F, num_nodes, out);
     if (p.splitk > 1) {
-      const int64_t tot = (int64_t)F * ldx;
-      hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
-                         stream, slabs, p.splitk, (int64_t)F, (int64_t)ldx, T, (int64_t)ldx);
+      splitk_reduce(stream, slabs, p.splitk, (int64_t)F, (int64_t)ldx, T, (int64_t)ldx);
     }
   } else if (weights) {
     // T[f][o] = Σ_k x[k][f] · dxs[k][o]   (both operands k-strided)
@@ -544,9 +542,7 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
     float* out = p.splitk > 1 ? slabs : T;
     launch_wgrad_slabs(p, stream, x, ld_x, dxs, ldx, F, ldx, num_nodes, avec, bvec, out);
     if (p.splitk > 1) {
-      const int64_t tot = (int64_t)F * ldx;
-      hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
-                         stream, slabs, p.splitk, (int64_t)F, (int64_t)ldx, T, (int64_t)ldx);
+      splitk_reduce(stream, slabs, p.splitk, (int64_t)F, (int64_t)ldx, T, (int64_t)ldx);
     }
   }
   const int nft = (F + WG_FT - 1) / WG_FT, not_ = (HC + WG_OT - 1) / WG_OT;
