@@ -184,13 +184,14 @@ def test_head_backward_repeatable(dev):
 
 
 @pytest.mark.parametrize("F,H,C,nodes", [(1260, 4, 100, 15360), (70, 3, 21, 300),
-                                         (300, 4, 48, 3000)])
+                                         (300, 4, 48, 3000), (40, 3, 5, 120), (16, 2, 1, 60)])
 def test_fused_wgrad_matches_gemm_and_fold(dev, F, H, C, nodes):
     """sv2n_gat_wgrad_node (split-K GEMM + fused epilogue) against the
     unfused sv2n_gemm_f32 + sv2n_gat_prep_bwd_node path it replaces; two
     accumulating calls, then a bias-only call.  Shapes: the C2 layer 0
     (k_gemm_tt3y, 208-column tiles), a ragged one on the same kernel (F 300:
-    a partial row block; 200 columns), and one on the f32 kernel."""
+    a partial row block; 200 columns), one on the f32 kernel, and narrow heads
+    (C 5, C 1)."""
     from spotv2net_amd import _lib
     from spotv2net_amd.ops import gemm_f32
     lib = _lib.load()
