@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 6
+#define SV2N_ABI_VERSION 7
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -282,6 +282,19 @@ int sv2n_gat_prep_bwd_edge(const float* dwfold, int hl_pad, int col0,
                            const float* W_edge, const float* att_edge, int heads,
                            int channels, int edge_dim, float* gW_edge,
                            float* g_att_edge, hipStream_t stream);
+
+/* sv2n_gat_prep_bwd_edge for every layer in ONE launch (ABI 7; the layers'
+ * gradient buffers are disjoint, each result as the per-layer call's). */
+typedef struct sv2n_edge_grad_layer {
+  const float* W_edge;    /* lin_edge.weight [H*C][edge_dim] */
+  const float* att_edge;  /* [H*C] */
+  float* gW_edge;         /* [H*C][edge_dim] or NULL */
+  float* g_att_edge;      /* [H*C] or NULL */
+  int heads, channels, col0;
+} sv2n_edge_grad_layer;
+int sv2n_gat_prep_bwd_edge_all(const float* dwfold, int hl_pad, int edge_dim,
+                               const sv2n_edge_grad_layer* layers, int num_layers,
+                               hipStream_t stream);
 
 /* torch.optim.Adam step (amsgrad=False) over flat buffers of n floats
  * (16-B aligned); *step is the already-incremented device step count. */

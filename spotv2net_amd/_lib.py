@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SV2N_LIB: an alternative build of the same library (diagnostic builds, e.g.
 # tools/stamps.py); default the in-tree one
 LIB_PATH = os.environ.get("SV2N_LIB") or os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p
@@ -33,6 +33,14 @@ class PrepLayer(ctypes.Structure):
         ("W_edge", _p), ("att_edge", _p),
         ("edge_dim", _i32), ("hl_pad", _i32), ("col0", _i32),
         ("wfold", _p), ("nplanes", _i32),
+    ]
+
+
+class EdgeGradLayer(ctypes.Structure):
+    """sv2n_edge_grad_layer (include/sv2n.h)."""
+    _fields_ = [
+        ("W_edge", _p), ("att_edge", _p), ("gW_edge", _p), ("g_att_edge", _p),
+        ("heads", _i32), ("channels", _i32), ("col0", _i32),
     ]
 
 
@@ -87,6 +95,7 @@ _SIGNATURES = {
     "sv2n_gat_prep_bwd_node": (_i32, [_p, _i32, _p, _p, _p, _i32, _i32, _i32, _p, _i32, _i32, _p,
                                       _p, _p, _p, _p, _i64, _p]),
     "sv2n_gat_prep_bwd_edge": (_i32, [_p, _i32, _i32, _p, _p, _i32, _i32, _i32, _p, _p, _p]),
+    "sv2n_gat_prep_bwd_edge_all": (_i32, [_p, _i32, _i32, _p, _i32, _p]),
     "sv2n_adam_f32": (_i32, [_p, _p, _p, _p, _i64, _p, _f32, _f32, _f32, _f32, _f32, _p]),
     "sv2n_adam_f32_step": (_i32, [_p, _p, _p, _p, _i64, _p, _p, _f32, _f32, _f32, _f32, _f32,
                                   _p]),

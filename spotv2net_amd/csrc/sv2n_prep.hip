@@ -14,6 +14,7 @@
 //   gW_e[hC+c][d] += dwfold[d][col0+h] · att_edge[h,c]
 //   g_att_edge[h,c] += Σ_d W_e[hC+c][d] · dwfold[d][col0+h]
 //   g_bias[o]     += Σ_g dbias_partial[g][o]
+#include <algorithm>
 #include "sv2n_common.h"
 #include "sv2n_gemm3_kernel.h"
 
@@ -165,6 +166,30 @@ __global__ __launch_bounds__(256) void k_prep_bwd_edge(const float* __restrict__
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) a += __shfl_xor(a, m, 64);
   if (lane == 0 && g_att_e) g_att_e[o] += a;
+}
+
+// every layer in one launch: blockIdx.y = layer (same body, same order)
+struct PrepBwdEdgeArgs {
+  sv2n_edge_grad_layer l[SV2N_MAX_LAYERS];
+};
+__global__ __launch_bounds__(256) void k_prep_bwd_edge_all(const float* __restrict__ dwfold,
+                                                           int hlp, int D, const PrepBwdEdgeArgs args) {
+  const sv2n_edge_grad_layer& P = args.l[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int C = P.channels;
+  if (o >= P.heads * C) return;
+  const int h = o / C;
+  const float ae = P.att_edge[o];
+  float a = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float g = dwfold[(int64_t)d * hlp + P.col0 + h];
+    a = fmaf(P.W_edge[(int64_t)o * D + d], g, a);
+    if (P.gW_edge) P.gW_edge[(int64_t)o * D + d] += g * ae;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) a += __shfl_xor(a, m, 64);
+  if (lane == 0 && P.g_att_edge) P.g_att_edge[o] += a;
 }
 
 // g[o] += Σ_b part[b][o] (fixed order): block = 16 columns x 16 row groups
@@ -435,6 +460,25 @@ extern "C" int sv2n_gat_prep_bwd_edge(const float* dwfold, int hl_pad, int col0,
   const int HC = heads * channels;
   hipLaunchKernelGGL(k_prep_bwd_edge, dim3((HC + 3) / 4), dim3(256), 0, stream, dwfold, hl_pad,
                      col0, W_edge, att_edge, heads, channels, edge_dim, gW_edge, g_att_edge);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_gat_prep_bwd_edge_all(const float* dwfold, int hl_pad, int edge_dim,
+                                          const sv2n_edge_grad_layer* layers, int num_layers,
+                                          hipStream_t stream) {
+  if (!dwfold || !layers || edge_dim < 1 || num_layers < 1 || num_layers > SV2N_MAX_LAYERS)
+    return SV2N_ERR_ARG;
+  PrepBwdEdgeArgs a{};
+  int maxhc = 0;
+  for (int l = 0; l < num_layers; ++l) {
+    const sv2n_edge_grad_layer& P = layers[l];
+    if (!P.W_edge || !P.att_edge || P.heads < 1 || P.channels < 1) return SV2N_ERR_ARG;
+    if (P.col0 < 0 || P.col0 + P.heads > hl_pad) return SV2N_ERR_SHAPE;
+    a.l[l] = P;
+    maxhc = std::max(maxhc, P.heads * P.channels);
+  }
+  hipLaunchKernelGGL(k_prep_bwd_edge_all, dim3((unsigned)((maxhc + 3) / 4), (unsigned)num_layers),
+                     dim3(256), 0, stream, dwfold, hl_pad, edge_dim, a);
   return (int)hipGetLastError();
 }
 

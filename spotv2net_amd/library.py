@@ -65,6 +65,9 @@ _SCHEMAS = {
                        "int heads, int num_graphs, int n, int hl_pad, bool planes) -> Tensor",
     "prep_bwd_edge": "(Tensor dwfold, int col0, Tensor W_edge, Tensor att_edge, int heads, "
                      "int channels, Tensor(a!)? gW_edge, Tensor(b!)? g_att_edge) -> ()",
+    "prep_bwd_edge_all": "(Tensor dwfold, int[] col0, Tensor[] W_edge, Tensor[] att_edge, "
+                         "int[] heads, int[] channels, Tensor(a!)[] gW_edge, "
+                         "Tensor(b!)[] g_att_edge) -> ()",
     "head_fwd": "(Tensor x, Tensor weight, Tensor? bias) -> Tensor",
     "head_bwd": "(Tensor x, Tensor weight, Tensor dout, Tensor(a!)? g_weight, "
                 "Tensor(b!)? g_bias) -> Tensor",
@@ -290,6 +293,26 @@ def _prep_bwd_edge(dwfold, col0, W_edge, att_edge, heads, channels, gW_edge, g_a
 
 @_fake("prep_bwd_edge")
 def _prep_bwd_edge_fake(dwfold, col0, W_edge, att_edge, heads, channels, gW_edge, g_att_edge):
+    return None
+
+
+@_impl("prep_bwd_edge_all")
+def _prep_bwd_edge_all(dwfold, col0, W_edge, att_edge, heads, channels, gW_edge, g_att_edge):
+    """prep_bwd_edge of every layer in one launch (sv2n_gat_prep_bwd_edge_all)."""
+    lib = _lib.load()
+    L = len(W_edge)
+    arr = (_lib.EdgeGradLayer * L)()
+    for l in range(L):
+        arr[l] = _lib.EdgeGradLayer(W_edge[l].data_ptr(), att_edge[l].data_ptr(),
+                                    gW_edge[l].data_ptr(), g_att_edge[l].data_ptr(), heads[l],
+                                    channels[l], col0[l])
+    _lib.check(lib.sv2n_gat_prep_bwd_edge_all(dwfold.data_ptr(), dwfold.shape[1],
+                                              W_edge[0].shape[1], arr, L, _st(dwfold)),
+               "sv2n_gat_prep_bwd_edge_all")
+
+
+@_fake("prep_bwd_edge_all")
+def _prep_bwd_edge_all_fake(dwfold, col0, W_edge, att_edge, heads, channels, gW_edge, g_att_edge):
     return None
 
 

@@ -391,10 +391,18 @@ class _GATStack(torch.autograd.Function):
                 if not fused:
                     dwf = ops.edge_logits_bwd(ea, ei, layout.canon, daes, H, B, n, hp,
                                               layout.tiled)
-                for l, c in enumerate(convs):
-                    gWe, gae = need_e[l]
-                    ops.prep_bwd_edge(dwf, l * H, c.lin_edge.weight, c.att_edge, c.heads,
-                                      c.out_channels, gWe, gae)
+                if all(a is not None and b is not None for a, b in need_e):
+                    # every layer's edge-fold backward in one launch
+                    ops.prep_bwd_edge_all(dwf, [l * H for l in range(L)],
+                                          [c.lin_edge.weight for c in convs],
+                                          [c.att_edge for c in convs], [c.heads for c in convs],
+                                          [c.out_channels for c in convs],
+                                          [a for a, _ in need_e], [b for _, b in need_e])
+                else:
+                    for l, c in enumerate(convs):
+                        gWe, gae = need_e[l]
+                        ops.prep_bwd_edge(dwf, l * H, c.lin_edge.weight, c.att_edge, c.heads,
+                                          c.out_channels, gWe, gae)
         dx0 = dy if need_x0 else None
         return (dx0, None, None, None, None, None, None, None) + grad_of.returned()
 

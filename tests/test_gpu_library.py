@@ -150,3 +150,27 @@ def test_invalid_edges_poison_then_raise(dev):
     with pytest.raises(UnsupportedLayout):
         check_pending(block=True)
     check_pending(block=True)  # reported once
+
+
+def test_prep_bwd_edge_all_matches_per_layer(dev):
+    """sv2n_gat_prep_bwd_edge_all (every layer's edge-fold backward in one
+    launch) == sv2n_gat_prep_bwd_edge per layer, bit for bit (C2's two layers
+    on one [126][8] fold gradient); opcheck of the op."""
+    ops = torch.ops.sv2n
+    g = torch.Generator(device="cpu").manual_seed(7)
+    D, hp = 126, 8
+    layers = [(4, 100), (4, 50)]
+    dwf = torch.randn(D, hp, generator=g).to(dev)
+    We = [torch.randn(H * C, D, generator=g).to(dev) for H, C in layers]
+    ae = [torch.randn(H * C, generator=g).to(dev) for H, C in layers]
+    gw1 = [torch.randn(H * C, D, generator=g).to(dev) for H, C in layers]
+    ga1 = [torch.randn(H * C, generator=g).to(dev) for H, C in layers]
+    gw2, ga2 = [t.clone() for t in gw1], [t.clone() for t in ga1]
+    for l, (H, C) in enumerate(layers):
+        ops.prep_bwd_edge(dwf, 4 * l, We[l], ae[l], H, C, gw1[l], ga1[l])
+    ops.prep_bwd_edge_all(dwf, [0, 4], We, ae, [4, 4], [100, 50], gw2, ga2)
+    for a, b in zip(gw1 + ga1, gw2 + ga2):
+        assert torch.equal(a, b)
+    torch.library.opcheck(ops.prep_bwd_edge_all,
+                          (dwf, [0, 4], We, ae, [4, 4], [100, 50], [t.clone() for t in gw2],
+                           [t.clone() for t in ga2]), test_utils=UTILS)
