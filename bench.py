@@ -174,11 +174,9 @@ def kernel_table(model, data, reps=50):
     rows = {
         "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * N0c * K0,
                         4.0 * (M0 * K0 + N0c * K0 + M0 * N0c), BF16X3_PEAK_TFLOPS),
-        # bf16x3 weight-gradient kernel (k_gemm_tt3w) unless SV2N_WGRAD3=0
+        # bf16x3 weight-gradient kernel (k_gemm_tt3y)
         "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * N0c * K0,
-                        4.0 * (M0 * K0 + M0 * N0c + N0c * K0),
-                        F32_MFMA_PEAK_TFLOPS if os.environ.get("SV2N_WGRAD3", "1") == "0"
-                        else BF16X3_PEAK_TFLOPS),
+                        4.0 * (M0 * K0 + M0 * N0c + N0c * K0), BF16X3_PEAK_TFLOPS),
         "edge_logits_fwd": (edge_fwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS),
                             None),
         "edge_logits_bwd": (edge_bwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS),
@@ -282,8 +280,7 @@ def kernel_table_tiled(model, data, cfg, reps=10):
         "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * Nc * K0, 4.0 * (M0 * K0 + Nc * K0 + M0 * Nc),
                         BF16X3_PEAK_TFLOPS),
         "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * Nd * K0, 4.0 * (M0 * K0 + M0 * Nd + Nd * K0),
-                        F32_MFMA_PEAK_TFLOPS if os.environ.get("SV2N_WGRAD3", "1") == "0"
-                        else BF16X3_PEAK_TFLOPS),
+                        BF16X3_PEAK_TFLOPS),
     }
     res = {}
     for name, (fn, bound, flops, nbytes, peak) in rows.items():
@@ -440,8 +437,9 @@ def step_roofline(cfg, train_gps: float, fwd_gps: float, dtype: str) -> dict:
 
 def reference_loop_rate(dev, cfg, data, args, world) -> float:
     """5_train_SpotV2Net.py:142-160 as written, eager: a NEW batch object with
-    a new edge_index every step (as PyG's DataLoader yields; layout analysed
-    without a host sync), model(data), nn.MSELoss, zero_grad, backward,
+    a new edge_index every step (as sv2n ``collate`` or PyG's DataLoader
+    yields, with the graph size known: layout analysed without a host sync),
+    model(data), nn.MSELoss, zero_grad, backward,
     torch.optim.Adam(fused) step and the per-step loss.item() sync.  Inputs
     stay device-resident (the DataLoader's CPU collation and H2D copy are
     not on the GPU path)."""
@@ -452,7 +450,7 @@ def reference_loop_rate(dev, cfg, data, args, world) -> float:
 
     def step():
         b = Batch(x=data.x, edge_index=data.edge_index.clone(), edge_attr=data.edge_attr,
-                  y_x=data.y_x, batch=data.batch, ptr=data.ptr)
+                  y_x=data.y_x, batch=data.batch, ptr=data.ptr, nodes_per_graph=cfg["n"])
         loss = crit(model(b), b.y_x)
         opt.zero_grad()
         loss.backward()
@@ -534,7 +532,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from spotv2net_amd import synthetic_batch
-    from spotv2net_amd.train import ForwardStep, TrainStep
+    from spotv2net_amd.train import ForwardStep, TrainStep, broadcast_params_
 
     cfg = CONFIGS[args.config]
     if args.batch is None:
@@ -543,8 +541,7 @@ def main():
         return main_c3(args, dev, cfg)
     model = build_model(dev, cfg).set_precision(args.precision)
     if world > 1:  # identical replicas: broadcast rank 0's weights
-        for p in model.parameters():
-            dist.broadcast(p.data, 0)
+        broadcast_params_(model, 0)
     data = synthetic_batch(args.batch, cfg["S"], n=cfg["n"], seed=1234 + rank, device=dev)
 
     step = TrainStep(model, data, lr=1e-3, use_graph=not args.no_graph)

@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 7
+#define SV2N_ABI_VERSION 8
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -471,9 +471,11 @@ int sv2n_block_rowmask_checked(const int64_t* edge_index, int64_t num_edges, int
  *             [0*S+t] upper-triangle volvol[t][min][max], [1*S+t] volvol[t][s][s],
  *             [2*S+t] volvol[t][g][g]
  *   y         [B*n*F]         y[(b*n+v)*F+k] = vol[starts[b]+S+k][v][v]
- * vol / volvol: [T][n][n] fp32 series; the caller guarantees
- * starts[b] + S + F - 1 < T. */
-int sv2n_window_gather(const float* vol, const float* volvol, int n, const int64_t* starts,
+ * vol / volvol: [T][n][n] fp32 series, T = num_matrices.  A window outside
+ * the series (starts[b] < 0 or starts[b] + S + F > T) reads nothing and its
+ * x / edge_attr / y rows are written as NaN (ABI 8). */
+int sv2n_window_gather(const float* vol, const float* volvol, int n, int64_t num_matrices,
+                       const int64_t* starts,
                        int64_t num_windows, int seq_length, int future_steps,
                        const uint16_t* canon, float* x, float* edge_attr, float* y,
                        hipStream_t stream);

@@ -586,13 +586,8 @@ using namespace sv2n;
 
 static constexpr int EDGE_BWD_GRID = 768;
 static constexpr int EDGE_FWD_GRID = 1024;
-// SV2N_EDGE_FWD_GRID / SV2N_EDGE_BWD_GRID: workgroup-count overrides for
-// tuning sweeps (the backward's is capped at EDGE_BWD_GRID: workspace size)
-static int edge_grid_env(const char* name, int dflt, int cap) {
-  const char* e = getenv(name);
-  const int v = e ? atoi(e) : 0;
-  return v > 0 ? std::min(v, cap) : dflt;
-}
+// persistent workgroup counts (MI355X sweeps: 512-6960 forward, 256-768
+// backward within noise of these; the backward's bounds its workspace)
 static constexpr int EDGE_SMALL_FWD_GRID = 4096;
 static constexpr int EDGE_SMALL_BWD_GRID = 1024;
 
@@ -708,7 +703,7 @@ static int edge_fwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
                                           wfold, hl_pad, lp, num_layers, heads, num_graphs, n,
                                           stream);
   const int64_t nchunks = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
-  static const int fwd_grid = edge_grid_env("SV2N_EDGE_FWD_GRID", EDGE_FWD_GRID, 1 << 20);
+  constexpr int fwd_grid = EDGE_FWD_GRID;
   const unsigned grid = (unsigned)std::min<int64_t>(nchunks, fwd_grid);
   const int rf = (EDGE_CHUNK * edge_dim / 4 + EDGE_THREADS - 1) / EDGE_THREADS;
   if (rf > EDGE_RF_MAX) return SV2N_ERR_SHAPE;
@@ -784,7 +779,7 @@ static int edge_bwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
                                           lp, num_layers, heads, num_graphs, n, workspace,
                                           workspace_floats, dwfold, hl_pad, stream);
   const int64_t nchunks = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
-  static const int bwd_grid = edge_grid_env("SV2N_EDGE_BWD_GRID", EDGE_BWD_GRID, EDGE_BWD_GRID);
+  constexpr int bwd_grid = EDGE_BWD_GRID;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(bwd_grid, nchunks));
   if (workspace_floats < (int64_t)grid * O) return SV2N_ERR_WORKSPACE;
   const int rf = (EDGE_CHUNK * edge_dim / 4 + EDGE_THREADS - 1) / EDGE_THREADS;

@@ -27,16 +27,6 @@ struct GemmPlan {
   int64_t kslice;
 };
 
-// f32 weight gradient on the bf16x3 kernel k_gemm_tt3w (SV2N_WGRAD3=0: the
-// exact-f32 MFMA kernel)
-static bool wgrad3_on() {
-  static const bool on = [] {
-    const char* e = getenv("SV2N_WGRAD3");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t K) {
   constexpr int BM = 128;
   GemmPlan p{};
@@ -46,10 +36,7 @@ static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + bn - 1) / bn);
   int64_t sk = 1;
   if (tiles < 240 && K >= 2048) {
-    static const int64_t target = [] {  // tuning override: workgroups aimed at
-      const char* e = getenv("SV2N_SPLITK_TARGET");
-      return e ? (int64_t)atoll(e) : (int64_t)480;
-    }();
+    constexpr int64_t target = 480;  // workgroups aimed at
     sk = std::min<int64_t>(32, (target + tiles - 1) / tiles);
     sk = std::min<int64_t>(sk, std::max<int64_t>(1, K / 256));
   }
@@ -255,15 +242,6 @@ extern "C" int sv2n_gemm_f32(int a_kmajor, int b_kmajor, const float* A, int64_t
   return (int)hipGetLastError();
 }
 
-// rows-tiles per wave of k_gemm_tt3w (SV2N_WGRAD3_MT = 1 / 2 forces; 0 auto)
-static int wgrad3_mt() {
-  static const int v = [] {
-    const char* e = getenv("SV2N_WGRAD3_MT");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 // How the slab GEMM of a weight gradient runs.  kind 0: exact-f32 kernel
 // (k_gemm_f32, XR slices); kind 1 / 2: bf16x3 k_gemm_tt3w<13, kind>.  For the
 // 208-column tiling the split count follows the bf16x3 kernel's rule — one
@@ -279,7 +257,7 @@ struct SlabPlan {
 static SlabPlan slab_plan(int64_t F, int64_t N, int64_t K, bool vec, int64_t lda, int64_t ldb) {
   const GemmPlan p = plan_gemm(F, N, K);
   SlabPlan sp{0, p.nt, p.splitk, p.kslice};
-  if (!(wgrad3_on() && p.splitk > 1)) return sp;
+  if (p.splitk <= 1) return sp;
   // column tiles of 208 (C2: N = 408, 208) or 144 (C5: N = 144), at most 25 % padding
   int bn = 0;
   for (const int w : {208, 144})
@@ -289,8 +267,7 @@ static SlabPlan slab_plan(int64_t F, int64_t N, int64_t K, bool vec, int64_t lda
     }
   if (bn == 0) return sp;
   const int64_t ntile = (N + bn - 1) / bn;
-  int mt = wgrad3_mt();
-  if (mt != 1 && mt != 2) mt = ((F + 255) / 256) * ntile >= 8 ? 2 : 1;
+  const int mt = ((F + 255) / 256) * ntile >= 8 ? 2 : 1;  // row tiles per wave
   const int64_t tiles = ((F + 128 * mt - 1) / (128 * mt)) * ntile;
   int64_t sk = 8 * std::max<int64_t>(1, 256 / (8 * tiles));
   sk = std::min<int64_t>(sk, std::min<int64_t>(256, std::max<int64_t>(8, K / 256 / 8 * 8)));
@@ -303,16 +280,6 @@ static SlabPlan slab_plan(int64_t F, int64_t N, int64_t K, bool vec, int64_t lda
   return sp;
 }
 
-// SV2N_WGRAD3Y=0: k_gemm_tt3w (staging between two barriers) instead of
-// k_gemm_tt3y (staging under the MFMAs)
-static bool wgrad3y_on() {
-  static const bool on = [] {
-    const char* e = getenv("SV2N_WGRAD3Y");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 template <int NT, int MT>
 static void launch_tt3w(const SlabPlan& p, hipStream_t stream, const float* x, int64_t ld_x,
                         const float* dxs, int64_t ldx, int64_t F, int64_t N, int64_t K,
@@ -322,19 +289,17 @@ static void launch_tt3w(const SlabPlan& p, hipStream_t stream, const float* x, i
   // tt3y where it measured faster: the 208-column tilings (C2 L0 dWᵀ 92.9 ->
   // 91.0 us, step 0.5476 -> 0.5424 ms); C5's 144-column one: 524 vs 530 us
   if constexpr (NT == 13 && CfgY::LDS <= 160 * 1024) {
-    if (wgrad3y_on()) {
-      static bool attr_y = [] {
-        (void)hipFuncSetAttribute((const void*)k_gemm_tt3y<NT, MT>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)CfgY::LDS);
-        return true;
-      }();
-      (void)attr_y;
-      const dim3 gy((unsigned)((F + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN),
-                    (unsigned)((p.splitk + 7) / 8 * 8));
-      hipLaunchKernelGGL((k_gemm_tt3y<NT, MT>), gy, dim3(Cfg::THREADS), CfgY::LDS, stream, x,
-                         ld_x, dxs, ldx, out, F, N, K, p.kslice, p.splitk);
-      return;
-    }
+    static bool attr_y = [] {
+      (void)hipFuncSetAttribute((const void*)k_gemm_tt3y<NT, MT>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)CfgY::LDS);
+      return true;
+    }();
+    (void)attr_y;
+    const dim3 gy((unsigned)((F + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN),
+                  (unsigned)((p.splitk + 7) / 8 * 8));
+    hipLaunchKernelGGL((k_gemm_tt3y<NT, MT>), gy, dim3(Cfg::THREADS), CfgY::LDS, stream, x,
+                       ld_x, dxs, ldx, out, F, N, K, p.kslice, p.splitk);
+    return;
   }
   static bool attr = [] {
     (void)hipFuncSetAttribute((const void*)k_gemm_tt3w<NT, MT>,

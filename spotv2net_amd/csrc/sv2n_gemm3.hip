@@ -39,15 +39,6 @@ __global__ void k_split3_t(const float* __restrict__ x, int64_t rows, int64_t K,
   }
 }
 
-// SV2N_GEMM3_PIPE=0: the compiler-scheduled fragment reads (A/B switch)
-static bool gemm3_pipe() {
-  static const bool on = [] {
-    const char* e = getenv("SV2N_GEMM3_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 template <int NW, int MT, int NT, int BK, int PIPE>
 static int launch_gemm3_p(hipStream_t st, const float* A, int64_t lda, const unsigned short* Bp,
                           int64_t Kp, int64_t N, float* C, int64_t ldc, int64_t M, int64_t K) {
@@ -63,20 +54,11 @@ static int launch_gemm3_p(hipStream_t st, const float* A, int64_t lda, const uns
   return (int)hipGetLastError();
 }
 
+// the LDS-staged kernel: shapes k_gemm3d does not take (K % 4 != 0)
 template <int NW, int MT, int NT, int BK>
 static int launch_gemm3(hipStream_t st, const float* A, int64_t lda, const unsigned short* Bp,
                         int64_t Kp, int64_t N, float* C, int64_t ldc, int64_t M, int64_t K) {
-  return gemm3_pipe() ? launch_gemm3_p<NW, MT, NT, BK, 1>(st, A, lda, Bp, Kp, N, C, ldc, M, K)
-                      : launch_gemm3_p<NW, MT, NT, BK, 0>(st, A, lda, Bp, Kp, N, C, ldc, M, K);
-}
-
-// SV2N_GEMM3D=0: the LDS-staged kernel for every shape (A/B switch)
-static bool gemm3d_on() {
-  static const bool on = [] {
-    const char* e = getenv("SV2N_GEMM3D");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  return launch_gemm3_p<NW, MT, NT, BK, 1>(st, A, lda, Bp, Kp, N, C, ldc, M, K);
 }
 
 // k_gemm3d: A straight to registers, B planes double-buffered, the next
@@ -169,7 +151,7 @@ extern "C" int sv2n_gemm_f32x3(const float* A, int64_t lda, const uint16_t* Bp, 
   const bool longk = K > 256;
   // 144-column tiles when they pad N less than 208-column ones (C5: N = 144)
   const bool t144 = (N + 143) / 144 * 144 < (N + 207) / 208 * 208 && mb * ((N + 143) / 144) >= 240;
-  if (gemm3d_on() && K % 4 == 0) {
+  if (K % 4 == 0) {
     if (t144) return launch_gemm3d<8, 1, 9, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
     if (wide) return launch_gemm3d<8, 1, 13, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
     return launch_gemm3d<8, 1, 7, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);

@@ -14,16 +14,20 @@
 // Every output element is written once, coalesced; the reads are gathers from
 // the window's S matrices (L2 / Infinity-Cache resident across the threads of
 // a window).  HBM-bound by the writes: B*(n*n*S + 3*E0*S + n*F)*4 bytes.
+// A window whose matrices fall outside the series (starts[b] < 0 or
+// starts[b] + S + F > T) reads nothing and is written as NaN (a device-side
+// error that needs no host round trip; the op stays capturable).
 #include "sv2n_common.h"
 
 namespace sv2n {
 
 __global__ __launch_bounds__(256) void k_window_gather(
-    const float* __restrict__ vol, const float* __restrict__ volvol, int n,
+    const float* __restrict__ vol, const float* __restrict__ volvol, int n, int64_t T,
     const int64_t* __restrict__ starts, int64_t B, int S, int F,
     const uint16_t* __restrict__ canon, float* __restrict__ x, float* __restrict__ ea,
     float* __restrict__ y) {
   const int64_t nn = (int64_t)n * n;
+  const float qnan = __builtin_nanf("");
   const int E0 = n * (n - 1);
   const int64_t nx = B * nn * S, ne = B * (int64_t)E0 * 3 * S, ny = B * (int64_t)n * F;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -35,7 +39,8 @@ __global__ __launch_bounds__(256) void k_window_gather(
       const int64_t b = row / n;
       const int v = (int)(row - b * n);
       const int c = j / S, t = j - c * S;
-      x[i] = vol[(starts[b] + t) * nn + v * n + c];
+      const int64_t st = starts[b];
+      x[i] = (st >= 0 && st + S + F <= T) ? vol[(st + t) * nn + v * n + c] : qnan;
     } else if (i < nx + ne) {
       const int64_t k0 = i - nx;
       const int64_t row = k0 / (3 * S);
@@ -52,14 +57,16 @@ __global__ __launch_bounds__(256) void k_window_gather(
       } else {
         r = c = (kind == 1) ? s : g;
       }
-      ea[k0] = volvol[(starts[b] + t) * nn + r * n + c];
+      const int64_t st = starts[b];
+      ea[k0] = (st >= 0 && st + S + F <= T) ? volvol[(st + t) * nn + r * n + c] : qnan;
     } else {
       const int64_t k0 = i - nx - ne;
       const int64_t row = k0 / F;
       const int k = (int)(k0 - row * F);
       const int64_t b = row / n;
       const int v = (int)(row - b * n);
-      y[k0] = vol[(starts[b] + S + k) * nn + v * n + v];
+      const int64_t st = starts[b];
+      y[k0] = (st >= 0 && st + S + F <= T) ? vol[(st + S + k) * nn + v * n + v] : qnan;
     }
   }
 }
@@ -73,7 +80,7 @@ __global__ __launch_bounds__(256) void k_window_gather(
 //   y[(b*n+u)*F .. +F)
 // 3 * S * (n+1) floats of LDS.
 __global__ __launch_bounds__(256) void k_window_rows(
-    const float* __restrict__ vol, const float* __restrict__ volvol, int n,
+    const float* __restrict__ vol, const float* __restrict__ volvol, int n, int64_t T,
     const int64_t* __restrict__ starts, int S, int F, float* __restrict__ x,
     float* __restrict__ ea, float* __restrict__ y) {
   extern __shared__ float lds[];
@@ -87,6 +94,17 @@ __global__ __launch_bounds__(256) void k_window_rows(
   const int64_t nn = (int64_t)n * n;
   const int64_t st = starts[b];
   const int E0 = n * (n - 1), P = E0 / 2;
+  if (st < 0 || st + S + F > T) {  // window outside the series: NaN rows, no reads
+    const float qnan = __builtin_nanf("");
+    if (t < F) y[(b * n + u) * F + t] = qnan;
+    float* xr = x + (b * n + u) * (int64_t)n * S;
+    for (int j = t; j < n * S; j += 256) xr[j] = qnan;
+    const int m = n - 1 - u, e0 = u * (2 * n - u - 1) / 2, RW = 3 * S;
+    float* up = ea + (b * E0 + e0) * (int64_t)RW;
+    float* lo = ea + (b * E0 + P + e0) * (int64_t)RW;
+    for (int j = t; j < m * RW; j += 256) up[j] = lo[j] = qnan;
+    return;
+  }
   for (int k = t; k < S * n; k += 256) {
     const int tt = k / n, v = k - tt * n;
     const int64_t base = (st + tt) * nn;
@@ -126,11 +144,12 @@ __global__ __launch_bounds__(256) void k_window_rows(
 using namespace sv2n;
 
 extern "C" int sv2n_window_gather(const float* vol, const float* volvol, int n,
-                                  const int64_t* starts, int64_t num_windows, int seq_length,
+                                  int64_t num_matrices, const int64_t* starts, int64_t num_windows, int seq_length,
                                   int future_steps, const uint16_t* canon, float* x,
                                   float* edge_attr, float* y, hipStream_t stream) {
   if (!vol || !volvol || !starts || !canon || !x || !edge_attr || !y) return SV2N_ERR_ARG;
-  if (n < 2 || n > SV2N_MAX_N_TILED || num_windows < 1 || seq_length < 1 || future_steps < 1)
+  if (n < 2 || n > SV2N_MAX_N_TILED || num_windows < 1 || seq_length < 1 || future_steps < 1 ||
+      num_matrices < 1)
     return SV2N_ERR_SHAPE;
   const int64_t total = num_windows * ((int64_t)n * n * seq_length +
                                        (int64_t)n * (n - 1) * 3 * seq_length +
@@ -138,11 +157,11 @@ extern "C" int sv2n_window_gather(const float* vol, const float* volvol, int n,
   const size_t lds = sizeof(float) * 3 * (size_t)seq_length * (n + 1);
   if (lds <= 64 * 1024 && future_steps <= 256) {
     hipLaunchKernelGGL(k_window_rows, dim3((unsigned)(num_windows * n)), dim3(256), lds, stream,
-                       vol, volvol, n, starts, seq_length, future_steps, x, edge_attr, y);
+                       vol, volvol, n, num_matrices, starts, seq_length, future_steps, x, edge_attr, y);
     return (int)hipGetLastError();
   }
   const int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);
   hipLaunchKernelGGL(k_window_gather, dim3((unsigned)blocks), dim3(256), 0, stream, vol, volvol,
-                     n, starts, num_windows, seq_length, future_steps, canon, x, edge_attr, y);
+                     n, num_matrices, starts, num_windows, seq_length, future_steps, canon, x, edge_attr, y);
   return (int)hipGetLastError();
 }

@@ -214,8 +214,10 @@ def _analyze_deferred(edge_index: torch.Tensor, N: int, n: int, key) -> GraphLay
 
 
 def analyze_edge_index(edge_index: torch.Tensor, num_nodes: int,
-                       n: Optional[int] = None) -> GraphLayout:
-    """Classify ``edge_index`` (see module docstring); cached per tensor."""
+                       n: Optional[int] = None, deferred: bool = True) -> GraphLayout:
+    """Classify ``edge_index`` (see module docstring); cached per tensor.
+    ``n``: the graph size when known (``deferred``: analysed without a host
+    round trip), or a candidate tried first by the synchronous analysis."""
     if edge_index.dim() != 2 or edge_index.size(0) != 2:
         raise ValueError("edge_index must have shape [2, E]")
     if edge_index.dtype != torch.long:
@@ -232,14 +234,16 @@ def analyze_edge_index(edge_index: torch.Tensor, num_nodes: int,
         raise UnsupportedLayout("empty graph batch")
     if _pending:
         check_pending()
-    if n is not None and device.type == "cuda":
+    if n is not None and deferred and device.type == "cuda":
         return _analyze_deferred(edge_index, N, int(n), key)
 
     # 1) block size
     cands = []
-    if n is not None:
+    if n is not None and deferred:
         cands = [int(n)]
     else:
+        if n is not None:
+            cands.append(int(n))
         if E > 0 and E % N == 0:
             guess = E // N + 1
             if N % guess == 0:

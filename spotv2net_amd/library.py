@@ -573,6 +573,7 @@ def _gat_wgrad(x, dxs, W, att_src, att_dst, dbias_partial, heads, channels, bf16
     _need(g_att_src is None or g_att_src.numel() == HC, "g_att_src shape")
     _need(g_att_dst is None or g_att_dst.numel() == HC, "g_att_dst shape")
     weights = gW is not None or g_att_src is not None or g_att_dst is not None
+    _need(x is not None or not weights, "x is required for weight gradients")
     use_bf16 = bf16 and weights and x.stride(0) % 4 == 0 and F >= 4 and \
         x.data_ptr() % 16 == 0 and dxs.data_ptr() % 16 == 0
     ws_fn = lib.sv2n_gat_wgrad_node_bf16_workspace if use_bf16 else \
@@ -744,8 +745,11 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
     _need(x.numel() == B * n * n * seq_length and
           edge_attr.numel() == B * n * (n - 1) * 3 * seq_length and
           y.numel() == B * n * future_steps, "window output buffer sizes")
+    _need(volvol.shape == vol.shape and vol.dim() == 3, "series shapes")
+    # windows outside the series come back as NaN (checked in the kernel:
+    # the starts live on the device, so no host round trip here)
     _lib.check(lib.sv2n_window_gather(vol.data_ptr(), volvol.data_ptr(), vol.shape[1],
-                                      starts.data_ptr(), starts.numel(), seq_length, future_steps,
+                                      vol.shape[0], starts.data_ptr(), starts.numel(), seq_length, future_steps,
                                       canon.data_ptr(), x.data_ptr(), edge_attr.data_ptr(),
                                       y.data_ptr(), _st(vol)), "sv2n_window_gather")
 

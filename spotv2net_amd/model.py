@@ -31,23 +31,47 @@ from .layout import GraphLayout, analyze_edge_index
 from .stack import gat_stack, head_mse_loss, linear_head
 
 
+def _equal_sizes_on_host(data) -> Optional[int]:
+    """Nodes per graph of a PyG ``Batch`` from its host-side slice table
+    (``_slice_dict['x']``, written by PyG's collate), when all graphs have the
+    same size; None when the batch carries no such table or is ragged."""
+    sl = getattr(data, "_slice_dict", None)
+    try:
+        cuts = sl["x"] if sl is not None else None
+    except (KeyError, TypeError):
+        return None
+    if cuts is None or not hasattr(cuts, "__len__") or len(cuts) < 2:
+        return None
+    if torch.is_tensor(cuts):
+        if cuts.device.type != "cpu":
+            return None
+        cuts = cuts.tolist()
+    sizes = {int(b) - int(a) for a, b in zip(cuts[:-1], cuts[1:])}
+    return sizes.pop() if len(sizes) == 1 else None
+
+
 def _layout_of(data, x: torch.Tensor, edge_index: torch.Tensor) -> GraphLayout:
     """The batch's graph layout: attached to it, cached on its edge_index, or
-    analysed — without a host synchronisation when the graph size is known
-    (``nodes_per_graph``, or N / ``num_graphs`` of a PyG / sv2n Batch)."""
+    analysed.  The analysis skips the host synchronisation only when the graph
+    size is KNOWN — ``nodes_per_graph`` (sv2n ``collate`` / window builders) or a
+    PyG Batch whose host-side slice table shows equal graph sizes — so a ragged
+    batch can never reach the kernels on the deferred (NaN-poisoning) check.
+    A size merely inferred as N / ``num_graphs`` is verified synchronously."""
     lay = getattr(data, "sv2n_layout", None)
     if isinstance(lay, GraphLayout) and lay.num_nodes == x.size(0):
         return lay
     N = x.size(0)
     hint = getattr(data, "nodes_per_graph", None)
     if hint is None:
-        try:
-            ng = int(data.num_graphs)  # PyG Batch: host int; sv2n Batch: ptr length
-        except (AttributeError, TypeError, RuntimeError):
-            ng = 0
-        if ng > 0 and N % ng == 0:
-            hint = N // ng
-    return analyze_edge_index(edge_index, N, hint)
+        hint = _equal_sizes_on_host(data)
+    if hint is not None:
+        return analyze_edge_index(edge_index, N, hint)
+    try:
+        ng = int(data.num_graphs)  # PyG Batch: host int; sv2n Batch: ptr length
+    except (AttributeError, TypeError, RuntimeError):
+        ng = 0
+    guess = N // ng if ng > 0 and N % ng == 0 else None
+    return analyze_edge_index(edge_index, N, guess, deferred=False)
 
 
 class GATModel(nn.Module):

@@ -15,8 +15,6 @@ The GAT layers themselves (a7-a12) run as one fused node: ``stack.gat_stack``.
 """
 from __future__ import annotations
 
-import os
-
 from typing import Optional, Sequence
 
 import torch
@@ -73,9 +71,9 @@ def gemm_f32(a: torch.Tensor, a_kmajor: bool, b: torch.Tensor, b_kmajor: bool,
 
 
 # Projection GEMMs with a small weight operand run on the bf16-split MFMA
-# kernel (sv2n_gemm_f32x3, f32-accurate); SV2N_GEMM=f32 selects the exact-f32
-# MFMA kernel instead.
-_SPLIT_GEMM = os.environ.get("SV2N_GEMM", "split3").lower() != "f32"
+# kernel (sv2n_gemm_f32x3, f32-accurate) whenever the activation operand is
+# 16-B aligned with a row stride of whole 16-B chunks; the exact-f32 MFMA
+# kernel (sv2n_gemm_f32) takes the rest.
 
 
 def weight_planes(w: torch.Tensor, transpose: bool) -> torch.Tensor:
@@ -91,7 +89,7 @@ def weight_planes(w: torch.Tensor, transpose: bool) -> torch.Tensor:
 
 
 def _split_ok(a: torch.Tensor) -> bool:
-    return _SPLIT_GEMM and a.stride(1) == 1 and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0
+    return a.stride(1) == 1 and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0
 
 
 def project(a: torch.Tensor, w: torch.Tensor, transpose_w: bool) -> torch.Tensor:

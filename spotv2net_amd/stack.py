@@ -154,11 +154,9 @@ LAST_PATH = {"attention": None}  # which attention path the last forward took (t
 
 def _overlap_edge(training: bool) -> bool:
     """Run the edge-logit pass on a side stream beside the layer-0 projection
-    GEMM.  Default: inference only (MI355X, C2 B = 512: forward 2.18-2.19 M ->
-    2.24-2.26 M graphs/s; the training step 0.5485 vs 0.5473 ms, within
-    noise).  SV2N_OVERLAP_EDGE=1 / 0 forces it on / off."""
-    v = os.environ.get("SV2N_OVERLAP_EDGE")
-    return (v == "1") if v in ("0", "1") else not training
+    GEMM: inference only (MI355X, C2 B = 512: forward 2.18-2.19 M -> 2.24-2.26
+    M graphs/s; in the training step 0.5485 vs 0.5473 ms, within noise)."""
+    return not training
 
 
 _SIDE = {}

@@ -77,15 +77,42 @@ class FlatAdam:
                                  self.wd)
 
 
+def _host_staged(t: torch.Tensor, group) -> bool:
+    """gloo moves host memory: device tensors go through a host copy."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def allreduce_mean_(flat: torch.Tensor, group=None) -> None:
-    """Average a flat gradient buffer across the data-parallel group in place."""
+    """Average a flat gradient buffer across the data-parallel group in place:
+    ONE all-reduce (RCCL over xGMI with the nccl backend; through a host copy
+    with gloo)."""
     if not (dist.is_available() and dist.is_initialized()):
         return
     ws = dist.get_world_size(group)
     if ws == 1:
         return
-    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    if _host_staged(flat, group):
+        host = flat.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        flat.copy_(host)
+    else:
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     flat.div_(ws)
+
+
+def broadcast_params_(module: torch.nn.Module, src: int = 0, group=None) -> None:
+    """Make every rank's parameters and buffers equal to rank ``src``'s (the
+    replicas of data-parallel training start identical)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            if _host_staged(t, group):
+                host = t.detach().cpu()
+                dist.broadcast(host, src, group=group)
+                t.copy_(host)
+            else:
+                dist.broadcast(t.data, src, group=group)
 
 
 def make_adam(params, lr: float):
@@ -122,7 +149,7 @@ class TrainStep:
     share the parameters, gradients and optimizer state.
 
     Constructing it applies no update: the warm-up steps before capture are
-    undone (parameters, optimizer state, RNG)."""
+    undone (parameters, buffers, optimizer state, RNG)."""
 
     def __init__(self, model: torch.nn.Module, data, lr: float = 1e-3,
                  loss_fn: Callable = torch.nn.functional.mse_loss, use_graph: bool = True,
@@ -201,8 +228,10 @@ class TrainStep:
     # -- graph capture ------------------------------------------------------
     def _snapshot(self) -> dict:
         """Everything the warm-up steps before capture advance: parameters,
+        module buffers (BatchNorm running statistics with ``standardize``),
         optimizer state, RNG streams."""
         snap = {"params": self.flat_params.clone(), "opt": None,
+                "buffers": [b.detach().clone() for b in self.model.buffers()],
                 "cpu_rng": torch.get_rng_state(),
                 "cuda_rng": torch.cuda.get_rng_state(self.flat.device)}
         if isinstance(self.opt, FlatAdam):
@@ -218,6 +247,8 @@ class TrainStep:
         same buffers), so that construction does not train the model."""
         with torch.no_grad():
             self.flat_params.copy_(snap["params"])
+            for b, old in zip(self.model.buffers(), snap["buffers"]):
+                b.copy_(old)
             self.flat.zero_()
             if isinstance(self.opt, FlatAdam):
                 m, v, t = snap["opt"]
@@ -241,7 +272,7 @@ class TrainStep:
 
     def _capture(self, sh: _Shape, warmup: int) -> None:
         """Warm up (allocator, lazy optimizer state), capture, then restore the
-        pre-warm-up parameters / optimizer state / RNG: constructing a
+        pre-warm-up parameters / buffers / optimizer state / RNG: constructing a
         TrainStep applies no update (k calls == k eager reference steps)."""
         snap = self._snapshot()
         s = torch.cuda.Stream()

@@ -122,7 +122,7 @@ def test_layout_analysis_has_no_host_sync(dev):
     d = _small(dev, B=4)
     m(d).sum().backward()  # warm caches (canonical table, workspaces)
     fresh = Batch(x=d.x, edge_index=d.edge_index.clone(), edge_attr=d.edge_attr, y_x=d.y_x,
-                  ptr=d.ptr, batch=d.batch)
+                  ptr=d.ptr, batch=d.batch, nodes_per_graph=30)
     torch.cuda.synchronize()
     torch.cuda.set_sync_debug_mode("error")
     try:
@@ -131,6 +131,50 @@ def test_layout_analysis_has_no_host_sync(dev):
     finally:
         torch.cuda.set_sync_debug_mode("default")
     assert_close(out, m(d), tol=1e-6, what="block path == canonical path")
+
+
+def test_pyg_slice_table_counts_as_known_size(dev):
+    """A PyG-style Batch (host-side ``_slice_dict`` with equal graph sizes, as
+    PyG's collate writes it) takes the sync-free analysis too."""
+    from spotv2net_amd import Batch, GATModel
+    torch.manual_seed(3)
+    m = GATModel(60, 6, 2, 1, [8, 4], concat_heads=True).to(dev)
+    d = _small(dev, B=4)
+    m(d).sum().backward()
+    fresh = Batch(x=d.x, edge_index=d.edge_index.clone(), edge_attr=d.edge_attr, y_x=d.y_x,
+                  ptr=d.ptr, batch=d.batch)
+    fresh._slice_dict = {"x": torch.tensor([0, 30, 60, 90, 120])}
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        out = m(fresh)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    assert_close(out, m(d), tol=1e-6, what="block path == canonical path")
+
+
+def test_inferred_size_is_verified_synchronously(dev):
+    """Graph size only inferred as N / num_graphs (no nodes_per_graph, no host
+    slice table): the layout is checked before any compute, so a ragged batch
+    (graphs of 20 and 40 nodes, N / num_graphs = 30) is never poisoned by the
+    deferred check — it runs as one 60-node block and matches the oracle."""
+    from helpers import twin_model
+    from spotv2net_amd import Batch
+    from spotv2net_amd.layout import canonical_edge_index
+    mine, ref = twin_model(seed=9, num_node_features=6, num_edge_features=3, num_heads=2,
+                           output_node_channels=1, dim_hidden_layers=[8, 4],
+                           concat_heads=True)
+    g = torch.Generator().manual_seed(4)
+    ei = torch.cat([canonical_edge_index(20, 1), canonical_edge_index(40, 1) + 20], 1)
+    x = torch.randn(60, 6, generator=g)
+    ea = torch.randn(ei.size(1), 3, generator=g)
+    ptr = torch.tensor([0, 20, 60])
+    mine = mine.to(dev)
+    out = mine(Batch(x=x.to(dev), edge_index=ei.to(dev), edge_attr=ea.to(dev),
+                     ptr=ptr.to(dev)))
+    want = ref(Batch(x=x, edge_index=ei, edge_attr=ea, ptr=ptr))
+    assert torch.isfinite(out).all()
+    assert_close(out, want, tol=1e-5, what="ragged batch")
 
 
 def test_invalid_edges_poison_then_raise(dev):
@@ -144,7 +188,7 @@ def test_invalid_edges_poison_then_raise(dev):
     ei = d.edge_index.clone()
     ei[:, 5] = ei[:, 6]  # a repeated (target, source) pair
     bad = Batch(x=d.x, edge_index=ei, edge_attr=d.edge_attr, y_x=d.y_x, ptr=d.ptr,
-                batch=d.batch)
+                batch=d.batch, nodes_per_graph=30)
     out = m(bad)
     assert torch.isnan(out).all()
     with pytest.raises(UnsupportedLayout):

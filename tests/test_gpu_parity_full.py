@@ -140,3 +140,40 @@ def test_window_gather_kernel_matches_builder(dev, n, S, Fs):
     ds.fill(got, idx)
     for key in ("x", "edge_attr", "y_x", "edge_index"):
         assert torch.equal(getattr(got, key), getattr(want, key)), key
+
+
+@pytest.mark.parametrize("n,S,Fs", [(30, 42, 1), (7, 3, 2), (30, 180, 1)])
+def test_window_gather_out_of_range_windows_are_nan(dev, n, S, Fs):
+    """torch.ops.sv2n.window_gather with starts outside the series (negative,
+    or starts + S + F past the last matrix): those windows come back as NaN,
+    nothing is read out of bounds, the in-range windows are unchanged (both
+    kernels: the LDS row kernel and, at S = 180, the element-wise gather one)."""
+    from spotv2net_amd import WindowDataset
+    from spotv2net_amd.data import synthetic_series
+    T = S + Fs + 10
+    V, W = synthetic_series(T, n, seed=3)
+    ds = WindowDataset(V.to(dev), W.to(dev), S, future_steps=Fs)
+    good = torch.tensor([0, 3, T - S - Fs], device=dev)
+    want = ds.empty_batch(3)
+    ds.fill(want, good)  # cut 0: window index == start
+    starts = torch.tensor([0, -1, 3, T - S - Fs + 1, T - S - Fs, 10 ** 6], device=dev)
+    B = starts.numel()
+    E0 = n * (n - 1)
+    x = torch.empty(B * n, n * S, device=dev)
+    ea = torch.empty(B * E0, 3 * S, device=dev)
+    y = torch.empty(B * n * Fs, device=dev)
+    from spotv2net_amd.layout import canonical_table
+    torch.ops.sv2n.window_gather(ds.vol.contiguous(), ds.volvol.contiguous(), starts, S, Fs,
+                                 canonical_table(n, dev), x, ea, y)
+    torch.cuda.synchronize()
+    bad = [1, 3, 5]
+    for b in range(B):
+        xs, es, ys = x[b * n:(b + 1) * n], ea[b * E0:(b + 1) * E0], y[b * n * Fs:(b + 1) * n * Fs]
+        if b in bad:
+            assert torch.isnan(xs).all() and torch.isnan(es).all() and torch.isnan(ys).all(), b
+        else:
+            assert torch.isfinite(xs).all() and torch.isfinite(es).all(), b
+    k = {0: 0, 2: 1, 4: 2}
+    for b, j in k.items():
+        assert torch.equal(x[b * n:(b + 1) * n], want.x[j * n:(j + 1) * n])
+        assert torch.equal(ea[b * E0:(b + 1) * E0], want.edge_attr[j * E0:(j + 1) * E0])

@@ -235,3 +235,33 @@ def test_fused_wgrad_matches_gemm_and_fold(dev, F, H, C, nodes):
                                        dbp.data_ptr(), B, HC, None, None, None, gb.data_ptr(),
                                        ws.data_ptr(), ws_n, st), "wgrad bias only")
     assert_close(gb, ref[3], tol=1e-6, what="bias only")
+
+
+def test_trainstep_standardize_matches_reference_steps(dev):
+    """standardize=True (BatchNorm over x and edge_attr, utils/models.py:76-78,
+    :141-143; the yaml grid's option, GNN_param.yaml:70): the captured step's
+    warm-up is undone for the running statistics too, so k TrainStep calls ==
+    k eager reference steps — parameters AND buffers."""
+    from spotv2net_amd import synthetic_batch
+    from spotv2net_amd.train import TrainStep
+    m1 = _model(dev, seed=12, standardize=True)
+    m2 = copy.deepcopy(m1)
+    data = synthetic_batch(8, 4, seed=3, device=dev)
+    step = TrainStep(m1, data, lr=1e-3, use_graph=True, warmup=3)
+    for (n, b), (_, c) in zip(m1.named_buffers(), m2.named_buffers()):
+        assert torch.equal(b, c), f"{n}: constructing a TrainStep must not move the buffers"
+    opt = torch.optim.Adam(m2.parameters(), lr=1e-3)
+    for _ in range(3):
+        step()
+        opt.zero_grad()
+        l2 = torch.nn.functional.mse_loss(m2(data), data.y_x)
+        l2.backward()
+        opt.step()
+        assert_close(step.loss, l2.detach(), tol=1e-5, what="loss")
+    for (n, p), (_, q) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert_close(p.detach(), q.detach(), tol=1e-5, what=n)
+    for (n, b), (_, c) in zip(m1.named_buffers(), m2.named_buffers()):
+        if b.dtype == torch.long:
+            assert torch.equal(b, c), n
+        else:
+            assert_close(b, c, tol=1e-6, what=n)
