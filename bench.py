@@ -435,29 +435,34 @@ def step_roofline(cfg, train_gps: float, fwd_gps: float, dtype: str) -> dict:
             "fwd_frac": round(fwd_gps / fwd_bound, 4), "train_frac": round(train_gps / train_bound, 4)}
 
 
-def reference_loop_rate(dev, cfg, data, args, world) -> float:
-    """5_train_SpotV2Net.py:142-160 as written, eager: a NEW batch object with
-    a new edge_index every step (as sv2n ``collate`` or PyG's DataLoader
-    yields, with the graph size known: layout analysed without a host sync),
-    model(data), nn.MSELoss, zero_grad, backward,
-    torch.optim.Adam(fused) step and the per-step loss.item() sync.  Inputs
-    stay device-resident (the DataLoader's CPU collation and H2D copy are
-    not on the GPU path)."""
+def reference_loop_rate(dev, cfg, data, args, world, canonical: bool = True) -> float:
+    """5_train_SpotV2Net.py:142-160 as written, eager Python: a NEW batch object
+    with a new edge_index every step, model(data), nn.MSELoss, zero_grad,
+    backward, torch.optim.Adam(fused) step and the per-step loss.item() sync.
+    The batch carries what sv2n ``collate`` attaches to a batch of the
+    reference's graphs: ``nodes_per_graph`` and, ``canonical``, the verified
+    canonical edge order (False: the same batch without it, analysed on the
+    device every step, block-layout kernels).  GATModel replays its forward
+    and backward as hipGraphs from the second step on (graphed.py).  Inputs
+    stay device-resident (the DataLoader's CPU collation and H2D copy are not
+    on the GPU path)."""
     from spotv2net_amd import Batch
     model = build_model(dev, cfg).set_precision(args.precision)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
     crit = torch.nn.MSELoss()
+    extra = {"canonical_edges": True} if canonical else {}
 
     def step():
         b = Batch(x=data.x, edge_index=data.edge_index.clone(), edge_attr=data.edge_attr,
-                  y_x=data.y_x, batch=data.batch, ptr=data.ptr, nodes_per_graph=cfg["n"])
+                  y_x=data.y_x, batch=data.batch, ptr=data.ptr, nodes_per_graph=cfg["n"],
+                  **extra)
         loss = crit(model(b), b.y_x)
         opt.zero_grad()
         loss.backward()
         opt.step()
         return loss.item()
 
-    for _ in range(max(2, args.warmup)):
+    for _ in range(max(3, args.warmup)):
         step()
     el = max_over_ranks(time_replays(step, args.steps), dev)
     return world * args.batch * args.steps / el
@@ -552,9 +557,10 @@ def main():
     value = world * args.batch * args.steps / el
     loss = float(step.loss.item())
 
-    ref_loop = None
+    ref_loop = ref_loop_block = None
     if not args.no_ref_loop:
         ref_loop = reference_loop_rate(dev, cfg, data, args, world)
+        ref_loop_block = reference_loop_rate(dev, cfg, data, args, world, canonical=False)
     model.eval()
     fstep = ForwardStep(model, data, use_graph=not args.no_graph)
     for _ in range(max(1, args.warmup)):
@@ -600,6 +606,8 @@ def main():
                        "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
             "fwd_graphs_per_s": round(fwd_value, 1),
             "ref_loop_graphs_per_s": round(ref_loop, 1) if ref_loop else None,
+            "ref_loop_block_layout_graphs_per_s": round(ref_loop_block, 1) if ref_loop_block
+            else None,
             "step_roofline": step_roofline(cfg, value, fwd_value, args.precision),
             "final_loss": loss,
             "roofline": roof,

@@ -22,7 +22,7 @@ from typing import Optional, Sequence
 
 import torch
 
-from .layout import canonical_edge_index, canonical_pairs
+from .layout import canonical_edge_index, canonical_pairs, is_canonical_graph
 
 _FIELDS = ("x", "edge_index", "edge_attr", "y_x")
 
@@ -72,7 +72,10 @@ class Batch(Data):
 
 def collate(graphs: Sequence[Data]) -> Batch:
     """PyG DataLoader collation: x/edge_attr/y_x concatenated, edge_index +=
-    cumulative node count, ``batch`` and ``ptr`` added."""
+    cumulative node count, ``batch`` and ``ptr`` added.  Equal graph sizes set
+    ``nodes_per_graph``; when every graph's edge_index is the canonical order
+    (checked here, on the host) the batch is marked ``canonical_edges`` and
+    its layout needs no analysis on the device."""
     xs, eis, eas, ys, sizes = [], [], [], [], []
     off = 0
     for g in graphs:
@@ -95,6 +98,16 @@ def collate(graphs: Sequence[Data]) -> Batch:
               ptr=ptr)
     if len(set(sizes)) == 1:
         b.nodes_per_graph = sizes[0]
+        seen = set()
+        canon = True
+        for g in graphs:
+            if id(g.edge_index) not in seen:
+                if not is_canonical_graph(g.edge_index, sizes[0]):
+                    canon = False
+                    break
+                seen.add(id(g.edge_index))
+        if canon:
+            b.canonical_edges = True
     return b
 
 

@@ -213,6 +213,37 @@ def _analyze_deferred(edge_index: torch.Tensor, N: int, n: int, key) -> GraphLay
     return _attach(edge_index, key, lay)
 
 
+def is_canonical_graph(edge_index: torch.Tensor, n: int) -> bool:
+    """Whether ONE graph's edge_index is the reference's canonical order
+    (checked on the host for host tensors; device tensors only when they are
+    the cached canonical tensor or carry a canonical layout: no round trip)."""
+    if edge_index.dim() != 2 or edge_index.size(0) != 2 or edge_index.size(1) != n * (n - 1):
+        return False
+    if edge_index.device.type == "cpu":
+        return bool(torch.equal(edge_index, canonical_edge_index(n, 1)))
+    for _, lay in (getattr(edge_index, "_sv2n_layouts", None) or {}).values():
+        if lay.kind == "canonical" and lay.n == n and lay.num_graphs == 1:
+            return True
+    return False
+
+
+def declare_canonical(edge_index: torch.Tensor, num_nodes: int, n: int) -> GraphLayout:
+    """The canonical layout of a batch its builder verified (``collate`` sets
+    ``canonical_edges`` after checking every graph on the host): no analysis,
+    the kernels never read edge_index."""
+    N, n = int(num_nodes), int(n)
+    if n < 1 or n > MAX_N or N % n != 0 or edge_index.size(1) != (N // n) * n * (n - 1):
+        raise UnsupportedLayout(f"batch marked canonical does not hold {N // max(n, 1)} "
+                                f"complete {n}-node graphs")
+    key = (N, n)
+    lay = _cached(edge_index, key)
+    if lay is not None and lay.kind == "canonical":
+        return lay
+    lay = GraphLayout("canonical", n, N // n, N, edge_index.size(1), None, None,
+                      canonical_table(n, edge_index.device))
+    return _attach(edge_index, key, lay)
+
+
 def analyze_edge_index(edge_index: torch.Tensor, num_nodes: int,
                        n: Optional[int] = None, deferred: bool = True) -> GraphLayout:
     """Classify ``edge_index`` (see module docstring); cached per tensor.

@@ -25,9 +25,9 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from . import ops
+from . import graphed, ops
 from .conv import GATConv
-from .layout import GraphLayout, analyze_edge_index
+from .layout import GraphLayout, analyze_edge_index, declare_canonical
 from .stack import gat_stack, head_mse_loss, linear_head
 
 
@@ -56,6 +56,8 @@ def _layout_of(data, x: torch.Tensor, edge_index: torch.Tensor) -> GraphLayout:
     size is KNOWN — ``nodes_per_graph`` (sv2n ``collate`` / window builders) or a
     PyG Batch whose host-side slice table shows equal graph sizes — so a ragged
     batch can never reach the kernels on the deferred (NaN-poisoning) check.
+    A batch ``collate`` verified as canonical (``canonical_edges``) needs no
+    analysis at all.
     A size merely inferred as N / ``num_graphs`` is verified synchronously."""
     lay = getattr(data, "sv2n_layout", None)
     if isinstance(lay, GraphLayout) and lay.num_nodes == x.size(0):
@@ -65,6 +67,8 @@ def _layout_of(data, x: torch.Tensor, edge_index: torch.Tensor) -> GraphLayout:
     if hint is None:
         hint = _equal_sizes_on_host(data)
     if hint is not None:
+        if getattr(data, "canonical_edges", False):
+            return declare_canonical(edge_index, N, hint)
         return analyze_edge_index(edge_index, N, hint)
     try:
         ng = int(data.num_graphs)  # PyG Batch: host int; sv2n Batch: ptr length
@@ -106,6 +110,10 @@ class GATModel(nn.Module):
         # execution mode of the GAT stack: None = fp32 unless inside
         # torch.autocast("cuda", dtype=torch.bfloat16); "f32" / "bf16" force it
         self.precision: Optional[str] = None
+        # forward / backward replayed as hipGraphs once a call signature repeats
+        # (graphed.py: the reference loop, 5_train_SpotV2Net.py:142-160, unchanged)
+        self.graph_replay = True
+        self._graph_cache = graphed.GraphCache()
 
         acts = {"relu": F.relu, "tanh": F.tanh, "sigmoid": F.sigmoid}
         if activation not in acts:
@@ -113,13 +121,14 @@ class GATModel(nn.Module):
         self.a = acts[activation]
         self._act_code = ops.ACT_CODES[activation]
 
-    def _hidden(self, data) -> torch.Tensor:
+    def _hidden(self, data, layout: Optional[GraphLayout] = None) -> torch.Tensor:
         x, edge_index, edge_attr = data.x, data.edge_index, data.edge_attr
         if self.standardize:
             x = self.bnorm_node(x)
             if edge_attr is not None:
                 edge_attr = self.bnorm_edge(edge_attr)
-        layout = _layout_of(data, x, edge_index)
+        if layout is None:
+            layout = _layout_of(data, x, edge_index)
         return gat_stack(x, edge_attr, tuple(self.gat_layers), layout, self._act_code,
                          float(self.dropout or 0.0), self.training, self.precision)
 
@@ -132,7 +141,14 @@ class GATModel(nn.Module):
         return self
 
     def forward(self, data):
-        return linear_head(self._hidden(data), self.linear).view(-1)
+        layout = None
+        if self.graph_replay and not self.standardize:
+            x, edge_index, edge_attr = data.x, data.edge_index, data.edge_attr
+            layout = _layout_of(data, x, edge_index)
+            out = graphed.forward(self, data, x, edge_index, edge_attr, layout)
+            if out is not None:
+                return out.view(-1)
+        return linear_head(self._hidden(data, layout), self.linear).view(-1)
 
     def mse_loss(self, data, target: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``nn.MSELoss()(self(data), target)`` (reference

@@ -91,6 +91,7 @@ class _GradTargets:
 
     def __init__(self, params, needs, direct: bool, device):
         self.direct = direct
+        self.flat: Optional[torch.Tensor] = None  # the one buffer behind every view (not direct)
         self._views = {}
         self._used = set()
         self._order = [id(p) for p in params]
@@ -103,6 +104,7 @@ class _GradTargets:
         if total == 0:
             return
         flat = torch.zeros(total, device=device, dtype=torch.float32)
+        self.flat = flat
         off = 0
         for p, nd in zip(params, needs):
             if nd:
@@ -192,216 +194,238 @@ def _opt(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return None if t is None or t.numel() == 0 else t
 
 
+class _StackMeta:
+    """What the backward needs besides the saved tensors (stack_forward)."""
+    __slots__ = ("dims", "bf16", "feid", "kscales")
+
+    def __init__(self, dims, bf16, feid, kscales):
+        self.dims, self.bf16, self.feid, self.kscales = dims, bf16, feid, kscales
+
+
+def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropout: float,
+                  training: bool, precision: str, need_saved: bool):
+    """The fused stack's forward launches (module docstring); returns the
+    output, the tensors the backward reads and a ``_StackMeta``.  Capturable:
+    no host synchronisation, every buffer from the caching allocator."""
+    ops = torch.ops.sv2n
+    dev = x.device
+    L = len(convs)
+    B, n, N = layout.num_graphs, layout.n, layout.num_nodes
+    use_edge = edge_attr is not None and all(c.lin_edge is not None for c in convs)
+    H = convs[0].heads
+    tiled = layout.tiled
+    bf16 = precision == "bf16"
+    if use_edge and any(c.heads != H for c in convs):
+        raise NotImplementedError("fused edge pass needs equal head counts across layers")
+
+    ea = None
+    hp = 0
+    if use_edge:
+        ea = edge_attr.view(-1, 1) if edge_attr.dim() == 1 else edge_attr
+        ea = _aligned(ea)
+        if ea.size(0) != layout.num_edges:
+            raise ValueError("edge_attr rows must match edge_index columns")
+        hp = _hp(L, H)
+
+    # 1) weight preparation: every layer's folded Waug, its bf16 split planes
+    #    (and the transposed ones the backward's dx GEMM needs) and the edge
+    #    fold, in one launch (sv2n::gat_prep)
+    need_t = [bool(training and (l > 0 or x.requires_grad)) for l in range(L)]
+    waugs, planes, planes_t, wf = ops.gat_prep(
+        [c.lin_src.weight for c in convs], [c.att_src for c in convs],
+        [c.att_dst for c in convs], [c.lin_edge.weight for c in convs] if use_edge else [],
+        [c.att_edge for c in convs] if use_edge else [], [c.heads for c in convs],
+        [c.out_channels for c in convs], hp, need_t, use_edge, bf16)
+
+    # 2) edge logits of every layer in one pass over edge_attr (sv2n::edge_logits),
+    #    unless the attention computes them itself (edge-fused mode)
+    aes = [None] * L
+    ei = layout.edge_index if layout.kind == "block" else None
+    # canonical batches: AE in edge order [E][H] (coalesced on both sides)
+    eo = bool(use_edge and not tiled and edge_order(ei, n))
+    fused = bool(use_edge and _use_fused(layout, convs, ea.size(1), ea.size(0)))
+    feid = layout.eid if (fused and layout.kind == "block") else None
+    LAST_PATH["attention"] = "fused" if fused else ("tiled" if tiled else "small")
+    overlap = None
+    if use_edge and not fused:
+        if _overlap_edge(need_saved) and dev.type == "cuda":
+            # the edge pass (HBM-bound) on a side stream beside the layer-0
+            # projection (MFMA-bound); joined before layer 0's attention
+            main = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                aes = list(ops.edge_logits(ea, wf, ei, layout.canon, L, H, B, n, tiled))
+            for a in aes:
+                a.record_stream(main)
+            overlap = (main, side)
+        else:
+            aes = list(ops.edge_logits(ea, wf, ei, layout.canon, L, H, B, n, tiled))
+        if tiled and ea.size(0) == 0:
+            aes = [None] * L
+
+    # 3) layers
+    xin = _aligned(x)
+    saved_x, saved_xs, saved_y, saved_p, saved_keep, saved_drop = [], [], [], [], [], []
+    saved_st = []
+    for l, c in enumerate(convs):
+        Hc, C = c.heads, c.out_channels
+        F = c.in_channels
+        if xin.size(1) != F:
+            raise ValueError(f"layer {l}: expected {F} input features, got {xin.size(1)}")
+        xs = ops.project(xin, planes[l], waugs[l], False, bf16)  # x · Waugᵀ
+        if overlap is not None:
+            overlap[0].wait_stream(overlap[1])
+            overlap = None
+        keep, kscale = None, 1.0
+        kn = n if tiled else 32  # keep-mask tile: [B][H][n][n] tiled, [B][H][32][32] per-graph
+        if training and c.dropout > 0.0:
+            if c.dropout >= 1.0:
+                keep = torch.zeros(B, Hc, kn, kn, device=dev, dtype=torch.uint8)
+                kscale = 0.0
+            else:
+                keep = (torch.rand(B, Hc, kn, kn, device=dev) >= c.dropout).to(torch.uint8)
+                kscale = 1.0 / (1.0 - c.dropout)
+        st = None
+        if fused:
+            # saved: pre-bias head aggregates + per-row softmax statistics
+            y, ps, st = ops.gat_attn_fused_fwd(xs, ea, wf, l * H, feid, c.bias, keep, kscale,
+                                               B, n, Hc, C, c.concat, act,
+                                               float(c.negative_slope), need_saved)
+        elif tiled:
+            # nothing saved: the backward recomputes the attention from xs and ae
+            y = ops.gat_attn_tiled_fwd(xs, aes[l], layout.num_edges, layout.eid,
+                                       layout.rowmask, c.bias, keep, kscale, B, n, Hc, C,
+                                       c.concat, act, float(c.negative_slope))
+            ps = aes[l]
+        else:
+            y, ps = ops.gat_attn_fwd(xs, aes[l], layout.rowmask, c.bias, keep, kscale, B, n,
+                                     Hc, C, c.concat, act, float(c.negative_slope), eo)
+        out = y
+        dmask = None
+        if training and post_dropout > 0.0:
+            if post_dropout >= 1.0:
+                dmask = torch.zeros_like(y)
+            else:
+                dmask = (torch.rand_like(y) >= post_dropout).to(torch.float32) * \
+                    (1.0 / (1.0 - post_dropout))
+            out = y * dmask
+        saved_x.append(xin)
+        saved_xs.append(xs)
+        saved_y.append(y)
+        saved_p.append(ps)
+        saved_st.append(st)
+        saved_keep.append(keep)
+        saved_drop.append(dmask)
+        xin = out
+
+    meta = _StackMeta((L, act, use_edge, hp, H, eo, fused), bf16, feid,
+                      [(1.0 / (1.0 - c.dropout)) if (training and 0.0 < c.dropout < 1.0) else
+                       (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs])
+    saved = [ea, wf if fused else None, *saved_x, *saved_xs, *saved_y, *saved_p, *saved_st,
+             *saved_keep, *saved_drop, *waugs, *planes_t]
+    return xin, saved, meta
+
+
+def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, need_x0: bool,
+                   grad_of: "_GradTargets"):
+    """The fused stack's backward launches, layers in reverse (module
+    docstring); parameter gradients go where ``grad_of`` says; returns dx."""
+    ops = torch.ops.sv2n
+    L, act, use_edge, hp, H, eo, fused = meta.dims
+    sv = saved
+    ea, wf = sv[0], sv[1]
+    k = 2
+    xs_in = sv[k:k + L]; k += L
+    xss = sv[k:k + L]; k += L
+    ys = sv[k:k + L]; k += L
+    pss = sv[k:k + L]; k += L
+    sts = sv[k:k + L]; k += L
+    keeps = sv[k:k + L]; k += L
+    drops = sv[k:k + L]; k += L
+    waugs = sv[k:k + L]; k += L
+    planes_t = sv[k:k + L]
+    dev = dout.device
+    B, n, N = layout.num_graphs, layout.n, layout.num_nodes
+
+    dy = dout.contiguous()
+    daes = [None] * L
+    dwf = torch.zeros_like(wf) if fused else None  # every layer writes its own columns
+    for l in range(L - 1, -1, -1):
+        c = convs[l]
+        Hc, C = c.heads, c.out_channels
+        if drops[l] is not None:
+            dy = dy * drops[l]
+        xs = xss[l]
+        if fused:  # pss[l], sts[l]: the forward's head aggregates and row statistics
+            dxs, dbp = ops.gat_attn_fused_bwd(
+                dy, ys[l], pss[l], sts[l], xs, ea, wf, l * H, meta.feid, keeps[l],
+                meta.kscales[l], dwf, B, n, Hc, C, c.concat, act, float(c.negative_slope))
+            dae = None
+        elif layout.tiled:  # pss[l] holds the layer's ae (or None without edges)
+            dxs, dae, dbp = ops.gat_attn_tiled_bwd(
+                dy, ys[l], xs, pss[l], layout.num_edges, layout.eid, keeps[l],
+                meta.kscales[l], layout.rowmask, B, n, Hc, C, c.concat, act,
+                float(c.negative_slope))
+        else:
+            dxs, dae, dbp = ops.gat_attn_bwd(
+                dy, ys[l], xs, pss[l], keeps[l], meta.kscales[l], layout.rowmask, use_edge,
+                B, n, Hc, C, c.concat, act, float(c.negative_slope), eo)
+        daes[l] = _opt(dae)
+        gW = grad_of(c.lin_src.weight)
+        gas = grad_of(c.att_src)
+        gad = grad_of(c.att_dst)
+        gb = grad_of(c.bias)
+        if any(g is not None for g in (gW, gas, gad, gb)):
+            # split-K dWaugᵀ GEMM + one fused epilogue (fold, transpose,
+            # att and bias grads), accumulated into the gradient buffers
+            ops.gat_wgrad(xs_in[l], dxs, c.lin_src.weight, c.att_src, c.att_dst, dbp, Hc, C,
+                          meta.bf16, gW, gas, gad, gb)
+        if l > 0 or need_x0:
+            dy = ops.project(dxs, _opt(planes_t[l]), waugs[l], True, meta.bf16)  # dxs · Waug
+
+    if use_edge and ea is not None:
+        # grads exist (zeros) even without edges, as in PyG
+        need_e = [(grad_of(c.lin_edge.weight), grad_of(c.att_edge)) for c in convs]
+        if ea.size(0) > 0 and any(a is not None or b is not None for a, b in need_e):
+            ei = layout.edge_index if layout.kind == "block" else None
+            if not fused:
+                dwf = ops.edge_logits_bwd(ea, ei, layout.canon, daes, H, B, n, hp,
+                                          layout.tiled)
+            if all(a is not None and b is not None for a, b in need_e):
+                # every layer's edge-fold backward in one launch
+                ops.prep_bwd_edge_all(dwf, [l * H for l in range(L)],
+                                      [c.lin_edge.weight for c in convs],
+                                      [c.att_edge for c in convs], [c.heads for c in convs],
+                                      [c.out_channels for c in convs],
+                                      [a for a, _ in need_e], [b for _, b in need_e])
+            else:
+                for l, c in enumerate(convs):
+                    gWe, gae = need_e[l]
+                    ops.prep_bwd_edge(dwf, l * H, c.lin_edge.weight, c.att_edge, c.heads,
+                                      c.out_channels, gWe, gae)
+    return dy if need_x0 else None
+
+
 class _GATStack(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, edge_attr, convs, layout: GraphLayout, act: int, post_dropout: float,
                 training: bool, precision: str, *params):
-        ops = torch.ops.sv2n
-        dev = x.device
-        L = len(convs)
-        B, n, N = layout.num_graphs, layout.n, layout.num_nodes
-        use_edge = edge_attr is not None and all(c.lin_edge is not None for c in convs)
-        H = convs[0].heads
-        tiled = layout.tiled
-        bf16 = precision == "bf16"
-        if use_edge and any(c.heads != H for c in convs):
-            raise NotImplementedError("fused edge pass needs equal head counts across layers")
-
-        ea = None
-        hp = 0
-        if use_edge:
-            ea = edge_attr.view(-1, 1) if edge_attr.dim() == 1 else edge_attr
-            ea = _aligned(ea)
-            if ea.size(0) != layout.num_edges:
-                raise ValueError("edge_attr rows must match edge_index columns")
-            hp = _hp(L, H)
-
-        # 1) weight preparation: every layer's folded Waug, its bf16 split planes
-        #    (and the transposed ones the backward's dx GEMM needs) and the edge
-        #    fold, in one launch (sv2n::gat_prep)
-        need_t = [bool(training and (l > 0 or x.requires_grad)) for l in range(L)]
-        waugs, planes, planes_t, wf = ops.gat_prep(
-            [c.lin_src.weight for c in convs], [c.att_src for c in convs],
-            [c.att_dst for c in convs], [c.lin_edge.weight for c in convs] if use_edge else [],
-            [c.att_edge for c in convs] if use_edge else [], [c.heads for c in convs],
-            [c.out_channels for c in convs], hp, need_t, use_edge, bf16)
-
-        # 2) edge logits of every layer in one pass over edge_attr (sv2n::edge_logits),
-        #    unless the attention computes them itself (edge-fused mode)
-        aes = [None] * L
-        ei = layout.edge_index if layout.kind == "block" else None
-        # canonical batches: AE in edge order [E][H] (coalesced on both sides)
-        eo = bool(use_edge and not tiled and edge_order(ei, n))
-        fused = bool(use_edge and _use_fused(layout, convs, ea.size(1), ea.size(0)))
-        feid = layout.eid if (fused and layout.kind == "block") else None
-        need_saved = training or any(ctx.needs_input_grad)
-        LAST_PATH["attention"] = "fused" if fused else ("tiled" if tiled else "small")
-        overlap = None
-        if use_edge and not fused:
-            if _overlap_edge(need_saved) and dev.type == "cuda":
-                # the edge pass (HBM-bound) on a side stream beside the layer-0
-                # projection (MFMA-bound); joined before layer 0's attention
-                main = torch.cuda.current_stream(dev)
-                side = _side_stream(dev)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    aes = list(ops.edge_logits(ea, wf, ei, layout.canon, L, H, B, n, tiled))
-                for a in aes:
-                    a.record_stream(main)
-                overlap = (main, side)
-            else:
-                aes = list(ops.edge_logits(ea, wf, ei, layout.canon, L, H, B, n, tiled))
-            if tiled and ea.size(0) == 0:
-                aes = [None] * L
-
-        # 3) layers
-        xin = _aligned(x)
-        saved_x, saved_xs, saved_y, saved_p, saved_keep, saved_drop = [], [], [], [], [], []
-        saved_st = []
-        for l, c in enumerate(convs):
-            Hc, C = c.heads, c.out_channels
-            F = c.in_channels
-            if xin.size(1) != F:
-                raise ValueError(f"layer {l}: expected {F} input features, got {xin.size(1)}")
-            xs = ops.project(xin, planes[l], waugs[l], False, bf16)  # x · Waugᵀ
-            if overlap is not None:
-                overlap[0].wait_stream(overlap[1])
-                overlap = None
-            keep, kscale = None, 1.0
-            kn = n if tiled else 32  # keep-mask tile: [B][H][n][n] tiled, [B][H][32][32] per-graph
-            if training and c.dropout > 0.0:
-                if c.dropout >= 1.0:
-                    keep = torch.zeros(B, Hc, kn, kn, device=dev, dtype=torch.uint8)
-                    kscale = 0.0
-                else:
-                    keep = (torch.rand(B, Hc, kn, kn, device=dev) >= c.dropout).to(torch.uint8)
-                    kscale = 1.0 / (1.0 - c.dropout)
-            st = None
-            if fused:
-                # saved: pre-bias head aggregates + per-row softmax statistics
-                y, ps, st = ops.gat_attn_fused_fwd(xs, ea, wf, l * H, feid, c.bias, keep, kscale,
-                                                   B, n, Hc, C, c.concat, act,
-                                                   float(c.negative_slope), need_saved)
-            elif tiled:
-                # nothing saved: the backward recomputes the attention from xs and ae
-                y = ops.gat_attn_tiled_fwd(xs, aes[l], layout.num_edges, layout.eid,
-                                           layout.rowmask, c.bias, keep, kscale, B, n, Hc, C,
-                                           c.concat, act, float(c.negative_slope))
-                ps = aes[l]
-            else:
-                y, ps = ops.gat_attn_fwd(xs, aes[l], layout.rowmask, c.bias, keep, kscale, B, n,
-                                         Hc, C, c.concat, act, float(c.negative_slope), eo)
-            out = y
-            dmask = None
-            if training and post_dropout > 0.0:
-                if post_dropout >= 1.0:
-                    dmask = torch.zeros_like(y)
-                else:
-                    dmask = (torch.rand_like(y) >= post_dropout).to(torch.float32) * \
-                        (1.0 / (1.0 - post_dropout))
-                out = y * dmask
-            saved_x.append(xin)
-            saved_xs.append(xs)
-            saved_y.append(y)
-            saved_p.append(ps)
-            saved_st.append(st)
-            saved_keep.append(keep)
-            saved_drop.append(dmask)
-            xin = out
-
+        out, saved, meta = stack_forward(x, edge_attr, convs, layout, act, post_dropout, training,
+                                         precision, training or any(ctx.needs_input_grad))
         ctx.convs = convs
         ctx.layout = layout
         ctx.direct = _direct_mode()
-        ctx.bf16 = bf16
-        ctx.meta = (L, act, use_edge, hp, H, eo, fused)
-        ctx.feid = feid
-        ctx.kscales = [(1.0 / (1.0 - c.dropout)) if (training and 0.0 < c.dropout < 1.0) else
-                       (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs]
-        ctx.save_for_backward(ea, wf if fused else None, *saved_x, *saved_xs, *saved_y,
-                              *saved_p, *saved_st, *saved_keep, *saved_drop, *waugs, *planes_t)
-        return xin
+        ctx.meta = meta
+        ctx.save_for_backward(*saved)
+        return out
 
     @staticmethod
     def backward(ctx, dout):
-        ops = torch.ops.sv2n
-        convs = ctx.convs
-        layout: GraphLayout = ctx.layout
-        L, act, use_edge, hp, H, eo, fused = ctx.meta
-        sv = ctx.saved_tensors
-        ea, wf = sv[0], sv[1]
-        k = 2
-        xs_in = sv[k:k + L]; k += L
-        xss = sv[k:k + L]; k += L
-        ys = sv[k:k + L]; k += L
-        pss = sv[k:k + L]; k += L
-        sts = sv[k:k + L]; k += L
-        keeps = sv[k:k + L]; k += L
-        drops = sv[k:k + L]; k += L
-        waugs = sv[k:k + L]; k += L
-        planes_t = sv[k:k + L]
-        dev = dout.device
-        B, n, N = layout.num_graphs, layout.n, layout.num_nodes
-
-        dy = dout.contiguous()
-        daes = [None] * L
-        need_x0 = ctx.needs_input_grad[0]
-        params = [p for c in convs for p in layer_params(c)]
-        grad_of = _GradTargets(params, ctx.needs_input_grad[8:], ctx.direct, dev)
-        dwf = torch.zeros_like(wf) if fused else None  # every layer writes its own columns
-        for l in range(L - 1, -1, -1):
-            c = convs[l]
-            Hc, C = c.heads, c.out_channels
-            if drops[l] is not None:
-                dy = dy * drops[l]
-            xs = xss[l]
-            if fused:  # pss[l], sts[l]: the forward's head aggregates and row statistics
-                dxs, dbp = ops.gat_attn_fused_bwd(
-                    dy, ys[l], pss[l], sts[l], xs, ea, wf, l * H, ctx.feid, keeps[l],
-                    ctx.kscales[l], dwf, B, n, Hc, C, c.concat, act, float(c.negative_slope))
-                dae = None
-            elif layout.tiled:  # pss[l] holds the layer's ae (or None without edges)
-                dxs, dae, dbp = ops.gat_attn_tiled_bwd(
-                    dy, ys[l], xs, pss[l], layout.num_edges, layout.eid, keeps[l],
-                    ctx.kscales[l], layout.rowmask, B, n, Hc, C, c.concat, act,
-                    float(c.negative_slope))
-            else:
-                dxs, dae, dbp = ops.gat_attn_bwd(
-                    dy, ys[l], xs, pss[l], keeps[l], ctx.kscales[l], layout.rowmask, use_edge,
-                    B, n, Hc, C, c.concat, act, float(c.negative_slope), eo)
-            daes[l] = _opt(dae)
-            gW = grad_of(c.lin_src.weight)
-            gas = grad_of(c.att_src)
-            gad = grad_of(c.att_dst)
-            gb = grad_of(c.bias)
-            if any(g is not None for g in (gW, gas, gad, gb)):
-                # split-K dWaugᵀ GEMM + one fused epilogue (fold, transpose,
-                # att and bias grads), accumulated into the gradient buffers
-                ops.gat_wgrad(xs_in[l], dxs, c.lin_src.weight, c.att_src, c.att_dst, dbp, Hc, C,
-                              ctx.bf16, gW, gas, gad, gb)
-            if l > 0 or need_x0:
-                dy = ops.project(dxs, _opt(planes_t[l]), waugs[l], True, ctx.bf16)  # dxs · Waug
-
-        if use_edge and ea is not None:
-            # grads exist (zeros) even without edges, as in PyG
-            need_e = [(grad_of(c.lin_edge.weight), grad_of(c.att_edge)) for c in convs]
-            if ea.size(0) > 0 and any(a is not None or b is not None for a, b in need_e):
-                ei = layout.edge_index if layout.kind == "block" else None
-                if not fused:
-                    dwf = ops.edge_logits_bwd(ea, ei, layout.canon, daes, H, B, n, hp,
-                                              layout.tiled)
-                if all(a is not None and b is not None for a, b in need_e):
-                    # every layer's edge-fold backward in one launch
-                    ops.prep_bwd_edge_all(dwf, [l * H for l in range(L)],
-                                          [c.lin_edge.weight for c in convs],
-                                          [c.att_edge for c in convs], [c.heads for c in convs],
-                                          [c.out_channels for c in convs],
-                                          [a for a, _ in need_e], [b for _, b in need_e])
-                else:
-                    for l, c in enumerate(convs):
-                        gWe, gae = need_e[l]
-                        ops.prep_bwd_edge(dwf, l * H, c.lin_edge.weight, c.att_edge, c.heads,
-                                          c.out_channels, gWe, gae)
-        dx0 = dy if need_x0 else None
+        params = [p for c in ctx.convs for p in layer_params(c)]
+        grad_of = _GradTargets(params, ctx.needs_input_grad[8:], ctx.direct, dout.device)
+        dx0 = stack_backward(ctx.saved_tensors, ctx.meta, ctx.convs, ctx.layout, dout,
+                             ctx.needs_input_grad[0], grad_of)
         return (dx0, None, None, None, None, None, None, None) + grad_of.returned()
 
 

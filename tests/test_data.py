@@ -78,3 +78,20 @@ def test_model_double_with_fp32_data_raises():
     from spotv2net_amd.stack import linear_head
     with pytest.raises(TypeError):
         linear_head(torch.randn(30, 4), m2.linear)
+
+
+def test_collate_marks_canonical_batches():
+    """collate checks every graph's edge_index on the host: canonical order
+    -> ``canonical_edges`` (no device analysis of the batch); a shuffled graph
+    or ragged sizes -> no mark."""
+    from spotv2net_amd import Data, collate
+    from spotv2net_amd.data import synthetic_series, window_graph
+    V, W = synthetic_series(8, 30, seed=1)
+    gs = [window_graph(V[k:k + 3], W[k:k + 3]) for k in range(3)]
+    assert getattr(collate(gs), "canonical_edges", False)
+    ei = gs[1].edge_index[:, torch.randperm(870, generator=torch.Generator().manual_seed(0))]
+    bad = [gs[0], Data(x=gs[1].x, edge_index=ei, edge_attr=gs[1].edge_attr, y_x=gs[1].y_x)]
+    assert not getattr(collate(bad), "canonical_edges", False)
+    small = Data(x=torch.zeros(5, 60), edge_index=torch.zeros(2, 0, dtype=torch.long),
+                 edge_attr=torch.zeros(0, 6), y_x=torch.zeros(5))
+    assert not getattr(collate([gs[0], small]), "canonical_edges", False)
