@@ -297,6 +297,102 @@ def kernel_table_tiled(model, data, cfg, reps=10):
     return res
 
 
+def kernel_table_c3(model, cfg, precision, reps=20):
+    """C3 (the yaml model: F 1260, 6 heads x 500, mean, B 128) in its execution
+    mode: the layer's projection GEMM, its weight-gradient GEMM with the fold
+    epilogue (sv2n_gat_wgrad_node[_bf16], slab reduce included), and the
+    attention forward / backward, HIP events on the launch stream.  Flops:
+    2·M·N·K of the GEMM; bytes: every operand once."""
+    from spotv2net_amd import ops, synthetic_batch
+    from spotv2net_amd.layout import canonical_edge_index
+    dev = next(model.parameters()).device
+    B, n, H = cfg["batch"], cfg["n"], cfg["heads"]
+    data = synthetic_batch(B, cfg["S"], n=n, seed=99, device=dev)
+    conv = model.gat_layers[0]
+    C = conv.out_channels
+    HC = H * C
+    lib = ops._lib.load()
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    x = data.x
+    N, F = x.shape
+    with torch.no_grad():
+        W = conv.projection_weight().contiguous()
+    ldx = W.shape[0]
+    bf16 = precision == "bf16"
+    planes = ops.weight_planes(W, False)
+    xs = torch.empty(N, ldx, device=dev)
+
+    def gemm_fwd():
+        (lib.sv2n_gemm_bf16 if bf16 else lib.sv2n_gemm_f32x3)(
+            x.data_ptr(), x.stride(0), planes.data_ptr(), xs.data_ptr(), xs.stride(0), N, ldx, F,
+            sh)
+
+    gemm_fwd()
+    dxs = torch.randn(N, ldx, device=dev) * 1e-3
+    att_s = conv.att_src.detach().reshape(-1).contiguous()
+    att_d = conv.att_dst.detach().reshape(-1).contiguous()
+    dbp = torch.randn(B, C, device=dev)
+    gW = torch.zeros(HC, F, device=dev)
+    ga, gd, gb = (torch.zeros(HC, device=dev), torch.zeros(HC, device=dev),
+                  torch.zeros(C, device=dev))
+    ws_fn = lib.sv2n_gat_wgrad_node_bf16_workspace if bf16 else lib.sv2n_gat_wgrad_node_workspace
+    ws_n = ws_fn(N, F, ldx, H, C)
+    ws = torch.empty(ws_n, device=dev)
+
+    def wgrad():
+        (lib.sv2n_gat_wgrad_node_bf16 if bf16 else lib.sv2n_gat_wgrad_node)(
+            x.data_ptr(), x.stride(0), dxs.data_ptr(), ldx, N, F, conv.lin_src.weight.data_ptr(),
+            att_s.data_ptr(), att_d.data_ptr(), H, C, dbp.data_ptr(), B, C, gW.data_ptr(),
+            ga.data_ptr(), gd.data_ptr(), gb.data_ptr(), ws.data_ptr(), ws_n, sh)
+
+    E = data.edge_attr.shape[0]
+    ae = torch.randn(E, H, device=dev)
+    y = torch.empty(N, C, device=dev)
+    ps = torch.empty(B, H, 32, 32, device=dev)
+
+    def attn_fwd():
+        lib.sv2n_gat_attn_fwd(xs.data_ptr(), ldx, ae.data_ptr(), 1, None, conv.bias.data_ptr(),
+                              None, 1.0, y.data_ptr(), ps.data_ptr(), B, n, H, C, 0, 1, 0.2, sh)
+
+    attn_fwd()
+    dy = torch.randn_like(y)
+    dxs2 = torch.empty_like(xs)
+    dae = torch.empty_like(ae)
+    dbp2 = torch.empty(B, C, device=dev)
+
+    def attn_bwd():
+        lib.sv2n_gat_attn_bwd(dy.data_ptr(), y.data_ptr(), xs.data_ptr(), ldx, ps.data_ptr(),
+                              None, 1.0, None, dxs2.data_ptr(), dae.data_ptr(), 1,
+                              dbp2.data_ptr(), B, n, H, C, 0, 1, 0.2, sh)
+
+    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else BF16X3_PEAK_TFLOPS
+    gflop = 2.0 * N * ldx * F
+    rows = {
+        "gemm_fwd": (gemm_fwd, "mfma", gflop, 4.0 * (N * F + N * ldx) + (2 if bf16 else 6) * ldx * F,
+                     peak),
+        "wgrad_node": (wgrad, "mfma", gflop, 4.0 * (N * F + N * ldx + 3 * HC * F), peak),
+        "gat_attn_fwd": (attn_fwd, "hbm", 2.0 * B * n * n * HC,
+                         4.0 * (xs.numel() + ae.numel() + y.numel() + ps.numel()), None),
+        "gat_attn_bwd": (attn_bwd, "hbm", 4.0 * B * n * n * HC,
+                         4.0 * (2 * y.numel() + 2 * xs.numel() + ps.numel() + ae.numel()), None),
+    }
+    res = {}
+    stream = torch.cuda.current_stream(dev)
+    for name, (fn, bound, flops, nbytes, pk) in rows.items():
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        res[name] = dict(avg_us=us, bound=bound, flops=flops, bytes=nbytes,
+                         tflops=flops / us / 1e6, gbs=nbytes / us / 1e3, peak_tflops=pk)
+    return res
+
+
 def roofline_entry(table, traffic=None):
     # dominant = largest time per training step (gemm rows run once per step at L0)
     name = max(table, key=lambda k: table[k]["avg_us"])
@@ -630,6 +726,10 @@ def main_c3(args, dev, cfg):
     main_run = res["runs"][args.precision]
     value = main_run["graphs_per_s"]
     cpu = None
+    roof, table = None, {}
+    if not args.no_kernel_table:
+        table = kernel_table_c3(build_model(dev, cfg), cfg, args.precision)
+        _, roof = roofline_entry(table)
     if not args.no_cpu_baseline:
         model = build_model(dev, cfg)
         cpu = cpu_baseline(model, cfg, min(args.cpu_batch, 16))
@@ -660,9 +760,14 @@ def main_c3(args, dev, cfg):
                             for r in v["history"]] for k, v in res["runs"].items()},
         "step_roofline": step_roofline(cfg, main_run["train_graphs_per_s_upper"], value,
                                        args.precision),
+        "roofline": roof,
+        "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv)
+                        for kk, vv in v.items() if kk in ("avg_us", "tflops", "gbs", "bound")}
+                    for k, v in table.items()},
         "cpu_baseline": cpu,
         "peaks_assumed": {"hbm_GBs": HBM_PEAK_GBS, "f32_mfma_TFLOPs": F32_MFMA_PEAK_TFLOPS,
-                          "bf16_mfma_TFLOPs": BF16_MFMA_PEAK_TFLOPS},
+                          "bf16_mfma_TFLOPs": BF16_MFMA_PEAK_TFLOPS,
+                          "bf16x3_f32eq_TFLOPs": BF16X3_PEAK_TFLOPS},
     }
     print(json.dumps(result), flush=True)
 

@@ -201,15 +201,28 @@ class OracleGATModel(nn.Module):
         # test hook: explicit post-layer dropout keep masks, one [N, out] 0/1
         # tensor per GAT layer (utils/models.py:148 draws them with F.dropout)
         self.post_keep: Optional[list] = None
+        # test hook (relu only): the active side of each layer's activation,
+        # one [N, out] bool tensor per layer, taken from the product's forward so
+        # that a pre-activation within rounding of 0 (where the two sides of the
+        # kink give gradients that differ by a whole node's contribution) takes
+        # the same branch in both; the pre-activations are kept in act_inputs
+        # for the test to check that masks differ only at such points
+        self.act_masks: Optional[list] = None
+        self.act_inputs: list = []
 
     def forward(self, data):
         x, edge_index, edge_attr = data.x, data.edge_index, data.edge_attr
         if self.standardize:
             x = self.bnorm_node(x)
             edge_attr = self.bnorm_edge(edge_attr)
+        self.act_inputs = []
         for i, l in enumerate(self.gat_layers):
             x = l(x, edge_index, edge_attr)
-            x = self.a(x)
+            if self.act_masks is not None and self.activation == "relu":
+                self.act_inputs.append(x.detach())
+                x = x * self.act_masks[i].to(x.dtype)
+            else:
+                x = self.a(x)
             if self.dropout:
                 if self.post_keep is not None and self.training:
                     x = x * self.post_keep[i].to(x.dtype) / (1.0 - self.dropout)

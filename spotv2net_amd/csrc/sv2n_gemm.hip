@@ -67,7 +67,6 @@ static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t K) {
 // 0): nothing sits behind a branch, each batch is one memory round trip.
 // ---------------------------------------------------------------------------
 constexpr int WG_FT = 16, WG_OT = 64;
-constexpr int WG_FPL = 24;  // f per lane in an att block (F <= 64 * 24 per pass)
 
 __global__ __launch_bounds__(256) void k_wgrad_epi(
     const float* __restrict__ T, int ldt, const float* __restrict__ W,
@@ -80,7 +79,10 @@ __global__ __launch_bounds__(256) void k_wgrad_epi(
   __shared__ float s_red[16][17];
   const int HC = H * C;
   const int t = threadIdx.x;
-  const int b = blockIdx.x;
+  // dispatch order: the att blocks (the longest) first, then the gW tiles,
+  // then the bias blocks; b is the block's number in tile/att/bias order
+  const int bx = blockIdx.x;
+  const int b = bx < natt ? ntile + bx : (bx < natt + ntile ? bx - natt : bx);
   const rsrc_t rt = make_rsrc(T, (uint32_t)F * (uint32_t)ldt * 4u);
   if (b >= ntile + natt) {  // ---- bias column sums: 16 columns x 16 row groups ----
     const rsrc_t rb = make_rsrc(dbp, (uint32_t)nparts * (uint32_t)OC * 4u);
@@ -107,40 +109,7 @@ __global__ __launch_bounds__(256) void k_wgrad_epi(
     }
     return;
   }
-  if (b >= ntile) {  // ---- att grads: one wave per row o ----
-    const int lane = t & 63;
-    const int o = (b - ntile) * 4 + (t >> 6);
-    if (o >= HC) return;
-    const int h = o / C;
-    const rsrc_t rw = make_rsrc(W + (int64_t)o * F, (uint32_t)F * 4u);
-    float as = 0.f, ad = 0.f;
-    for (int f0 = 0; f0 < F; f0 += 64 * WG_FPL) {
-      float w[WG_FPL], gs[WG_FPL], gd[WG_FPL];
-#pragma unroll
-      for (int u = 0; u < WG_FPL; ++u) {
-        const int f = f0 + lane + 64 * u;
-        const bool ok = f < F;
-        w[u] = bld(rw, ok ? f * 4 : OOB);
-        gs[u] = bld(rt, ok ? (f * ldt + HC + h) * 4 : OOB);
-        gd[u] = bld(rt, ok ? (f * ldt + HC + H + h) * 4 : OOB);
-      }
-#pragma unroll
-      for (int u = 0; u < WG_FPL; ++u) {
-        as = fmaf(gs[u], w[u], as);
-        ad = fmaf(gd[u], w[u], ad);
-      }
-    }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      as += __shfl_xor(as, m, 64);
-      ad += __shfl_xor(ad, m, 64);
-    }
-    if (lane == 0) {
-      if (g_as) g_as[o] += as;
-      if (g_ad) g_ad[o] += ad;
-    }
-    return;
-  }
+  if (b >= ntile) return;  // (att blocks: k_wgrad_att)
   // ---- gW tile: 16 f x 64 o ----
   const int ft = b % nft, ot = b / nft;
   const int f0 = ft * WG_FT, o0 = ot * WG_OT;
@@ -179,6 +148,90 @@ __global__ __launch_bounds__(256) void k_wgrad_epi(
     const int h = min(o, HC - 1) / C;
     const float v = gv[q] + (tile[fl][orow] + sfold[fl][h] * av[q] + sfold[fl][H + h] * dv[q]);
     bst(rg, (o < HC && f < F) ? (o * F + f) * 4 : OOB, v);
+  }
+}
+// Att-vector gradients of one layer: g_att_s[o] += Σ_f T[f][HC+h]·W[o][f]
+// (and dst), h = o / C.  A block owns ATT_RB consecutive rows o (their heads
+// [h0, h1]); it stages those heads' fold columns of T (strided by ldt) into
+// LDS once, [q][h - h0][f], then each wave takes ATT_RB/4 rows and reads W
+// rows coalesced, all of them in flight at once.  (Per-wave loads of the
+// strided columns — one 64-line gather per lane slot, once per row — cost
+// 41 us at C3, HC 3000 x F 1260.)  Sums in a fixed order.
+constexpr int ATT_RB = 16;           // rows per block
+constexpr int ATT_RW = ATT_RB / 4;   // rows per wave
+constexpr int ATT_FPL = 24;          // f per lane per pass (F <= 1536: one pass)
+
+__global__ __launch_bounds__(256) void k_wgrad_att(const float* __restrict__ T, int ldt,
+                                                   const float* __restrict__ W, int H, int C, int F,
+                                                   float* __restrict__ g_as,
+                                                   float* __restrict__ g_ad) {
+  extern __shared__ float s_fold[];  // [2][nh][F]
+  const int HC = H * C, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int o0 = blockIdx.x * ATT_RB, o1 = min(HC, o0 + ATT_RB);
+  const int h0 = o0 / C, nh = (o1 - 1) / C - h0 + 1;
+  const rsrc_t rt = make_rsrc(T, (uint32_t)F * (uint32_t)ldt * 4u);
+  {
+    const int n = 2 * nh * F;
+    for (int k0 = 0; k0 < n; k0 += 8 * 256) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + t + 256 * u;
+        const int q = k / (nh * F), r = k - q * nh * F, hh = r / F, f = r - hh * F;
+        v[u] = bld(rt, k < n ? (f * ldt + HC + q * H + h0 + hh) * 4 : OOB);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 + t + 256 * u < n) s_fold[k0 + t + 256 * u] = v[u];
+    }
+  }
+  __syncthreads();
+  const int ob = o0 + wv * ATT_RW;
+  float as[ATT_RW], ad[ATT_RW];
+#pragma unroll
+  for (int r = 0; r < ATT_RW; ++r) as[r] = ad[r] = 0.f;
+  for (int f0 = 0; f0 < F; f0 += 64 * ATT_FPL) {
+    float w[ATT_RW][ATT_FPL];
+#pragma unroll
+    for (int r = 0; r < ATT_RW; ++r) {
+      const int o = ob + r;
+      const rsrc_t rw = make_rsrc(W + (int64_t)min(o, HC - 1) * F, o < o1 ? (uint32_t)F * 4u : 0u);
+#pragma unroll
+      for (int u = 0; u < ATT_FPL; ++u) {
+        const int f = f0 + lane + 64 * u;
+        w[r][u] = bld(rw, f < F ? f * 4 : OOB);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < ATT_RW; ++r) {
+      const int hh = min(ob + r, o1 - 1) / C - h0;
+      const float* gs = s_fold + hh * F;
+      const float* gd = s_fold + (nh + hh) * F;
+#pragma unroll
+      for (int u = 0; u < ATT_FPL; ++u) {
+        const int f = min(f0 + lane + 64 * u, F - 1);  // w is 0 past F
+        as[r] = fmaf(gs[f], w[r][u], as[r]);
+        ad[r] = fmaf(gd[f], w[r][u], ad[r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < ATT_RW; ++r) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      as[r] += __shfl_xor(as[r], m, 64);
+      ad[r] += __shfl_xor(ad[r], m, 64);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < ATT_RW; ++r) {
+      const int o = ob + r;
+      if (o < o1) {
+        if (g_as) g_as[o] += as[r];
+        if (g_ad) g_ad[o] += ad[r];
+      }
+    }
   }
 }
 }  // namespace sv2n
@@ -512,7 +565,21 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
   }
   const int nft = (F + WG_FT - 1) / WG_FT, not_ = (HC + WG_OT - 1) / WG_OT;
   const int ntile = gW ? nft * not_ : 0;
-  const int natt = (g_att_src || g_att_dst) ? (HC + 3) / 4 : 0;
+  const int natt = 0;  // att gradients: k_wgrad_att
+  if (g_att_src || g_att_dst) {
+    const int nblk = (HC + ATT_RB - 1) / ATT_RB;
+    const int nh_max = std::min(H, (ATT_RB - 1) / C + 2);
+    const size_t lds = sizeof(float) * 2 * (size_t)nh_max * F;
+    if (lds > 160 * 1024) return SV2N_ERR_SHAPE;
+    static bool attr = [] {
+      (void)hipFuncSetAttribute((const void*)k_wgrad_att,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      return true;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(k_wgrad_att, dim3((unsigned)nblk), dim3(256), lds, stream, T, ldx, W, H, C,
+                       F, g_att_src, g_att_dst);
+  }
   const int nbias = bias ? (bias_len + 15) / 16 : 0;
   hipLaunchKernelGGL(k_wgrad_epi, dim3((unsigned)(ntile + natt + nbias)), dim3(256), 0, stream, T,
                      ldx, W, att_src, att_dst, H, C, F, gW, g_att_src, g_att_dst, ntile, nft, natt,

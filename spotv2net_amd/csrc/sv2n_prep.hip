@@ -20,7 +20,139 @@
 
 namespace sv2n {
 
-// grid (ceil(max(F, D)/64), 2H), block 256 = 64 columns x 4 row groups
+// ---------------------------------------------------------------------------
+// Forward prep blocks.  A block owns 64 columns (f, or d for the edge fold) of
+// one head; its 256 threads are 16 row groups x 16 lanes of 4 columns each.
+// Row c of the head belongs to group c % 16; a group walks its rows in
+// increasing c, RB rows per round with all their loads in flight, and the
+// 16 group partials of a fold are added in a fixed tree (fold_tree16).  The
+// same order is used wherever a fold row is recomputed (the T blocks of
+// k_prep_fwd_all), so every copy of a fold row is bit-identical.  Depth:
+// ceil(C / (16·RB)) rounds (C3: C = 500, 4 rounds; 4 groups of one column per
+// lane took 125 dependent rows per thread, 38 us).
+// ---------------------------------------------------------------------------
+constexpr int PREP_G = 16, PREP_RB = 8;
+
+__device__ __forceinline__ void put3(uint16_t* planes, int64_t plane, int64_t idx, float v,
+                                     int np = 3) {
+  unsigned short h0, h1, h2;
+  split3(v, h0, h1, h2);
+  planes[idx] = h0;
+  if (np == 3) {
+    planes[plane + idx] = h1;
+    planes[2 * plane + idx] = h2;
+  }
+}
+
+__device__ __forceinline__ float fold_tree16(const float* v, int stride) {
+  float a[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = v[(2 * i) * stride] + v[(2 * i + 1) * stride];
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+// rows [cb, ce) of head h copied (waug; planes when given: kp columns, zero
+// past F); with fold, the att_src / att_dst folds over ALL C rows written to
+// waug rows HC+h and HC+H+h (and their planes).  cols: F (node) or D (edge).
+struct PrepBlock {
+  const float* W; const float* att_s; const float* att_d; int H, C, F, ldx;
+  float* waug; uint16_t* planes; int64_t kp, plane; int np;
+};
+
+__device__ __forceinline__ void prep_node_block(const PrepBlock& P, int h, int col0, int cb, int ce,
+                                                bool fold, float (*s_red)[PREP_G][64], int t) {
+  const int g = t >> 4, lq = t & 15, col = col0 + 4 * lq;
+  const int C = P.C, F = P.F, HC = P.H * P.C;
+  float ss[4] = {0.f, 0.f, 0.f, 0.f}, sd[4] = {0.f, 0.f, 0.f, 0.f};
+  const int cs = fold ? 0 : cb, cend = fold ? C : ce;
+  const int first = cs + ((g - cs) % PREP_G + PREP_G) % PREP_G;
+  for (int c0 = first; c0 < cend; c0 += PREP_G * PREP_RB) {
+    float w[PREP_RB][4], as[PREP_RB], ad[PREP_RB];
+#pragma unroll
+    for (int u = 0; u < PREP_RB; ++u) {
+      const int c = min(c0 + PREP_G * u, C - 1);
+      const int64_t row = (int64_t)h * C + c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[u][j] = col + j < F ? P.W[row * F + col + j] : 0.f;
+      as[u] = P.att_s[row];
+      ad[u] = P.att_d[row];
+    }
+#pragma unroll
+    for (int u = 0; u < PREP_RB; ++u) {
+      const int c = c0 + PREP_G * u;
+      if (c < cend) {
+        const int64_t row = (int64_t)h * C + c;
+        if (c >= cb && c < ce) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (col + j < F) P.waug[row * F + col + j] = w[u][j];
+            if (P.planes && col + j < P.kp)
+              put3(P.planes, P.plane, row * P.kp + col + j, w[u][j], P.np);
+          }
+        }
+        if (fold) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            ss[j] = fmaf(as[u], w[u][j], ss[j]);
+            sd[j] = fmaf(ad[u], w[u][j], sd[j]);
+          }
+        }
+      }
+    }
+  }
+  if (!fold) return;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s_red[0][g][4 * lq + j] = ss[j];
+    s_red[1][g][4 * lq + j] = sd[j];
+  }
+  __syncthreads();
+  if (t < 128) {
+    const int q = t >> 6, cl = t & 63, c = col0 + cl;
+    const float v = fold_tree16(&s_red[q][0][cl], 64);
+    const int64_t row = HC + q * P.H + h;
+    if (c < F) P.waug[row * F + c] = v;
+    if (P.planes && c < P.kp) put3(P.planes, P.plane, row * P.kp + c, v, P.np);
+  }
+  if (h == 0) {  // zero padding rows
+    for (int k = t; k < (P.ldx - HC - 2 * P.H) * 64; k += 256) {
+      const int64_t row = HC + 2 * P.H + k / 64;
+      const int c = col0 + (k & 63);
+      if (c < F) P.waug[row * F + c] = 0.f;
+      if (P.planes && c < P.kp) put3(P.planes, P.plane, row * P.kp + c, 0.f, P.np);
+    }
+  }
+}
+
+// wfold[d][col0h + h] = Σ_c att_edge[h,c] · W_edge[h*C+c][d], columns [col0, col0+64)
+__device__ __forceinline__ void prep_edge_block(const float* We, const float* att_e, int C, int D,
+                                                int h, int col0, float* wfold, int hlp, int col0h,
+                                                float (*s_red)[PREP_G][64], int t) {
+  const int g = t >> 4, lq = t & 15, col = col0 + 4 * lq;
+  float se[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = g; c0 < C; c0 += PREP_G * PREP_RB) {
+    float w[PREP_RB][4], ae[PREP_RB];
+#pragma unroll
+    for (int u = 0; u < PREP_RB; ++u) {
+      const int64_t row = (int64_t)h * C + min(c0 + PREP_G * u, C - 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[u][j] = col + j < D ? We[row * D + col + j] : 0.f;
+      ae[u] = att_e[row];
+    }
+#pragma unroll
+    for (int u = 0; u < PREP_RB; ++u)
+      if (c0 + PREP_G * u < C)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) se[j] = fmaf(ae[u], w[u][j], se[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s_red[0][g][4 * lq + j] = se[j];
+  __syncthreads();
+  if (t < 64 && col0 + t < D)
+    wfold[(int64_t)(col0 + t) * hlp + col0h + h] = fold_tree16(&s_red[0][0][t], 64);
+}
+
+// grid (ceil(max(F, D)/64), 2H), block 256: one P block per (64 columns, head)
 __global__ __launch_bounds__(256) void k_prep_fwd(const float* __restrict__ W,
                                                   const float* __restrict__ att_s,
                                                   const float* __restrict__ att_d, int H, int C,
@@ -28,49 +160,15 @@ __global__ __launch_bounds__(256) void k_prep_fwd(const float* __restrict__ W,
                                                   const float* __restrict__ We,
                                                   const float* __restrict__ att_e, int D,
                                                   float* __restrict__ wfold, int hlp, int col0) {
-  __shared__ float s_red[2][4][64];
-  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + lane;
-  const int y = blockIdx.y;
+  __shared__ float s_red[2][PREP_G][64];
+  const int y = blockIdx.y, c0 = blockIdx.x * 64;
   if (y < H) {
-    const int h = y;
-    float ss = 0.f, sd = 0.f;
-    if (col < F) {
-      for (int c = grp; c < C; c += 4) {
-        const int row = h * C + c;
-        const float w = W[(int64_t)row * F + col];
-        waug[(int64_t)row * F + col] = w;
-        ss = fmaf(att_s[row], w, ss);
-        sd = fmaf(att_d[row], w, sd);
-      }
-    }
-    s_red[0][grp][lane] = ss;
-    s_red[1][grp][lane] = sd;
-    __syncthreads();
-    if (grp == 0 && col < F) {
-      waug[(int64_t)(H * C + h) * F + col] =
-          (s_red[0][0][lane] + s_red[0][1][lane]) + (s_red[0][2][lane] + s_red[0][3][lane]);
-      waug[(int64_t)(H * C + H + h) * F + col] =
-          (s_red[1][0][lane] + s_red[1][1][lane]) + (s_red[1][2][lane] + s_red[1][3][lane]);
-    }
-    if (h == 0 && col < F) {  // zero padding rows
-      for (int r = H * C + 2 * H + grp; r < ldx; r += 4) waug[(int64_t)r * F + col] = 0.f;
-    }
+    if (c0 >= F) return;
+    const PrepBlock P{W, att_s, att_d, H, C, F, ldx, waug, nullptr, 0, 0, 1};
+    prep_node_block(P, y, c0, 0, C, true, s_red, threadIdx.x);
   } else {
-    if (!We) return;
-    const int h = y - H;
-    float s = 0.f;
-    if (col < D) {
-      for (int c = grp; c < C; c += 4) {
-        const int row = h * C + c;
-        s = fmaf(att_e[row], We[(int64_t)row * D + col], s);
-      }
-    }
-    s_red[0][grp][lane] = s;
-    __syncthreads();
-    if (grp == 0 && col < D)
-      wfold[(int64_t)col * hlp + col0 + h] =
-          (s_red[0][0][lane] + s_red[0][1][lane]) + (s_red[0][2][lane] + s_red[0][3][lane]);
+    if (!We || c0 >= D) return;
+    prep_edge_block(We, att_e, C, D, y - H, c0, wfold, hlp, col0, s_red, threadIdx.x);
   }
 }
 
@@ -243,19 +341,8 @@ struct PrepAllArgs {
   int L;
 };
 
-__device__ __forceinline__ void put3(uint16_t* planes, int64_t plane, int64_t idx, float v,
-                                     int np = 3) {
-  unsigned short h0, h1, h2;
-  split3(v, h0, h1, h2);
-  planes[idx] = h0;
-  if (np == 3) {
-    planes[plane + idx] = h1;
-    planes[2 * plane + idx] = h2;
-  }
-}
-
 __global__ __launch_bounds__(256) void k_prep_fwd_all(const PrepAllArgs a) {
-  __shared__ float s_red[2][4][64];
+  __shared__ float s_red[2][PREP_G][64];
   __shared__ float tile[32][33];
   const int t = threadIdx.x;
   const int b = blockIdx.x;
@@ -273,79 +360,20 @@ __global__ __launch_bounds__(256) void k_prep_fwd_all(const PrepAllArgs a) {
   const int np = P.nplanes == 1 ? 1 : 3;
   if (!tblock) {
     const int64_t kp = a.kp[l], plane = (int64_t)ldx * kp;
-    const int lane = t & 63, grp = t >> 6;
     const int nxy = a.px[l] * (P.W_edge ? 2 * H : H);
     const int part = local / nxy, lxy = local - part * nxy;
     const int bx = lxy % a.px[l], y = lxy / a.px[l];
-    const int col = bx * 64 + lane;
     // the block's copy rows [cb, ce) of head h; part 0 also folds all C rows
     const int RPn = a.rp[l], CR = (C + RPn - 1) / RPn;
     const int cb = part * CR, ce = min(C, cb + CR);
     if (y < H) {
-      const int h = y;
-      float ss = 0.f, sd = 0.f;
-      const int cend = part == 0 ? C : ce;
-      // rows c = grp, grp+4, ...: 16 rows' loads issued before any store (W
-      // is reached through the argument struct, so the compiler cannot move
-      // a load above an earlier store itself)
-      constexpr int RB = 16;
-      for (int c0 = (part == 0 ? 0 : cb) + grp; c0 < cend; c0 += 4 * RB) {
-        float w[RB], as[RB], ad[RB];
-#pragma unroll
-        for (int u = 0; u < RB; ++u) {
-          const int c = c0 + 4 * u;
-          const int row = h * C + min(c, C - 1);
-          const bool ok = c < cend && col < F;
-          w[u] = ok ? P.W[(int64_t)row * F + min(col, F - 1)] : 0.f;
-          as[u] = P.att_src[row];
-          ad[u] = P.att_dst[row];
-        }
-#pragma unroll
-        for (int u = 0; u < RB; ++u) {
-          const int c = c0 + 4 * u;
-          if (c < cend) {
-            const int row = h * C + c;
-            if (c >= cb && c < ce) {
-              if (col < F) P.waug[(int64_t)row * F + col] = w[u];
-              if (col < kp) put3(P.planes, plane, (int64_t)row * kp + col, w[u], np);
-            }
-            ss = fmaf(as[u], w[u], ss);
-            sd = fmaf(ad[u], w[u], sd);
-          }
-        }
-      }
-      if (part != 0) return;
-      s_red[0][grp][lane] = ss;
-      s_red[1][grp][lane] = sd;
-      __syncthreads();
-      if (grp < 2 && col < kp) {
-        const float v = (s_red[grp][0][lane] + s_red[grp][1][lane]) +
-                        (s_red[grp][2][lane] + s_red[grp][3][lane]);
-        const int row = HC + grp * H + h;
-        if (col < F) P.waug[(int64_t)row * F + col] = v;
-        put3(P.planes, plane, (int64_t)row * kp + col, v, np);
-      }
-      if (h == 0 && col < kp) {  // zero padding rows
-        for (int r = HC + 2 * H + grp; r < ldx; r += 4) {
-          if (col < F) P.waug[(int64_t)r * F + col] = 0.f;
-          put3(P.planes, plane, (int64_t)r * kp + col, 0.f, np);
-        }
-      }
+      if (bx * 64 >= kp) return;
+      const PrepBlock B{P.W, P.att_src, P.att_dst, H, C, F, ldx, P.waug, P.planes, kp, plane, np};
+      prep_node_block(B, y, bx * 64, cb, ce, part == 0, s_red, t);
     } else {
-      if (!P.W_edge || part != 0) return;
-      const int h = y - H, D = P.edge_dim;
-      float se = 0.f;
-      if (col < D) {
-        for (int c = grp; c < C; c += 4) {
-          const int row = h * C + c;
-          se = fmaf(P.att_edge[row], P.W_edge[(int64_t)row * D + col], se);
-        }
-      }
-      s_red[0][grp][lane] = se;
-      __syncthreads();
-      if (grp == 0 && col < D)
-        P.wfold[(int64_t)col * P.hl_pad + P.col0 + h] =
-            (s_red[0][0][lane] + s_red[0][1][lane]) + (s_red[0][2][lane] + s_red[0][3][lane]);
+      if (!P.W_edge || part != 0 || bx * 64 >= P.edge_dim) return;
+      prep_edge_block(P.W_edge, P.att_edge, C, P.edge_dim, y - H, bx * 64, P.wfold, P.hl_pad,
+                      P.col0, s_red, t);
     }
     return;
   }
@@ -363,9 +391,10 @@ __global__ __launch_bounds__(256) void k_prep_fwd_all(const PrepAllArgs a) {
       } else if (f < F && o < HC + 2 * H) {
         const int q = o - HC, h = q % H;
         const float* att = q < H ? P.att_src : P.att_dst;
-        float p4[4] = {0.f, 0.f, 0.f, 0.f};
-        // k_prep_fwd's four row groups (row c in group c % 4, in c order),
-        // 8 rows of each group loaded per round
+        float p16[PREP_G];
+#pragma unroll
+        for (int k = 0; k < PREP_G; ++k) p16[k] = 0.f;
+        // the P blocks' 16 row groups (row c in group c % 16, in c order)
         for (int c0 = 0; c0 < C; c0 += 32) {
           float w[32], at[32];
 #pragma unroll
@@ -376,9 +405,9 @@ __global__ __launch_bounds__(256) void k_prep_fwd_all(const PrepAllArgs a) {
           }
 #pragma unroll
           for (int u = 0; u < 32; ++u)
-            if (c0 + u < C) p4[u & 3] = fmaf(at[u], w[u], p4[u & 3]);
+            if (c0 + u < C) p16[u & 15] = fmaf(at[u], w[u], p16[u & 15]);
         }
-        v = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+        v = fold_tree16(p16, 1);
       }
       tile[oi][fl] = v;
     }

@@ -105,12 +105,28 @@ __global__ __launch_bounds__(256) void k_window_rows(
     for (int j = t; j < m * RW; j += 256) up[j] = lo[j] = qnan;
     return;
   }
-  for (int k = t; k < S * n; k += 256) {
-    const int tt = k / n, v = k - tt * n;
-    const int64_t base = (st + tt) * nn;
-    sv[tt * NP + v] = vol[base + (int64_t)u * n + v];
-    sw[tt * NP + v] = volvol[base + (int64_t)u * n + v];
-    sd[tt * NP + v] = volvol[base + (int64_t)v * n + v];
+  // staging: every load of a round issued before its LDS stores (the rolled
+  // loop made one memory round trip per 256 elements: C3, S 42, 5 rounds)
+  for (int k0 = 0; k0 < S * n; k0 += 8 * 256) {
+    float a[8], w[8], d[8];
+    int dst[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int k = min(k0 + t + 256 * r, S * n - 1);
+      const int tt = k / n, v = k - tt * n;
+      const int64_t base = (st + tt) * nn;
+      dst[r] = tt * NP + v;
+      a[r] = vol[base + (int64_t)u * n + v];
+      w[r] = volvol[base + (int64_t)u * n + v];
+      d[r] = volvol[base + (int64_t)v * n + v];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      if (k0 + t + 256 * r < S * n) {
+        sv[dst[r]] = a[r];
+        sw[dst[r]] = w[r];
+        sd[dst[r]] = d[r];
+      }
   }
   if (t < F) y[(b * n + u) * F + t] = vol[(st + S + t) * nn + (int64_t)u * n + u];
   __syncthreads();
@@ -127,12 +143,38 @@ __global__ __launch_bounds__(256) void k_window_rows(
   const int RW = 3 * S;
   float* up = ea + (b * E0 + e0) * (int64_t)RW;
   float* lo = ea + (b * E0 + P + e0) * (int64_t)RW;
+  if (RW <= 4 * 64) {
+    // one wave per edge row, a lane's columns fixed: (kind, t) decoded once
+    // (the flat element loop divided twice per element)
+    const int lane = t & 63, wv = t >> 6;
+    int kind[4], tq[4];
+#pragma unroll
+    for (int qi = 0; qi < 4; ++qi) {
+      const int q = lane + 64 * qi;
+      kind[qi] = q / S;
+      tq[qi] = q - kind[qi] * S;
+    }
+    for (int r = wv; r < m; r += 4) {
+      const int w = u + 1 + r;
+#pragma unroll
+      for (int qi = 0; qi < 4; ++qi) {
+        const int q = lane + 64 * qi;
+        if (q < RW) {
+          const int tt = tq[qi];
+          // upper edge u -> w: (covol, var_u, var_w); swapped w -> u: (covol, var_w, var_u)
+          const float cov = sw[tt * NP + w], du = sw[tt * NP + u], dw = sd[tt * NP + w];
+          up[r * RW + q] = kind[qi] == 0 ? cov : (kind[qi] == 1 ? du : dw);
+          lo[r * RW + q] = kind[qi] == 0 ? cov : (kind[qi] == 1 ? dw : du);
+        }
+      }
+    }
+    return;
+  }
   for (int j = t; j < m * RW; j += 256) {
     const int r = j / RW, q = j - r * RW;
     const int kind = q / S, tt = q - kind * S;
     const int w = u + 1 + r;
     const float cov = sw[tt * NP + w];
-    // upper edge u -> w: (covol, var_u, var_w); swapped edge w -> u: (covol, var_w, var_u)
     const float du = sw[tt * NP + u], dw = sd[tt * NP + w];
     up[j] = kind == 0 ? cov : (kind == 1 ? du : dw);
     lo[j] = kind == 0 ? cov : (kind == 1 ? dw : du);
