@@ -68,88 +68,6 @@ static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t K) {
 // ---------------------------------------------------------------------------
 constexpr int WG_FT = 16, WG_OT = 64;
 
-__global__ __launch_bounds__(256) void k_wgrad_epi(
-    const float* __restrict__ T, int ldt, const float* __restrict__ W,
-    const float* __restrict__ att_s, const float* __restrict__ att_d, int H, int C, int F,
-    float* __restrict__ gW, float* __restrict__ g_as, float* __restrict__ g_ad, int ntile,
-    int nft, int natt, const float* __restrict__ dbp, int nparts, int OC,
-    float* __restrict__ g_bias) {
-  __shared__ float tile[WG_FT][WG_OT + 1];
-  __shared__ float sfold[WG_FT][2 * SV2N_MAX_HEADS];
-  __shared__ float s_red[16][17];
-  const int HC = H * C;
-  const int t = threadIdx.x;
-  // dispatch order: the att blocks (the longest) first, then the gW tiles,
-  // then the bias blocks; b is the block's number in tile/att/bias order
-  const int bx = blockIdx.x;
-  const int b = bx < natt ? ntile + bx : (bx < natt + ntile ? bx - natt : bx);
-  const rsrc_t rt = make_rsrc(T, (uint32_t)F * (uint32_t)ldt * 4u);
-  if (b >= ntile + natt) {  // ---- bias column sums: 16 columns x 16 row groups ----
-    const rsrc_t rb = make_rsrc(dbp, (uint32_t)nparts * (uint32_t)OC * 4u);
-    const int lo = t & 15, grp = t >> 4;
-    const int o = (b - ntile - natt) * 16 + lo;
-    float a = 0.f;
-    for (int q0 = 0; q0 < nparts; q0 += 16 * 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int q = q0 + grp + 16 * u;
-        v[u] = bld(rb, (o < OC && q < nparts) ? (q * OC + o) * 4 : OOB);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a += v[u];
-    }
-    s_red[grp][lo] = a;
-    __syncthreads();
-    if (grp == 0 && o < OC) {
-      float sb = 0.f;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) sb += s_red[k][lo];
-      g_bias[o] += sb;
-    }
-    return;
-  }
-  if (b >= ntile) return;  // (att blocks: k_wgrad_att)
-  // ---- gW tile: 16 f x 64 o ----
-  const int ft = b % nft, ot = b / nft;
-  const int f0 = ft * WG_FT, o0 = ot * WG_OT;
-  {
-    const int ol = t & 63, fr = t >> 6;
-    const int o = o0 + ol;
-    constexpr int R = WG_FT / 4;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int f = f0 + fr + 4 * r;
-      tile[fr + 4 * r][ol] = bld(rt, (o < HC && f < F) ? (f * ldt + o) * 4 : OOB);
-    }
-    if (t < WG_FT * 2 * H) {  // 16 x 2H <= 256
-      const int fl = t / (2 * H), k = t - fl * 2 * H;
-      const int f = f0 + fl;
-      sfold[fl][k] = bld(rt, f < F ? (f * ldt + HC + k) * 4 : OOB);
-    }
-  }
-  __syncthreads();
-  const int fl = t & (WG_FT - 1), og = t / WG_FT;  // 256 / WG_FT o-rows per pass
-  const int f = f0 + fl;
-  constexpr int OPP = 256 / WG_FT, Q = WG_OT / OPP;
-  const rsrc_t rg = make_rsrc(gW, (uint32_t)HC * (uint32_t)F * 4u);
-  const rsrc_t ras = make_rsrc(att_s, (uint32_t)HC * 4u), rad = make_rsrc(att_d, (uint32_t)HC * 4u);
-  float gv[Q], av[Q], dv[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {  // all loads first
-    const int o = o0 + og + OPP * q;
-    gv[q] = bld(rg, (o < HC && f < F) ? (o * F + f) * 4 : OOB);
-    av[q] = bld(ras, o < HC ? o * 4 : OOB);
-    dv[q] = bld(rad, o < HC ? o * 4 : OOB);
-  }
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int orow = og + OPP * q, o = o0 + orow;
-    const int h = min(o, HC - 1) / C;
-    const float v = gv[q] + (tile[fl][orow] + sfold[fl][h] * av[q] + sfold[fl][H + h] * dv[q]);
-    bst(rg, (o < HC && f < F) ? (o * F + f) * 4 : OOB, v);
-  }
-}
 // Att-vector gradients of one layer: g_att_s[o] += Σ_f T[f][HC+h]·W[o][f]
 // (and dst), h = o / C.  A block owns ATT_RB consecutive rows o (their heads
 // [h0, h1]); it stages those heads' fold columns of T (strided by ldt) into
@@ -157,17 +75,17 @@ __global__ __launch_bounds__(256) void k_wgrad_epi(
 // rows coalesced, all of them in flight at once.  (Per-wave loads of the
 // strided columns — one 64-line gather per lane slot, once per row — cost
 // 41 us at C3, HC 3000 x F 1260.)  Sums in a fixed order.
-constexpr int ATT_RB = 16;           // rows per block
+constexpr int ATT_RB = 8;            // rows per block
 constexpr int ATT_RW = ATT_RB / 4;   // rows per wave
 constexpr int ATT_FPL = 24;          // f per lane per pass (F <= 1536: one pass)
 
-__global__ __launch_bounds__(256) void k_wgrad_att(const float* __restrict__ T, int ldt,
-                                                   const float* __restrict__ W, int H, int C, int F,
-                                                   float* __restrict__ g_as,
-                                                   float* __restrict__ g_ad) {
-  extern __shared__ float s_fold[];  // [2][nh][F]
+__device__ __forceinline__ void wgrad_att_block(int blk, const float* __restrict__ T, int ldt,
+                                                const float* __restrict__ W, int H, int C, int F,
+                                                float* __restrict__ g_as, float* __restrict__ g_ad,
+                                                float* __restrict__ s_fold) {
+  // s_fold: [2][nh][F] (dynamic LDS)
   const int HC = H * C, t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int o0 = blockIdx.x * ATT_RB, o1 = min(HC, o0 + ATT_RB);
+  const int o0 = blk * ATT_RB, o1 = min(HC, o0 + ATT_RB);
   const int h0 = o0 / C, nh = (o1 - 1) / C - h0 + 1;
   const rsrc_t rt = make_rsrc(T, (uint32_t)F * (uint32_t)ldt * 4u);
   {
@@ -232,6 +150,93 @@ __global__ __launch_bounds__(256) void k_wgrad_att(const float* __restrict__ T, 
         if (g_ad) g_ad[o] += ad[r];
       }
     }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_wgrad_epi(
+    const float* __restrict__ T, int ldt, const float* __restrict__ W,
+    const float* __restrict__ att_s, const float* __restrict__ att_d, int H, int C, int F,
+    float* __restrict__ gW, float* __restrict__ g_as, float* __restrict__ g_ad, int ntile,
+    int nft, int natt, const float* __restrict__ dbp, int nparts, int OC,
+    float* __restrict__ g_bias) {
+  __shared__ float tile[WG_FT][WG_OT + 1];
+  __shared__ float sfold[WG_FT][2 * SV2N_MAX_HEADS];
+  __shared__ float s_red[16][17];
+  const int HC = H * C;
+  const int t = threadIdx.x;
+  // dispatch order: the att blocks (the longest) first, then the gW tiles,
+  // then the bias blocks; b is the block's number in tile/att/bias order
+  const int bx = blockIdx.x;
+  const int b = bx < natt ? ntile + bx : (bx < natt + ntile ? bx - natt : bx);
+  const rsrc_t rt = make_rsrc(T, (uint32_t)F * (uint32_t)ldt * 4u);
+  if (b >= ntile + natt) {  // ---- bias column sums: 16 columns x 16 row groups ----
+    const rsrc_t rb = make_rsrc(dbp, (uint32_t)nparts * (uint32_t)OC * 4u);
+    const int lo = t & 15, grp = t >> 4;
+    const int o = (b - ntile - natt) * 16 + lo;
+    float a = 0.f;
+    for (int q0 = 0; q0 < nparts; q0 += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = q0 + grp + 16 * u;
+        v[u] = bld(rb, (o < OC && q < nparts) ? (q * OC + o) * 4 : OOB);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a += v[u];
+    }
+    s_red[grp][lo] = a;
+    __syncthreads();
+    if (grp == 0 && o < OC) {
+      float sb = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) sb += s_red[k][lo];
+      g_bias[o] += sb;
+    }
+    return;
+  }
+  if (b >= ntile) {  // att blocks (dispatched first)
+    extern __shared__ float s_dyn[];
+    wgrad_att_block(b - ntile, T, ldt, W, H, C, F, g_as, g_ad, s_dyn);
+    return;
+  }
+  // ---- gW tile: 16 f x 64 o ----
+  const int ft = b % nft, ot = b / nft;
+  const int f0 = ft * WG_FT, o0 = ot * WG_OT;
+  {
+    const int ol = t & 63, fr = t >> 6;
+    const int o = o0 + ol;
+    constexpr int R = WG_FT / 4;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int f = f0 + fr + 4 * r;
+      tile[fr + 4 * r][ol] = bld(rt, (o < HC && f < F) ? (f * ldt + o) * 4 : OOB);
+    }
+    if (t < WG_FT * 2 * H) {  // 16 x 2H <= 256
+      const int fl = t / (2 * H), k = t - fl * 2 * H;
+      const int f = f0 + fl;
+      sfold[fl][k] = bld(rt, f < F ? (f * ldt + HC + k) * 4 : OOB);
+    }
+  }
+  __syncthreads();
+  const int fl = t & (WG_FT - 1), og = t / WG_FT;  // 256 / WG_FT o-rows per pass
+  const int f = f0 + fl;
+  constexpr int OPP = 256 / WG_FT, Q = WG_OT / OPP;
+  const rsrc_t rg = make_rsrc(gW, (uint32_t)HC * (uint32_t)F * 4u);
+  const rsrc_t ras = make_rsrc(att_s, (uint32_t)HC * 4u), rad = make_rsrc(att_d, (uint32_t)HC * 4u);
+  float gv[Q], av[Q], dv[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {  // all loads first
+    const int o = o0 + og + OPP * q;
+    gv[q] = bld(rg, (o < HC && f < F) ? (o * F + f) * 4 : OOB);
+    av[q] = bld(ras, o < HC ? o * 4 : OOB);
+    dv[q] = bld(rad, o < HC ? o * 4 : OOB);
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int orow = og + OPP * q, o = o0 + orow;
+    const int h = min(o, HC - 1) / C;
+    const float v = gv[q] + (tile[fl][orow] + sfold[fl][h] * av[q] + sfold[fl][H + h] * dv[q]);
+    bst(rg, (o < HC && f < F) ? (o * F + f) * 4 : OOB, v);
   }
 }
 }  // namespace sv2n
@@ -565,23 +570,21 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
   }
   const int nft = (F + WG_FT - 1) / WG_FT, not_ = (HC + WG_OT - 1) / WG_OT;
   const int ntile = gW ? nft * not_ : 0;
-  const int natt = 0;  // att gradients: k_wgrad_att
-  if (g_att_src || g_att_dst) {
-    const int nblk = (HC + ATT_RB - 1) / ATT_RB;
+  const int natt = (g_att_src || g_att_dst) ? (HC + ATT_RB - 1) / ATT_RB : 0;
+  size_t lds = 0;
+  if (natt) {
     const int nh_max = std::min(H, (ATT_RB - 1) / C + 2);
-    const size_t lds = sizeof(float) * 2 * (size_t)nh_max * F;
-    if (lds > 160 * 1024) return SV2N_ERR_SHAPE;
+    lds = sizeof(float) * 2 * (size_t)nh_max * F;
+    if (lds > 140 * 1024) return SV2N_ERR_SHAPE;
     static bool attr = [] {
-      (void)hipFuncSetAttribute((const void*)k_wgrad_att,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_wgrad_epi,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 140 * 1024);
       return true;
     }();
     (void)attr;
-    hipLaunchKernelGGL(k_wgrad_att, dim3((unsigned)nblk), dim3(256), lds, stream, T, ldx, W, H, C,
-                       F, g_att_src, g_att_dst);
   }
   const int nbias = bias ? (bias_len + 15) / 16 : 0;
-  hipLaunchKernelGGL(k_wgrad_epi, dim3((unsigned)(ntile + natt + nbias)), dim3(256), 0, stream, T,
+  hipLaunchKernelGGL(k_wgrad_epi, dim3((unsigned)(ntile + natt + nbias)), dim3(256), lds, stream, T,
                      ldx, W, att_src, att_dst, H, C, F, gW, g_att_src, g_att_dst, ntile, nft, natt,
                      dbias_partial, num_parts, bias_len, g_bias);
   return (int)hipGetLastError();

@@ -6,6 +6,7 @@
 // MI355X (profiles/gemm3_tune_r01.txt).
 #include "sv2n_common.h"
 #include "sv2n_gemm3_kernel.h"
+#include "sv2n_gemm_bf16.h"
 
 #include <algorithm>
 
@@ -112,6 +113,18 @@ extern "C" int sv2n_gemm_bf16(const float* A, int64_t lda, const uint16_t* Bp, f
   if (((uintptr_t)A & 15) || (lda & 3) || ((uintptr_t)Bp & 15)) return SV2N_ERR_ALIGN;
   const int64_t Kp = sv2n_split3_kpad(K);
   const unsigned short* B = reinterpret_cast<const unsigned short*>(Bp);
+  if (K % 4 == 0) {  // k_gemm_bf16nt (sv2n_gemm_bf16.h)
+    static bool attr = [] {
+      (void)hipFuncSetAttribute((const void*)k_gemm_bf16nt,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)BF_LDS);
+      return true;
+    }();
+    (void)attr;
+    const int nm = (int)((M + BF_BM - 1) / BF_BM), nn = (int)((N + BF_BN - 1) / BF_BN);
+    hipLaunchKernelGGL(k_gemm_bf16nt, dim3((unsigned)(((nm + 7) / 8) * 8 * nn)), dim3(256), BF_LDS,
+                       stream, A, lda, B, Kp, C, ldc, M, N, K, nm, nn);
+    return (int)hipGetLastError();
+  }
   const int64_t mb = (M + 127) / 128;
   const bool wide = mb * ((N + 207) / 208) >= 240;
   if (wide) return launch_gemm_bf16<8, 1, 13, 64>(stream, A, lda, B, Kp, N, C, ldc, M, K);
