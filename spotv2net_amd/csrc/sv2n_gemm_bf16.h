@@ -23,7 +23,7 @@ constexpr int BF_BM = 128, BF_BN = 128, BF_BK = 64, BF_ROW = BF_BK + 16;
 constexpr int BF_STAGE = (BF_BM + BF_BN) * BF_ROW;  // bf16 elements per stage
 constexpr size_t BF_LDS = sizeof(unsigned short) * 2 * BF_STAGE;
 
-__global__ __launch_bounds__(256, 2) void k_gemm_bf16nt(const float* __restrict__ A, int64_t lda,
+static __global__ __attribute__((unused)) __launch_bounds__(256, 2) void k_gemm_bf16nt(const float* __restrict__ A, int64_t lda,
                                                          const unsigned short* __restrict__ Bp,
                                                          int64_t ldb, float* __restrict__ C,
                                                          int64_t ldc, int64_t M, int64_t N,
