@@ -55,18 +55,31 @@ __device__ __forceinline__ void bst_s(rsrc_t r, int voff, int soff, float v) {
 }
 
 // ---------------------------------------------------------------------------
-// forward: one 256-thread workgroup per graph.
+// forward: S 256-thread workgroups per graph (S = 1 when the batch alone
+// fills the chip, C2; C3's 128 graphs of 6 x 500 columns run S = 4).  Each
+// computes the whole softmax (cheap) and aggregates its share of the work
+// items.  Block b -> graph 8·(b / 8S) + b % 8, split (b / 8) % S: the splits of
+// a graph run on one XCD (they share its logits and xs rows through L2).
 // LDS: sP[H][32][PS] (dropped-out probabilities, the MFMA A operand) |
 //      sAS[H][32] a_src | sAD[H][32] a_dst | sAE[E0·H]
-// Work items of a wave (after the softmax): concat — (head h, 32-column tile
-// tc) pairs w, w+4, ...; mean — tiles tc = w, w+4, ..., each summed over the
-// heads (sub-items h = 0..H-1 on one accumulator, in head order).
+// Work items of wave slot u = 4s + w (after the softmax): concat — (head h,
+// 32-column tile tc) pairs u, u + 4S, ...; mean — tiles tc = u, u + 4S, ...,
+// each summed over the heads (sub-items h = 0..H-1 on one accumulator, in head
+// order).  The saved probabilities are stored by split 0.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ bool graph_split(int64_t B, int S, int64_t& g, int& s) {
+  const int64_t b = blockIdx.x;
+  g = (b / (8 * S)) * 8 + (b & 7);
+  s = (int)((b >> 3) % S);
+  return g < B;
+}
+
 template <int ACT, bool CONCAT, bool KEEP>
 __global__ __launch_bounds__(THREADS) void k_fwd(
     const float* __restrict__ xs, int ldx, const float* __restrict__ ae, int ae_edge_order,
     const uint32_t* __restrict__ rowmask, const float* __restrict__ bias, const uint8_t* __restrict__ keep, float keep_scale,
-    float* __restrict__ y, float* __restrict__ psave, int n, int H, int C, float slope) {
+    float* __restrict__ y, float* __restrict__ psave, int n, int H, int C, float slope, int S,
+    int64_t B) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sP = smem;
   float* sAS = sP + H * 32 * PS;
@@ -75,8 +88,11 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 
   SV2N_STAMP(0, SV2N_RT());
   SV2N_STAMP(1, SV2N_T());
-  const int g = blockIdx.x;
+  int64_t g;
+  int split;
+  if (!graph_split(B, S, g, split)) return;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int slot = 4 * split + wave, NS = 4 * S;
   const int l32 = lane & 31, half = lane >> 5;
   const int HC = H * C, OC = CONCAT ? HC : C;
   const int E0 = n * (n - 1), P = E0 / 2;
@@ -88,16 +104,17 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
   const rsrc_t rb = make_rsrc(bias, bias ? (uint32_t)OC * 4u : 0u);
 
   // ---- work items of this wave: q -> (head, tile), first / last sub-item ----
-  const int nq = CONCAT ? (H * ntc - wave + 3) / 4 : ((ntc - wave + 3) / 4) * H;
+  const int nq = CONCAT ? max(0, (H * ntc - slot + NS - 1) / NS)
+                        : max(0, (ntc - slot + NS - 1) / NS) * H;
   auto item = [&](int q, int& h, int& tc) {
     if constexpr (CONCAT) {
-      const int s = wave + 4 * q;
+      const int s = slot + NS * q;
       h = s / ntc;
       tc = s - h * ntc;
     } else {
       const int k = q / H;
       h = q - k * H;
-      tc = wave + 4 * k;
+      tc = slot + NS * k;
     }
   };
   // xs rows 16·half + kk of head h's columns of tile tc: the B operand
@@ -242,7 +259,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
     const int h = wave + 4 * s2;
-    if (h >= H) break;
+    if (h >= H || split != 0) break;
     const int off = ((h * 32 + i) * 32 + 16 * half) * 4;
 #pragma unroll
     for (int k4 = 0; k4 < 4; ++k4)
@@ -283,7 +300,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       }
     }
   };
-  for (int q0 = 0; q0 < nq; q0 += 4) {
+  for (int q0 = 0; q0 < nq; q0 += 4) {  // (nq = 0: a split past the last tile)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int q = q0 + u;
@@ -299,20 +316,27 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 
 
 // ---------------------------------------------------------------------------
-// backward: one 256-thread workgroup per graph, wave w owns heads w, w + 4.
-// Per head h (all in the wave's registers and its own LDS area):
+// backward: S workgroups per graph (graph_split), split s owning heads
+// [s·HS, s·HS + HS).  Its waves form 4/WPH groups of WPH waves; group q owns
+// the split's heads q, q + 4/WPH, ... and wave k of a group takes chunks
+// k, k + WPH, ... of each.  Per head h (wave registers + the wave's LDS area):
 //   dZ_h[i][c] = act'(dy, y) (· 1/H for the head mean),
 //   G[j][i]    = Σ_c xs[j][h·C + c] · dZ_h[i][c]          (dP_dᵀ: lane i, rows j)
 //   dxs[j][h·C + c] = Σ_i P_d[i][j] · dZ_h[i][c]
-// over 32-column chunks of the head staged through the wave's LDS area (xs and
-// dZ rows, stride 33: conflict-free row and column operand reads); then the
-// dropout / softmax / leaky_relu backward of G in the MFMA output layout
-// (lane i holds rows j = crow(r, half) — the positions its saved probabilities
-// are loaded at) -> dl in sDL.  After a barrier: d ae in edge order (one
-// decode per edge), d a_src = column sums of dl, d a_dst, zero padding.
-// LDS: sP[H][32][PS] (P_d, the A operand of dxs) | per wave 2 x [32][33]
-//      chunk area | sDL[H][32][33] | sSh[H][32] (self-loop share of row i) |
-//      sDad[H][32] | sDec[P] (pair p -> (u, w), u < w)
+// over 32-column chunks staged through the wave's LDS area (xs and dZ rows,
+// stride CS: conflict-free row and column operand reads); with WPH > 1 the
+// group's partial G are added in wave order through LDS after a barrier.
+// Then the dropout / softmax / leaky_relu backward of G in the MFMA output
+// layout (lane i holds rows j = crow(r, half) — the positions its saved
+// probabilities are loaded at) -> dl in sDL.  After a barrier: d ae of the
+// split's heads in edge order (one decode per edge), d a_src = column sums
+// of dl, d a_dst, zero padding (split 0).
+// C3 (128 graphs, H 6 x 500 columns) runs S 6, HS 1, WPH 4; S = 1, HS = H,
+// WPH = 1 (C2: 512 graphs) is one workgroup per graph with wave w owning
+// heads w, w + 4.
+// LDS: sP[HS][32][PS] (P_d, the A operand of dxs) | per wave 2 x [32][CS]
+//      chunk area | sDL[HS][32][DS] | sSh[HS][32] (self-loop share of row i) |
+//      sDad[HS][32] | sRB[32] | sDec[P] (pair p -> (u, w), u < w)
 // ---------------------------------------------------------------------------
 constexpr int CS = 36;  // chunk row stride (floats): 16-B rows, conflict-free b128 row reads
 constexpr int DS = 33;  // dl row stride (floats): conflict-free column sums
@@ -322,43 +346,49 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ xs,
     int ldx, const float* __restrict__ psave, const uint8_t* __restrict__ keep, float keep_scale,
     const uint32_t* __restrict__ rowmask, float* __restrict__ dxs, float* __restrict__ dae,
-    int ae_edge_order, float* __restrict__ dbias_part, int n, int H, int C, float slope) {
+    int ae_edge_order, float* __restrict__ dbias_part, int n, int H, int C, float slope, int S,
+    int HS, int WPH, int64_t B) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sP = smem;
-  float* sArea = sP + H * 32 * PS;
+  float* sArea = sP + HS * 32 * PS;
   float* sDL = sArea + 4 * 2 * 32 * CS;
-  float* sSh = sDL + H * 32 * DS;
-  float* sDad = sSh + H * 32;
-  uint32_t* sRB = reinterpret_cast<uint32_t*>(sDad + H * 32);  // source bits of row i
-  uint16_t* sDec = reinterpret_cast<uint16_t*>(sRB + 32);       // pair p -> (u << 8 | w)
+  float* sSh = sDL + HS * 32 * DS;
+  float* sDad = sSh + HS * 32;
+  uint32_t* sRB = reinterpret_cast<uint32_t*>(sDad + HS * 32);  // source bits of row i
+  uint16_t* sDec = reinterpret_cast<uint16_t*>(sRB + 32);        // pair p -> (u << 8 | w)
 
   SV2N_STAMP(0, SV2N_RT());
   SV2N_STAMP(1, SV2N_T());
-  const int g = blockIdx.x;
+  int64_t g;
+  int split;
+  if (!graph_split(B, S, g, split)) return;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int l32 = lane & 31, half = lane >> 5;
   const int HC = H * C, OC = CONCAT ? HC : C;
   const int E0 = n * (n - 1);
   const float invH = 1.f / (float)H;
-  const rsrc_t rx = make_rsrc(xs + (int64_t)g * n * ldx, (uint32_t)(n * ldx) * 4u);
-  const rsrc_t rdx = make_rsrc(dxs + (int64_t)g * n * ldx, (uint32_t)(n * ldx) * 4u);
-  const rsrc_t rdy = make_rsrc(dy + (int64_t)g * n * OC, (uint32_t)(n * OC) * 4u);
-  const rsrc_t ryy = make_rsrc(y + (int64_t)g * n * OC, (uint32_t)(n * OC) * 4u);
-  const rsrc_t rps = make_rsrc(psave + (int64_t)g * H * 1024, (uint32_t)H * 4096u);
-  const rsrc_t rdb = make_rsrc(dbias_part + (int64_t)g * OC, (uint32_t)OC * 4u);
+  const int h0 = split * HS, nhs = min(HS, H - h0);  // this split's heads
+  const rsrc_t rx = make_rsrc(xs + g * n * ldx, (uint32_t)(n * ldx) * 4u);
+  const rsrc_t rdx = make_rsrc(dxs + g * n * ldx, (uint32_t)(n * ldx) * 4u);
+  const rsrc_t rdy = make_rsrc(dy + g * n * OC, (uint32_t)(n * OC) * 4u);
+  const rsrc_t ryy = make_rsrc(y + g * n * OC, (uint32_t)(n * OC) * 4u);
+  const rsrc_t rps = make_rsrc(psave + g * H * 1024, (uint32_t)H * 4096u);
+  const rsrc_t rdb = make_rsrc(dbias_part + g * OC, (uint32_t)OC * 4u);
 
   float* sX = sArea + wave * 2 * 32 * CS;
   float* sZ = sX + 32 * CS;
   const int nch = (C + 31) >> 5;
   const int cwb = (C + nch - 1) / nch;  // balanced chunk width (<= 32)
-  const int nhw = (H - wave + 3) / 4;  // heads of this wave
-  const int nseq = nhw * nch;          // (head, chunk) steps of this wave
+  const int NG = 4 / WPH, grp = wave / WPH, sub = wave - grp * WPH;
+  const int nhw = grp < nhs ? (nhs - grp + NG - 1) / NG : 0;   // heads of this wave
+  const int ncw = sub < nch ? (nch - sub + WPH - 1) / WPH : 0;  // chunks per head
+  const int nseq = nhw * ncw;                                  // (head, chunk) steps
 
   // chunk step q: rows 2m + half, column l32 of the chunk (dword loads, the
   // row stride in the scalar offset)
   float rx_[16], rdy_[16], ry_[16];
   auto load_chunk = [&](int q) {
-    const int hq = q / nch, ch = q - hq * nch, h = wave + 4 * hq;
+    const int hq = q / ncw, ch = sub + WPH * (q - hq * ncw), h = h0 + grp + NG * hq;
     const int c = cwb * ch + l32;
     const bool cv = l32 < cwb && c < C;
     const int xo = cv ? (half * ldx + h * C + c) * 4 : OOB;
@@ -379,20 +409,20 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 #pragma unroll
     for (int m = 0; m < 4; ++m) pr[m] = bld4(rps, base + 32 * m);
     if constexpr (KEEP) {
-      const rsrc_t rk = make_rsrc(keep + ((int64_t)g * H + h) * 1024, 1024u);
+      const rsrc_t rk = make_rsrc(keep + (g * H + h) * 1024, 1024u);
 #pragma unroll
       for (int m = 0; m < 4; ++m) kb[m] = bld_u32(rk, (l32 * 32 + 4 * half) + 8 * m);
     }
   };
 
   if (nseq > 0) {
-    load_p(wave);
+    load_p(h0 + grp);
     load_chunk(0);
   }
   // sources of target row l32 (block layouts: the row mask; else all n)
   const uint32_t allm = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
   const uint32_t rbits =
-      (rowmask ? bld_u32(make_rsrc(rowmask + (int64_t)g * n, (uint32_t)n * 4u), l32 * 4) : allm) &
+      (rowmask ? bld_u32(make_rsrc(rowmask + g * n, (uint32_t)n * 4u), l32 * 4) : allm) &
       ~(1u << l32);
   if (t < 32) sRB[t] = rbits;
   if (dae && ae_edge_order && t < n) {  // row u of the pair table (read after the final barrier)
@@ -405,12 +435,53 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   const int i = l32;
   const bool iv = i < n;
 
+  // ---- softmax / leaky_relu backward of head h (local hl) from G: lane (i,
+  //      half), rows j = crow(r, half) ----
+  auto softmax_bwd = [&](int hl) {
+    float ps[16], dp[16];
+    float tl = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jr = crow(r, half);
+      ps[r] = pr[r >> 2][r & 3];
+      const bool valid = iv && (jr == i || ((rbits >> jr) & 1u));
+      float d = valid ? (CONCAT ? G[r] : G[r] * invH) : 0.f;
+      if constexpr (KEEP) d = ((kb[r >> 2] >> (8 * (r & 3))) & 0xffu) ? d * keep_scale : 0.f;
+      dp[r] = d;
+      tl += fabsf(ps[r]) * d;
+    }
+    tl += __shfl_xor(tl, 32, 64);
+    float dad = 0.f, mine = 0.f;
+    const int ri = (i & 3) + 4 * (i >> 3), hi = (i >> 2) & 1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jr = crow(r, half);
+      const bool valid = iv && (jr == i || ((rbits >> jr) & 1u));
+      const float ds = fabsf(ps[r]) * (dp[r] - tl);
+      const float dl = valid ? (signbit(ps[r]) ? ds * slope : ds) : 0.f;
+      dad += dl;
+      mine = (r == ri) ? dl : mine;
+      sDL[(hl * 32 + i) * DS + jr] = dl;
+    }
+    dad += __shfl_xor(dad, 32, 64);
+    const float other = __shfl_xor(mine, 32, 64);
+    const float dlii = (half == hi) ? mine : other;
+    if (half == 0) {
+      sDad[hl * 32 + i] = iv ? dad : 0.f;
+      const int cnt = __popc(rbits);
+      sSh[hl * 32 + i] = (iv && cnt > 0) ? dlii / (float)cnt : 0.f;
+    }
+  };
+
   for (int q = 0; q < nseq; ++q) {
-    const int hq = q / nch, ch = q - hq * nch, h = wave + 4 * hq;
+    const int hq = q / ncw, chi = q - hq * ncw, ch = sub + WPH * chi;
+    const int hl = grp + NG * hq, h = h0 + hl;
     const int c0 = cwb * ch, cw = min(cwb, C - c0);
-    if (ch == 0) {
-      // P_d of head h -> sP rows (each lane: its 16 positions of row i)
-      float* prow = sP + (h * 32 + l32) * PS + 4 * half;
+    if (chi == 0) {
+      // P_d of head h -> sP rows (each lane: its 16 positions of row i).  With
+      // WPH > 1 every wave of the group writes the same values: each reads
+      // only what it wrote itself.
+      float* prow = sP + (hl * 32 + l32) * PS + 4 * half;
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         f32x4 v;
@@ -462,7 +533,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     floatx16 D;
 #pragma unroll
     for (int r = 0; r < 16; ++r) D[r] = 0.f;
-    const float* pcol = sP + (h * 32 + 16 * half) * PS + l32;
+    const float* pcol = sP + (hl * 32 + 16 * half) * PS + l32;
     const float* zcol = sZ + (16 * half) * CS + l32;
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk)
@@ -473,107 +544,102 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       for (int r = 0; r < 16; ++r)
         bst_s(rdx, voff, ((r & 3) + 8 * (r >> 2)) * ldx * 4, CONCAT ? D[r] : D[r] * invH);
     }
-    if (ch == nch - 1) {
-      // ---- softmax / leaky_relu backward of head h: lane (i, half), rows j = crow(r, half)
-      float ps[16], dp[16];
-      float tl = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int jr = crow(r, half);
-        ps[r] = pr[r >> 2][r & 3];
-        const bool valid = iv && (jr == i || ((rbits >> jr) & 1u));
-        float d = valid ? (CONCAT ? G[r] : G[r] * invH) : 0.f;
-        if constexpr (KEEP) d = ((kb[r >> 2] >> (8 * (r & 3))) & 0xffu) ? d * keep_scale : 0.f;
-        dp[r] = d;
-        tl += fabsf(ps[r]) * d;
-      }
-      tl += __shfl_xor(tl, 32, 64);
-      float dad = 0.f, mine = 0.f;
-      const int ri = (i & 3) + 4 * (i >> 3), hi = (i >> 2) & 1;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int jr = crow(r, half);
-        const bool valid = iv && (jr == i || ((rbits >> jr) & 1u));
-        const float ds = fabsf(ps[r]) * (dp[r] - tl);
-        const float dl = valid ? (signbit(ps[r]) ? ds * slope : ds) : 0.f;
-        dad += dl;
-        mine = (r == ri) ? dl : mine;
-        sDL[(h * 32 + i) * DS + jr] = dl;
-      }
-      dad += __shfl_xor(dad, 32, 64);
-      const float other = __shfl_xor(mine, 32, 64);
-      const float dlii = (half == hi) ? mine : other;
-      if (half == 0) {
-        sDad[h * 32 + i] = iv ? dad : 0.f;
-        const int cnt = __popc(rbits);
-        sSh[h * 32 + i] = (iv && cnt > 0) ? dlii / (float)cnt : 0.f;
-      }
+    if (WPH == 1 && chi == ncw - 1) {
+      softmax_bwd(hl);
 #pragma unroll
       for (int r = 0; r < 16; ++r) G[r] = 0.f;
-      if (hq + 1 < nhw) load_p(h + 4);
+      if (hq + 1 < nhw) load_p(h + NG);
+    }
+  }
+  if (WPH > 1) {
+    // one head per group: the group's partial G, added in wave order
+    float* sG = sArea + wave * 2 * 32 * CS;  // the wave's own chunk area (its reads are done)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sG[r * 64 + lane] = G[r];
+    __syncthreads();
+    if (sub == 0 && nhw > 0) {
+      for (int k = 1; k < WPH; ++k) {
+        const float* o = sArea + (wave + k) * 2 * 32 * CS;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) G[r] += o[r * 64 + lane];
+      }
+      softmax_bwd(grp);
     }
   }
   SV2N_STAMP(10, SV2N_T());
   __syncthreads();
   SV2N_STAMP(11, SV2N_T());
 
-  // ---- d ae in canonical edge order [E0][H]: pair p = (u, w), u < w, is edge
-  //      p (target w, source u) and edge P + p (target u, source w) ----
+  // ---- d ae of this split's heads in canonical edge order [E0][H]: pair
+  //      p = (u, w), u < w, is edge p (target w, source u) and edge P + p
+  //      (target u, source w) ----
+  const bool vec4 = H == 4 && nhs == 4, vec2 = nhs == 2 && (H & 1) == 0 && (h0 & 1) == 0;
   if (dae && !ae_edge_order) {
     // ---- dense [n][n][H] block (block layouts): zeros off the edge set ----
     const int nae = n * n * H;
-    const rsrc_t rdae = make_rsrc(dae + (int64_t)g * nae, (uint32_t)nae * 4u);
+    const rsrc_t rdae = make_rsrc(dae + g * nae, (uint32_t)nae * 4u);
     for (int k = t; k < n * n; k += THREADS) {
       const int ti = k / n, tj = k - ti * n;
       const bool e = tj != ti && ((sRB[ti] >> tj) & 1u);
-      if (H == 4) {
+      if (vec4) {
         f32x4 v;
 #pragma unroll
         for (int h = 0; h < 4; ++h) v[h] = e ? sDL[(h * 32 + ti) * DS + tj] + sSh[h * 32 + ti] : 0.f;
         bst4(rdae, k * 16, v);
+      } else if (vec2) {
+        bst2(rdae, (k * H + h0) * 4, e ? sDL[ti * DS + tj] + sSh[ti] : 0.f,
+             e ? sDL[(32 + ti) * DS + tj] + sSh[32 + ti] : 0.f);
       } else {
-        for (int h = 0; h < H; ++h)
-          bst(rdae, (k * H + h) * 4, e ? sDL[(h * 32 + ti) * DS + tj] + sSh[h * 32 + ti] : 0.f);
+        for (int hl = 0; hl < nhs; ++hl)
+          bst(rdae, (k * H + h0 + hl) * 4,
+              e ? sDL[(hl * 32 + ti) * DS + tj] + sSh[hl * 32 + ti] : 0.f);
       }
     }
   } else if (dae) {
     const int P = E0 / 2, nae = E0 * H;
-    const rsrc_t rdae = make_rsrc(dae + (int64_t)g * nae, (uint32_t)nae * 4u);
+    const rsrc_t rdae = make_rsrc(dae + g * nae, (uint32_t)nae * 4u);
     for (int p = t; p < P; p += THREADS) {
       const uint32_t uw = sDec[p];
       const int u = uw >> 8, w = uw & 0xff;
 #pragma unroll
       for (int side = 0; side < 2; ++side) {
         const int ti = side ? u : w, tj = side ? w : u, e = side ? P + p : p;
-        if (H == 4) {
+        if (vec4) {
           f32x4 v;
 #pragma unroll
           for (int h = 0; h < 4; ++h) v[h] = sDL[(h * 32 + ti) * DS + tj] + sSh[h * 32 + ti];
           bst4(rdae, e * 16, v);
+        } else if (vec2) {
+          bst2(rdae, (e * H + h0) * 4, sDL[ti * DS + tj] + sSh[ti],
+               sDL[(32 + ti) * DS + tj] + sSh[32 + ti]);
         } else {
-          for (int h = 0; h < H; ++h)
-            bst(rdae, (e * H + h) * 4, sDL[(h * 32 + ti) * DS + tj] + sSh[h * 32 + ti]);
+          for (int hl = 0; hl < nhs; ++hl)
+            bst(rdae, (e * H + h0 + hl) * 4, sDL[(hl * 32 + ti) * DS + tj] + sSh[hl * 32 + ti]);
         }
       }
     }
   }
   // ---- dxs columns [HC, ldx): d a_src[h][j] = Σ_i dl[h][i][j] (two lanes per
-  //      column, 16 rows each), d a_dst, zero padding ----
-  for (int q = t; q < 2 * 32 * H; q += THREADS) {
-    const int h = q >> 6, j = (q >> 1) & 31, part = q & 1;
-    const float* col = sDL + (h * 32 + 16 * part) * DS + j;
+  //      column, 16 rows each), d a_dst, zero padding (split 0) ----
+  for (int q = t; q < 2 * 32 * nhs; q += THREADS) {
+    const int hl = q >> 6, j = (q >> 1) & 31, part = q & 1;
+    const float* col = sDL + (hl * 32 + 16 * part) * DS + j;
     float v = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) v += col[r * DS];
     v += __shfl_xor(v, 1, 64);
-    bst(rdx, (part == 0 && j < n) ? (j * ldx + HC + h) * 4 : OOB, v);
+    bst(rdx, (part == 0 && j < n) ? (j * ldx + HC + h0 + hl) * 4 : OOB, v);
   }
-  const int ntail = ldx - HC - H;  // d a_dst columns, then zero padding
-  for (int q = t; q < 32 * ntail; q += THREADS) {
-    const int j = q & 31, c2 = q >> 5;
-    const float v = c2 < H ? sDad[c2 * 32 + j] : 0.f;
-    bst(rdx, j < n ? (j * ldx + HC + H + c2) * 4 : OOB, v);
+  for (int q = t; q < 32 * nhs; q += THREADS) {
+    const int j = q & 31, hl = q >> 5;
+    bst(rdx, j < n ? (j * ldx + HC + H + h0 + hl) * 4 : OOB, sDad[hl * 32 + j]);
   }
+  const int npad = ldx - HC - 2 * H;
+  if (split == 0)
+    for (int q = t; q < 32 * npad; q += THREADS) {
+      const int j = q & 31, c2 = q >> 5;
+      bst(rdx, j < n ? (j * ldx + HC + 2 * H + c2) * 4 : OOB, 0.f);
+    }
   SV2N_STAMP(12, SV2N_T());
   SV2N_STAMP(13, SV2N_RT());
 }
@@ -588,9 +654,43 @@ extern "C" int sv2n_diag_stamps(unsigned long long* out, int64_t count) {
 #endif
 
 // ---- launchers (called by the C-ABI entry points in sv2n_attn.hip) ---------
-size_t attn_canon_bwd_lds(int H) {
-  return sizeof(float) * ((size_t)H * 32 * canon::PS + 4 * 2 * 32 * canon::CS +
-                          (size_t)H * 32 * canon::DS + 2 * (size_t)H * 32 + 32) +
+// Workgroups per graph.  The batch alone fills the chip at >= 512 blocks
+// (2 per CU: C2's 512 graphs ran slower split, 27.8 vs 21 us forward); below that a graph's work is split: forward by work items
+// (every split recomputes the softmax), backward by heads and, inside a
+// split, a head's chunks over WPH waves.
+constexpr int64_t CANON_FILL = 512;
+
+static int canon_fwd_splits(int64_t B, int H, int C, bool concat) {
+  const int ntc = (C + 31) >> 5, items = concat ? H * ntc : ntc;
+  int S = 1;
+  while (B * S < CANON_FILL && 4 * 2 * S <= items) S *= 2;
+  return S;
+}
+
+struct CanonBwdPlan {
+  int S, HS, WPH;
+};
+static CanonBwdPlan canon_bwd_plan(int64_t B, int H, int C) {
+  const int nch = (C + 31) >> 5;
+  int S = 1;
+  for (int s = 1; s <= H; ++s) {
+    const int hs = (H + s - 1) / s;
+    if ((H + hs - 1) / hs != s) continue;  // no split without heads
+    S = s;
+    if (B * s >= CANON_FILL) break;
+  }
+  const int HS = (H + S - 1) / S;
+  const int WPH = HS <= 4 ? max(1, min(4 / HS, nch)) : 1;
+  return {S, HS, WPH == 3 ? 2 : WPH};  // WPH divides 4
+}
+
+static unsigned canon_grid(int64_t B, int S) {
+  return (unsigned)(S == 1 ? B : ((B + 7) / 8) * 8 * S);
+}
+
+size_t attn_canon_bwd_lds(int HS) {
+  return sizeof(float) * ((size_t)HS * 32 * canon::PS + 4 * 2 * 32 * canon::CS +
+                          (size_t)HS * 32 * canon::DS + 2 * (size_t)HS * 32 + 32) +
          sizeof(uint16_t) * 32 * 31 / 2;
 }
 
@@ -599,13 +699,15 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
                              const float* xs, int ldx, const float* psave, const uint8_t* keep,
                              float keep_scale, const uint32_t* rowmask, float* dxs, float* dae,
                              int ae_edge_order, float* dbias, int n, int H, int C, float slope) {
-  const size_t lds = attn_canon_bwd_lds(H);
+  const CanonBwdPlan pl = canon_bwd_plan(B, H, C);
+  const size_t lds = attn_canon_bwd_lds(pl.HS);
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)canon::k_bwd<ACT, CONCAT, KEEP>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL((canon::k_bwd<ACT, CONCAT, KEEP>), dim3((unsigned)B), dim3(canon::THREADS),
-                     lds, st, dy, y, xs, ldx, psave, keep, keep_scale, rowmask, dxs, dae,
-                     ae_edge_order, dbias, n, H, C, slope);
+  hipLaunchKernelGGL((canon::k_bwd<ACT, CONCAT, KEEP>), dim3(canon_grid(B, pl.S)),
+                     dim3(canon::THREADS), lds, st, dy, y, xs, ldx, psave, keep, keep_scale,
+                     rowmask, dxs, dae, ae_edge_order, dbias, n, H, C, slope, pl.S, pl.HS, pl.WPH,
+                     B);
 }
 
 void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, const float* xs,
@@ -646,9 +748,10 @@ static void launch_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)canon::k_fwd<ACT, CONCAT, KEEP>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL((canon::k_fwd<ACT, CONCAT, KEEP>), dim3((unsigned)B), dim3(canon::THREADS),
-                     lds, st, xs, ldx, ae, ae_edge_order, rowmask, bias, keep, keep_scale, y,
-                     psave, n, H, C, slope);
+  const int S = canon_fwd_splits(B, H, C, CONCAT);
+  hipLaunchKernelGGL((canon::k_fwd<ACT, CONCAT, KEEP>), dim3(canon_grid(B, S)),
+                     dim3(canon::THREADS), lds, st, xs, ldx, ae, ae_edge_order, rowmask, bias, keep,
+                     keep_scale, y, psave, n, H, C, slope, S, B);
 }
 
 void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,

@@ -132,6 +132,40 @@ __device__ __forceinline__ bool last_block_sc1_2(unsigned* cnt, unsigned nblocks
   return *s_flag != 0;
 }
 
+// Two-level reduction in one launch: every block publishes its partial
+// (st_sc1), the last block of group g = b % 8 sums its group's partials in
+// block order into a group slab (st_sc1), and the last group finisher sums the
+// group slabs in group order.  Deterministic; the serial tail reads nblocks/8
+// + 8 partials per column instead of nblocks.
+__device__ __forceinline__ bool group_last_sc1(unsigned* cnt, unsigned nblocks, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned g = blockIdx.x & 7u;
+    const unsigned members = (nblocks - g + 7u) / 8u;
+    unsigned* gc = cnt + (1 + g) * SV2N_TICKET_STRIDE;
+    const unsigned tk = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = tk == members - 1u;
+    if (last) __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+__device__ __forceinline__ bool top_last_sc1(unsigned* cnt, unsigned nblocks, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned groups = nblocks < 8u ? nblocks : 8u;
+    const unsigned tk = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = tk == groups - 1u;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 // Last-arriving workgroup WITHOUT publication: for when the last arriver
 // reads nothing the others wrote and only needs "everyone is past this
 // point" (e.g. a value every block read at its start may now be replaced).
@@ -251,6 +285,11 @@ __device__ __forceinline__ u32x4 bld4_u32(rsrc_t r, int off) {
 }
 __device__ __forceinline__ void bst(rsrc_t r, int off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void bst2(rsrc_t r, int off, float a, float b) {
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(a), __float_as_uint(b)}, r, off, 0,
+                                        0);
 }
 __device__ __forceinline__ void bst4(rsrc_t r, int off, f32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);

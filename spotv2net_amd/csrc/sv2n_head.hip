@@ -453,6 +453,157 @@ __global__ __launch_bounds__(256) void k_head_mse_train(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Head + MSE training launch, wave-per-rows form (out_features·ceil(C/64) <=
+// 32; every SpotV2Net head: out 1, C 50 / 500).  Wave w of block b owns rows
+// [(4b + w)·RW, +RW); lane l holds columns l + 64k (k < KC) of W in registers
+// and of each row it reads (dword loads, 256 B per instruction; RB rows in
+// flight).  Per row: the dot by a wave reduction, diff, the squared-error
+// term, dx = dout ⊗ W (coalesced stores), and the weight / bias gradient
+// partials in registers.  The block adds its 4 waves' partials in wave order
+// through LDS and publishes one [OUT][C+1] + loss partial; the launch then
+// reduces the partials in two levels (group_last_sc1 / top_last_sc1: group
+// g = b % 8 sums blocks g, g + 8, ... in order, the last group finisher the 8
+// groups in order).  The block-at-a-time kernel above read every partial in
+// one workgroup: C3 (240 partials of 502 floats) spent most of its 33 us there.
+// ---------------------------------------------------------------------------
+template <int OUT, int KC>
+__global__ __launch_bounds__(256) void k_head_mse_train_w(
+    const float* __restrict__ x, int64_t N, int C, const float* __restrict__ W,
+    const float* __restrict__ b, const float* __restrict__ target, float* __restrict__ dx,
+    float* __restrict__ ws, float* __restrict__ gW, float* __restrict__ gb,
+    float* __restrict__ loss, float inv_count, float scale, int RW) {
+  constexpr int RB = KC >= 8 ? 4 : (KC >= 4 ? 8 : 16);  // rows in flight per wave
+  extern __shared__ __attribute__((aligned(16))) float s_w4[];  // [4][stride] wave partials
+  __shared__ int s_flag;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int CP = C + 1, stride = OUT * CP + 1;  // [o][c], [o][C] bias, [OUT·CP] loss
+  float w[OUT][KC], bo[OUT], gw[OUT][KC], gbs[OUT];
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) {
+    bo[o] = b ? b[o] : 0.f;
+    gbs[o] = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int c = lane + 64 * k;
+      w[o][k] = c < C ? W[o * C + c] : 0.f;
+      gw[o][k] = 0.f;
+    }
+  }
+  float sq = 0.f;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * RW;
+  const int nr = (int)max((int64_t)0, min((int64_t)RW, N - r0));
+  for (int i0 = 0; i0 < nr; i0 += RB) {
+    float xv[RB][KC], tv[RB][OUT];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const bool rv = i0 + u < nr;
+      const int64_t r = r0 + i0 + u;
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        const int c = lane + 64 * k;
+        xv[u][k] = (rv && c < C) ? x[r * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) tv[u][o] = rv ? target[r * OUT + o] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      if (i0 + u >= nr) continue;  // wave-uniform
+      const int64_t r = r0 + i0 + u;
+      float d[OUT];
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) {
+        float p = 0.f;
+#pragma unroll
+        for (int k = 0; k < KC; ++k) p = fmaf(xv[u][k], w[o][k], p);
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) p += __shfl_xor(p, m, 64);
+        const float e = p + bo[o] - tv[u][o];
+        sq = fmaf(e, e, sq);
+        d[o] = e * scale;
+        gbs[o] += d[o];
+      }
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        const int c = lane + 64 * k;
+        float v = 0.f;
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) {
+          v = fmaf(d[o], w[o][k], v);
+          gw[o][k] = fmaf(d[o], xv[u][k], gw[o][k]);
+        }
+        if (c < C) dx[r * C + c] = v;
+      }
+    }
+  }
+  // block partial: the 4 waves in order
+  float* sp = s_w4 + wave * stride;
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) {
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int c = lane + 64 * k;
+      if (c < C) sp[o * CP + c] = gw[o][k];
+    }
+    if (lane == 0) sp[o * CP + C] = gbs[o];
+  }
+  if (lane == 0) sp[OUT * CP] = sq;  // every lane holds the same sum
+  __syncthreads();
+  float* part = ws + HEAD_WS_HDR;
+  const unsigned nb = gridDim.x;
+  for (int oc = t; oc < stride; oc += 256)
+    st_sc1(part + (int64_t)blockIdx.x * stride + oc,
+           (s_w4[oc] + s_w4[stride + oc]) + (s_w4[2 * stride + oc] + s_w4[3 * stride + oc]));
+  if (!group_last_sc1(reinterpret_cast<unsigned*>(ws), nb, &s_flag)) return;
+  // group g: blocks g, g + 8, ... in order -> group slab g
+  float* gslab = part + (int64_t)nb * stride;
+  const unsigned g = blockIdx.x & 7u, members = (nb - g + 7u) / 8u;
+  for (int oc = t; oc < stride; oc += 256) {
+    float s = 0.f;
+    for (unsigned m0 = 0; m0 < members; m0 += 32) {
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
+        v[u] = m0 + u < members ? ld_sc1(part + (int64_t)(g + 8u * (m0 + u)) * stride + oc) : 0.f;
+#pragma unroll
+      for (int u = 0; u < 32; ++u) s += v[u];
+    }
+    st_sc1(gslab + (int64_t)g * stride + oc, s);
+  }
+  if (!top_last_sc1(reinterpret_cast<unsigned*>(ws), nb, &s_flag)) return;
+  const int groups = nb < 8u ? (int)nb : 8;
+  for (int oc = t; oc < stride; oc += 256) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = u < groups ? ld_sc1(gslab + (int64_t)u * stride + oc) : 0.f;
+    const float s = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+    if (oc == OUT * CP) {
+      loss[0] = s * inv_count;
+    } else {
+      const int o = oc / CP, c = oc - o * CP;
+      if (c < C) {
+        if (gW) gW[o * C + c] += s;
+      } else if (gb) {
+        gb[o] += s;
+      }
+    }
+  }
+}
+
+// rows per wave of k_head_mse_train_w: enough waves to fill the chip once
+// (<= 256 blocks of 4 waves)
+static inline int head_w_rows(int64_t N) { return (int)std::max<int64_t>(1, (N + 1023) / 1024); }
+static inline int head_w_kc(int C) {
+  const int kc = (C + 63) / 64;
+  return kc <= 1 ? 1 : kc <= 2 ? 2 : kc <= 4 ? 4 : kc <= 8 ? 8 : 16;
+}
+static inline bool head_w_ok(int C, int O) { return O <= 4 && O * head_w_kc(C) <= 32; }
+static inline int64_t head_w_blocks(int64_t N) {
+  const int64_t rw = head_w_rows(N);
+  return (N + 4 * rw - 1) / (4 * rw);
+}
+
 }  // namespace sv2n
 
 using namespace sv2n;
@@ -572,8 +723,10 @@ extern "C" int sv2n_head_mse_bwd(const float* x, int64_t num_rows, int in_featur
 
 extern "C" int64_t sv2n_head_mse_train_workspace(int64_t num_rows, int in_features,
                                                  int out_features) {
-  return HEAD_WS_HDR + head_bwd_blocks(num_rows, in_features, out_features) *
-                           ((int64_t)out_features * (in_features + 1) + 1);
+  const int64_t stride = (int64_t)out_features * (in_features + 1) + 1;
+  if (head_w_ok(in_features, out_features))  // block partials + 8 group slabs
+    return HEAD_WS_HDR + (head_w_blocks(num_rows) + 8) * stride;
+  return HEAD_WS_HDR + head_bwd_blocks(num_rows, in_features, out_features) * stride;
 }
 
 extern "C" int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_features,
@@ -587,11 +740,28 @@ extern "C" int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_feat
   if (workspace_floats < sv2n_head_mse_train_workspace(num_rows, in_features, out_ch))
     return SV2N_ERR_WORKSPACE;
   if ((uintptr_t)workspace & 15) return SV2N_ERR_ALIGN;
+  const float inv_count = 1.f / (float)(num_rows * out_ch);
+  const float scale = 2.f / (float)(num_rows * (int64_t)out_ch);
+  if (head_w_ok(in_features, out_ch)) {
+    const int C = in_features, RW = head_w_rows(num_rows), kc = head_w_kc(C);
+    const unsigned grid = (unsigned)head_w_blocks(num_rows);
+    const size_t lds = sizeof(float) * 4 * ((size_t)out_ch * (C + 1) + 1);
+#define SV2N_HW(O, K)                                                                           \
+  if (out_ch == O && kc == K) {                                                                 \
+    hipLaunchKernelGGL((k_head_mse_train_w<O, K>), dim3(grid), dim3(256), lds, stream, x,      \
+                       num_rows, C, weight, bias, target, dx, workspace, g_weight, g_bias, loss, \
+                       inv_count, scale, RW);                                                   \
+    return (int)hipGetLastError();                                                              \
+  }
+    SV2N_HW(1, 1) SV2N_HW(1, 2) SV2N_HW(1, 4) SV2N_HW(1, 8) SV2N_HW(1, 16)
+    SV2N_HW(2, 1) SV2N_HW(2, 2) SV2N_HW(2, 4) SV2N_HW(2, 8) SV2N_HW(2, 16)
+    SV2N_HW(3, 1) SV2N_HW(3, 2) SV2N_HW(3, 4) SV2N_HW(3, 8)
+    SV2N_HW(4, 1) SV2N_HW(4, 2) SV2N_HW(4, 4) SV2N_HW(4, 8)
+#undef SV2N_HW
+  }
   const int R = head_rows_per_block(in_features, out_ch, num_rows);
   const unsigned grid = (unsigned)((num_rows + R - 1) / R);
   const size_t lds = head_lds_bytes(in_features, out_ch, num_rows);
-  const float inv_count = 1.f / (float)(num_rows * out_ch);
-  const float scale = 2.f / (float)(num_rows * (int64_t)out_ch);
   SV2N_HEAD_DISPATCH(k_head_mse_train, dim3(grid), dim3(256), lds, stream, x, num_rows,
                      in_features, weight, bias, target, dx, workspace, g_weight, g_bias, loss,
                      inv_count, scale, R)

@@ -141,3 +141,26 @@ def test_no_bias(dev, concat):
     mine, ref = twin_conv(12, 7, 3, concat, 4, seed=12, bias=False)
     ei = block_graphs(2, 30)
     _run(mine, ref, torch.randn(60, 12), ei, torch.randn(ei.size(1), 4), dev)
+
+
+@pytest.mark.parametrize("B,heads,C,concat", [
+    (3, 6, 70, True),     # fwd 4 splits; bwd 6 splits of 1 head, 3 chunks over 2 waves
+    (3, 6, 70, False),    # the same for the head mean (bias partial from head 0's split)
+    (3, 2, 260, False),   # fwd: 9 tiles over 2 splits (mean over heads per tile); bwd 4 waves
+    (3, 2, 100, True),    # bwd: 2 splits, a head's 4 chunks over 4 waves
+    (300, 3, 40, True),   # bwd: 2 splits of 2 + 1 heads (the last split half empty)
+    (100, 5, 40, False),  # bwd: 5 splits of 1 head, 2 chunks over 2 waves
+    (1024, 8, 4, True),   # one workgroup per graph, 2 heads per wave (at B = 1000 / 1100
+                          # these seeds put an attention logit on the leaky-ReLU kink)
+])
+def test_workgroup_splits(dev, B, heads, C, concat):
+    """n <= 32 attention with a graph's work spread over several workgroups
+    (sv2n_attn_canon.hip: canon_fwd_splits / canon_bwd_plan pick the split
+    from the batch size; C3's 128 graphs of 6 x 500 columns run 4 forward and
+    6 backward workgroups per graph)."""
+    n = 30
+    mine, ref = twin_conv(12, C, heads, concat, 3, seed=B + heads)
+    torch.manual_seed(B)
+    x = torch.randn(B * n, 12)
+    ei = block_graphs(B, n)
+    _run(mine, ref, x, ei, torch.randn(ei.size(1), 3), dev)

@@ -104,16 +104,16 @@ def test_fused_head_mse_matches_unfused(dev, out_ch):
         assert_close(p.grad, q.grad, tol=1e-6, what=n)
 
 
-@pytest.mark.parametrize("out_ch,rows", [(1, 15360), (3, 180), (14, 1000)])
-def test_head_mse_train_matches_fwd_bwd(dev, out_ch, rows):
+@pytest.mark.parametrize("out_ch,rows,C", [(1, 15360, 50), (3, 180, 50), (14, 1000, 50),
+                                           (1, 3840, 500), (4, 1001, 500), (2, 777, 130)])
+def test_head_mse_train_matches_fwd_bwd(dev, out_ch, rows, C):
     """sv2n_head_mse_train (one launch: loss, dx, accumulated head grads) ==
-    sv2n_head_mse_fwd + sv2n_head_mse_bwd with grad_loss = 1: dx bit for bit
-    (same products and order), the parameter gradients and the loss within
-    float rounding (the last-block combine groups the per-block partials
-    differently: both orders fixed); the C2 head shape (15,360 x 50) included."""
+    sv2n_head_mse_fwd + sv2n_head_mse_bwd with grad_loss = 1, within float
+    rounding (the wave-per-rows kernel for out <= 4 sums each row's dot product
+    and the gradient partials in its own fixed order); the C2 (15,360 x 50) and
+    C3 (3,840 x 500) head shapes included; deterministic."""
     ops = torch.ops.sv2n
     torch.manual_seed(3)
-    C = 50
     x = torch.randn(rows, C, device=dev)
     W = torch.randn(out_ch, C, device=dev) * 0.1
     b = torch.randn(out_ch, device=dev)
@@ -124,12 +124,13 @@ def test_head_mse_train_matches_fwd_bwd(dev, out_ch, rows):
     loss2, diff = ops.head_mse_fwd(x, W, b, y)
     dx2 = ops.head_mse_bwd(x, W, diff, torch.ones((), device=dev), gw2, gb2)
     assert_close(loss1, loss2, tol=1e-6, what="loss")
-    assert torch.equal(dx1, dx2)
+    assert_close(dx1, dx2, tol=1e-6, what="dx")
     assert_close(gw1, gw2, tol=1e-6, what="g_weight")
     assert_close(gb1, gb2, tol=1e-6, what="g_bias")
     gw3, gb3 = torch.full_like(W, 0.5), torch.full_like(b, 0.25)
-    ops.head_mse_train(x, W, b, y, gw3, gb3)
+    loss3, dx3 = ops.head_mse_train(x, W, b, y, gw3, gb3)
     assert torch.equal(gw1, gw3) and torch.equal(gb1, gb3)  # deterministic
+    assert torch.equal(loss1, loss3) and torch.equal(dx1, dx3)
 
 
 def test_trainstep_fused_head_matches_reference_steps(dev):

@@ -1,7 +1,7 @@
 """Phase timeline of the canonical attention kernels (diagnostic build).
 
 Build:  make STAMPS=1 LIB=spotv2net_amd/libsv2n_stamps.so BUILD=build/stamps
-Run:    SV2N_LIB=spotv2net_amd/libsv2n_stamps.so python tools/stamps.py [B]
+Run:    SV2N_LIB=spotv2net_amd/libsv2n_stamps.so python tools/stamps.py [B | c3]
 
 Launches the C2 layer-0 attention forward and backward once each (after a
 warm-up) through the C-ABI and prints, per phase, the median and max over
@@ -36,6 +36,51 @@ def report(name, st, phases, rt0, rt1):
     for a, b, label in phases:
         d = st[:, :, b] - st[:, :, a]
         print(f"   {label:28s} median {np.median(d):8.0f}  p90 {np.percentile(d, 90):8.0f}  max {d.max():8.0f} cyc")
+
+
+def main_c3(B=128):
+    """C3 shape: 6 heads x 500, head mean, F 1260 (ldx 3012), split launches."""
+    dev = torch.device("cuda", 0)
+    lib = ops._lib.load()
+    lib.sv2n_diag_stamps.restype = ctypes.c_int
+    lib.sv2n_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    n, H, C, ldx = 30, 6, 500, 3012
+    torch.manual_seed(0)
+    xs = torch.randn(B * n, ldx, device=dev) * 0.1
+    ae = torch.randn(B * n * (n - 1), H, device=dev)
+    bias = torch.randn(C, device=dev)
+    y = torch.empty(B * n, C, device=dev)
+    ps = torch.empty(B, H, 32, 32, device=dev)
+    dy = torch.randn_like(y)
+    dxs = torch.empty_like(xs)
+    dae = torch.empty_like(ae)
+    dbp = torch.empty(B, C, device=dev)
+
+    def fwd():
+        assert lib.sv2n_gat_attn_fwd(xs.data_ptr(), ldx, ae.data_ptr(), 1, None, bias.data_ptr(),
+                                     None, 1.0, y.data_ptr(), ps.data_ptr(), B, n, H, C, 0, 1,
+                                     0.2, sh) == 0
+
+    def bwd():
+        assert lib.sv2n_gat_attn_bwd(dy.data_ptr(), y.data_ptr(), xs.data_ptr(), ldx,
+                                     ps.data_ptr(), None, 1.0, None, dxs.data_ptr(),
+                                     dae.data_ptr(), 1, dbp.data_ptr(), B, n, H, C, 0, 1, 0.2,
+                                     sh) == 0
+
+    for _ in range(5):
+        fwd()
+        bwd()
+    fwd()
+    report("fwd C3", read(lib, B * 4),
+           [(1, 2, "prologue loads -> AE staged"), (2, 3, "softmax"), (3, 4, "barrier"),
+            (4, 5, "aggregation + stores")], 0, 6)
+    bwd()
+    report("bwd C3", read(lib, B * 6),
+           [(1, 2, "prologue -> chunk 0 wait"), (2, 3, "stage chunk 0"), (3, 4, "compute 0 + wait 1"),
+            (4, 5, "stage chunk 1"), (5, 6, "compute 1 + wait 2"), (6, 7, "stage chunk 2"),
+            (7, 8, "compute 2 + wait 3"), (8, 9, "stage chunk 3"), (9, 10, "compute 3 + softmax bwd"),
+            (10, 11, "barrier"), (11, 12, "d ae + tail")], 0, 13)
 
 
 def main(B=512):
@@ -88,4 +133,7 @@ def main(B=512):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 512)
+    if len(sys.argv) > 1 and sys.argv[1] == "c3":
+        main_c3()
+    else:
+        main(int(sys.argv[1]) if len(sys.argv) > 1 else 512)
