@@ -128,7 +128,7 @@ def kernel_table(model, data, reps=50):
     def attn_fwd():
         lib.sv2n_gat_attn_fwd(xs0.data_ptr(), xs0.stride(0), ae[0].data_ptr(), 1, None,
                               conv0.bias.data_ptr(), None, 1.0, y0.data_ptr(), ps0.data_ptr(),
-                              B, N_NODES, HEADS, conv0.out_channels, 1, 1, 0.2, sh)
+                              None, 0.0, None, B, N_NODES, HEADS, conv0.out_channels, 1, 1, 0.2, sh)
 
     dy0 = torch.randn_like(y0)
     dxs0 = torch.empty_like(xs0)
@@ -137,7 +137,8 @@ def kernel_table(model, data, reps=50):
 
     def attn_bwd():
         lib.sv2n_gat_attn_bwd(dy0.data_ptr(), y0.data_ptr(), xs0.data_ptr(), xs0.stride(0),
-                              ps0.data_ptr(), None, 1.0, None, dxs0.data_ptr(), dae0.data_ptr(),
+                              ps0.data_ptr(), None, 1.0, None, 0.0, None, dxs0.data_ptr(),
+                              dae0.data_ptr(),
                               1, dbp.data_ptr(), B, N_NODES, HEADS, conv0.out_channels, 1, 1, 0.2,
                               sh)
 
@@ -352,7 +353,8 @@ def kernel_table_c3(model, cfg, precision, reps=20):
 
     def attn_fwd():
         lib.sv2n_gat_attn_fwd(xs.data_ptr(), ldx, ae.data_ptr(), 1, None, conv.bias.data_ptr(),
-                              None, 1.0, y.data_ptr(), ps.data_ptr(), B, n, H, C, 0, 1, 0.2, sh)
+                              None, 1.0, y.data_ptr(), ps.data_ptr(), None, 0.0, None, B, n, H,
+                              C, 0, 1, 0.2, sh)
 
     attn_fwd()
     dy = torch.randn_like(y)
@@ -362,7 +364,7 @@ def kernel_table_c3(model, cfg, precision, reps=20):
 
     def attn_bwd():
         lib.sv2n_gat_attn_bwd(dy.data_ptr(), y.data_ptr(), xs.data_ptr(), ldx, ps.data_ptr(),
-                              None, 1.0, None, dxs2.data_ptr(), dae.data_ptr(), 1,
+                              None, 1.0, None, 0.0, None, dxs2.data_ptr(), dae.data_ptr(), 1,
                               dbp2.data_ptr(), B, n, H, C, 0, 1, 0.2, sh)
 
     peak = BF16_MFMA_PEAK_TFLOPS if bf16 else BF16X3_PEAK_TFLOPS

@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 8
+#define SV2N_ABI_VERSION 9
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -128,11 +128,17 @@ int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, int edge_dim
  *   y       [N][concat ? H*C : C] = act(concat|mean(Σ_j p_ij·xs_j) + bias).
  *   psave   [num_graphs][H][32][32] softmax probabilities (pre-dropout; rows
  *           padded to 32, absent edges 0) whose sign bit records leaky_relu's
- *           negative side (for the backward). */
+ *           negative side (for the backward).
+ *   post_u  GATModel's dropout after the layer (utils/models.py:148, ABI 9):
+ *           NULL, or [N][OC] uniform draws; then post_out [N][OC] =
+ *           y · (post_u >= post_p) / (1 - post_p), 0 <= post_p < 1, written
+ *           beside y (the layer's output; y stays the activation the backward
+ *           reads). */
 int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, int ae_edge_order,
                       const uint32_t* rowmask,
                       const float* bias, const uint8_t* keep, float keep_scale,
                       float* y, float* psave,
+                      const float* post_u, float post_p, float* post_out,
                       int64_t num_graphs, int n, int heads, int channels, int concat,
                       int act, float negative_slope, hipStream_t stream);
 
@@ -142,9 +148,12 @@ int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, int ae_edge_ord
  *   dae     gradient w.r.t. ae in the layout ae_edge_order names
  *           ([num_graphs][n][n][H] with diagonal / absent entries 0, or
  *           [num_graphs*n(n-1)][H]), or NULL when the forward ran without ae.
- *   dbias_partial [num_graphs][OC] per-graph bias-gradient partial sums. */
+ *   dbias_partial [num_graphs][OC] per-graph bias-gradient partial sums.
+ *   post_u, post_p  the forward's post-layer dropout draws (or NULL): dy is
+ *           then the gradient w.r.t. post_out and is masked and scaled first. */
 int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* xs, int ldx,
                       const float* psave, const uint8_t* keep, float keep_scale,
+                      const float* post_u, float post_p,
                       const uint32_t* rowmask, float* dxs, float* dae, int ae_edge_order,
                       float* dbias_partial,
                       int64_t num_graphs, int n, int heads, int channels, int concat,

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SV2N_LIB: an alternative build of the same library (diagnostic builds, e.g.
 # tools/stamps.py); default the in-tree one
 LIB_PATH = os.environ.get("SV2N_LIB") or os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p
@@ -52,10 +52,10 @@ _SIGNATURES = {
     "sv2n_edge_logits_bwd_workspace": (_i64, [_i32, _i32]),
     "sv2n_edge_logits_bwd": (_i32, [_p, _i64, _i32, _p, _p, _p, _i32, _i32, _i64, _i32, _p, _i64, _p,
                                     _i32, _p]),
-    "sv2n_gat_attn_fwd": (_i32, [_p, _i32, _p, _i32, _p, _p, _p, _f32, _p, _p, _i64, _i32, _i32, _i32,
-                                 _i32, _i32, _f32, _p]),
-    "sv2n_gat_attn_bwd": (_i32, [_p, _p, _p, _i32, _p, _p, _f32, _p, _p, _p, _i32, _p, _i64, _i32,
-                                 _i32, _i32, _i32, _i32, _f32, _p]),
+    "sv2n_gat_attn_fwd": (_i32, [_p, _i32, _p, _i32, _p, _p, _p, _f32, _p, _p, _p, _f32, _p, _i64,
+                                 _i32, _i32, _i32, _i32, _i32, _f32, _p]),
+    "sv2n_gat_attn_bwd": (_i32, [_p, _p, _p, _i32, _p, _p, _f32, _p, _f32, _p, _p, _p, _i32, _p,
+                                 _i64, _i32, _i32, _i32, _i32, _i32, _f32, _p]),
     "sv2n_gat_attn_tiled_workspace": (_i64, [_i64, _i32, _i32, _i32, _i32]),
     "sv2n_gat_attn_tiled_fwd": (_i32, [_p, _i32, _p, _i64, _p, _p, _p, _p, _f32, _p, _p, _i64,
                                        _i64, _i32, _i32, _i32, _i32, _i32, _f32, _p]),

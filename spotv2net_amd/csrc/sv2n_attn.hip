@@ -13,11 +13,12 @@
 namespace sv2n {
 void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
                     int ae_edge_order, const uint32_t* rowmask, const float* bias,
-                    const uint8_t* keep, float keep_scale, float* y, float* psave, int n, int H,
-                    int C, int concat, int act, float slope);
+                    const uint8_t* keep, float keep_scale, float* y, float* psave,
+                    const float* post_u, float post_p, float* post_out, int n, int H, int C,
+                    int concat, int act, float slope);
 void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, const float* xs,
                     int ldx, const float* psave, const uint8_t* keep, float keep_scale,
-                    const uint32_t* rowmask, float* dxs, float* dae, int ae_edge_order,
+                    const float* post_u, float post_p, const uint32_t* rowmask, float* dxs, float* dae, int ae_edge_order,
                     float* dbias, int n, int H, int C, int concat, int act, float slope);
 }  // namespace sv2n
 
@@ -33,27 +34,32 @@ static int check_attn_args(int64_t B, int n, int H, int C, int ldx, int act) {
 
 extern "C" int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, int ae_edge_order,
                                  const uint32_t* rowmask, const float* bias, const uint8_t* keep,
-                                 float keep_scale, float* y, float* psave, int64_t num_graphs,
-                                 int n, int heads, int channels, int concat, int act,
+                                 float keep_scale, float* y, float* psave, const float* post_u,
+                                 float post_p, float* post_out, int64_t num_graphs, int n,
+                                 int heads, int channels, int concat, int act,
                                  float negative_slope, hipStream_t stream) {
   if (!xs || !y || !psave) return SV2N_ERR_ARG;
   if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
   if (ae_edge_order && (rowmask || n < 2)) return SV2N_ERR_ARG;  // complete graphs only
+  if (post_u && (!post_out || !(post_p >= 0.f && post_p < 1.f))) return SV2N_ERR_ARG;
   attn_canon_fwd(num_graphs, stream, xs, ldx, ae, ae_edge_order, rowmask, bias, keep,
-                 keep_scale, y, psave, n, heads, channels, concat, act, negative_slope);
+                 keep_scale, y, psave, post_u, post_p, post_out, n, heads, channels, concat, act,
+                 negative_slope);
   return (int)hipGetLastError();
 }
 
 extern "C" int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* xs, int ldx,
                                  const float* psave, const uint8_t* keep, float keep_scale,
-                                 const uint32_t* rowmask, float* dxs, float* dae,
-                                 int ae_edge_order, float* dbias_partial, int64_t num_graphs, int n,
-                                 int heads, int channels, int concat, int act,
-                                 float negative_slope, hipStream_t stream) {
+                                 const float* post_u, float post_p, const uint32_t* rowmask,
+                                 float* dxs, float* dae, int ae_edge_order, float* dbias_partial,
+                                 int64_t num_graphs, int n, int heads, int channels, int concat,
+                                 int act, float negative_slope, hipStream_t stream) {
   if (!dy || !y || !xs || !psave || !dxs || !dbias_partial) return SV2N_ERR_ARG;
   if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
   if (ae_edge_order && (rowmask || n < 2)) return SV2N_ERR_ARG;  // complete graphs only
-  attn_canon_bwd(num_graphs, stream, dy, y, xs, ldx, psave, keep, keep_scale, rowmask, dxs,
+  if (post_u && !(post_p >= 0.f && post_p < 1.f)) return SV2N_ERR_ARG;
+  attn_canon_bwd(num_graphs, stream, dy, y, xs, ldx, psave, keep, keep_scale, post_u, post_p,
+                 rowmask, dxs,
                  dae, ae_edge_order, dbias_partial, n, heads, channels, concat, act,
                  negative_slope);
   return (int)hipGetLastError();

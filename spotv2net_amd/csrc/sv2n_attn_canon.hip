@@ -78,8 +78,9 @@ template <int ACT, bool CONCAT, bool KEEP>
 __global__ __launch_bounds__(THREADS) void k_fwd(
     const float* __restrict__ xs, int ldx, const float* __restrict__ ae, int ae_edge_order,
     const uint32_t* __restrict__ rowmask, const float* __restrict__ bias, const uint8_t* __restrict__ keep, float keep_scale,
-    float* __restrict__ y, float* __restrict__ psave, int n, int H, int C, float slope, int S,
-    int64_t B) {
+    float* __restrict__ y, float* __restrict__ psave, const float* __restrict__ post_u,
+    float post_p, float post_scale, float* __restrict__ post_out, int n, int H, int C, float slope,
+    int S, int64_t B) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sP = smem;
   float* sAS = sP + H * 32 * PS;
@@ -102,6 +103,10 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
   const rsrc_t ry = make_rsrc(y + (int64_t)g * n * OC, (uint32_t)(n * OC) * 4u);
   const rsrc_t rp = make_rsrc(psave + (int64_t)g * H * 1024, (uint32_t)H * 4096u);
   const rsrc_t rb = make_rsrc(bias, bias ? (uint32_t)OC * 4u : 0u);
+  const bool post = post_u != nullptr;  // dropout after the layer, fused into the store
+  const rsrc_t ru = make_rsrc(post ? post_u + g * n * OC : nullptr, post ? (uint32_t)(n * OC) * 4u : 0u);
+  const rsrc_t ro = make_rsrc(post ? post_out + g * n * OC : nullptr,
+                              post ? (uint32_t)(n * OC) * 4u : 0u);
 
   // ---- work items of this wave: q -> (head, tile), first / last sub-item ----
   const int nq = CONCAT ? max(0, (H * ntc - slot + NS - 1) / NS)
@@ -276,9 +281,16 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const float invH = 1.f / (float)H;
+  float uv[16];  // post-dropout draws of the work item's outputs (loaded at its first sub-item)
   auto run = [&](int q, const float (&b)[16]) {
     int h, tc;
     item(q, h, tc);
+    if (post && (CONCAT || h == 0)) {
+      const int c = 32 * tc + l32;
+      const int voff = c < C ? (4 * half * OC + (CONCAT ? h * C : 0) + c) * 4 : OOB;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) uv[r] = bld_s(ru, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4);
+    }
     const f32x4* pa = reinterpret_cast<const f32x4*>(sP + (h * 32 + l32) * PS + 16 * half);
     f32x4 a4[4];
 #pragma unroll
@@ -295,7 +307,10 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float z = (CONCAT ? acc[r] : acc[r] * invH) + bv;
-        bst_s(ry, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4, act_fwd<ACT>(z));
+        const float a = act_fwd<ACT>(z);
+        bst_s(ry, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4, a);
+        if (post)
+          bst_s(ro, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4, uv[r] >= post_p ? a * post_scale : 0.f);
         acc[r] = 0.f;
       }
     }
@@ -345,6 +360,7 @@ template <int ACT, bool CONCAT, bool KEEP>
 __global__ __launch_bounds__(THREADS) void k_bwd(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ xs,
     int ldx, const float* __restrict__ psave, const uint8_t* __restrict__ keep, float keep_scale,
+    const float* __restrict__ post_u, float post_p, float post_scale,
     const uint32_t* __restrict__ rowmask, float* __restrict__ dxs, float* __restrict__ dae,
     int ae_edge_order, float* __restrict__ dbias_part, int n, int H, int C, float slope, int S,
     int HS, int WPH, int64_t B) {
@@ -374,6 +390,8 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   const rsrc_t ryy = make_rsrc(y + g * n * OC, (uint32_t)(n * OC) * 4u);
   const rsrc_t rps = make_rsrc(psave + g * H * 1024, (uint32_t)H * 4096u);
   const rsrc_t rdb = make_rsrc(dbias_part + g * OC, (uint32_t)OC * 4u);
+  const bool post = post_u != nullptr;  // dy is the gradient of the post-dropout output
+  const rsrc_t ru = make_rsrc(post ? post_u + g * n * OC : nullptr, post ? (uint32_t)(n * OC) * 4u : 0u);
 
   float* sX = sArea + wave * 2 * 32 * CS;
   float* sZ = sX + 32 * CS;
@@ -386,7 +404,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 
   // chunk step q: rows 2m + half, column l32 of the chunk (dword loads, the
   // row stride in the scalar offset)
-  float rx_[16], rdy_[16], ry_[16];
+  float rx_[16], rdy_[16], ry_[16], ru_[16];
   auto load_chunk = [&](int q) {
     const int hq = q / ncw, ch = sub + WPH * (q - hq * ncw), h = h0 + grp + NG * hq;
     const int c = cwb * ch + l32;
@@ -398,6 +416,10 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       rx_[m] = bld_s(rx, xo, 2 * m * ldx * 4);
       rdy_[m] = bld_s(rdy, zo, 2 * m * OC * 4);
       ry_[m] = bld_s(ryy, zo, 2 * m * OC * 4);
+    }
+    if (post) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) ru_[m] = bld_s(ru, zo, 2 * m * OC * 4);
     }
   };
   // saved probabilities / keep bytes of head h at lane i's output rows
@@ -500,7 +522,8 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     for (int m = 0; m < 16; ++m) {
       const int row = 2 * m + half;
       sX[row * CS + l32] = rx_[m];
-      sZ[row * CS + l32] = act_bwd<ACT>(rdy_[m], ry_[m]);
+      const float d = post ? (ru_[m] >= post_p ? rdy_[m] * post_scale : 0.f) : rdy_[m];
+      sZ[row * CS + l32] = act_bwd<ACT>(d, ry_[m]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes, in order
     SV2N_STAMP(3 + 2 * min(q, 3), SV2N_T());
@@ -697,7 +720,8 @@ size_t attn_canon_bwd_lds(int HS) {
 template <int ACT, bool CONCAT, bool KEEP>
 static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y,
                              const float* xs, int ldx, const float* psave, const uint8_t* keep,
-                             float keep_scale, const uint32_t* rowmask, float* dxs, float* dae,
+                             float keep_scale, const float* post_u, float post_p,
+                             const uint32_t* rowmask, float* dxs, float* dae,
                              int ae_edge_order, float* dbias, int n, int H, int C, float slope) {
   const CanonBwdPlan pl = canon_bwd_plan(B, H, C);
   const size_t lds = attn_canon_bwd_lds(pl.HS);
@@ -705,18 +729,19 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
     (void)hipFuncSetAttribute((const void*)canon::k_bwd<ACT, CONCAT, KEEP>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipLaunchKernelGGL((canon::k_bwd<ACT, CONCAT, KEEP>), dim3(canon_grid(B, pl.S)),
-                     dim3(canon::THREADS), lds, st, dy, y, xs, ldx, psave, keep, keep_scale,
-                     rowmask, dxs, dae, ae_edge_order, dbias, n, H, C, slope, pl.S, pl.HS, pl.WPH,
-                     B);
+                     dim3(canon::THREADS), lds, st, dy, y, xs, ldx, psave, keep, keep_scale, post_u,
+                     post_p, post_u ? (float)(1.0 / (1.0 - (double)post_p)) : 1.f, rowmask, dxs,
+                     dae, ae_edge_order, dbias, n, H, C, slope, pl.S, pl.HS, pl.WPH, B);
 }
 
 void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, const float* xs,
                     int ldx, const float* psave, const uint8_t* keep, float keep_scale,
-                    const uint32_t* rowmask, float* dxs, float* dae, int ae_edge_order,
-                    float* dbias, int n, int H, int C, int concat, int act, float slope) {
-#define SV2N_CB(A, CC, K)                                                                  \
-  launch_canon_bwd<A, CC, K>(B, st, dy, y, xs, ldx, psave, keep, keep_scale, rowmask, dxs, dae, \
-                             ae_edge_order, dbias, n, H, C, slope)
+                    const float* post_u, float post_p, const uint32_t* rowmask, float* dxs,
+                    float* dae, int ae_edge_order, float* dbias, int n, int H, int C, int concat,
+                    int act, float slope) {
+#define SV2N_CB(A, CC, K)                                                                      \
+  launch_canon_bwd<A, CC, K>(B, st, dy, y, xs, ldx, psave, keep, keep_scale, post_u, post_p,   \
+                             rowmask, dxs, dae, ae_edge_order, dbias, n, H, C, slope)
 #define SV2N_CB_ACT(CC, K)                 \
   switch (act) {                           \
     case 0: SV2N_CB(0, CC, K); break;      \
@@ -742,8 +767,9 @@ size_t attn_canon_fwd_lds(int n, int H, bool has_ae, bool edge_order) {
 template <int ACT, bool CONCAT, bool KEEP>
 static void launch_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
                              int ae_edge_order, const uint32_t* rowmask, const float* bias,
-                             const uint8_t* keep, float keep_scale, float* y, float* psave, int n,
-                             int H, int C, float slope) {
+                             const uint8_t* keep, float keep_scale, float* y, float* psave,
+                             const float* post_u, float post_p, float* post_out, int n, int H,
+                             int C, float slope) {
   const size_t lds = attn_canon_fwd_lds(n, H, ae != nullptr, ae_edge_order != 0);
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)canon::k_fwd<ACT, CONCAT, KEEP>,
@@ -751,16 +777,19 @@ static void launch_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx
   const int S = canon_fwd_splits(B, H, C, CONCAT);
   hipLaunchKernelGGL((canon::k_fwd<ACT, CONCAT, KEEP>), dim3(canon_grid(B, S)),
                      dim3(canon::THREADS), lds, st, xs, ldx, ae, ae_edge_order, rowmask, bias, keep,
-                     keep_scale, y, psave, n, H, C, slope, S, B);
+                     keep_scale, y, psave, post_u, post_p,
+                     post_u ? (float)(1.0 / (1.0 - (double)post_p)) : 1.f, post_out, n, H, C,
+                     slope, S, B);
 }
 
 void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
                     int ae_edge_order, const uint32_t* rowmask, const float* bias,
-                    const uint8_t* keep, float keep_scale, float* y, float* psave, int n, int H,
-                    int C, int concat, int act, float slope) {
+                    const uint8_t* keep, float keep_scale, float* y, float* psave,
+                    const float* post_u, float post_p, float* post_out, int n, int H, int C,
+                    int concat, int act, float slope) {
 #define SV2N_CF(A, CC, K)                                                                     \
   launch_canon_fwd<A, CC, K>(B, st, xs, ldx, ae, ae_edge_order, rowmask, bias, keep, keep_scale, \
-                             y, psave, n, H, C, slope)
+                             y, psave, post_u, post_p, post_out, n, H, C, slope)
 #define SV2N_CF_ACT(CC, K)                 \
   switch (act) {                           \
     case 0: SV2N_CF(0, CC, K); break;      \

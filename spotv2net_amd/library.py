@@ -39,6 +39,10 @@ _SCHEMAS = {
     "gat_attn_fwd": "(Tensor xs, Tensor? ae, Tensor? rowmask, Tensor? bias, Tensor? keep, "
                     "float keep_scale, int num_graphs, int n, int heads, int channels, "
                     "bool concat, int act, float slope, bool edge_order=False) -> (Tensor, Tensor)",
+    "gat_attn_fwd_post": "(Tensor xs, Tensor? ae, Tensor? rowmask, Tensor? bias, Tensor? keep, "
+                         "float keep_scale, Tensor post_u, float post_p, int num_graphs, int n, "
+                         "int heads, int channels, bool concat, int act, float slope, "
+                         "bool edge_order=False) -> (Tensor, Tensor, Tensor)",
     "gat_attn_tiled_fwd": "(Tensor xs, Tensor? ae, int num_edges, Tensor? eid, Tensor? rowmask, "
                           "Tensor? bias, Tensor? keep, float keep_scale, int num_graphs, int n, "
                           "int heads, int channels, bool concat, int act, float slope) -> Tensor",
@@ -53,7 +57,8 @@ _SCHEMAS = {
     "gat_attn_bwd": "(Tensor dy, Tensor y, Tensor xs, Tensor psave, Tensor? keep, "
                     "float keep_scale, Tensor? rowmask, bool with_ae, int num_graphs, int n, "
                     "int heads, int channels, bool concat, int act, float slope, "
-                    "bool edge_order=False) -> (Tensor, Tensor, Tensor)",
+                    "bool edge_order=False, Tensor? post_u=None, float post_p=0.0) "
+                    "-> (Tensor, Tensor, Tensor)",
     "gat_attn_tiled_bwd": "(Tensor dy, Tensor y, Tensor xs, Tensor? ae, int num_edges, "
                           "Tensor? eid, Tensor? keep, float keep_scale, Tensor? rowmask, "
                           "int num_graphs, int n, int heads, int channels, bool concat, int act, "
@@ -339,26 +344,36 @@ def _oc(heads, channels, concat):
     return heads * channels if concat else channels
 
 
-@_impl("gat_attn_fwd")
-def _gat_attn_fwd(xs, ae, rowmask, bias, keep, keep_scale, num_graphs, n, heads, channels,
-                  concat, act, slope, edge_order=False):
+def _attn_fwd(xs, ae, rowmask, bias, keep, keep_scale, post_u, post_p, num_graphs, n, heads,
+              channels, concat, act, slope, edge_order):
     lib = _lib.load()
-    _f32(xs, ae, bias)
-    N = num_graphs * n
+    _f32(xs, ae, bias, post_u)
+    N, OC = num_graphs * n, _oc(heads, channels, concat)
     _rows(xs, N, heads * channels + 2 * heads, "xs")
-    _dense(ae, rowmask, bias, keep)
+    _dense(ae, rowmask, bias, keep, post_u)
     _need(ae is None or ae.numel() == num_graphs * n * (n - int(edge_order)) * heads, "ae shape")
     _need(not edge_order or rowmask is None, "edge-ordered ae needs complete graphs")
-    _need(bias is None or bias.numel() == _oc(heads, channels, concat), "bias shape")
+    _need(bias is None or bias.numel() == OC, "bias shape")
     _need(keep is None or keep.numel() == num_graphs * heads * 1024, "keep shape")
     _need(rowmask is None or rowmask.numel() >= N, "rowmask shape")
-    y = torch.empty(N, _oc(heads, channels, concat), device=xs.device)
+    _need(post_u is None or (post_u.numel() == N * OC and 0.0 <= post_p < 1.0), "post_u / post_p")
+    y = torch.empty(N, OC, device=xs.device)
     ps = torch.empty(num_graphs, heads, 32, 32, device=xs.device)
+    out = torch.empty(N, OC, device=xs.device) if post_u is not None else None
     _lib.check(lib.sv2n_gat_attn_fwd(xs.data_ptr(), xs.stride(0), _p(ae), int(edge_order),
                                      _p(rowmask), _p(bias),
                                      _p(keep), keep_scale, y.data_ptr(), ps.data_ptr(),
+                                     _p(post_u), post_p, _p(out),
                                      num_graphs, n, heads, channels, int(concat), act, slope,
                                      _st(xs)), "sv2n_gat_attn_fwd")
+    return y, ps, out
+
+
+@_impl("gat_attn_fwd")
+def _gat_attn_fwd(xs, ae, rowmask, bias, keep, keep_scale, num_graphs, n, heads, channels,
+                  concat, act, slope, edge_order=False):
+    y, ps, _ = _attn_fwd(xs, ae, rowmask, bias, keep, keep_scale, None, 0.0, num_graphs, n, heads,
+                         channels, concat, act, slope, edge_order)
     return y, ps
 
 
@@ -367,6 +382,23 @@ def _gat_attn_fwd_fake(xs, ae, rowmask, bias, keep, keep_scale, num_graphs, n, h
                        concat, act, slope, edge_order=False):
     return (xs.new_empty((num_graphs * n, _oc(heads, channels, concat))),
             xs.new_empty((num_graphs, heads, 32, 32)))
+
+
+@_impl("gat_attn_fwd_post")
+def _gat_attn_fwd_post(xs, ae, rowmask, bias, keep, keep_scale, post_u, post_p, num_graphs, n,
+                       heads, channels, concat, act, slope, edge_order=False):
+    """gat_attn_fwd with GATModel's post-layer dropout fused into the store
+    (utils/models.py:148): also returns out = y · (post_u >= post_p) / (1 - post_p)."""
+    return _attn_fwd(xs, ae, rowmask, bias, keep, keep_scale, post_u, post_p, num_graphs, n,
+                     heads, channels, concat, act, slope, edge_order)
+
+
+@_fake("gat_attn_fwd_post")
+def _gat_attn_fwd_post_fake(xs, ae, rowmask, bias, keep, keep_scale, post_u, post_p, num_graphs,
+                            n, heads, channels, concat, act, slope, edge_order=False):
+    oc = _oc(heads, channels, concat)
+    return (xs.new_empty((num_graphs * n, oc)), xs.new_empty((num_graphs, heads, 32, 32)),
+            xs.new_empty((num_graphs * n, oc)))
 
 
 @_impl("gat_attn_tiled_fwd")
@@ -491,13 +523,14 @@ def _dae_shape(edge_order, num_graphs, n, heads):
 
 @_impl("gat_attn_bwd")
 def _gat_attn_bwd(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_graphs, n, heads,
-                  channels, concat, act, slope, edge_order=False):
+                  channels, concat, act, slope, edge_order=False, post_u=None, post_p=0.0):
     lib = _lib.load()
-    _f32(dy, y, xs, psave)
+    _f32(dy, y, xs, psave, post_u)
     N, OC = num_graphs * n, _oc(heads, channels, concat)
     _rows(xs, N, heads * channels + 2 * heads, "xs")
-    _dense(dy, y, psave, keep, rowmask)
+    _dense(dy, y, psave, keep, rowmask, post_u)
     _need(dy.numel() == N * OC and y.numel() == N * OC, "dy / y shape")
+    _need(post_u is None or (post_u.numel() == N * OC and 0.0 <= post_p < 1.0), "post_u / post_p")
     _need(psave.numel() == num_graphs * heads * 1024, "psave shape")
     _need(keep is None or keep.numel() == num_graphs * heads * 1024, "keep shape")
     dev = xs.device
@@ -507,8 +540,9 @@ def _gat_attn_bwd(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_grap
         torch.empty(0, device=dev)
     dbp = torch.empty(num_graphs, _oc(heads, channels, concat), device=dev)
     _lib.check(lib.sv2n_gat_attn_bwd(dy.data_ptr(), y.data_ptr(), xs.data_ptr(), xs.stride(0),
-                                     psave.data_ptr(), _p(keep), keep_scale, _p(rowmask),
-                                     dxs.data_ptr(), _p(dae), int(edge_order), dbp.data_ptr(),
+                                     psave.data_ptr(), _p(keep), keep_scale, _p(post_u), post_p,
+                                     _p(rowmask), dxs.data_ptr(), _p(dae), int(edge_order),
+                                     dbp.data_ptr(),
                                      num_graphs, n,
                                      heads, channels, int(concat), act, slope, _st(xs)),
                "sv2n_gat_attn_bwd")
@@ -517,7 +551,8 @@ def _gat_attn_bwd(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_grap
 
 @_fake("gat_attn_bwd")
 def _gat_attn_bwd_fake(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_graphs, n,
-                       heads, channels, concat, act, slope, edge_order=False):
+                       heads, channels, concat, act, slope, edge_order=False, post_u=None,
+                       post_p=0.0):
     return (torch.empty_like(xs),
             xs.new_empty(_dae_shape(edge_order, num_graphs, n, heads) if with_ae else (0,)),
             xs.new_empty((num_graphs, _oc(heads, channels, concat))))

@@ -196,10 +196,13 @@ def _opt(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 
 class _StackMeta:
     """What the backward needs besides the saved tensors (stack_forward)."""
-    __slots__ = ("dims", "bf16", "feid", "kscales")
+    __slots__ = ("dims", "bf16", "feid", "kscales", "post_p")
 
-    def __init__(self, dims, bf16, feid, kscales):
+    def __init__(self, dims, bf16, feid, kscales, post_p=None):
         self.dims, self.bf16, self.feid, self.kscales = dims, bf16, feid, kscales
+        # per layer: the post-layer dropout probability when its draws (not a
+        # mask) are saved, i.e. the attention kernels apply it themselves
+        self.post_p = post_p or [None] * len(kscales)
 
 
 def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropout: float,
@@ -268,6 +271,7 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
     xin = _aligned(x)
     saved_x, saved_xs, saved_y, saved_p, saved_keep, saved_drop = [], [], [], [], [], []
     saved_st = []
+    post_p = []
     for l, c in enumerate(convs):
         Hc, C = c.heads, c.out_channels
         F = c.in_channels
@@ -298,12 +302,24 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
                                        layout.rowmask, c.bias, keep, kscale, B, n, Hc, C,
                                        c.concat, act, float(c.negative_slope))
             ps = aes[l]
-        else:
+        post_u = None
+        if not (fused or tiled) and training and 0.0 < post_dropout < 1.0:
+            # the post-layer dropout (utils/models.py:148) fused into the
+            # attention's store: torch draws the uniforms (same stream as
+            # rand_like(y) >= p), the kernel masks, scales and writes both y
+            # (for the activation's backward) and the layer output
+            post_u = torch.rand(N, Hc * C if c.concat else C, device=dev)
+            y, ps, out = ops.gat_attn_fwd_post(xs, aes[l], layout.rowmask, c.bias, keep, kscale,
+                                               post_u, float(post_dropout), B, n, Hc, C,
+                                               c.concat, act, float(c.negative_slope), eo)
+        elif not (fused or tiled):
             y, ps = ops.gat_attn_fwd(xs, aes[l], layout.rowmask, c.bias, keep, kscale, B, n,
                                      Hc, C, c.concat, act, float(c.negative_slope), eo)
-        out = y
-        dmask = None
-        if training and post_dropout > 0.0:
+        if post_u is None:
+            out = y
+        dmask = post_u
+        post_p.append(float(post_dropout) if post_u is not None else None)
+        if post_u is None and training and post_dropout > 0.0:
             if post_dropout >= 1.0:
                 dmask = torch.zeros_like(y)
             else:
@@ -321,7 +337,7 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
 
     meta = _StackMeta((L, act, use_edge, hp, H, eo, fused), bf16, feid,
                       [(1.0 / (1.0 - c.dropout)) if (training and 0.0 < c.dropout < 1.0) else
-                       (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs])
+                       (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs], post_p)
     saved = [ea, wf if fused else None, *saved_x, *saved_xs, *saved_y, *saved_p, *saved_st,
              *saved_keep, *saved_drop, *waugs, *planes_t]
     return xin, saved, meta
@@ -354,7 +370,8 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
     for l in range(L - 1, -1, -1):
         c = convs[l]
         Hc, C = c.heads, c.out_channels
-        if drops[l] is not None:
+        post_u = drops[l] if meta.post_p[l] is not None else None
+        if drops[l] is not None and post_u is None:
             dy = dy * drops[l]
         xs = xss[l]
         if fused:  # pss[l], sts[l]: the forward's head aggregates and row statistics
@@ -370,7 +387,8 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
         else:
             dxs, dae, dbp = ops.gat_attn_bwd(
                 dy, ys[l], xs, pss[l], keeps[l], meta.kscales[l], layout.rowmask, use_edge,
-                B, n, Hc, C, c.concat, act, float(c.negative_slope), eo)
+                B, n, Hc, C, c.concat, act, float(c.negative_slope), eo, post_u,
+                meta.post_p[l] or 0.0)
         daes[l] = _opt(dae)
         gW = grad_of(c.lin_src.weight)
         gas = grad_of(c.att_src)

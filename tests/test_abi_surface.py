@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     for name in names:
         assert hasattr(lib, name), f"libsv2n.so lacks {name}"
     assert set(names) == set(_lib.EXPORTED_SYMBOLS), "ctypes table and header disagree"
-    assert lib.sv2n_abi_version() == _lib.ABI_VERSION == 8
+    assert lib.sv2n_abi_version() == _lib.ABI_VERSION == 9
     assert b"invalid argument" in lib.sv2n_strerror(-1)
 
 
@@ -33,8 +33,8 @@ def test_argument_errors_without_gpu():
     """Argument validation happens before any HIP call, so it runs on CPU."""
     from spotv2net_amd import _lib
     lib = _lib.load()
-    assert lib.sv2n_gat_attn_fwd(None, 8, None, 0, None, None, None, 1.0, None, None, 1, 30, 4,
-                                 8, 1, 1, 0.2, None) == -1
+    assert lib.sv2n_gat_attn_fwd(None, 8, None, 0, None, None, None, 1.0, None, None, None, 0.0,
+                                 None, 1, 30, 4, 8, 1, 1, 0.2, None) == -1
     assert lib.sv2n_gemm_f32(1, 1, None, 4, None, 4, None, 4, 4, 4, 4, None, 0, None) == -1
     assert lib.sv2n_edge_logits_bwd_workspace(126, 8) == 768 * 126 * 8
 

@@ -65,6 +65,22 @@ def test_opcheck_backward_ops(dev):
                                              True, 1, 0.2), test_utils=UTILS)
     dxs, dae, dbp = ops.gat_attn_bwd(dy, y, xs, ps, None, 1.0, None, True, B, n, H, C, True, 1,
                                      0.2)
+    # post-layer dropout fused into the attention (ABI 9): out == y masked and
+    # scaled exactly as torch does it, and the backward masks dy first
+    u = torch.rand(B * n, H * C, generator=g).to(dev)
+    torch.library.opcheck(ops.gat_attn_fwd_post, (xs, ae, None, None, None, 1.0, u, 0.25, B, n,
+                                                  H, C, True, 1, 0.2), test_utils=UTILS)
+    y3, ps3, out3 = ops.gat_attn_fwd_post(xs, ae, None, None, None, 1.0, u, 0.25, B, n, H, C,
+                                          True, 1, 0.2)
+    assert torch.equal(y3, y) and torch.equal(ps3, ps)
+    assert torch.equal(out3, y * ((u >= 0.25).to(torch.float32) * (1.0 / 0.75)))
+    torch.library.opcheck(ops.gat_attn_bwd, (dy, y, xs, ps, None, 1.0, None, True, B, n, H, C,
+                                             True, 1, 0.2, False, u, 0.25), test_utils=UTILS)
+    dxs3, dae3, dbp3 = ops.gat_attn_bwd(dy, y, xs, ps, None, 1.0, None, True, B, n, H, C, True, 1,
+                                        0.2, False, u, 0.25)
+    dxs4, dae4, dbp4 = ops.gat_attn_bwd(dy * ((u >= 0.25).to(torch.float32) * (1.0 / 0.75)), y,
+                                        xs, ps, None, 1.0, None, True, B, n, H, C, True, 1, 0.2)
+    assert torch.equal(dxs3, dxs4) and torch.equal(dae3, dae4) and torch.equal(dbp3, dbp4)
     x = torch.randn(B * n, 12, generator=g).to(dev)
     W = torch.randn(H * C, 12, generator=g).to(dev)
     a_s = torch.randn(1, H, C, generator=g).to(dev)

@@ -59,12 +59,12 @@ def main_c3(B=128):
 
     def fwd():
         assert lib.sv2n_gat_attn_fwd(xs.data_ptr(), ldx, ae.data_ptr(), 1, None, bias.data_ptr(),
-                                     None, 1.0, y.data_ptr(), ps.data_ptr(), B, n, H, C, 0, 1,
-                                     0.2, sh) == 0
+                                     None, 1.0, y.data_ptr(), ps.data_ptr(), None, 0.0, None, B,
+                                     n, H, C, 0, 1, 0.2, sh) == 0
 
     def bwd():
         assert lib.sv2n_gat_attn_bwd(dy.data_ptr(), y.data_ptr(), xs.data_ptr(), ldx,
-                                     ps.data_ptr(), None, 1.0, None, dxs.data_ptr(),
+                                     ps.data_ptr(), None, 1.0, None, 0.0, None, dxs.data_ptr(),
                                      dae.data_ptr(), 1, dbp.data_ptr(), B, n, H, C, 0, 1, 0.2,
                                      sh) == 0
 
@@ -110,11 +110,12 @@ def main(B=512):
     def fwd():
         lib.sv2n_gat_attn_fwd(xs0.data_ptr(), xs0.stride(0), ae.data_ptr(), 1, None,
                               conv0.bias.data_ptr(), None, 1.0, y0.data_ptr(), ps0.data_ptr(),
-                              B, n, H, conv0.out_channels, 1, 1, 0.2, sh)
+                              None, 0.0, None, B, n, H, conv0.out_channels, 1, 1, 0.2, sh)
 
     def bwd():
         lib.sv2n_gat_attn_bwd(dy0.data_ptr(), y0.data_ptr(), xs0.data_ptr(), xs0.stride(0),
-                              ps0.data_ptr(), None, 1.0, None, dxs0.data_ptr(), dae0.data_ptr(),
+                              ps0.data_ptr(), None, 1.0, None, 0.0, None, dxs0.data_ptr(),
+                              dae0.data_ptr(),
                               1, dbp.data_ptr(), B, n, H, conv0.out_channels, 1, 1, 0.2, sh)
 
     for _ in range(5):
