@@ -59,6 +59,37 @@ struct PrepBlock {
   float* waug; uint16_t* planes; int64_t kp, plane; int np;
 };
 
+// one row piece (4 columns) of waug and its bf16 planes; 16-B / 8-B stores when
+// the piece lies inside the row
+__device__ __forceinline__ void prep_put_piece(const PrepBlock& P, int64_t row, int col,
+                                               const float (&w)[4]) {
+  const int F = P.F;
+  if ((F & 3) == 0 && col + 3 < F) {
+    *reinterpret_cast<f32x4*>(P.waug + row * F + col) = f32x4{w[0], w[1], w[2], w[3]};
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (col + j < F) P.waug[row * F + col + j] = w[j];
+  }
+  if (!P.planes) return;
+  if ((P.kp & 3) == 0 && col + 3 < P.kp) {
+    unsigned short h[3][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split3(w[j], h[0][j], h[1][j], h[2][j]);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      if (q > 0 && P.np != 3) break;
+      const uint32_t lo = (uint32_t)h[q][0] | ((uint32_t)h[q][1] << 16);
+      const uint32_t hi = (uint32_t)h[q][2] | ((uint32_t)h[q][3] << 16);
+      *reinterpret_cast<uint2*>(P.planes + q * P.plane + row * P.kp + col) = make_uint2(lo, hi);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (col + j < P.kp) put3(P.planes, P.plane, row * P.kp + col + j, w[j], P.np);
+  }
+}
+
 __device__ __forceinline__ void prep_node_block(const PrepBlock& P, int h, int col0, int cb, int ce,
                                                 bool fold, float (*s_red)[PREP_G][64], int t) {
   const int g = t >> 4, lq = t & 15, col = col0 + 4 * lq;
@@ -66,30 +97,38 @@ __device__ __forceinline__ void prep_node_block(const PrepBlock& P, int h, int c
   float ss[4] = {0.f, 0.f, 0.f, 0.f}, sd[4] = {0.f, 0.f, 0.f, 0.f};
   const int cs = fold ? 0 : cb, cend = fold ? C : ce;
   const int first = cs + ((g - cs) % PREP_G + PREP_G) % PREP_G;
-  for (int c0 = first; c0 < cend; c0 += PREP_G * PREP_RB) {
-    float w[PREP_RB][4], as[PREP_RB], ad[PREP_RB];
+  const bool vec = (F & 3) == 0 && col + 3 < F;
+  // the next round's rows are loaded before this round's stores (software
+  // pipelined: one memory round trip per round overlapped with the stores)
+  auto load = [&](int c0, float (&w)[PREP_RB][4], float (&as)[PREP_RB], float (&ad)[PREP_RB]) {
 #pragma unroll
     for (int u = 0; u < PREP_RB; ++u) {
       const int c = min(c0 + PREP_G * u, C - 1);
       const int64_t row = (int64_t)h * C + c;
+      if (vec) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(P.W + row * F + col);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[u][j] = col + j < F ? P.W[row * F + col + j] : 0.f;
+        for (int j = 0; j < 4; ++j) w[u][j] = v[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[u][j] = col + j < F ? P.W[row * F + col + j] : 0.f;
+      }
       as[u] = P.att_s[row];
       ad[u] = P.att_d[row];
     }
+  };
+  float w[PREP_RB][4], as[PREP_RB], ad[PREP_RB];
+  if (first < cend) load(first, w, as, ad);
+  for (int c0 = first; c0 < cend; c0 += PREP_G * PREP_RB) {
+    const bool more = c0 + PREP_G * PREP_RB < cend;
+    float wn[PREP_RB][4], asn[PREP_RB], adn[PREP_RB];
+    if (more) load(c0 + PREP_G * PREP_RB, wn, asn, adn);
 #pragma unroll
     for (int u = 0; u < PREP_RB; ++u) {
       const int c = c0 + PREP_G * u;
       if (c < cend) {
         const int64_t row = (int64_t)h * C + c;
-        if (c >= cb && c < ce) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (col + j < F) P.waug[row * F + col + j] = w[u][j];
-            if (P.planes && col + j < P.kp)
-              put3(P.planes, P.plane, row * P.kp + col + j, w[u][j], P.np);
-          }
-        }
+        if (c >= cb && c < ce) prep_put_piece(P, row, col, w[u]);
         if (fold) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -97,6 +136,15 @@ __device__ __forceinline__ void prep_node_block(const PrepBlock& P, int h, int c
             sd[j] = fmaf(ad[u], w[u][j], sd[j]);
           }
         }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < PREP_RB; ++u) {
+        as[u] = asn[u];
+        ad[u] = adn[u];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[u][j] = wn[u][j];
       }
     }
   }

@@ -130,11 +130,24 @@ __global__ __launch_bounds__(256) void k_window_rows(
   }
   if (t < F) y[(b * n + u) * F + t] = vol[(st + S + t) * nn + (int64_t)u * n + u];
   __syncthreads();
-  // x[b*n+u][c*S + tt] = vol[tt][u][c]
+  // x[b*n+u][c*S + tt] = vol[tt][u][c]: 16-B stores when the row allows
   float* xr = x + (b * n + u) * (int64_t)n * S;
-  for (int j = t; j < n * S; j += 256) {
-    const int c = j / S, tt = j - c * S;
-    xr[j] = sv[tt * NP + c];
+  const int nxr = n * S;
+  if ((nxr & 3) == 0 && (((uintptr_t)xr) & 15) == 0) {
+    for (int j4 = t; j4 < nxr / 4; j4 += 256) {
+      f32x4 v;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int j = 4 * j4 + k, c = j / S, tt = j - c * S;
+        v[k] = sv[tt * NP + c];
+      }
+      *reinterpret_cast<f32x4*>(xr + 4 * j4) = v;
+    }
+  } else {
+    for (int j = t; j < nxr; j += 256) {
+      const int c = j / S, tt = j - c * S;
+      xr[j] = sv[tt * NP + c];
+    }
   }
   // upper pairs (u, w > u): e = off(u) + (w - u - 1), off(u) = u*(2n-u-1)/2
   const int m = n - 1 - u;
@@ -143,6 +156,30 @@ __global__ __launch_bounds__(256) void k_window_rows(
   const int RW = 3 * S;
   float* up = ea + (b * E0 + e0) * (int64_t)RW;
   float* lo = ea + (b * E0 + P + e0) * (int64_t)RW;
+  if ((S & 1) == 0 && RW <= 2 * 64 && (((uintptr_t)up) & 7) == 0 && (((uintptr_t)lo) & 7) == 0) {
+    // one wave per edge row, two adjacent columns per lane (8-B stores; S even:
+    // both columns have the same kind), (kind, t) decoded once
+    const int lane = t & 63, wv = t >> 6;
+    const int q = 2 * lane, kind = q / S, tq = q - kind * S;
+    const bool qv = q < RW;
+    for (int r = wv; r < m; r += 4) {
+      const int w = u + 1 + r;
+      float cu[2], cl[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int tt = tq + k;
+        // upper edge u -> w: (covol, var_u, var_w); swapped w -> u: (covol, var_w, var_u)
+        const float cov = sw[tt * NP + w], du = sw[tt * NP + u], dw = sd[tt * NP + w];
+        cu[k] = kind == 0 ? cov : (kind == 1 ? du : dw);
+        cl[k] = kind == 0 ? cov : (kind == 1 ? dw : du);
+      }
+      if (qv) {
+        *reinterpret_cast<float2*>(up + r * RW + q) = make_float2(cu[0], cu[1]);
+        *reinterpret_cast<float2*>(lo + r * RW + q) = make_float2(cl[0], cl[1]);
+      }
+    }
+    return;
+  }
   if (RW <= 4 * 64) {
     // one wave per edge row, a lane's columns fixed: (kind, t) decoded once
     // (the flat element loop divided twice per element)
@@ -161,7 +198,6 @@ __global__ __launch_bounds__(256) void k_window_rows(
         const int q = lane + 64 * qi;
         if (q < RW) {
           const int tt = tq[qi];
-          // upper edge u -> w: (covol, var_u, var_w); swapped w -> u: (covol, var_w, var_u)
           const float cov = sw[tt * NP + w], du = sw[tt * NP + u], dw = sd[tt * NP + w];
           up[r * RW + q] = kind[qi] == 0 ? cov : (kind[qi] == 1 ? du : dw);
           lo[r * RW + q] = kind[qi] == 0 ? cov : (kind[qi] == 1 ? dw : du);
