@@ -79,15 +79,19 @@ constexpr int ATT_RB = 8;            // rows per block
 constexpr int ATT_RW = ATT_RB / 4;   // rows per wave
 constexpr int ATT_FPL = 24;          // f per lane per pass (F <= 1536: one pass)
 
+// SLABS = false: the fold columns are columns HC.. of T [F][ldt].  SLABS =
+// true (bf16 path, k_wgrad_epi_t): they are rows HC.. of nslab split-K slabs
+// [ldt][F] (ldt = rows), summed here in slab order.
+template <bool SLABS>
 __device__ __forceinline__ void wgrad_att_block(int blk, const float* __restrict__ T, int ldt,
                                                 const float* __restrict__ W, int H, int C, int F,
                                                 float* __restrict__ g_as, float* __restrict__ g_ad,
-                                                float* __restrict__ s_fold) {
+                                                float* __restrict__ s_fold, int nslab = 1) {
   // s_fold: [2][nh][F] (dynamic LDS)
   const int HC = H * C, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int o0 = blk * ATT_RB, o1 = min(HC, o0 + ATT_RB);
   const int h0 = o0 / C, nh = (o1 - 1) / C - h0 + 1;
-  const rsrc_t rt = make_rsrc(T, (uint32_t)F * (uint32_t)ldt * 4u);
+  const rsrc_t rt = make_rsrc(T, (uint32_t)F * (uint32_t)ldt * 4u * (uint32_t)nslab);
   {
     const int n = 2 * nh * F;
     for (int k0 = 0; k0 < n; k0 += 8 * 256) {
@@ -96,7 +100,14 @@ __device__ __forceinline__ void wgrad_att_block(int blk, const float* __restrict
       for (int u = 0; u < 8; ++u) {
         const int k = k0 + t + 256 * u;
         const int q = k / (nh * F), r = k - q * nh * F, hh = r / F, f = r - hh * F;
-        v[u] = bld(rt, k < n ? (f * ldt + HC + q * H + h0 + hh) * 4 : OOB);
+        if constexpr (SLABS) {
+          const int off = ((HC + q * H + h0 + hh) * F + f) * 4;
+          v[u] = bld(rt, k < n ? off : OOB);
+          for (int sl = 1; sl < nslab; ++sl)
+            v[u] += bld(rt, k < n ? off + sl * F * ldt * 4 : OOB);
+        } else {
+          v[u] = bld(rt, k < n ? (f * ldt + HC + q * H + h0 + hh) * 4 : OOB);
+        }
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u)
@@ -153,6 +164,36 @@ __device__ __forceinline__ void wgrad_att_block(int blk, const float* __restrict
   }
 }
 
+// g_bias[o] += Σ_b dbp[b][o] for 16 columns o: 16 row groups, 8 loads in
+// flight each, the groups added in order
+__device__ __forceinline__ void wgrad_bias_block(int blk, const float* __restrict__ dbp, int nparts,
+                                                 int OC, float* __restrict__ g_bias,
+                                                 float (*s_red)[17]) {
+  const int t = threadIdx.x;
+  const rsrc_t rb = make_rsrc(dbp, (uint32_t)nparts * (uint32_t)OC * 4u);
+  const int lo = t & 15, grp = t >> 4;
+  const int o = blk * 16 + lo;
+  float a = 0.f;
+  for (int q0 = 0; q0 < nparts; q0 += 16 * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = q0 + grp + 16 * u;
+      v[u] = bld(rb, (o < OC && q < nparts) ? (q * OC + o) * 4 : OOB);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a += v[u];
+  }
+  s_red[grp][lo] = a;
+  __syncthreads();
+  if (grp == 0 && o < OC) {
+    float sb = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sb += s_red[k][lo];
+    g_bias[o] += sb;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_wgrad_epi(
     const float* __restrict__ T, int ldt, const float* __restrict__ W,
     const float* __restrict__ att_s, const float* __restrict__ att_d, int H, int C, int F,
@@ -169,34 +210,13 @@ __global__ __launch_bounds__(256) void k_wgrad_epi(
   const int bx = blockIdx.x;
   const int b = bx < natt ? ntile + bx : (bx < natt + ntile ? bx - natt : bx);
   const rsrc_t rt = make_rsrc(T, (uint32_t)F * (uint32_t)ldt * 4u);
-  if (b >= ntile + natt) {  // ---- bias column sums: 16 columns x 16 row groups ----
-    const rsrc_t rb = make_rsrc(dbp, (uint32_t)nparts * (uint32_t)OC * 4u);
-    const int lo = t & 15, grp = t >> 4;
-    const int o = (b - ntile - natt) * 16 + lo;
-    float a = 0.f;
-    for (int q0 = 0; q0 < nparts; q0 += 16 * 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int q = q0 + grp + 16 * u;
-        v[u] = bld(rb, (o < OC && q < nparts) ? (q * OC + o) * 4 : OOB);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a += v[u];
-    }
-    s_red[grp][lo] = a;
-    __syncthreads();
-    if (grp == 0 && o < OC) {
-      float sb = 0.f;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) sb += s_red[k][lo];
-      g_bias[o] += sb;
-    }
+  if (b >= ntile + natt) {  // ---- bias column sums ----
+    wgrad_bias_block(b - ntile - natt, dbp, nparts, OC, g_bias, s_red);
     return;
   }
   if (b >= ntile) {  // att blocks (dispatched first)
     extern __shared__ float s_dyn[];
-    wgrad_att_block(b - ntile, T, ldt, W, H, C, F, g_as, g_ad, s_dyn);
+    wgrad_att_block<false>(b - ntile, T, ldt, W, H, C, F, g_as, g_ad, s_dyn);
     return;
   }
   // ---- gW tile: 16 f x 64 o ----
@@ -237,6 +257,86 @@ __global__ __launch_bounds__(256) void k_wgrad_epi(
     const int h = min(o, HC - 1) / C;
     const float v = gv[q] + (tile[fl][orow] + sfold[fl][h] * av[q] + sfold[fl][H + h] * dv[q]);
     bst(rg, (o < HC && f < F) ? (o * F + f) * 4 : OOB, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bf16 path: the GEMM writes dWaug itself (rows o' = the ldt projection rows,
+// F columns) as nslab split-K slabs S[s][o'][f], and this one launch sums the
+// slabs while applying the fold (no reduce launch, no transposition):
+//   row blocks  gW[o][f] += (Σ_s S[s][o][f]) + fs_h[f]·att_s[o] + fd_h[f]·att_d[o],
+//               fs_h / fd_h = Σ_s S[s][HC+h][f] / Σ_s S[s][HC+H+h][f], h = o / C;
+//               a block = WT_RB rows x 256 f, a wave per row, float4 per lane
+//   att blocks  as in k_wgrad_epi, the fold rows summed from the slabs
+//   bias blocks as in k_wgrad_epi
+// ---------------------------------------------------------------------------
+constexpr int WT_RB = 32;
+
+__global__ __launch_bounds__(256) void k_wgrad_epi_t(
+    const float* __restrict__ S, int nslab, int ldt, const float* __restrict__ W,
+    const float* __restrict__ att_s, const float* __restrict__ att_d, int H, int C, int F,
+    float* __restrict__ gW, float* __restrict__ g_as, float* __restrict__ g_ad, int nrow,
+    int nfc, int natt, const float* __restrict__ dbp, int nparts, int OC,
+    float* __restrict__ g_bias) {
+  __shared__ float s_red[16][17];
+  const int HC = H * C;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int bx = blockIdx.x;  // att blocks first, then the row blocks, then bias
+  if (bx < natt) {
+    extern __shared__ float s_dyn[];
+    wgrad_att_block<true>(bx, S, ldt, W, H, C, F, g_as, g_ad, s_dyn, nslab);
+    return;
+  }
+  const int b = bx - natt;
+  if (b >= nrow * nfc) {
+    wgrad_bias_block(b - nrow * nfc, dbp, nparts, OC, g_bias, s_red);
+    return;
+  }
+  const int fc = b % nfc, rg = b / nfc;
+  const int o0 = rg * WT_RB, o1 = min(HC, o0 + WT_RB);
+  const int f = 4 * (fc * 64 + lane);
+  const bool fv = f < F;
+  const int64_t sstride = (int64_t)ldt * F;
+  const rsrc_t rs = make_rsrc(S, (uint32_t)(sstride * nslab * 4));
+  const rsrc_t rg_ = make_rsrc(gW, (uint32_t)HC * (uint32_t)F * 4u);
+  // fold rows of the (at most two) heads the block's rows touch
+  const int ha = o0 / C, hb = (o1 - 1) / C;
+  f32x4 fs[2], fd[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int h = k ? hb : ha;
+    const int offs = ((HC + h) * F + f) * 4, offd = ((HC + H + h) * F + f) * 4;
+    fs[k] = bld4(rs, fv ? offs : OOB);
+    fd[k] = bld4(rs, fv ? offd : OOB);
+    for (int sl = 1; sl < nslab; ++sl) {
+      fs[k] += bld4(rs, fv ? offs + (int)(sl * sstride * 4) : OOB);
+      fd[k] += bld4(rs, fv ? offd + (int)(sl * sstride * 4) : OOB);
+    }
+  }
+  constexpr int RPW = WT_RB / 4;  // rows per wave
+  f32x4 gv[RPW], tv[RPW];
+  float av[RPW], dv[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {  // every load of the wave's rows in flight
+    const int o = o0 + wv + 4 * r;
+    const bool ov = o < o1 && fv;
+    const int off = (o * F + f) * 4;
+    gv[r] = bld4(rg_, ov ? off : OOB);
+    tv[r] = bld4(rs, ov ? off : OOB);
+    for (int sl = 1; sl < nslab; ++sl) tv[r] += bld4(rs, ov ? off + (int)(sl * sstride * 4) : OOB);
+    av[r] = o < o1 ? att_s[o] : 0.f;
+    dv[r] = o < o1 ? att_d[o] : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int o = o0 + wv + 4 * r;
+    if (o < o1 && fv) {
+      const int k = (o / C) == ha ? 0 : 1;
+      f32x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = gv[r][j] + (tv[r][j] + fs[k][j] * av[r] + fd[k][j] * dv[r]);
+      bst4(rg_, (o * F + f) * 4, v);
+    }
   }
 }
 }  // namespace sv2n
@@ -485,6 +585,18 @@ static void launch_wgrad_bf16(const GemmPlan& p, hipStream_t st, const float* x,
                      out, ldx, F, ldx, K, p.kslice);
 }
 
+// the same product transposed, dWaug = dxsᵀ·x [ldx][F] (operands swapped):
+// the epilogue (k_wgrad_epi_t) then works along rows of gW
+static void launch_wgrad_bf16_t(const GemmPlan& p, hipStream_t st, const float* x, int64_t ld_x,
+                                const float* dxs, int64_t ldx, int64_t F, int64_t K, float* out) {
+  using Cfg = GemmTTCfg<TT_BM, TT_BN, 1>;
+  constexpr size_t lds = Cfg::LDS;
+  const dim3 grid((unsigned)((ldx + TT_BM - 1) / TT_BM), (unsigned)((F + TT_BN - 1) / TT_BN),
+                  (unsigned)p.splitk);
+  hipLaunchKernelGGL((k_gemm_tt<TT_BM, TT_BN, 1>), grid, dim3(256), lds, st, dxs, ldx, x, ld_x,
+                     out, F, ldx, F, K, p.kslice);
+}
+
 static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* dxs, int ldx,
                       int64_t num_nodes, int in_features, const float* W, const float* att_src,
                       const float* att_dst, int heads, int channels, const float* dbias_partial,
@@ -552,6 +664,31 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
       return SV2N_ERR_ALIGN;
     if (num_nodes * std::max<int64_t>(ld_x, ldx) * 4 > 0x7fffffff) return SV2N_ERR_SHAPE;
     const GemmPlan p = plan_gemm_bf16t(F, ldx, num_nodes);
+    if ((F & 3) == 0 && gW) {
+      // dWaug [ldx][F] as p.splitk slabs, summed by the epilogue launch itself
+      float* S = p.splitk > 1 ? slabs : T;
+      launch_wgrad_bf16_t(p, stream, x, ld_x, dxs, ldx, F, num_nodes, S);
+      const int nfc = (F / 4 + 63) / 64, nrow = (HC + WT_RB - 1) / WT_RB;
+      const int natt = (g_att_src || g_att_dst) ? (HC + ATT_RB - 1) / ATT_RB : 0;
+      size_t lds = 0;
+      if (natt) {
+        const int nh_max = std::min(H, (ATT_RB - 1) / C + 2);
+        lds = sizeof(float) * 2 * (size_t)nh_max * F;
+        if (lds > 140 * 1024) return SV2N_ERR_SHAPE;
+        static bool attr = [] {
+          (void)hipFuncSetAttribute((const void*)k_wgrad_epi_t,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 140 * 1024);
+          return true;
+        }();
+        (void)attr;
+      }
+      const int nbias = bias ? (bias_len + 15) / 16 : 0;
+      hipLaunchKernelGGL(k_wgrad_epi_t, dim3((unsigned)(natt + nrow * nfc + nbias)), dim3(256),
+                         lds, stream, S, p.splitk, ldx, W, att_src, att_dst, H, C, F, gW,
+                         g_att_src, g_att_dst, nrow, nfc, natt, dbias_partial, num_parts,
+                         bias_len, g_bias);
+      return (int)hipGetLastError();
+    }
     float* out = p.splitk > 1 ? slabs : T;
     launch_wgrad_bf16(p, stream, x, ld_x, dxs, ldx, F, num_nodes, out);
     if (p.splitk > 1) {

@@ -55,17 +55,22 @@ def test_project_planes_bf16_unaligned_rows(dev):
 
 
 @pytest.mark.parametrize("F,H,C,nodes", [(1260, 6, 500, 3840), (1260, 4, 100, 15360),
-                                         (72, 3, 21, 300)])
+                                         (72, 3, 21, 300), (70, 3, 21, 300)])
 def test_wgrad_bf16_equals_f32_on_rounded_operands(dev, F, H, C, nodes):
     """sv2n_gat_wgrad_node_bf16 == sv2n_gat_wgrad_node (exact f32) fed the
     bf16-rounded x and dxs: the bf16 GEMM's products are exact, so only the
-    summation order differs."""
+    summation order differs.  F % 4 == 0 runs the transposed product with the
+    slab-summing epilogue (k_wgrad_epi_t); F = 70 (x rows padded to 72) the
+    [F][ldx] product, the reduce launch and k_wgrad_epi."""
     from spotv2net_amd import _lib
     lib = _lib.load()
     g = torch.Generator().manual_seed(F + C)
     HC = H * C
     ldx = (HC + 2 * H + 3) // 4 * 4
-    x = torch.randn(nodes, F, generator=g).to(dev)
+    ldin = (F + 3) // 4 * 4
+    x = torch.zeros(nodes, ldin)
+    x[:, :F] = torch.randn(nodes, F, generator=g)
+    x = x.to(dev)
     dxs = (torch.randn(nodes, ldx, generator=g) * 1e-3).to(dev)
     W = (torch.randn(HC, F, generator=g) * 0.03).to(dev)
     a_s = torch.randn(H, C, generator=g).to(dev)
@@ -79,7 +84,7 @@ def test_wgrad_bf16_equals_f32_on_rounded_operands(dev, F, H, C, nodes):
                 torch.zeros(H, C, device=dev), torch.zeros(HC, device=dev)]
         n = wsfn(nodes, F, ldx, H, C)
         ws = torch.zeros(n, device=dev)
-        _lib.check(fn(xx.data_ptr(), F, dd.data_ptr(), ldx, nodes, F, W.data_ptr(),
+        _lib.check(fn(xx.data_ptr(), ldin, dd.data_ptr(), ldx, nodes, F, W.data_ptr(),
                       a_s.data_ptr(), a_d.data_ptr(), H, C, dbp.data_ptr(), B, HC,
                       *[o.data_ptr() for o in outs], ws.data_ptr(), n, st), "wgrad")
         return outs
