@@ -474,17 +474,19 @@ int sv2n_block_rowmask_checked(const int64_t* edge_index, int64_t num_edges, int
 
 /* Device-side CovarianceLaggedDataset window builder (reference
  * utils/dataset.py:200-282; multi-output targets :385-405): for window b with
- * first matrix starts[b] (int64, device), fills the PyG batch layout
- *   x         [B*n][n*S]      x[b*n+v][c*S+t] = vol[starts[b]+t][v][c]
+ * first matrix st_b = starts[b] + start_offset (starts int64, device; the
+ * offset is WindowDataset's cut, so a batch index vector is passed as is —
+ * ABI 9), fills the PyG batch layout
+ *   x         [B*n][n*S]      x[b*n+v][c*S+t] = vol[st_b+t][v][c]
  *   edge_attr [B*n(n-1)][3S]  canonical edge order (canon = target<<8|source):
  *             [0*S+t] upper-triangle volvol[t][min][max], [1*S+t] volvol[t][s][s],
  *             [2*S+t] volvol[t][g][g]
- *   y         [B*n*F]         y[(b*n+v)*F+k] = vol[starts[b]+S+k][v][v]
+ *   y         [B*n*F]         y[(b*n+v)*F+k] = vol[st_b+S+k][v][v]
  * vol / volvol: [T][n][n] fp32 series, T = num_matrices.  A window outside
- * the series (starts[b] < 0 or starts[b] + S + F > T) reads nothing and its
+ * the series (st_b < 0 or st_b + S + F > T) reads nothing and its
  * x / edge_attr / y rows are written as NaN (ABI 8). */
 int sv2n_window_gather(const float* vol, const float* volvol, int n, int64_t num_matrices,
-                       const int64_t* starts,
+                       const int64_t* starts, int64_t start_offset,
                        int64_t num_windows, int seq_length, int future_steps,
                        const uint16_t* canon, float* x, float* edge_attr, float* y,
                        hipStream_t stream);

@@ -23,7 +23,7 @@ namespace sv2n {
 
 __global__ __launch_bounds__(256) void k_window_gather(
     const float* __restrict__ vol, const float* __restrict__ volvol, int n, int64_t T,
-    const int64_t* __restrict__ starts, int64_t B, int S, int F,
+    const int64_t* __restrict__ starts, int64_t soff, int64_t B, int S, int F,
     const uint16_t* __restrict__ canon, float* __restrict__ x, float* __restrict__ ea,
     float* __restrict__ y) {
   const int64_t nn = (int64_t)n * n;
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k_window_gather(
       const int64_t b = row / n;
       const int v = (int)(row - b * n);
       const int c = j / S, t = j - c * S;
-      const int64_t st = starts[b];
+      const int64_t st = starts[b] + soff;
       x[i] = (st >= 0 && st + S + F <= T) ? vol[(st + t) * nn + v * n + c] : qnan;
     } else if (i < nx + ne) {
       const int64_t k0 = i - nx;
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void k_window_gather(
       } else {
         r = c = (kind == 1) ? s : g;
       }
-      const int64_t st = starts[b];
+      const int64_t st = starts[b] + soff;
       ea[k0] = (st >= 0 && st + S + F <= T) ? volvol[(st + t) * nn + r * n + c] : qnan;
     } else {
       const int64_t k0 = i - nx - ne;
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void k_window_gather(
       const int k = (int)(k0 - row * F);
       const int64_t b = row / n;
       const int v = (int)(row - b * n);
-      const int64_t st = starts[b];
+      const int64_t st = starts[b] + soff;
       y[k0] = (st >= 0 && st + S + F <= T) ? vol[(st + S + k) * nn + v * n + v] : qnan;
     }
   }
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void k_window_gather(
 // 3 * S * (n+1) floats of LDS.
 __global__ __launch_bounds__(256) void k_window_rows(
     const float* __restrict__ vol, const float* __restrict__ volvol, int n, int64_t T,
-    const int64_t* __restrict__ starts, int S, int F, float* __restrict__ x,
+    const int64_t* __restrict__ starts, int64_t soff, int S, int F, float* __restrict__ x,
     float* __restrict__ ea, float* __restrict__ y) {
   extern __shared__ float lds[];
   const int NP = n + 1;
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void k_window_rows(
   const int64_t b = blockIdx.x / n;
   const int t = threadIdx.x;
   const int64_t nn = (int64_t)n * n;
-  const int64_t st = starts[b];
+  const int64_t st = starts[b] + soff;
   const int E0 = n * (n - 1), P = E0 / 2;
   if (st < 0 || st + S + F > T) {  // window outside the series: NaN rows, no reads
     const float qnan = __builtin_nanf("");
@@ -222,7 +222,8 @@ __global__ __launch_bounds__(256) void k_window_rows(
 using namespace sv2n;
 
 extern "C" int sv2n_window_gather(const float* vol, const float* volvol, int n,
-                                  int64_t num_matrices, const int64_t* starts, int64_t num_windows, int seq_length,
+                                  int64_t num_matrices, const int64_t* starts,
+                                  int64_t start_offset, int64_t num_windows, int seq_length,
                                   int future_steps, const uint16_t* canon, float* x,
                                   float* edge_attr, float* y, hipStream_t stream) {
   if (!vol || !volvol || !starts || !canon || !x || !edge_attr || !y) return SV2N_ERR_ARG;
@@ -235,11 +236,13 @@ extern "C" int sv2n_window_gather(const float* vol, const float* volvol, int n,
   const size_t lds = sizeof(float) * 3 * (size_t)seq_length * (n + 1);
   if (lds <= 64 * 1024 && future_steps <= 256) {
     hipLaunchKernelGGL(k_window_rows, dim3((unsigned)(num_windows * n)), dim3(256), lds, stream,
-                       vol, volvol, n, num_matrices, starts, seq_length, future_steps, x, edge_attr, y);
+                       vol, volvol, n, num_matrices, starts, start_offset, seq_length, future_steps,
+                       x, edge_attr, y);
     return (int)hipGetLastError();
   }
   const int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);
   hipLaunchKernelGGL(k_window_gather, dim3((unsigned)blocks), dim3(256), 0, stream, vol, volvol,
-                     n, num_matrices, starts, num_windows, seq_length, future_steps, canon, x, edge_attr, y);
+                     n, num_matrices, starts, start_offset, num_windows, seq_length, future_steps,
+                     canon, x, edge_attr, y);
   return (int)hipGetLastError();
 }

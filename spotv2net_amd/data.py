@@ -218,6 +218,7 @@ class WindowDataset:
         self.vol, self.volvol, self.S = vol, volvol, seq_length
         self.future_steps = int(future_steps)
         last = vol.shape[0] - seq_length - self.future_steps + 1
+        self.cut = int(cut)
         self.starts = torch.arange(cut, max(cut, last), device=vol.device)
         n = vol.shape[1]
         self.n = n
@@ -254,16 +255,19 @@ class WindowDataset:
         Same values as ``batch(idx)``."""
         B, n, S, Fs = idx.numel(), self.n, self.S, self.future_steps
         P = self._up_s.numel()
-        st = self.starts.index_select(0, idx)
         if self.vol.is_cuda and self.vol.dtype == torch.float32 and \
                 self.volvol.dtype == torch.float32:
-            # one sv2n::window_gather launch (include/sv2n.h sv2n_window_gather)
+            # one sv2n::window_gather launch (include/sv2n.h sv2n_window_gather):
+            # starts[idx] = cut + idx, added in the kernel (no gather launch);
+            # an index past the windows names matrices past the series: NaN rows
             from . import library  # noqa: F401
             from .layout import canonical_table
-            torch.ops.sv2n.window_gather(self.vol.contiguous(), self.volvol.contiguous(), st, S,
-                                         Fs, canonical_table(n, self.vol.device), out.x,
-                                         out.edge_attr, out.y_x)
+            torch.ops.sv2n.window_gather(self.vol.contiguous(), self.volvol.contiguous(),
+                                         idx if idx.dtype == torch.long else idx.long(), S, Fs,
+                                         canonical_table(n, self.vol.device), out.x,
+                                         out.edge_attr, out.y_x, self.cut)
             return
+        st = self.starts.index_select(0, idx)
         tidx = st.view(B, 1) + self._arS.view(1, S)                               # [B, S]
         V = self.vol[tidx]                                                        # [B, S, n, n]
         W = self.volvol[tidx]

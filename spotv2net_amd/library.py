@@ -86,7 +86,7 @@ _SCHEMAS = {
                  "float eps, float weight_decay) -> ()",
     "window_gather": "(Tensor vol, Tensor volvol, Tensor starts, int seq_length, "
                      "int future_steps, Tensor canon, Tensor(a!) x, Tensor(b!) edge_attr, "
-                     "Tensor(c!) y) -> ()",
+                     "Tensor(c!) y, int start_offset=0) -> ()",
 }
 for _name, _schema in _SCHEMAS.items():
     LIB.define(_name + _schema)
@@ -770,7 +770,8 @@ def _adam_step_fake(param, grad, exp_avg, exp_avg_sq, step, ticket, lr, beta1, b
 
 
 @_impl("window_gather")
-def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y):
+def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y,
+                   start_offset=0):
     lib = _lib.load()
     _f32(vol, volvol, x, edge_attr, y)
     _need(vol.is_contiguous() and volvol.is_contiguous(), "series must be contiguous")
@@ -784,13 +785,15 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
     # windows outside the series come back as NaN (checked in the kernel:
     # the starts live on the device, so no host round trip here)
     _lib.check(lib.sv2n_window_gather(vol.data_ptr(), volvol.data_ptr(), vol.shape[1],
-                                      vol.shape[0], starts.data_ptr(), starts.numel(), seq_length, future_steps,
+                                      vol.shape[0], starts.data_ptr(), start_offset,
+                                      starts.numel(), seq_length, future_steps,
                                       canon.data_ptr(), x.data_ptr(), edge_attr.data_ptr(),
                                       y.data_ptr(), _st(vol)), "sv2n_window_gather")
 
 
 @_fake("window_gather")
-def _window_gather_fake(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y):
+def _window_gather_fake(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y,
+                        start_offset=0):
     return None
 
 

@@ -149,13 +149,19 @@ class TrainStep:
     share the parameters, gradients and optimizer state.
 
     Constructing it applies no update: the warm-up steps before capture are
-    undone (parameters, buffers, optimizer state, RNG)."""
+    undone (parameters, buffers, optimizer state, RNG).
+
+    ``loss_sum``: a device scalar every step adds its loss to inside the
+    captured step (the reference's per-epoch running loss,
+    5_train_SpotV2Net.py:160-163, without an eager launch per step)."""
 
     def __init__(self, model: torch.nn.Module, data, lr: float = 1e-3,
                  loss_fn: Callable = torch.nn.functional.mse_loss, use_graph: bool = True,
                  group=None, warmup: int = 3, optimizer: str = "sv2n",
-                 prepare: Optional[Callable[[], None]] = None):
+                 prepare: Optional[Callable[[], None]] = None,
+                 loss_sum: Optional[torch.Tensor] = None):
         self.model = model
+        self.loss_sum = loss_sum
         self.loss_fn = loss_fn
         self.group = group
         self.warmup = warmup
@@ -207,12 +213,18 @@ class TrainStep:
                     loss, dh = res
                     torch.autograd.backward(h, dh)
                     sh.loss = loss.detach()
+                    self._accumulate(sh)
                     return
                 loss = self.model.mse_loss(sh.data)
             else:
                 loss = self.loss_fn(self.model(sh.data), sh.data.y_x)
             torch.autograd.backward(loss, self._one)
         sh.loss = loss.detach()
+        self._accumulate(sh)
+
+    def _accumulate(self, sh: _Shape) -> None:
+        if self.loss_sum is not None:
+            self.loss_sum.add_(sh.loss)
 
     def _opt_step(self) -> None:
         self.opt.step()
@@ -231,6 +243,7 @@ class TrainStep:
         module buffers (BatchNorm running statistics with ``standardize``),
         optimizer state, RNG streams."""
         snap = {"params": self.flat_params.clone(), "opt": None,
+                "loss_sum": None if self.loss_sum is None else self.loss_sum.clone(),
                 "buffers": [b.detach().clone() for b in self.model.buffers()],
                 "cpu_rng": torch.get_rng_state(),
                 "cuda_rng": torch.cuda.get_rng_state(self.flat.device)}
@@ -247,6 +260,8 @@ class TrainStep:
         same buffers), so that construction does not train the model."""
         with torch.no_grad():
             self.flat_params.copy_(snap["params"])
+            if snap["loss_sum"] is not None:
+                self.loss_sum.copy_(snap["loss_sum"])
             for b, old in zip(self.model.buffers(), snap["buffers"]):
                 b.copy_(old)
             self.flat.zero_()
@@ -318,12 +333,15 @@ class ForwardStep:
     TrainStep."""
 
     def __init__(self, model: torch.nn.Module, data, use_graph: bool = True, warmup: int = 2,
-                 fn: Optional[Callable] = None, prepare: Optional[Callable[[], None]] = None):
+                 fn: Optional[Callable] = None, prepare: Optional[Callable[[], None]] = None,
+                 out_sum: Optional[torch.Tensor] = None):
         self.model, self.data = model, data
+        self.out_sum = out_sum  # device scalar each call adds fn's (scalar) output to
         self.fn = fn or (lambda m, d: m(d))
         self.prepare = prepare
         self.out: Optional[torch.Tensor] = None
         self.graph = None
+        saved = None if out_sum is None else out_sum.clone()
         with torch.no_grad():
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -337,11 +355,15 @@ class ForwardStep:
                 with torch.cuda.graph(self.graph):
                     self._run()
                 torch.cuda.synchronize()
+            if self.out_sum is not None:
+                self.out_sum.copy_(saved)  # undo the warm-up and capture calls
 
     def _run(self) -> None:
         if self.prepare is not None:
             self.prepare()
         self.out = self.fn(self.model, self.data)
+        if self.out_sum is not None:
+            self.out_sum.add_(self.out)
 
     def __call__(self) -> torch.Tensor:
         if self.graph is None:
@@ -389,12 +411,16 @@ class Fit:
             sizes.append(self.n_train % self.bs)
         self._train_shape = {}
         self.step = None
+        # per-epoch loss sums, accumulated inside the captured steps
+        self._tot_train = torch.zeros((), device=dev)
+        self._tot_test = torch.zeros((), device=dev)
         model.train()  # the training graphs are captured in train mode (dropout on)
         for b in sizes:
             data, prep = self._static(b)
             if self.step is None:
                 self.step = TrainStep(model, data, lr=lr, use_graph=self.use_graph,
-                                      optimizer=optimizer, prepare=prep)
+                                      optimizer=optimizer, prepare=prep,
+                                      loss_sum=self._tot_train)
                 self._train_shape[b] = 0
             else:
                 self._train_shape[b] = self.step.add_shape(data, prep)
@@ -416,7 +442,8 @@ class Fit:
             was = self.model.training
             self.model.eval()
             self._eval[b] = ForwardStep(self.model, data, use_graph=self.use_graph,
-                                        fn=lambda m, d: m.mse_loss(d).reshape(()), prepare=prep)
+                                        fn=lambda m, d: m.mse_loss(d).reshape(()), prepare=prep,
+                                        out_sum=self._tot_test)
             self.model.train(was)
         return self._eval[b]
 
@@ -424,7 +451,7 @@ class Fit:
         """One epoch: training pass, test pass, history entry (and checkpoint)."""
         dev = self.dev
         perm = torch.randperm(self.n_train, generator=self.gen).to(dev, non_blocking=True)
-        tot_train = torch.zeros((), device=dev)
+        self._tot_train.zero_()
         self.model.train()
         nb = 0
         for k in range(0, self.n_train, self.bs):
@@ -432,21 +459,22 @@ class Fit:
             self._idx[b].copy_(perm[k:k + b])
             if self.step_hook is not None:
                 self.step_hook(self.epoch, nb)
-            tot_train += self.step(self._train_shape[b])
+            self.step(self._train_shape[b])   # adds its loss to _tot_train
             nb += 1
-        tot_test = torch.zeros((), device=dev)
         nt = 0
         self.model.eval()
         test_idx = torch.arange(self.n_train, self.n_train + self.n_test, device=dev)
         for k in range(0, self.n_test, self.bs):
             b = min(self.bs, self.n_test - k)
             fs = self._eval_step(b)
+            if nt == 0:
+                self._tot_test.zero_()
             self._idx[b].copy_(test_idx[k:k + b])
-            tot_test += fs()
+            fs()                               # adds its loss to _tot_test
             nt += 1
         self.model.train()
-        train_loss = float(tot_train) / max(nb, 1)   # one host sync per epoch
-        test_loss = float(tot_test) / max(nt, 1)
+        train_loss = float(self._tot_train) / max(nb, 1)   # one host sync per epoch
+        test_loss = float(self._tot_test) / max(nt, 1)
         rec = {"epoch": self.epoch + 1, "train_loss": train_loss, "test_loss": test_loss,
                "train_rmse": train_loss ** 0.5, "test_rmse": test_loss ** 0.5}
         if checkpoint_path is not None and (self.epoch == 0 or
