@@ -332,9 +332,9 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 
 // ---------------------------------------------------------------------------
 // backward: S workgroups per graph (graph_split), split s owning heads
-// [s·HS, s·HS + HS).  Its waves form 4/WPH groups of WPH waves; group q owns
-// the split's heads q, q + 4/WPH, ... and wave k of a group takes chunks
-// k, k + WPH, ... of each.  Per head h (wave registers + the wave's LDS area):
+// [s·HS, s·HS + HS), HS <= 4.  Its waves form 4/WPH groups of WPH waves;
+// group q owns the split's head q and wave k of a group takes its chunks
+// k, k + WPH, ...  Per head h (wave registers + the wave's LDS area):
 //   dZ_h[i][c] = act'(dy, y) (· 1/H for the head mean),
 //   G[j][i]    = Σ_c xs[j][h·C + c] · dZ_h[i][c]          (dP_dᵀ: lane i, rows j)
 //   dxs[j][h·C + c] = Σ_i P_d[i][j] · dZ_h[i][c]
@@ -346,15 +346,24 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 // probabilities are loaded at) -> dl in sDL.  After a barrier: d ae of the
 // split's heads in edge order (one decode per edge), d a_src = column sums
 // of dl, d a_dst, zero padding (split 0).
-// C3 (128 graphs, H 6 x 500 columns) runs S 6, HS 1, WPH 4; S = 1, HS = H,
-// WPH = 1 (C2: 512 graphs) is one workgroup per graph with wave w owning
-// heads w, w + 4.
-// LDS: sP[HS][32][PS] (P_d, the A operand of dxs) | per wave 2 x [32][CS]
-//      chunk area | sDL[HS][32][DS] | sSh[HS][32] (self-loop share of row i) |
-//      sDad[HS][32] | sRB[32] | sDec[P] (pair p -> (u, w), u < w)
+// C3 (128 graphs, H 6 x 500 columns) runs S 6, HS 1, WPH 4; C2 (512 graphs,
+// H 4) S 1, HS 4, WPH 1: one workgroup per graph, wave w owning head w; 8
+// heads run at least two workgroups per graph.
+// LDS: sP[HS][32][PB] (P_d, the A operand of dxs) | per wave 2 x [32][CS]
+//      chunk area.  After the chunk loop (and a barrier) the chunk areas are
+//      reused for sDL[HS][32][DS] | sSh[HS][32] (self-loop share of row i) |
+//      sDad[HS][32] | sRB[32] | sDec[P] (pair p -> (u, w), u < w): 52 KB at
+//      C2's HS = 4, three workgroups per CU (74 KB and two before).
+//      HS <= 4 (canon_bwd_plan): each wave owns at most one head and keeps its
+//      G in registers until then.
 // ---------------------------------------------------------------------------
 constexpr int CS = 36;  // chunk row stride (floats): 16-B rows, conflict-free b128 row reads
 constexpr int DS = 33;  // dl row stride (floats): conflict-free column sums
+constexpr int PB = 32;  // P_d row stride: column reads only (conflict-free at any stride)
+
+__host__ __device__ inline int canon_bwd_tail_floats(int HS) {  // sDL .. sDec
+  return HS * 32 * DS + 2 * HS * 32 + 32 + (32 * 31 / 2 + 1) / 2;
+}
 
 template <int ACT, bool CONCAT, bool KEEP>
 __global__ __launch_bounds__(THREADS) void k_bwd(
@@ -366,8 +375,8 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     int HS, int WPH, int64_t B) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sP = smem;
-  float* sArea = sP + HS * 32 * PS;
-  float* sDL = sArea + 4 * 2 * 32 * CS;
+  float* sArea = sP + HS * 32 * PB;
+  float* sDL = sArea;  // after the chunk loop
   float* sSh = sDL + HS * 32 * DS;
   float* sDad = sSh + HS * 32;
   uint32_t* sRB = reinterpret_cast<uint32_t*>(sDad + HS * 32);  // source bits of row i
@@ -391,14 +400,15 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   const rsrc_t rps = make_rsrc(psave + g * H * 1024, (uint32_t)H * 4096u);
   const rsrc_t rdb = make_rsrc(dbias_part + g * OC, (uint32_t)OC * 4u);
   const bool post = post_u != nullptr;  // dy is the gradient of the post-dropout output
-  const rsrc_t ru = make_rsrc(post ? post_u + g * n * OC : nullptr, post ? (uint32_t)(n * OC) * 4u : 0u);
+  const rsrc_t ru =
+      make_rsrc(post ? post_u + g * n * OC : nullptr, post ? (uint32_t)(n * OC) * 4u : 0u);
 
   float* sX = sArea + wave * 2 * 32 * CS;
   float* sZ = sX + 32 * CS;
   const int nch = (C + 31) >> 5;
   const int cwb = (C + nch - 1) / nch;  // balanced chunk width (<= 32)
-  const int NG = 4 / WPH, grp = wave / WPH, sub = wave - grp * WPH;
-  const int nhw = grp < nhs ? (nhs - grp + NG - 1) / NG : 0;   // heads of this wave
+  const int grp = wave / WPH, sub = wave - grp * WPH;
+  const int nhw = grp < nhs ? 1 : 0;                            // heads of this wave (HS <= NG)
   const int ncw = sub < nch ? (nch - sub + WPH - 1) / WPH : 0;  // chunks per head
   const int nseq = nhw * ncw;                                  // (head, chunk) steps
 
@@ -406,7 +416,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   // row stride in the scalar offset)
   float rx_[16], rdy_[16], ry_[16], ru_[16];
   auto load_chunk = [&](int q) {
-    const int hq = q / ncw, ch = sub + WPH * (q - hq * ncw), h = h0 + grp + NG * hq;
+    const int ch = sub + WPH * q, h = h0 + grp;  // the wave's one head
     const int c = cwb * ch + l32;
     const bool cv = l32 < cwb && c < C;
     const int xo = cv ? (half * ldx + h * C + c) * 4 : OOB;
@@ -446,20 +456,15 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   const uint32_t rbits =
       (rowmask ? bld_u32(make_rsrc(rowmask + g * n, (uint32_t)n * 4u), l32 * 4) : allm) &
       ~(1u << l32);
-  if (t < 32) sRB[t] = rbits;
-  if (dae && ae_edge_order && t < n) {  // row u of the pair table (read after the final barrier)
-    const int base = (t * (2 * n - 1 - t)) >> 1;
-    for (int w = t + 1; w < n; ++w) sDec[base + w - t - 1] = (uint16_t)((t << 8) | w);
-  }
   floatx16 G;
 #pragma unroll
   for (int r = 0; r < 16; ++r) G[r] = 0.f;
   const int i = l32;
   const bool iv = i < n;
 
-  // ---- softmax / leaky_relu backward of head h (local hl) from G: lane (i,
+  // ---- softmax / leaky_relu backward of head h (local hl) from Gh: lane (i,
   //      half), rows j = crow(r, half) ----
-  auto softmax_bwd = [&](int hl) {
+  auto softmax_bwd = [&](int hl, const floatx16& Gh) {
     float ps[16], dp[16];
     float tl = 0.f;
 #pragma unroll
@@ -467,7 +472,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       const int jr = crow(r, half);
       ps[r] = pr[r >> 2][r & 3];
       const bool valid = iv && (jr == i || ((rbits >> jr) & 1u));
-      float d = valid ? (CONCAT ? G[r] : G[r] * invH) : 0.f;
+      float d = valid ? (CONCAT ? Gh[r] : Gh[r] * invH) : 0.f;
       if constexpr (KEEP) d = ((kb[r >> 2] >> (8 * (r & 3))) & 0xffu) ? d * keep_scale : 0.f;
       dp[r] = d;
       tl += fabsf(ps[r]) * d;
@@ -495,88 +500,85 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     }
   };
 
-  for (int q = 0; q < nseq; ++q) {
-    const int hq = q / ncw, chi = q - hq * ncw, ch = sub + WPH * chi;
-    const int hl = grp + NG * hq, h = h0 + hl;
-    const int c0 = cwb * ch, cw = min(cwb, C - c0);
-    if (chi == 0) {
-      // P_d of head h -> sP rows (each lane: its 16 positions of row i).  With
-      // WPH > 1 every wave of the group writes the same values: each reads
-      // only what it wrote itself.
-      float* prow = sP + (hl * 32 + l32) * PS + 4 * half;
+  if (nhw > 0) {  // wave-uniform
+    const int hl = grp, h = h0 + hl;
+    for (int chi = 0; chi < ncw; ++chi) {
+      const int q = chi, ch = sub + WPH * chi;
+      const int c0 = cwb * ch, cw = min(cwb, C - c0);
+      if (chi == 0) {
+        // P_d of head h -> sP rows (each lane: its 16 positions of row i).
+        // With WPH > 1 every wave of the group writes the same values: each
+        // reads only what it wrote itself.
+        float* prow = sP + (hl * 32 + l32) * PB + 4 * half;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        f32x4 v;
+        for (int m = 0; m < 4; ++m) {
+          f32x4 v;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float a = fabsf(pr[m][e]);
-          if constexpr (KEEP) a = ((kb[m] >> (8 * e)) & 0xffu) ? a * keep_scale : 0.f;
-          v[e] = iv ? a : 0.f;
+          for (int e = 0; e < 4; ++e) {
+            float a = fabsf(pr[m][e]);
+            if constexpr (KEEP) a = ((kb[m] >> (8 * e)) & 0xffu) ? a * keep_scale : 0.f;
+            v[e] = iv ? a : 0.f;
+          }
+          *reinterpret_cast<f32x4*>(prow + 8 * m) = v;
         }
-        *reinterpret_cast<f32x4*>(prow + 8 * m) = v;
       }
-    }
-    // stage the chunk: sX[row][c] = xs, sZ[row][c] = act'(dy, y)
-    SV2N_STAMP(2 + 2 * min(q, 3), SV2N_T());
+      // stage the chunk: sX[row][c] = xs, sZ[row][c] = act'(dy, y)
+      SV2N_STAMP(2 + 2 * min(q, 3), SV2N_T());
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const int row = 2 * m + half;
-      sX[row * CS + l32] = rx_[m];
-      const float d = post ? (ru_[m] >= post_p ? rdy_[m] * post_scale : 0.f) : rdy_[m];
-      sZ[row * CS + l32] = act_bwd<ACT>(d, ry_[m]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes, in order
-    SV2N_STAMP(3 + 2 * min(q, 3), SV2N_T());
-    if (q + 1 < nseq) load_chunk(q + 1);
-    // bias partials: column sums of dz (concat: this head's columns; mean: once)
-    if (CONCAT || h == 0) {
-      float sb = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sb += sZ[(16 * half + r) * CS + l32];
-      sb += __shfl_xor(sb, 32, 64);
-      bst(rdb, (half == 0 && l32 < cw) ? ((CONCAT ? h * C : 0) + c0 + l32) * 4 : OOB, sb);
-    }
-    // G[j][i] += Σ_c xs[j][c] · dZ[i][c]    (step kk pairs columns kk and 16 + kk;
-    // the chunk's columns past cw are staged zeros)
-    {
-      const f32x4* xa = reinterpret_cast<const f32x4*>(sX + l32 * CS + 16 * half);
-      const f32x4* zb = reinterpret_cast<const f32x4*>(sZ + l32 * CS + 16 * half);
-      f32x4 a4[4], b4[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        a4[m] = xa[m];
-        b4[m] = zb[m];
+      for (int m = 0; m < 16; ++m) {
+        const int row = 2 * m + half;
+        sX[row * CS + l32] = rx_[m];
+        const float d = post ? (ru_[m] >= post_p ? rdy_[m] * post_scale : 0.f) : rdy_[m];
+        sZ[row * CS + l32] = act_bwd<ACT>(d, ry_[m]);
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes, in order
+      SV2N_STAMP(3 + 2 * min(q, 3), SV2N_T());
+      if (q + 1 < nseq) load_chunk(q + 1);
+      // bias partials: column sums of dz (concat: this head's columns; mean: once)
+      if (CONCAT || h == 0) {
+        float sb = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sb += sZ[(16 * half + r) * CS + l32];
+        sb += __shfl_xor(sb, 32, 64);
+        bst(rdb, (half == 0 && l32 < cw) ? ((CONCAT ? h * C : 0) + c0 + l32) * 4 : OOB, sb);
+      }
+      // G[j][i] += Σ_c xs[j][c] · dZ[i][c]    (step kk pairs columns kk and 16 + kk;
+      // the chunk's columns past cw are staged zeros)
+      {
+        const f32x4* xa = reinterpret_cast<const f32x4*>(sX + l32 * CS + 16 * half);
+        const f32x4* zb = reinterpret_cast<const f32x4*>(sZ + l32 * CS + 16 * half);
+        f32x4 a4[4], b4[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          a4[m] = xa[m];
+          b4[m] = zb[m];
+        }
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk)
+          G = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[kk >> 2][kk & 3], b4[kk >> 2][kk & 3], G,
+                                                   0, 0, 0);
+      }
+      // dxs[j][c] = Σ_i P_d[i][j] · dZ[i][c]    (k: i = 16·half + kk)
+      floatx16 D;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) D[r] = 0.f;
+      const float* pcol = sP + (hl * 32 + 16 * half) * PB + l32;
+      const float* zcol = sZ + (16 * half) * CS + l32;
 #pragma unroll
       for (int kk = 0; kk < 16; ++kk)
-        G = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[kk >> 2][kk & 3], b4[kk >> 2][kk & 3], G, 0, 0,
-                                                 0);
-    }
-    // dxs[j][c] = Σ_i P_d[i][j] · dZ[i][c]    (k: i = 16·half + kk)
-    floatx16 D;
+        D = __builtin_amdgcn_mfma_f32_32x32x2f32(pcol[kk * PB], zcol[kk * CS], D, 0, 0, 0);
+      {
+        const int voff = l32 < cw ? (4 * half * ldx + h * C + c0 + l32) * 4 : OOB;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) D[r] = 0.f;
-    const float* pcol = sP + (hl * 32 + 16 * half) * PS + l32;
-    const float* zcol = sZ + (16 * half) * CS + l32;
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk)
-      D = __builtin_amdgcn_mfma_f32_32x32x2f32(pcol[kk * PS], zcol[kk * CS], D, 0, 0, 0);
-    {
-      const int voff = l32 < cw ? (4 * half * ldx + h * C + c0 + l32) * 4 : OOB;
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        bst_s(rdx, voff, ((r & 3) + 8 * (r >> 2)) * ldx * 4, CONCAT ? D[r] : D[r] * invH);
-    }
-    if (WPH == 1 && chi == ncw - 1) {
-      softmax_bwd(hl);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) G[r] = 0.f;
-      if (hq + 1 < nhw) load_p(h + NG);
+        for (int r = 0; r < 16; ++r)
+          bst_s(rdx, voff, ((r & 3) + 8 * (r >> 2)) * ldx * 4, CONCAT ? D[r] : D[r] * invH);
+      }
     }
   }
+  __syncthreads();  // every wave is done with the chunk areas (reused below)
   if (WPH > 1) {
     // one head per group: the group's partial G, added in wave order
-    float* sG = sArea + wave * 2 * 32 * CS;  // the wave's own chunk area (its reads are done)
+    float* sG = sArea + wave * 2 * 32 * CS;
 #pragma unroll
     for (int r = 0; r < 16; ++r) sG[r * 64 + lane] = G[r];
     __syncthreads();
@@ -586,8 +588,14 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 #pragma unroll
         for (int r = 0; r < 16; ++r) G[r] += o[r * 64 + lane];
       }
-      softmax_bwd(grp);
     }
+    __syncthreads();  // partials read: the area now takes sDL
+  }
+  if (nhw > 0 && sub == 0) softmax_bwd(grp, G);  // pr still holds this head's P
+  if (t < 32) sRB[t] = rbits;
+  if (dae && ae_edge_order && t < n) {  // row u of the pair table
+    const int base = (t * (2 * n - 1 - t)) >> 1;
+    for (int w = t + 1; w < n; ++w) sDec[base + w - t - 1] = (uint16_t)((t << 8) | w);
   }
   SV2N_STAMP(10, SV2N_T());
   __syncthreads();
@@ -698,12 +706,12 @@ static CanonBwdPlan canon_bwd_plan(int64_t B, int H, int C) {
   int S = 1;
   for (int s = 1; s <= H; ++s) {
     const int hs = (H + s - 1) / s;
-    if ((H + hs - 1) / hs != s) continue;  // no split without heads
+    if (hs > 4 || (H + hs - 1) / hs != s) continue;  // one head per wave; no empty split
     S = s;
     if (B * s >= CANON_FILL) break;
   }
   const int HS = (H + S - 1) / S;
-  const int WPH = HS <= 4 ? max(1, min(4 / HS, nch)) : 1;
+  const int WPH = max(1, min(4 / HS, nch));
   return {S, HS, WPH == 3 ? 2 : WPH};  // WPH divides 4
 }
 
@@ -712,9 +720,9 @@ static unsigned canon_grid(int64_t B, int S) {
 }
 
 size_t attn_canon_bwd_lds(int HS) {
-  return sizeof(float) * ((size_t)HS * 32 * canon::PS + 4 * 2 * 32 * canon::CS +
-                          (size_t)HS * 32 * canon::DS + 2 * (size_t)HS * 32 + 32) +
-         sizeof(uint16_t) * 32 * 31 / 2;
+  const int area = 4 * 2 * 32 * canon::CS;
+  return sizeof(float) * ((size_t)HS * 32 * canon::PB +
+                          (size_t)std::max(area, canon::canon_bwd_tail_floats(HS)));
 }
 
 template <int ACT, bool CONCAT, bool KEEP>

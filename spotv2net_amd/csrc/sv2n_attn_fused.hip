@@ -35,19 +35,21 @@
 //          (= Σ_j p·dP, the softmax row term), the self loop's whole gradient,
 //          and per-chunk bias partials;
 //   bwd    one 8-wave workgroup per (graph, 32-source tile) walking all
-//          targets in blocks of 16: recompute logits and P from the saved
-//          statistics, dP = dOut·xsᵀ and dxs += Pᵀ·dOut on MFMA (wave h: head
-//          h, the softmax backward in the MFMA output layout, P in registers),
-//          d a_src complete in the workgroup, d a_dst partial per source tile,
-//          dW̃ = Σ edge_attr ⊗ d logit in registers (edge rows split over 4
-//          lanes; one partial per workgroup);
+//          targets in blocks of 16, wave h doing all of head h's work on a
+//          block (k_fattn_bwd2): logits recomputed from the block's edge rows
+//          (staged once in LDS, double-buffered: one barrier per block) in the
+//          forward's summation order, dP = dOut·xsᵀ and dxs += Pᵀ·dOut on
+//          MFMA, the softmax backward in the MFMA output layout, d a_src
+//          complete in the workgroup, d a_dst partial per source tile, dW̃[:, h]
+//          in registers; 128 VGPRs so two workgroups share a CU (round 3: the
+//          three-phase form with logit / d-logit planes exchanged between
+//          waves ran one workgroup per CU, 2.20 -> 1.63 ms per C5 layer);
 //   finish d a_dst = Σ partials + self term, dW̃ = fixed-order sum of partials.
 // No atomics; every sum has a fixed order (deterministic).
 #include "sv2n_common.h"
 
-// tools/fattn_ablate.py builds variants with parts removed (timing only):
-// forward: 1 no edge_attr loads, 2 no softmax / MFMA phase, 3 no logit arithmetic;
-// backward: 4 no edge_attr loads, 5 no per-head phase [B], 6 no dW̃ phase [C]
+// tools/fattn_ablate.py builds forward variants with parts removed (timing
+// only): 1 no edge_attr loads, 2 no softmax / MFMA phase, 3 no logit arithmetic
 #ifndef SV2N_FATTN_ABLATE
 #define SV2N_FATTN_ABLATE 0
 #endif
@@ -646,49 +648,51 @@ __global__ __launch_bounds__(PT) void k_fattn_bprep(
 }
 
 // ---------------------------------------------------------------------------
-// backward: one 8-wave workgroup per (graph, 32-source tile)
-//   [A] slot owners (4 lanes per edge row, D/4 floats each): logits of the
-//       block's edges -> LDS; dOut rows and the per-target vectors staged
-//   [B] wave h: dP = dOut·xsᵀ on MFMA, the softmax / leaky / dropout backward
-//       in the MFMA output layout (lane (li, lk) holds targets 4lk+r, sources
-//       16jt+li), P kept in registers as the A operand of dxs += Pᵀ·dOut;
-//       d a_src accumulated in registers, d a_dst row sums stored per source
-//       tile, d logit (+ the self loop's share) -> LDS
-//   [C] slot owners: dW̃ += edge_attr ⊗ d logit in registers
+// backward, head-per-wave form: one 8-wave workgroup per (graph, 32-source
+// tile), walking the targets in blocks of 16 like k_fattn_bwd, but wave h
+// does ALL of head h's work on a block: its logits from the block's edge rows
+// (staged once in LDS for every head, double-buffered: one barrier per
+// block), the softmax / leaky / dropout backward in the MFMA output layout,
+// dW̃[:, h] accumulated in registers (D per lane), d a_src / d a_dst, and
+// dxs_h.  No logit or d-logit planes cross between waves, the xs rows and the
+// W̃ column of the wave's head live in registers, and the logits are summed
+// in the forward's order (even / odd d on packed FMAs), so the recomputed
+// probabilities are the forward's bit for bit.  Two workgroups fit a CU (128
+// VGPRs, 71 KB of LDS): the next block's rows are loaded after this block's
+// work, their latency covered by the other workgroup.
+// LDS: sEA[2][BT·BS][DP] edge rows | sO[2][BT][XW] dOut rows | sV[2][5][MH·BT]
+//      per-target vectors (max, 1/sum, r, a_dst, self-loop share) | sPres[2][BT]
 // ---------------------------------------------------------------------------
-constexpr int BHS = BT * RS + 16;  // backward: LDS stride of a head's [16][RS] block (≡ 16 mod 64)
-
 template <int D, bool EIDM, bool KEEP>
-__global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
+__global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
     const float* __restrict__ xs, int ldx, const float* __restrict__ ea,
     const float* __restrict__ wf, int hl_pad, int col0, const int32_t* __restrict__ eid,
     const uint8_t* __restrict__ keep, float keep_scale, const float* __restrict__ dout,
     const float* __restrict__ stats, const float* __restrict__ rs, float* __restrict__ dxs,
     float* __restrict__ adst_part, float* __restrict__ wpart, int n, int H, int C, float slope) {
-  __shared__ __attribute__((aligned(16))) float sXs[BS * XW];   // source rows, [j][h*16+c]
-  __shared__ __attribute__((aligned(16))) float sE[MH * BHS];   // edge logits of the block
-  __shared__ __attribute__((aligned(16))) float sD[MH * BHS];   // d logit (+ share) of the block
-  __shared__ __attribute__((aligned(16))) float sO[BT * XW];    // dOut rows of the block
-  __shared__ __attribute__((aligned(16))) float sM[MH * BT], sInv[MH * BT], sR[MH * BT],
-      sAd[MH * BT], sSh[MH * BT];
+  constexpr int DP = dpad<D>(), EV = DP / 4, NE = BT * BS, DH = (D + 1) / 2;
+  __shared__ __attribute__((aligned(16))) float sEA[2][NE * DP];
+  __shared__ __attribute__((aligned(16))) float sO[2][BT * XW];
+  __shared__ __attribute__((aligned(16))) float sV[2][5][MH * BT];
+  __shared__ __attribute__((aligned(16))) float sWT[MH * DP];  // W̃ columns, [h][d]
   __shared__ uint32_t sPres[2][BT];
-  // W̃ in four head orders: variant q holds head p ^ q at position p, so the
-  // quad's reduce-scatter of the partial logits needs no selects
-  __shared__ __attribute__((aligned(16))) float sW[4 * D * MH];
 
   const int NS = (n + BS - 1) / BS;
   int64_t g;
   int js;
   block_gt(NS, g, js);
-  const int t = threadIdx.x, lane = t & 63, hh = t >> 6;  // wave hh: head hh in [B]
+  const int t = threadIdx.x, lane = t & 63, hh = t >> 6;  // wave hh: head hh
+  for (int k = t; k < MH * DP; k += WT) {
+    const int h = k / DP, d = k - h * DP;
+    sWT[k] = (h < H && d < D) ? wf[d * hl_pad + col0 + h] : 0.f;
+  }
   const int li = lane & 15, lk = lane >> 4;
   const int j0 = js * BS;
   const int HC = H * C;
   const int64_t row0 = g * n;
   const int64_t Ntot = (int64_t)gridDim.x / NS * n;
   const int E0 = n * (n - 1);
-  constexpr bool eidm = EIDM;
-  const rsrc_t rea = eidm ? make_rsrc(nullptr, 0u)
+  const rsrc_t rea = EIDM ? make_rsrc(nullptr, 0u)
                           : make_rsrc(ea + g * (int64_t)E0 * D, (uint32_t)(4 * E0 * D));
   const rsrc_t rdo = make_rsrc(dout + row0 * HC, (uint32_t)(4 * n * HC));
   const rsrc_t rst = make_rsrc(stats + row0 * 4 * H, (uint32_t)(16 * n * H));
@@ -699,84 +703,61 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
   const bool hv = hh < H;
   float* const adst_row = adst_part + ((int64_t)js * Ntot + row0) * H + hh;  // + i*H
 
-  for (int k = t; k < 4 * D * MH; k += WT) {
-    const int qv = k / (D * MH), rem = k - qv * D * MH, d = rem / MH, hq = (rem % MH) ^ qv;
-    sW[k] = hq < H ? wf[d * hl_pad + col0 + hq] : 0.f;
-  }
-  if (eidm && t < 2 * BT) sPres[t >> 4][t & 15] = 0u;
-  // source rows of the tile (constant): xs_h padded to 16 columns per head
-  for (int idx = t; idx < BS * MH * 16; idx += WT) {
-    const int jl = idx >> 7, hc16 = idx & 127, h = hc16 >> 4, c = hc16 & 15, j = j0 + jl;
-    sXs[jl * XW + hc16] = (j < n && h < H && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
-  }
-  for (int idx = t; idx < BT * XW; idx += WT) sO[idx] = 0.f;  // padding columns stay zero
-  // a_src of this lane's sources (j = j0 + 16jt + li) for head hh
+  for (int idx = t; idx < 2 * BT * XW; idx += WT) (&sO[0][0])[idx] = 0.f;  // padding stays 0
+  // this wave's head: xs_h of the tile's sources (the B operand of dP, channels
+  // 4lk..4lk+3 of source 16jt + li) and a_src, and the W̃ column, in registers
+  f4 xb[2];
   float asrc[2];
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt) {
     const int j = j0 + 16 * jt + li;
-    asrc[jt] = (hv && j < n) ? xs[(row0 + j) * ldx + HC + hh] : 0.f;
+    const bool ok = hv && j < n;
+    xb[jt] = (ok && 4 * lk < C) ? bld4(rxs, 4 * (j * ldx + hh * C + 4 * lk)) : f4{0.f, 0.f, 0.f, 0.f};
+    asrc[jt] = ok ? bld(rxs, 4 * (j * ldx + HC + hh)) : 0.f;
   }
-  __syncthreads();
 
-  // edge slots: 512 per block, each split over 4 lanes (quarter = lane & 3)
-  constexpr int DQ = (D + 3) / 4;
-  const int qtr = t & 3, d0 = qtr * DQ;
-  const float* sWq = sW + qtr * D * MH;
-  // dW̃ accumulators as (head 2p, head 2p+1) pairs: packed FMAs (the kernel
-  // is VALU-issue-bound)
-  f2 wacc[DQ][MH / 2];
-#pragma unroll
-  for (int d = 0; d < DQ; ++d)
-#pragma unroll
-    for (int h2 = 0; h2 < MH / 2; ++h2) wacc[d][h2] = f2{0.f, 0.f};
-  f4 dacc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-  float das[2] = {0.f, 0.f};
-
-  // the next block's edge quarters, dOut chunk and target vectors (prefetch)
-  float evn[4][DQ], evc[4][DQ];
+  // prefetch registers: this thread's edge slot of the next block, a dOut
+  // chunk and a per-target vector
+  f32x4 evn[EV];
+  bool presn = false;
+  int sil = 0, sjl = 0;
   f32x4 don;
   float vecn[5];
-  auto slot = [&](int k, int i0, int& il, int& jl) {
-    const int s = (t >> 2) + 128 * k;
-    const bool along_i = !eidm && (j0 + BS <= i0);
-    il = along_i ? (s & 15) : (s >> 5);
-    jl = along_i ? (s >> 4) : (s & 31);
-  };
   auto issue = [&](int i0) {
+    const bool along_i = !EIDM && (j0 + BS <= i0);  // contiguous canonical runs
+    sil = along_i ? (t & 15) : (t >> 5);
+    sjl = along_i ? (t >> 4) : (t & 31);
+    const int i = i0 + sil, j = j0 + sjl;
+    if constexpr (EIDM) {
+      const int64_t gid = (i < n && j < n && i != j) ? eid[(row0 + i) * n + j] : -1;
+      presn = gid >= 0;
+      const float* p = ea + (presn ? gid : 0) * D;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      int il, jl;
-      slot(k, i0, il, jl);
-      const int i = i0 + il, j = j0 + jl;
-      int cid = -1;
-      int64_t gid = -1;
-      if constexpr (eidm) gid = (i < n && j < n && i != j) ? eid[(row0 + i) * n + j] : -1;
-      else cid = canon_id(i, j, n);
-      if constexpr (eidm) {
-        const bool ok = gid >= 0;
-        const float* p = ea + (ok ? gid : 0) * D + d0;
+      for (int q = 0; q < EV; ++q)
 #pragma unroll
-        for (int dd = 0; dd < DQ; ++dd) evn[k][dd] = (ok && d0 + dd < D) ? p[dd] : 0.f;
-      } else if (SV2N_FATTN_ABLATE == 4) {
+        for (int c = 0; c < 4; ++c) evn[q][c] = (presn && 4 * q + c < D) ? p[4 * q + c] : 0.f;
+    } else {
+      const int cid = canon_id(i, j, n);
+      if constexpr (D % 4 == 0) {
 #pragma unroll
-        for (int dd = 0; dd < DQ; ++dd) evn[k][dd] = (float)(cid & 7) * 0.01f;
+        for (int q = 0; q < EV; ++q) evn[q] = bld4(rea, cid >= 0 ? 4 * (cid * D + 4 * q) : OOB);
       } else {
 #pragma unroll
-        for (int dd = 0; dd < DQ; ++dd)
-          evn[k][dd] = (d0 + dd < D) ? bld(rea, cid >= 0 ? 4 * (__mul24(cid, D) + d0 + dd) : OOB) : 0.f;
+        for (int q = 0; q < EV; ++q)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            evn[q][c] = 4 * q + c < D ? bld(rea, cid >= 0 ? 4 * (cid * D + 4 * q + c) : OOB) : 0.f;
       }
     }
     {
-      const int r = t / HQ, cq = t - r * HQ, i = i0 + r;
-      don = bld4(rdo, (r < BT && i < n) ? 4 * (i * HC + 4 * cq) : OOB);
+      const int r = t / HQ, cq = t - r * HQ, i2 = i0 + r;
+      don = bld4(rdo, (r < BT && i2 < n) ? 4 * (i2 * HC + 4 * cq) : OOB);
     }
     if (t < MH * BT) {
-      // graph-local buffer offsets (a miss reads 0)
-      const int h = t >> 4, il = t & 15, i = i0 + il;
-      const bool ok = h < H && i < n;
-      const int o4 = ok ? 4 * (__mul24(i, 4 * H) + h) : OOB;
-      const int ox = ok ? 4 * (__mul24(i, ldx) + HC + H + h) : OOB;
+      const int h = t >> 4, il = t & 15, i2 = i0 + il;
+      const bool ok = h < H && i2 < n;
+      const int o4 = ok ? 4 * (__mul24(i2, 4 * H) + h) : OOB;
+      const int ox = ok ? 4 * (__mul24(i2, ldx) + HC + H + h) : OOB;
       vecn[0] = bld(rst, o4);
       vecn[1] = bld(rst, ok ? o4 + 4 * H : OOB);
       vecn[2] = bld(rrs, o4);
@@ -784,165 +765,129 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
       vecn[4] = bld(rrs, ok ? o4 + 12 * H : OOB);
     }
   };
-
-  issue(0);
-  int par = 0;
-  for (int i0 = 0; i0 < n; i0 += BT, par ^= 1) {
-    // ---- [A] stage the block: logits (2 heads per lane of a quad), dOut, vectors ----
+  auto stage = [&](int buf) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int d = 0; d < DQ; ++d) evc[k][d] = evn[k][d];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      // partial logits over this lane's quarter of the row (scalar FMAs: no
-      // packed copies of the prefetched values), completed over the quad
-      // position p holds head p ^ qtr (this lane's W̃ variant)
-      float lf[MH];
-#pragma unroll
-      for (int h = 0; h < MH; ++h) lf[h] = 0.f;
-      f2 lf2[MH / 2] = {f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}};
-#pragma unroll
-      for (int dd = 0; dd < DQ; ++dd) {
-        const float* wr = sWq + min(d0 + dd, D - 1) * MH;
-        const f4 wa = *reinterpret_cast<const f4*>(wr);
-        const f4 wb = *reinterpret_cast<const f4*>(wr + 4);
-        const f2 e2 = f2{evc[k][dd], evc[k][dd]};
-        lf2[0] = __builtin_elementwise_fma(e2, f2{wa.x, wa.y}, lf2[0]);
-        lf2[1] = __builtin_elementwise_fma(e2, f2{wa.z, wa.w}, lf2[1]);
-        lf2[2] = __builtin_elementwise_fma(e2, f2{wb.x, wb.y}, lf2[2]);
-        lf2[3] = __builtin_elementwise_fma(e2, f2{wb.z, wb.w}, lf2[3]);
-      }
-#pragma unroll
-      for (int h = 0; h < MH; ++h) lf[h] = lf2[h >> 1][h & 1];
-      // quad reduce-scatter: partner q^1's position p^1 holds this lane's
-      // head p^q, then partner q^2's s1[i^1] holds s1[i]'s head; lane q ends
-      // with heads q (position 0) and q + 4 (position 4)
-      float s1[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) s1[i] = lf[2 * i] + dpp_xor1(lf[2 * i + 1]);
-      const float hq0 = s1[0] + dpp_xor2(s1[1]);
-      const float hq4 = s1[2] + dpp_xor2(s1[3]);
-      int il, jl;
-      slot(k, i0, il, jl);
-      float* dst = sE + il * RS + jl;
-      dst[qtr * BHS] = hq0;
-      dst[(qtr + 4) * BHS] = hq4;
-      if (eidm && qtr == 0) {
-        const int i = i0 + il, j = j0 + jl;
-        const bool pres = i < n && j < n && i != j && eid[(row0 + i) * n + j] >= 0;
-        if (pres) atomicOr(&sPres[par][il], 1u << jl);
-      }
-    }
+    for (int q = 0; q < EV; ++q)
+      *reinterpret_cast<f32x4*>(&sEA[buf][(sil * BS + sjl) * DP + 4 * q]) = evn[q];
     {
       const int r = t / HQ, cq = t - r * HQ;
       if (r < BT) {
         const int cg = 4 * cq, h = cg / C, c = cg - h * C;
-        *reinterpret_cast<f4*>(sO + r * XW + h * 16 + c) = f4{don.x, don.y, don.z, don.w};
+        *reinterpret_cast<f32x4*>(&sO[buf][r * XW + h * 16 + c]) = don;
       }
     }
     if (t < MH * BT) {
-      sM[t] = vecn[0];
-      sInv[t] = vecn[1];
-      sR[t] = vecn[2];
-      sAd[t] = vecn[3];
-      sSh[t] = vecn[4];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) sV[buf][k][t] = vecn[k];
     }
-    if (i0 + BT < n) issue(i0 + BT);
-    __syncthreads();
+    if constexpr (EIDM) {  // row sil = 32 consecutive threads: one ballot per half-wave
+      const uint64_t m = __ballot(presn);
+      if ((lane & 31) == 0) sPres[buf][sil] = (uint32_t)(m >> (lane & 32));
+    }
+  };
 
-    // ---- [B] wave hh ----
-    if (hv && SV2N_FATTN_ABLATE != 5) {
+  f2 wacc[DH];
+#pragma unroll
+  for (int d = 0; d < DH; ++d) wacc[d] = f2{0.f, 0.f};
+  f4 dacc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  float das[2] = {0.f, 0.f};
+
+  issue(0);
+  stage(0);
+  __syncthreads();
+  int par = 0;
+  for (int i0 = 0; i0 < n; i0 += BT, par ^= 1) {
+    if (hv) {
       const bool clean =
-          !eidm && (j0 + BS <= i0 || i0 + BT <= j0) && j0 + BS <= n && i0 + BT <= n;
+          !EIDM && (j0 + BS <= i0 || i0 + BT <= j0) && j0 + BS <= n && i0 + BT <= n;
+      const float* sEAb = sEA[par];
+      const float* sOb = sO[par];
       // dP[i][j] = dOut_h[i] · xs_h[j]: rows i = 4lk + r, columns j = 16jt + li
       f4 pacc[2];
-      const f4 oa = *reinterpret_cast<const f4*>(sO + li * XW + hh * 16 + 4 * lk);
+      const f4 oa = *reinterpret_cast<const f4*>(sOb + li * XW + hh * 16 + 4 * lk);
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt) {
-        const f4 xb = *reinterpret_cast<const f4*>(sXs + (16 * jt + li) * XW + hh * 16 + 4 * lk);
         f4 pa = {0.f, 0.f, 0.f, 0.f};
-        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.x, xb.x, pa, 0, 0, 0);
-        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.y, xb.y, pa, 0, 0, 0);
-        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.z, xb.z, pa, 0, 0, 0);
-        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.w, xb.w, pa, 0, 0, 0);
+        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.x, xb[jt].x, pa, 0, 0, 0);
+        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.y, xb[jt].y, pa, 0, 0, 0);
+        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.z, xb[jt].z, pa, 0, 0, 0);
+        pa = __builtin_amdgcn_mfma_f32_16x16x4f32(oa.w, xb[jt].w, pa, 0, 0, 0);
         pacc[jt] = pa;
       }
       const int q0 = hh * BT + 4 * lk;
-      const f4 m4 = *reinterpret_cast<const f4*>(sM + q0);
-      const f4 inv4 = *reinterpret_cast<const f4*>(sInv + q0);
-      const f4 r4 = *reinterpret_cast<const f4*>(sR + q0);
-      const f4 ad4 = *reinterpret_cast<const f4*>(sAd + q0);
-      const f4 sh4 = *reinterpret_cast<const f4*>(sSh + q0);
-      const float mv[4] = {m4.x, m4.y, m4.z, m4.w}, iv[4] = {inv4.x, inv4.y, inv4.z, inv4.w};
-      const float rv[4] = {r4.x, r4.y, r4.z, r4.w}, av[4] = {ad4.x, ad4.y, ad4.z, ad4.w};
-      const float shv[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
-      float pd[2][4], rowacc[4] = {0.f, 0.f, 0.f, 0.f};
+      const f4* wt = reinterpret_cast<const f4*>(sWT + hh * DP);  // broadcast reads
+      // target rows r of the lane one at a time (rolled: only the two edges of
+      // one row are live), each finishing its d a_dst partial and its k-slice
+      // of dxs += Pᵀ·dOut right away
+#pragma unroll 1
+      for (int r = 0; r < 4; ++r) {
+        const int il = 4 * lk + r, i = i0 + il;
+        const float mv = sV[par][0][q0 + r], iv = sV[par][1][q0 + r], rv = sV[par][2][q0 + r];
+        const float av = sV[par][3][q0 + r], shv = sV[par][4][q0 + r];
+        const float ob = sOb[il * XW + hh * 16 + li];  // dOut_h[i][c = li]
+        float rowacc = 0.f;
 #pragma unroll
-      for (int jt = 0; jt < 2; ++jt) {
-        const float dpv[4] = {pacc[jt].x, pacc[jt].y, pacc[jt].z, pacc[jt].w};
-        const int jl = 16 * jt + li, j = j0 + jl;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int il = 4 * lk + r, i = i0 + il;
+        for (int jt = 0; jt < 2; ++jt) {
+          const int jl = 16 * jt + li, j = j0 + jl;
           bool valid = true;
           if (!clean) {
             valid = i < n && j < n && i != j;
-            if constexpr (eidm) valid = valid && ((sPres[par][il] >> jl) & 1u);
+            if constexpr (EIDM) valid = valid && ((sPres[par][il] >> jl) & 1u);
           }
-          const int e = hh * BHS + il * RS + jl;
-          const float v = asrc[jt] + av[r] + sE[e];
-          const float p = valid ? fexp2(v * (v > 0.f ? L2E : slope2) - mv[r]) * iv[r] : 0.f;
-          float pk = p, dP = dpv[r];
+          // the edge row and its logit, in the forward's order (even / odd d)
+          const f4* er = reinterpret_cast<const f4*>(sEAb + (il * BS + jl) * DP);
+          float ev[DP];
+#pragma unroll
+          for (int q = 0; q < EV; ++q) {
+            const f4 w = er[q];
+            ev[4 * q] = w.x; ev[4 * q + 1] = w.y; ev[4 * q + 2] = w.z; ev[4 * q + 3] = w.w;
+          }
+          f2 a2 = f2{0.f, 0.f};
+#pragma unroll
+          for (int q = 0; q < EV; ++q) {
+            const f4 w4 = wt[q];
+            if (4 * q < D)
+              a2 = __builtin_elementwise_fma(f2{ev[4 * q], 4 * q + 1 < D ? ev[4 * q + 1] : 0.f},
+                                             f2{w4.x, w4.y}, a2);
+            if (4 * q + 2 < D)
+              a2 = __builtin_elementwise_fma(
+                  f2{ev[4 * q + 2], 4 * q + 3 < D ? ev[4 * q + 3] : 0.f}, f2{w4.z, w4.w}, a2);
+          }
+          const float v = asrc[jt] + av + (a2.x + a2.y);
+          const float p = valid ? fexp2(v * (v > 0.f ? L2E : slope2) - mv) * iv : 0.f;
+          const f4 pa = pacc[jt];
+          float dP = r == 0 ? pa.x : (r == 1 ? pa.y : (r == 2 ? pa.z : pa.w));
+          float pk = p;
           if constexpr (KEEP) {
             const bool kp = valid && keep[((g * H + hh) * (int64_t)n + i) * n + j] != 0;
             pk = kp ? p * keep_scale : 0.f;
             dP = kp ? dP * keep_scale : 0.f;
           }
-          const float ds = p * (dP - rv[r]);
+          const float ds = p * (dP - rv);
           const float dl = valid ? (v > 0.f ? ds : ds * slope) : 0.f;
-          pd[jt][r] = pk;
           das[jt] += dl;
-          rowacc[r] += dl;
-          sD[e] = valid ? dl + shv[r] : 0.f;
-        }
-      }
-      // d a_dst partial of this source tile: row sums over the 16 lanes li
+          rowacc += dl;
+          // dxs_h[j][c] += P[i][j] dOut_h[i][c]: this row's k-slice (A = P, lane (j, lk))
+          dacc[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pk, ob, dacc[jt], 0, 0, 0);
+          // dW̃[:, h] += edge row ⊗ (d logit + the self loop's share)
+          const float wsc = valid ? dl + shv : 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float s = row16_sum(rowacc[r]);
-        const int i = i0 + 4 * lk + r;
+          for (int d = 0; d < DH; ++d)
+            wacc[d] = __builtin_elementwise_fma(f2{ev[2 * d], 2 * d + 1 < D ? ev[2 * d + 1] : 0.f},
+                                                f2{wsc, wsc}, wacc[d]);
+        }
+        // d a_dst partial of this source tile: the row sum over the 16 lanes li
+        const float s = row16_sum(rowacc);
         if (li == 0 && i < n) adst_row[__mul24(i, H)] = s;
       }
-      // dxs_h[j][c] += Σ_i P[i][j] dOut_h[i][c]: A = P from registers (k = 4lk + s)
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const float ob = sO[(4 * lk + s) * XW + hh * 16 + li];
-          dacc[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pd[jt][s], ob, dacc[jt], 0, 0, 0);
-        }
-      }
     }
-    if constexpr (eidm) {
-      if (t < BT) sPres[par ^ 1][t] = 0u;
+    // the next block to the other buffer (last read before the previous
+    // barrier); its loads wait here, under the other workgroup on the CU
+    if (i0 + BT < n) {
+      issue(i0 + BT);
+      stage(par ^ 1);
     }
     __syncthreads();
-
-    // ---- [C] dW̃ += edge_attr ⊗ (d logit + the self loop's share) ----
-#pragma unroll
-    for (int k = 0; k < (SV2N_FATTN_ABLATE == 6 ? 0 : 4); ++k) {
-      int il, jl;
-      slot(k, i0, il, jl);
-      const float* dr = sD + il * RS + jl;
-#pragma unroll
-      for (int h2 = 0; h2 < MH / 2; ++h2) {
-        const f2 dlw = f2{dr[(2 * h2) * BHS], dr[(2 * h2 + 1) * BHS]};
-#pragma unroll
-        for (int d = 0; d < DQ; ++d)
-          wacc[d][h2] = __builtin_elementwise_fma(f2{evc[k][d], evc[k][d]}, dlw, wacc[d][h2]);
-      }
-    }
   }
 
   // ---- d a_src (complete: every target was visited) + the self loop ----
@@ -978,29 +923,18 @@ __global__ __launch_bounds__(WT, 2) void k_fattn_bwd(
       if (j < n) dxs[(row0 + j) * ldx + HC + 2 * H + (idx - jl * padc)] = 0.f;
     }
   }
-  // ---- dW̃ partial of the workgroup: the 4 same-quarter lanes of each 16-lane
-  //      row (DPP), then the 32 rows of the workgroup ----
-  __syncthreads();
-  float* sRed = sE;  // [32][D*MH] <= MH*BHS floats
+  // ---- dW̃[:, h] partial of the workgroup: the wave's 64 lanes ----
+  if (hv) {
+    const int64_t P = (int64_t)gridDim.x;
+    const int64_t part = g * NS + js;
 #pragma unroll
-  for (int d = 0; d < DQ; ++d)
+    for (int d = 0; d < DH; ++d) {
 #pragma unroll
-    for (int h = 0; h < MH; ++h) {
-      float v = wacc[d][h >> 1][h & 1];
-      v += dppf<0x124>(v);
-      v += dppf<0x128>(v);
-      if (li < 4 && d0 + d < D) sRed[(hh * 4 + lk) * (D * MH) + (d0 + d) * MH + h] = v;
-    }
-  __syncthreads();
-  const int64_t P = (int64_t)gridDim.x;
-  const int64_t part = g * NS + js;
-  if (t < D * MH) {
-    const int d = t / MH, h = t - d * MH;
-    if (h < H) {
-      float s = 0.f;
-#pragma unroll
-      for (int r = 0; r < 32; ++r) s += sRed[r * (D * MH) + t];
-      wpart[(int64_t)(d * H + h) * P + part] = s;
+      for (int e = 0; e < 2; ++e) {
+        const int dd = 2 * d + e;
+        const float v = lk_sum(row16_sum(wacc[d][e]));
+        if (lane == 0 && dd < D) wpart[(int64_t)(dd * H + hh) * P + part] = v;
+      }
     }
   }
 }
@@ -1142,7 +1076,7 @@ extern "C" int sv2n_gat_attn_fused_bwd(const float* dy, const float* y, const fl
                      act, concat, negative_slope);
   const dim3 grid((unsigned)(num_graphs * NS));
 #define SV2N_FBWD1(DD, EM, KP)                                                                  \
-  hipLaunchKernelGGL((k_fattn_bwd<DD, EM, KP>), grid, dim3(WT), 0, stream, xs, ldx, edge_attr, wfold,     \
+  hipLaunchKernelGGL((k_fattn_bwd2<DD, EM, KP>), grid, dim3(WT), 0, stream, xs, ldx, edge_attr, wfold, \
                      hl_pad, col0, eid, keep, keep_scale, dout, stats, rs, dxs, adst, wpart, n, \
                      H, C, negative_slope)
   switch (edge_dim) {

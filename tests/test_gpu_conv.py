@@ -150,8 +150,9 @@ def test_no_bias(dev, concat):
     (3, 2, 100, True),    # bwd: 2 splits, a head's 4 chunks over 4 waves
     (300, 3, 40, True),   # bwd: 2 splits of 2 + 1 heads (the last split half empty)
     (100, 5, 40, False),  # bwd: 5 splits of 1 head, 2 chunks over 2 waves
-    (1024, 8, 4, True),   # one workgroup per graph, 2 heads per wave (at B = 1000 / 1100
-                          # these seeds put an attention logit on the leaky-ReLU kink)
+    (1024, 8, 4, True),   # 8 heads with the batch filling the chip: bwd 2 splits of 4 heads
+                          # (at B = 1000 / 1100 these seeds put an attention logit on the
+                          # leaky-ReLU kink)
 ])
 def test_workgroup_splits(dev, B, heads, C, concat):
     """n <= 32 attention with a graph's work spread over several workgroups

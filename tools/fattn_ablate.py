@@ -10,8 +10,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "spotv2net_amd", "csrc", "sv2n_attn_fused.hip")
+# (round 3 replaced the backward by the head-per-wave kernel; its round-2
+# ablations 4-6 belonged to the three-phase kernel and are gone)
 VARIANTS = {0: "product", 1: "no edge_attr loads", 2: "no softmax/MFMA", 3: "no logit math",
-            4: "bwd: no edge_attr loads", 5: "bwd: no per-head phase", 6: "bwd: no dW phase",
             7: "bwd: product"}
 
 
