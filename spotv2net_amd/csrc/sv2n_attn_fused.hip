@@ -47,6 +47,7 @@
 //   finish d a_dst = Σ partials + self term, dW̃ = fixed-order sum of partials.
 // No atomics; every sum has a fixed order (deterministic).
 #include "sv2n_common.h"
+#include <type_traits>
 
 // tools/fattn_ablate.py builds forward variants with parts removed (timing
 // only): 1 no edge_attr loads, 2 no softmax / MFMA phase, 3 no logit arithmetic
@@ -670,12 +671,21 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
     const uint8_t* __restrict__ keep, float keep_scale, const float* __restrict__ dout,
     const float* __restrict__ stats, const float* __restrict__ rs, float* __restrict__ dxs,
     float* __restrict__ adst_part, float* __restrict__ wpart, int n, int H, int C, float slope) {
-  constexpr int DP = dpad<D>(), EV = DP / 4, NE = BT * BS, DH = (D + 1) / 2;
-  __shared__ __attribute__((aligned(16))) float sEA[2][NE * DP];
-  __shared__ __attribute__((aligned(16))) float sO[2][BT * XW];
-  __shared__ __attribute__((aligned(16))) float sV[2][5][MH * BT];
-  __shared__ __attribute__((aligned(16))) float sWT[MH * DP];  // W̃ columns, [h][d]
-  __shared__ uint32_t sPres[2][BT];
+  constexpr int DP = dpad<D>(), EV = DP / 4, DH = (D + 1) / 2;
+  // edge rows of one target: BS·DP floats + 16 of padding (the along-i staging
+  // writes of 16 consecutive targets then spread over the banks; the row
+  // loop's b128 reads stay conflict-free)
+  constexpr int ES = BS * DP + 16;
+  // one LDS block, the small per-block arrays first (their reads in the row
+  // loop take immediate offsets from one base register)
+  constexpr int O_V = 0, O_WT = O_V + 2 * 5 * MH * BT, O_PR = O_WT + MH * DP;
+  constexpr int O_O = (O_PR + 2 * BT + 3) & ~3, O_EA = O_O + 2 * BT * XW;
+  __shared__ __attribute__((aligned(16))) float smem[O_EA + 2 * BT * ES];
+  float(*const sV)[5][MH * BT] = reinterpret_cast<float(*)[5][MH * BT]>(smem + O_V);
+  float* const sWT = smem + O_WT;  // W̃ columns, [h][d]
+  uint32_t(*const sPres)[BT] = reinterpret_cast<uint32_t(*)[BT]>(smem + O_PR);
+  float(*const sO)[BT * XW] = reinterpret_cast<float(*)[BT * XW]>(smem + O_O);
+  float(*const sEA)[BT * ES] = reinterpret_cast<float(*)[BT * ES]>(smem + O_EA);
 
   const int NS = (n + BS - 1) / BS;
   int64_t g;
@@ -768,7 +778,7 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
   auto stage = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < EV; ++q)
-      *reinterpret_cast<f32x4*>(&sEA[buf][(sil * BS + sjl) * DP + 4 * q]) = evn[q];
+      *reinterpret_cast<f32x4*>(&sEA[buf][sil * ES + sjl * DP + 4 * q]) = evn[q];
     {
       const int r = t / HQ, cq = t - r * HQ;
       if (r < BT) {
@@ -797,9 +807,10 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
   __syncthreads();
   int par = 0;
   for (int i0 = 0; i0 < n; i0 += BT, par ^= 1) {
-    if (hv) {
-      const bool clean =
-          !EIDM && (j0 + BS <= i0 || i0 + BT <= j0) && j0 + BS <= n && i0 + BT <= n;
+    // the block's work for this wave's head; CLEAN: no diagonal, no edge-id
+    // map, no partial tile (every (target, source) pair is an edge)
+    auto head_block = [&](auto clean_tag) __attribute__((always_inline)) {
+      constexpr bool CLEAN = decltype(clean_tag)::value;
       const float* sEAb = sEA[par];
       const float* sOb = sO[par];
       // dP[i][j] = dOut_h[i] · xs_h[j]: rows i = 4lk + r, columns j = 16jt + li
@@ -822,20 +833,21 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
 #pragma unroll 1
       for (int r = 0; r < 4; ++r) {
         const int il = 4 * lk + r, i = i0 + il;
-        const float mv = sV[par][0][q0 + r], iv = sV[par][1][q0 + r], rv = sV[par][2][q0 + r];
-        const float av = sV[par][3][q0 + r], shv = sV[par][4][q0 + r];
+        const float* vr = &sV[par][0][q0 + r];
+        const float mv = vr[0], iv = vr[MH * BT], rv = vr[2 * MH * BT];
+        const float av = vr[3 * MH * BT], shv = vr[4 * MH * BT];
         const float ob = sOb[il * XW + hh * 16 + li];  // dOut_h[i][c = li]
         float rowacc = 0.f;
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt) {
           const int jl = 16 * jt + li, j = j0 + jl;
           bool valid = true;
-          if (!clean) {
+          if constexpr (!CLEAN) {
             valid = i < n && j < n && i != j;
             if constexpr (EIDM) valid = valid && ((sPres[par][il] >> jl) & 1u);
           }
           // the edge row and its logit, in the forward's order (even / odd d)
-          const f4* er = reinterpret_cast<const f4*>(sEAb + (il * BS + jl) * DP);
+          const f4* er = reinterpret_cast<const f4*>(sEAb + il * ES + jl * DP);
           float ev[DP];
 #pragma unroll
           for (int q = 0; q < EV; ++q) {
@@ -853,8 +865,9 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
               a2 = __builtin_elementwise_fma(
                   f2{ev[4 * q + 2], 4 * q + 3 < D ? ev[4 * q + 3] : 0.f}, f2{w4.z, w4.w}, a2);
           }
-          const float v = asrc[jt] + av + (a2.x + a2.y);
-          const float p = valid ? fexp2(v * (v > 0.f ? L2E : slope2) - mv) * iv : 0.f;
+          const float v = (asrc[jt] + av) + (a2.x + a2.y);
+          float p = fexp2(v * (v > 0.f ? L2E : slope2) - mv) * iv;
+          if constexpr (!CLEAN) p = valid ? p : 0.f;
           const f4 pa = pacc[jt];
           float dP = r == 0 ? pa.x : (r == 1 ? pa.y : (r == 2 ? pa.z : pa.w));
           float pk = p;
@@ -864,13 +877,15 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
             dP = kp ? dP * keep_scale : 0.f;
           }
           const float ds = p * (dP - rv);
-          const float dl = valid ? (v > 0.f ? ds : ds * slope) : 0.f;
+          float dl = v > 0.f ? ds : ds * slope;
+          if constexpr (!CLEAN) dl = valid ? dl : 0.f;
           das[jt] += dl;
           rowacc += dl;
           // dxs_h[j][c] += P[i][j] dOut_h[i][c]: this row's k-slice (A = P, lane (j, lk))
           dacc[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pk, ob, dacc[jt], 0, 0, 0);
           // dW̃[:, h] += edge row ⊗ (d logit + the self loop's share)
-          const float wsc = valid ? dl + shv : 0.f;
+          float wsc = dl + shv;
+          if constexpr (!CLEAN) wsc = valid ? wsc : 0.f;
 #pragma unroll
           for (int d = 0; d < DH; ++d)
             wacc[d] = __builtin_elementwise_fma(f2{ev[2 * d], 2 * d + 1 < D ? ev[2 * d + 1] : 0.f},
@@ -880,6 +895,12 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
         const float s = row16_sum(rowacc);
         if (li == 0 && i < n) adst_row[__mul24(i, H)] = s;
       }
+    };
+    if (hv) {
+      if (!EIDM && (j0 + BS <= i0 || i0 + BT <= j0) && j0 + BS <= n && i0 + BT <= n)
+        head_block(std::true_type{});
+      else
+        head_block(std::false_type{});
     }
     // the next block to the other buffer (last read before the previous
     // barrier); its loads wait here, under the other workgroup on the CU

@@ -1,6 +1,6 @@
 #!/bin/bash
-# C5 fused backward A/B: the product library vs spotv2net_amd/libsv2n_oldbwd.so
-# (the same tree built with -DSV2N_FBWD_KERNEL=k_fattn_bwd), fused tests first.
+# C5 A/B: the product library vs an alternative build of the same tree
+# (tools/c5_ab.sh OUT [ALT_LIB]; default spotv2net_amd/libsv2n_alt.so), fused tests first.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-c5ab}
@@ -10,7 +10,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_til
 echo "tests rc=$rc"; tail -2 $O/tests.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --config c5 --no-cpu-baseline --no-ref-loop > $O/new.json 2>$O/new.err || exit 2
-SV2N_LIB=$R/spotv2net_amd/libsv2n_oldbwd.so timeout -k 10 300 python bench.py --config c5 --no-cpu-baseline --no-ref-loop > $O/old.json 2>$O/old.err || exit 3
+SV2N_LIB=$R/${2:-spotv2net_amd/libsv2n_alt.so} timeout -k 10 300 python bench.py --config c5 --no-cpu-baseline --no-ref-loop > $O/old.json 2>$O/old.err || exit 3
 python - $O <<'PY'
 import json, sys
 for k in ("new", "old"):
