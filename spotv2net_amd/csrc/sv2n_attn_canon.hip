@@ -365,7 +365,7 @@ __host__ __device__ inline int canon_bwd_tail_floats(int HS) {  // sDL .. sDec
   return HS * 32 * DS + 2 * HS * 32 + 32 + (32 * 31 / 2 + 1) / 2;
 }
 
-template <int ACT, bool CONCAT, bool KEEP>
+template <int ACT, bool CONCAT, bool KEEP, int DEPTH>
 __global__ __launch_bounds__(THREADS) void k_bwd(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ xs,
     int ldx, const float* __restrict__ psave, const uint8_t* __restrict__ keep, float keep_scale,
@@ -408,28 +408,52 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   const int nch = (C + 31) >> 5;
   const int cwb = (C + nch - 1) / nch;  // balanced chunk width (<= 32)
   const int grp = wave / WPH, sub = wave - grp * WPH;
+  // chunk ch of the wave's head: columns [c0, c0 + cw).  When the dy / y rows
+  // are 64-B aligned (OC % 16 == 0: C2's 400) the chunk edges sit on their
+  // 64-B segments — the first chunk ends at the head's first segment edge past
+  // 16 columns, then 32 columns each — so no segment is fetched by two chunks
+  // (balanced 25-column chunks re-fetched every edge segment: PMC reads 1.9x
+  // the algorithmic bytes).  Otherwise, or if that takes an extra chunk,
+  // balanced widths.
+  const int hoff = CONCAT ? (h0 + grp) * C : 0;
+  const int al = (16 - (hoff & 15)) & 15;
+  const int f1 = al == 0 ? 32 : al + 16;
+  const bool seg = (OC & 15) == 0 && (C > f1 ? 1 + (C - f1 + 31) / 32 : 1) == nch;
+  auto chunk_range = [&](int ch, int& c0, int& cw) {
+    if (seg) {
+      c0 = ch == 0 ? 0 : f1 + 32 * (ch - 1);
+      cw = min(ch == 0 ? f1 : 32, C - c0);
+    } else {
+      c0 = cwb * ch;
+      cw = min(cwb, C - c0);
+    }
+  };
   const int nhw = grp < nhs ? 1 : 0;                            // heads of this wave (HS <= NG)
   const int ncw = sub < nch ? (nch - sub + WPH - 1) / WPH : 0;  // chunks per head
   const int nseq = nhw * ncw;                                  // (head, chunk) steps
 
   // chunk step q: rows 2m + half, column l32 of the chunk (dword loads, the
-  // row stride in the scalar offset)
-  float rx_[16], rdy_[16], ry_[16], ru_[16];
-  auto load_chunk = [&](int q) {
+  // row stride in the scalar offset).  DEPTH register sets: chunk q lives in
+  // set q % DEPTH, so DEPTH chunks are in flight (C2: two, at 2 waves/SIMD).
+  float rx_[DEPTH][16], rdy_[DEPTH][16], ry_[DEPTH][16], ru_[DEPTH][16];
+  auto load_chunk = [&](int q, auto set_tag) __attribute__((always_inline)) {
+    constexpr int b = decltype(set_tag)::value;
     const int ch = sub + WPH * q, h = h0 + grp;  // the wave's one head
-    const int c = cwb * ch + l32;
-    const bool cv = l32 < cwb && c < C;
+    int c0, cw;
+    chunk_range(ch, c0, cw);
+    const int c = c0 + l32;
+    const bool cv = l32 < cw;
     const int xo = cv ? (half * ldx + h * C + c) * 4 : OOB;
     const int zo = cv ? (half * OC + (CONCAT ? h * C : 0) + c) * 4 : OOB;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
-      rx_[m] = bld_s(rx, xo, 2 * m * ldx * 4);
-      rdy_[m] = bld_s(rdy, zo, 2 * m * OC * 4);
-      ry_[m] = bld_s(ryy, zo, 2 * m * OC * 4);
+      rx_[b][m] = bld_s(rx, xo, 2 * m * ldx * 4);
+      rdy_[b][m] = bld_s(rdy, zo, 2 * m * OC * 4);
+      ry_[b][m] = bld_s(ryy, zo, 2 * m * OC * 4);
     }
     if (post) {
 #pragma unroll
-      for (int m = 0; m < 16; ++m) ru_[m] = bld_s(ru, zo, 2 * m * OC * 4);
+      for (int m = 0; m < 16; ++m) ru_[b][m] = bld_s(ru, zo, 2 * m * OC * 4);
     }
   };
   // saved probabilities / keep bytes of head h at lane i's output rows
@@ -449,7 +473,9 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 
   if (nseq > 0) {
     load_p(h0 + grp);
-    load_chunk(0);
+    load_chunk(0, std::integral_constant<int, 0>{});
+    if constexpr (DEPTH > 1)
+      if (nseq > 1) load_chunk(1, std::integral_constant<int, DEPTH - 1>{});
   }
   // sources of target row l32 (block layouts: the row mask; else all n)
   const uint32_t allm = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
@@ -502,9 +528,11 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 
   if (nhw > 0) {  // wave-uniform
     const int hl = grp, h = h0 + hl;
-    for (int chi = 0; chi < ncw; ++chi) {
+    auto chunk_step = [&](int chi, auto set_tag) __attribute__((always_inline)) {
+      constexpr int b = decltype(set_tag)::value;
       const int q = chi, ch = sub + WPH * chi;
-      const int c0 = cwb * ch, cw = min(cwb, C - c0);
+      int c0, cw;
+      chunk_range(ch, c0, cw);
       if (chi == 0) {
         // P_d of head h -> sP rows (each lane: its 16 positions of row i).
         // With WPH > 1 every wave of the group writes the same values: each
@@ -527,13 +555,14 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int row = 2 * m + half;
-        sX[row * CS + l32] = rx_[m];
-        const float d = post ? (ru_[m] >= post_p ? rdy_[m] * post_scale : 0.f) : rdy_[m];
-        sZ[row * CS + l32] = act_bwd<ACT>(d, ry_[m]);
+        sX[row * CS + l32] = rx_[b][m];
+        const float d =
+            post ? (ru_[b][m] >= post_p ? rdy_[b][m] * post_scale : 0.f) : rdy_[b][m];
+        sZ[row * CS + l32] = act_bwd<ACT>(d, ry_[b][m]);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes, in order
       SV2N_STAMP(3 + 2 * min(q, 3), SV2N_T());
-      if (q + 1 < nseq) load_chunk(q + 1);
+      if (q + DEPTH < nseq) load_chunk(q + DEPTH, set_tag);  // refill this set
       // bias partials: column sums of dz (concat: this head's columns; mean: once)
       if (CONCAT || h == 0) {
         float sb = 0.f;
@@ -573,6 +602,11 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
         for (int r = 0; r < 16; ++r)
           bst_s(rdx, voff, ((r & 3) + 8 * (r >> 2)) * ldx * 4, CONCAT ? D[r] : D[r] * invH);
       }
+    };
+    for (int chi = 0; chi < ncw; chi += DEPTH) {
+      chunk_step(chi, std::integral_constant<int, 0>{});
+      if constexpr (DEPTH > 1)
+        if (chi + 1 < ncw) chunk_step(chi + 1, std::integral_constant<int, DEPTH - 1>{});
     }
   }
   __syncthreads();  // every wave is done with the chunk areas (reused below)
@@ -690,6 +724,7 @@ extern "C" int sv2n_diag_stamps(unsigned long long* out, int64_t count) {
 // (every split recomputes the softmax), backward by heads and, inside a
 // split, a head's chunks over WPH waves.
 constexpr int64_t CANON_FILL = 512;
+constexpr unsigned CANON_CUS = 256;  // MI355X compute units
 
 static int canon_fwd_splits(int64_t B, int H, int C, bool concat) {
   const int ntc = (C + 31) >> 5, items = concat ? H * ntc : ntc;
@@ -733,13 +768,23 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
                              int ae_edge_order, float* dbias, int n, int H, int C, float slope) {
   const CanonBwdPlan pl = canon_bwd_plan(B, H, C);
   const size_t lds = attn_canon_bwd_lds(pl.HS);
-  if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)canon::k_bwd<ACT, CONCAT, KEEP>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL((canon::k_bwd<ACT, CONCAT, KEEP>), dim3(canon_grid(B, pl.S)),
-                     dim3(canon::THREADS), lds, st, dy, y, xs, ldx, psave, keep, keep_scale, post_u,
-                     post_p, post_u ? (float)(1.0 / (1.0 - (double)post_p)) : 1.f, rowmask, dxs,
-                     dae, ae_edge_order, dbias, n, H, C, slope, pl.S, pl.HS, pl.WPH, B);
+  const unsigned grid = canon_grid(B, pl.S);
+  // two chunks in flight per wave when every workgroup is resident at 2 waves
+  // per SIMD (the deeper register sets cost the third workgroup per CU)
+  auto launch = [&](auto kern) {
+    if (lds > 65536)
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(canon::THREADS), lds, st, dy, y, xs, ldx, psave,
+                       keep, keep_scale, post_u, post_p,
+                       post_u ? (float)(1.0 / (1.0 - (double)post_p)) : 1.f, rowmask, dxs, dae,
+                       ae_edge_order, dbias, n, H, C, slope, pl.S, pl.HS, pl.WPH, B);
+  };
+  const int nch = (C + 31) >> 5;
+  if (grid <= 2 * CANON_CUS && nch > 1)
+    launch(canon::k_bwd<ACT, CONCAT, KEEP, 2>);
+  else
+    launch(canon::k_bwd<ACT, CONCAT, KEEP, 1>);
 }
 
 void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, const float* xs,
