@@ -71,7 +71,8 @@ def remove_self_loops(edge_index: Tensor, edge_attr: Optional[Tensor]):
 
 def add_self_loops(edge_index: Tensor, edge_attr: Optional[Tensor], fill_value: str,
                    num_nodes: int):
-    loop_index = torch.arange(num_nodes, dtype=torch.long).unsqueeze(0).repeat(2, 1)
+    loop_index = torch.arange(num_nodes, dtype=torch.long,
+                              device=edge_index.device).unsqueeze(0).repeat(2, 1)
     if edge_attr is not None:
         assert fill_value == "mean"
         loop_attr = scatter_mean(edge_attr, edge_index[1], num_nodes)

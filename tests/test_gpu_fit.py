@@ -26,10 +26,16 @@ def _seed(epoch, k):
     torch.cuda.manual_seed(1000 * epoch + k)
 
 
-def _oracle_curve(ds_cpu, init_state, epochs, dev):
+def _oracle_curve(ds_cpu, init_state, epochs, dev, BS=BS, on=None):
+    """The oracle's curve; ``on``: the device its (unchanged) PyTorch ops run
+    on — the CPU by default, the GPU for the full-size C3 run (minutes of
+    unfolded lin_edge GEMMs on the host otherwise; f32 matmuls are exact f32
+    on gfx950, which has no reduced-precision f32 MFMA)."""
     from oracle.pyg_gatconv import OracleGATModel
+    on = on or torch.device("cpu")
     ref = OracleGATModel(30 * S, 3 * S, 6, 1, [500], dropout=P_DROP, concat_heads=True)
     ref.load_state_dict(init_state)
+    ref = ref.to(on)
     opt = torch.optim.Adam(ref.parameters(), lr=LR)
     gen = torch.Generator().manual_seed(7)
     n = len(ds_cpu)
@@ -41,9 +47,9 @@ def _oracle_curve(ds_cpu, init_state, epochs, dev):
         tot, nb = 0.0, 0
         for k in range(0, n_train, BS):
             idx = perm[k:k + BS]
-            b = ds_cpu.batch(idx)
+            b = ds_cpu.batch(idx).to(on)
             _seed(e, nb)
-            keep = (torch.rand(idx.numel() * 30, 500, device=dev) >= P_DROP).float().cpu()
+            keep = (torch.rand(idx.numel() * 30, 500, device=dev) >= P_DROP).float().to(on)
             ref.post_keep = [keep]
             loss = torch.nn.functional.mse_loss(ref(b), b.y_x)
             opt.zero_grad()
@@ -55,7 +61,7 @@ def _oracle_curve(ds_cpu, init_state, epochs, dev):
         tt, nt = 0.0, 0
         with torch.no_grad():
             for k in range(n_train, n, BS):
-                b = ds_cpu.batch(torch.arange(k, min(n, k + BS)))
+                b = ds_cpu.batch(torch.arange(k, min(n, k + BS))).to(on)
                 tt += torch.nn.functional.mse_loss(ref(b), b.y_x).item()
                 nt += 1
         hist.append((tot / nb, tt / nt))
@@ -112,3 +118,55 @@ def test_fit_graph_replay_equals_eager(dev):
     for a, b in zip(*hs):
         assert abs(a["train_loss"] - b["train_loss"]) <= 1e-6 * abs(b["train_loss"])
         assert abs(a["test_loss"] - b["test_loss"]) <= 1e-6 * abs(b["test_loss"])
+
+
+# ---- C3 at its stated size: config/GNN_param.yaml:26-39 batch 128, 3 epochs;
+#      2,157 windows = what CovarianceLaggedDataset yields from 10,556 matrices
+#      after the [8357:] cut (utils/dataset.py:200, :288) ----
+BS_FULL, EPOCHS_FULL = 128, 3
+
+
+@pytest.fixture(scope="module")
+def curves_full(dev):
+    from spotv2net_amd import GATModel, WindowDataset
+    from spotv2net_amd.data import synthetic_series
+    from spotv2net_amd.train import fit
+    V, W = synthetic_series(10556, 30, seed=1234)
+    ds_cpu = WindowDataset(V, W, S, cut=8357)
+    ds_gpu = WindowDataset(V.to(dev), W.to(dev), S, cut=8357)
+    assert len(ds_cpu) == len(ds_gpu) == 2157
+    torch.manual_seed(5154)
+    m0 = GATModel(30 * S, 3 * S, 6, 1, [500], dropout=P_DROP, concat_heads=True)
+    init = {k: v.clone() for k, v in m0.state_dict().items()}
+    out = {"oracle": _oracle_curve(ds_cpu, init, EPOCHS_FULL, dev, BS=BS_FULL, on=dev)}
+    for prec in ("f32", "bf16"):
+        m = GATModel(30 * S, 3 * S, 6, 1, [500], dropout=P_DROP, concat_heads=True)
+        m.load_state_dict(init)
+        m = m.to(dev).set_precision(prec)
+        h = fit(m, ds_gpu, num_epochs=EPOCHS_FULL, batch_size=BS_FULL, lr=LR,
+                generator=torch.Generator().manual_seed(7), step_hook=_seed)
+        out[prec] = [(r["train_loss"], r["test_loss"]) for r in h]
+    return out
+
+
+def test_c3_full_size_fp32_curve_matches_oracle(curves_full):
+    """3e-3: 42 Adam steps here against 6 in the small run above.  The
+    per-step gradients agree to ~1e-6, but Adam's update m/sqrt(v) is close to
+    a sign for coordinates whose gradient is small against its history, so
+    summation-order differences turn into parameter differences of ~lr per
+    step on those coordinates and the curves drift apart slowly.  Measured
+    (MI355X): the oracle alone, rerun (its GPU index_add_ sums in atomic
+    order), moved its epoch-3 test loss by 1.2e-3 (1.03532 vs 1.03650); the
+    HIP path sat within 1.6e-4 / 5.3e-4 (train / test) of it in epoch 1 and
+    4.5e-4 / 1.7e-4 in epoch 3."""
+    print("C3 full-size curves (train, test) per epoch:", curves_full)
+    assert len(curves_full["f32"]) == EPOCHS_FULL
+    for (tr, te), (rtr, rte) in zip(curves_full["f32"], curves_full["oracle"]):
+        assert _rel(tr, rtr) < 3e-3, (tr, rtr)
+        assert _rel(te, rte) < 3e-3, (te, rte)
+
+
+def test_c3_full_size_bf16_curve_matches_oracle(curves_full):
+    for (tr, te), (rtr, rte) in zip(curves_full["bf16"], curves_full["oracle"]):
+        assert _rel(tr, rtr) < 3e-2, (tr, rtr)
+        assert _rel(te, rte) < 3e-2, (te, rte)
