@@ -135,11 +135,14 @@ def kernel_table(model, data, reps=50):
     dae0 = torch.empty_like(ae[0])
     dbp = torch.empty(B, conv0.out_dim, device=dev)
 
+    # as the step runs it: layer 1's dx GEMM stores dZ = relu'(y0)·dy0
+    # (sv2n_gemm_f32x3_relu), so layer 0's backward runs with act = identity
+    # and reads no y
     def attn_bwd():
         lib.sv2n_gat_attn_bwd(dy0.data_ptr(), y0.data_ptr(), xs0.data_ptr(), xs0.stride(0),
                               ps0.data_ptr(), None, 1.0, None, 0.0, None, dxs0.data_ptr(),
                               dae0.data_ptr(),
-                              1, dbp.data_ptr(), B, N_NODES, HEADS, conv0.out_channels, 1, 1, 0.2,
+                              1, dbp.data_ptr(), B, N_NODES, HEADS, conv0.out_channels, 1, 0, 0.2,
                               sh)
 
     ws_n = lib.sv2n_edge_logits_bwd_workspace(D, hp)
@@ -184,8 +187,10 @@ def kernel_table(model, data, reps=50):
                             None),
         "gat_attn_fwd_l0": (attn_fwd, "hbm", 2.0 * B * N_NODES * N_NODES * HEADS * conv0.out_channels,
                             4.0 * (xs0.numel() + ae[0].numel() + y0.numel() + ps0.numel()), None),
+        # dZ, xs and psave read; dxs, d ae and the bias partials written
         "gat_attn_bwd_l0": (attn_bwd, "hbm", 4.0 * B * N_NODES * N_NODES * HEADS * conv0.out_channels,
-                            4.0 * (2 * y0.numel() + 2 * xs0.numel() + 2 * ps0.numel() + ae[0].numel()),
+                            4.0 * (y0.numel() + 2 * xs0.numel() + ps0.numel() + ae[0].numel() +
+                                   dbp.numel()),
                             None),
     }
     res = {}

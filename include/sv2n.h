@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 9
+#define SV2N_ABI_VERSION 10
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -187,6 +187,16 @@ int sv2n_split3(const float* in, int64_t rows, int64_t K, int64_t ld, int transp
                 uint16_t* out, hipStream_t stream);
 int sv2n_gemm_f32x3(const float* A, int64_t lda, const uint16_t* Bp, float* C, int64_t ldc,
                     int64_t M, int64_t N, int64_t K, hipStream_t stream);
+/* The same product with the consumer's ReLU backward applied as it is stored
+ * (ABI 10): C = (Y > 0) ? A·Bᵀ : 0, Y [M][ldy] the activation the layer saved
+ * (act_bwd of ReLU, bit for bit).  The backward of a GAT stack writes the
+ * previous layer's dZ here instead of its dy (dy·relu'(y) of GATModel's
+ * act after every layer, utils/models.py:147), and that layer's
+ * sv2n_gat_attn_bwd then runs with act = identity and reads no y.
+ * K % 4 == 0 only (else SV2N_ERR_SHAPE; nothing is launched). */
+int sv2n_gemm_f32x3_relu(const float* A, int64_t lda, const uint16_t* Bp, float* C, int64_t ldc,
+                         int64_t M, int64_t N, int64_t K, const float* Y, int64_t ldy,
+                         hipStream_t stream);
 
 /* bf16 execution mode of the same projection (the reference run under
  * torch.autocast(dtype=bfloat16), BASELINE config C3): C = bf16(A)·bf16(B)ᵀ

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SV2N_LIB: an alternative build of the same library (diagnostic builds, e.g.
 # tools/stamps.py); default the in-tree one
 LIB_PATH = os.environ.get("SV2N_LIB") or os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p
@@ -75,6 +75,7 @@ _SIGNATURES = {
     "sv2n_split3_kpad": (_i64, [_i64]),
     "sv2n_split3": (_i32, [_p, _i64, _i64, _i64, _i32, _p, _p]),
     "sv2n_gemm_f32x3": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "sv2n_gemm_f32x3_relu": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "sv2n_gemm_bf16": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "sv2n_gemm_f32_workspace": (_i64, [_i64, _i64, _i64]),
     "sv2n_gemm_f32_slabs_count": (_i32, [_i64, _i64, _i64]),

@@ -399,7 +399,9 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   const rsrc_t ryy = make_rsrc(y + g * n * OC, (uint32_t)(n * OC) * 4u);
   const rsrc_t rps = make_rsrc(psave + g * H * 1024, (uint32_t)H * 4096u);
   const rsrc_t rdb = make_rsrc(dbias_part + g * OC, (uint32_t)OC * 4u);
-  const bool post = post_u != nullptr;  // dy is the gradient of the post-dropout output
+  // dy is the gradient of the post-dropout output (never with DEPTH 3: its
+  // register sets leave no room for the draws)
+  const bool post = DEPTH < 3 && post_u != nullptr;
   const rsrc_t ru =
       make_rsrc(post ? post_u + g * n * OC : nullptr, post ? (uint32_t)(n * OC) * 4u : 0u);
 
@@ -434,7 +436,10 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 
   // chunk step q: rows 2m + half, column l32 of the chunk (dword loads, the
   // row stride in the scalar offset).  DEPTH register sets: chunk q lives in
-  // set q % DEPTH, so DEPTH chunks are in flight (C2: two, at 2 waves/SIMD).
+  // set q % DEPTH, so DEPTH chunks are in flight (C2: two, at 2 waves/SIMD;
+  // three when ACT is the identity — dy arrives as dZ from the producer's
+  // ReLU-masked store (sv2n_gemm_f32x3_relu) and no y is read; four sets
+  // spill at the 256-register budget of 2 waves/SIMD).
   float rx_[DEPTH][16], rdy_[DEPTH][16], ry_[DEPTH][16], ru_[DEPTH][16];
   auto load_chunk = [&](int q, auto set_tag) __attribute__((always_inline)) {
     constexpr int b = decltype(set_tag)::value;
@@ -449,7 +454,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     for (int m = 0; m < 16; ++m) {
       rx_[b][m] = bld_s(rx, xo, 2 * m * ldx * 4);
       rdy_[b][m] = bld_s(rdy, zo, 2 * m * OC * 4);
-      ry_[b][m] = bld_s(ryy, zo, 2 * m * OC * 4);
+      if constexpr (ACT != ACT_ID) ry_[b][m] = bld_s(ryy, zo, 2 * m * OC * 4);
     }
     if (post) {
 #pragma unroll
@@ -475,7 +480,9 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     load_p(h0 + grp);
     load_chunk(0, std::integral_constant<int, 0>{});
     if constexpr (DEPTH > 1)
-      if (nseq > 1) load_chunk(1, std::integral_constant<int, DEPTH - 1>{});
+      if (nseq > 1) load_chunk(1, std::integral_constant<int, 1>{});
+    if constexpr (DEPTH > 2)
+      if (nseq > 2) load_chunk(2, std::integral_constant<int, 2>{});
   }
   // sources of target row l32 (block layouts: the row mask; else all n)
   const uint32_t allm = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
@@ -558,7 +565,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
         sX[row * CS + l32] = rx_[b][m];
         const float d =
             post ? (ru_[b][m] >= post_p ? rdy_[b][m] * post_scale : 0.f) : rdy_[b][m];
-        sZ[row * CS + l32] = act_bwd<ACT>(d, ry_[b][m]);
+        sZ[row * CS + l32] = ACT == ACT_ID ? d : act_bwd<ACT>(d, ry_[b][m]);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes, in order
       SV2N_STAMP(3 + 2 * min(q, 3), SV2N_T());
@@ -606,7 +613,9 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     for (int chi = 0; chi < ncw; chi += DEPTH) {
       chunk_step(chi, std::integral_constant<int, 0>{});
       if constexpr (DEPTH > 1)
-        if (chi + 1 < ncw) chunk_step(chi + 1, std::integral_constant<int, DEPTH - 1>{});
+        if (chi + 1 < ncw) chunk_step(chi + 1, std::integral_constant<int, 1>{});
+      if constexpr (DEPTH > 2)
+        if (chi + 2 < ncw) chunk_step(chi + 2, std::integral_constant<int, 2>{});
     }
   }
   __syncthreads();  // every wave is done with the chunk areas (reused below)
@@ -781,7 +790,14 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
                        ae_edge_order, dbias, n, H, C, slope, pl.S, pl.HS, pl.WPH, B);
   };
   const int nch = (C + 31) >> 5;
-  if (grid <= 2 * CANON_CUS && nch > 1)
+  const bool resident = grid <= 2 * CANON_CUS;
+  if constexpr (ACT == ACT_ID) {
+    if (resident && nch > 2 && !post_u) {
+      launch(canon::k_bwd<ACT, CONCAT, KEEP, 3>);
+      return;
+    }
+  }
+  if (resident && nch > 1)
     launch(canon::k_bwd<ACT, CONCAT, KEEP, 2>);
   else
     launch(canon::k_bwd<ACT, CONCAT, KEEP, 1>);

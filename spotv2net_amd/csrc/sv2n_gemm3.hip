@@ -68,22 +68,23 @@ static int launch_gemm3(hipStream_t st, const float* A, int64_t lda, const unsig
 // -> k_gemm3d: C2 L0 fwd 15360 x 408 x 1260 104.3 -> 89.8 us, L1 fwd x 208 x
 // 400 25.9 -> 22.1, L1 dX x 400 x 208 27.0 -> 22.6, C5 L0 fwd 262144 x 144 x
 // 1024 596 -> 567).  Needs K % 4 == 0 (whole 16-B A chunks per row).
-template <int NW, int MT, int NT, int AP>
+template <int NW, int MT, int NT, int AP, bool MASK = false>
 static int launch_gemm3d(hipStream_t st, const float* A, int64_t lda, const unsigned short* Bp,
-                         int64_t Kp, int64_t N, float* C, int64_t ldc, int64_t M, int64_t K) {
+                         int64_t Kp, int64_t N, float* C, int64_t ldc, int64_t M, int64_t K,
+                         const float* Y = nullptr, int64_t ldy = 0) {
   using Cfg = Gemm3bCfg<NW, MT, NT, 32>;
   constexpr size_t lds = Cfg::LDS;
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)k_gemm3d<NW, MT, NT, AP>,
+    (void)hipFuncSetAttribute((const void*)k_gemm3d<NW, MT, NT, AP, MASK>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     return true;
   }();
   (void)attr;
   const int nm = (int)((M + Cfg::BM - 1) / Cfg::BM), nn = (int)((N + Cfg::BN - 1) / Cfg::BN);
   const unsigned grid = (unsigned)(((nm + 7) / 8) * 8 * nn);
-  hipLaunchKernelGGL((k_gemm3d<NW, MT, NT, AP>), dim3(grid), dim3(Cfg::THREADS), lds, st, A, lda,
-                     Bp, Kp, N * Kp, C, ldc, M, N, K, nm, nn);
+  hipLaunchKernelGGL((k_gemm3d<NW, MT, NT, AP, MASK>), dim3(grid), dim3(Cfg::THREADS), lds, st, A, lda,
+                     Bp, Kp, N * Kp, C, ldc, M, N, K, nm, nn, Y, ldy);
   return (int)hipGetLastError();
 }
 
@@ -177,4 +178,26 @@ extern "C" int sv2n_gemm_f32x3(const float* A, int64_t lda, const uint16_t* Bp, 
                  : launch_gemm3<8, 1, 13, 32>(stream, A, lda, B, Kp, N, C, ldc, M, K);
   return longk ? launch_gemm3<8, 1, 7, 64>(stream, A, lda, B, Kp, N, C, ldc, M, K)
                : launch_gemm3<8, 1, 7, 32>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+}
+
+// sv2n_gemm_f32x3 with the consumer's ReLU backward in the store: C = (Y > 0)
+// ? A·Bᵀ : 0 (Y [M][ldy], the layer's saved activation).  k_gemm3d only (K %
+// 4 == 0, else SV2N_ERR_SHAPE: the caller then masks in the attention kernel).
+extern "C" int sv2n_gemm_f32x3_relu(const float* A, int64_t lda, const uint16_t* Bp, float* C,
+                                    int64_t ldc, int64_t M, int64_t N, int64_t K, const float* Y,
+                                    int64_t ldy, hipStream_t stream) {
+  if (!A || !Bp || !C || !Y || M <= 0 || N <= 0 || K <= 0 || lda < K || ldc < N || ldy < N)
+    return SV2N_ERR_ARG;
+  if (((uintptr_t)A & 15) || (lda & 3) || ((uintptr_t)Bp & 15)) return SV2N_ERR_ALIGN;
+  if (K % 4 != 0) return SV2N_ERR_SHAPE;
+  const int64_t Kp = sv2n_split3_kpad(K);
+  const unsigned short* B = reinterpret_cast<const unsigned short*>(Bp);
+  const int64_t mb = (M + 127) / 128;
+  const bool wide = mb * ((N + 207) / 208) >= 240;
+  const bool t144 = (N + 143) / 144 * 144 < (N + 207) / 208 * 208 && mb * ((N + 143) / 144) >= 240;
+  if (t144)
+    return launch_gemm3d<8, 1, 9, 2, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
+  if (wide)
+    return launch_gemm3d<8, 1, 13, 2, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
+  return launch_gemm3d<8, 1, 7, 2, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
 }

@@ -800,12 +800,13 @@ __device__ __forceinline__ void static_for(F&& f) {
 // so after the barrier a wave only waits for its first B fragments.
 // Scheduling-group barriers hold the compiler to that interleave.
 // ---------------------------------------------------------------------------
-template <int NW, int MT, int NT, int AP>
+template <int NW, int MT, int NT, int AP, bool MASK = false>
 __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A, int64_t lda,
                                                     const unsigned short* __restrict__ Bp,
                                                     int64_t ldb, int64_t bplane,
                                                     float* __restrict__ C, int64_t ldc, int64_t M,
-                                                    int64_t N, int64_t K, int nm, int nn) {
+                                                    int64_t N, int64_t K, int nm, int nn,
+                                                    const float* __restrict__ Y, int64_t ldy) {
   constexpr int BK = 32;
   using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
   constexpr int TH = Cfg::THREADS, BN = Cfg::BN, ROW = Cfg::ROW, BV = Cfg::BV;
@@ -881,6 +882,25 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
     dst[a][2][qd] = w2;
   };
 
+  // MASK: the ReLU backward of the consumer fused into the store, C = (Y > 0)
+  // ? A·Bᵀ : 0 (act_bwd<ACT_RELU> exactly; the n <= 32 attention backward then
+  // reads dZ instead of dy and y).  Y is loaded before the main loop so its
+  // latency hides under the MFMAs (loaded after it, the epilogue waited on
+  // it: C2 L1 dX 24 -> 37 us).
+  float yv[MASK ? MT : 1][MASK ? NT : 1][4];
+  if constexpr (MASK) {
+    const rsrc_t ry = make_rsrc(Y + (arow0 > M ? 0 : arow0 * ldy),
+                                arows > 0 ? (uint32_t)(min(arows, (int64_t)16 * MT) * ldy * 4) : 0u);
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        const int gn = (int)n0 + 16 * b + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          yv[a][b][r] = bld(ry, gn < N ? (int)(((16 * a + 4 * lg + r) * ldy + gn) * 4) : OOB);
+      }
+  }
   const int nk = (int)((K + BK - 1) / BK);
 #pragma unroll
   for (int s = 0; s < AP; ++s)
@@ -895,6 +915,14 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
 #pragma unroll
   for (int pr = 0; pr < NPAIR; ++pr) split_pair(afc, ra[0], pr);
   __syncthreads();
+  if constexpr (MASK) {  // the mask lives in registers from here (no sinking into the epilogue)
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(yv[a][b][r]));
+  }
 
   auto step = [&](int s, auto set_c) __attribute__((always_inline)) {
     constexpr int set = decltype(set_c)::value, nset = (set + 1) % AP;
@@ -963,7 +991,9 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t gm = arow0 + 16 * a + 4 * lg + r;
-          if (gm < M) C[gm * ldc + gn] = acc[a][b][r];
+          float v = acc[a][b][r];
+          if constexpr (MASK) v = yv[a][b][r] > 0.f ? v : 0.f;
+          if (gm < M) C[gm * ldc + gn] = v;
         }
       }
     }

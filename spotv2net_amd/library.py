@@ -35,7 +35,8 @@ _SCHEMAS = {
                 "bool use_edge, bool bf16=False) -> (Tensor[], Tensor[], Tensor[], Tensor)",
     "edge_logits": "(Tensor edge_attr, Tensor wfold, Tensor? edge_index, Tensor canon, "
                    "int num_layers, int heads, int num_graphs, int n, bool planes) -> Tensor[]",
-    "project": "(Tensor a, Tensor? planes, Tensor w, bool transpose_w, bool bf16) -> Tensor",
+    "project": "(Tensor a, Tensor? planes, Tensor w, bool transpose_w, bool bf16, "
+               "Tensor? relu_y=None) -> Tensor",
     "gat_attn_fwd": "(Tensor xs, Tensor? ae, Tensor? rowmask, Tensor? bias, Tensor? keep, "
                     "float keep_scale, int num_graphs, int n, int heads, int channels, "
                     "bool concat, int act, float slope, bool edge_order=False) -> (Tensor, Tensor)",
@@ -325,14 +326,16 @@ def _prep_bwd_edge_all_fake(dwfold, col0, W_edge, att_edge, heads, channels, gW_
 # projection GEMMs (sv2n_gemm_f32x3 / sv2n_gemm_bf16 / sv2n_gemm_f32)
 # --------------------------------------------------------------------------
 @_impl("project")
-def _project(a, planes, w, transpose_w, bf16):
+def _project(a, planes, w, transpose_w, bf16, relu_y=None):
+    """relu_y: the consumer's ReLU backward fused into the store, out = (relu_y
+    > 0) ? a·w : 0 (sv2n_gemm_f32x3_relu; f32 planes path only)."""
     from .ops import project_planes
-    _f32(a, w)
-    return project_planes(a, planes, w, transpose_w, bf16)
+    _f32(a, w, relu_y)
+    return project_planes(a, planes, w, transpose_w, bf16, relu_y)
 
 
 @_fake("project")
-def _project_fake(a, planes, w, transpose_w, bf16):
+def _project_fake(a, planes, w, transpose_w, bf16, relu_y=None):
     N = w.shape[1] if transpose_w else w.shape[0]
     return a.new_empty((a.shape[0], N))
 

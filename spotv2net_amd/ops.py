@@ -108,15 +108,36 @@ def project(a: torch.Tensor, w: torch.Tensor, transpose_w: bool) -> torch.Tensor
     return gemm_f32(a, True, w, not transpose_w, M, N, K)
 
 
+def relu_mask_fusable(a: torch.Tensor, planes: Optional[torch.Tensor], bf16: bool) -> bool:
+    """Whether project_planes(..., relu_y) runs the masked f32 GEMM
+    (sv2n_gemm_f32x3_relu: the split planes exist, A is 16-B rows, K % 4 == 0)."""
+    return not bf16 and planes is not None and _split_ok(a) and a.shape[1] % 4 == 0
+
+
 def project_planes(a: torch.Tensor, planes: Optional[torch.Tensor], w: torch.Tensor,
-                   transpose_w: bool, bf16: bool = False) -> torch.Tensor:
+                   transpose_w: bool, bf16: bool = False,
+                   relu_y: Optional[torch.Tensor] = None) -> torch.Tensor:
     """project(a, w, transpose_w) with w's bf16 split planes already made
     (sv2n_gat_prep_fwd_all); exact-f32 fallback on w as in project().
     ``bf16``: the bf16 execution mode (sv2n_gemm_bf16: bf16 operands, fp32
-    accumulation, on plane 0 = bf16_rn(w))."""
+    accumulation, on plane 0 = bf16_rn(w)).  ``relu_y`` [M][N]: the result
+    is masked by relu_y > 0 (ReLU's backward, in the GEMM's store when
+    relu_mask_fusable, else as a separate elementwise step)."""
     lib = _lib.load()
     M, K = a.shape
     N = w.shape[1] if transpose_w else w.shape[0]
+    if relu_y is not None:
+        if relu_y.shape != (M, N) or relu_y.stride(1) != 1:
+            raise ValueError(f"relu_y: expected [{M}, {N}] rows, got {tuple(relu_y.shape)}")
+        if relu_mask_fusable(a, planes, bf16):
+            out = torch.empty(M, N, device=a.device, dtype=torch.float32)
+            _lib.check(lib.sv2n_gemm_f32x3_relu(a.data_ptr(), a.stride(0), planes.data_ptr(),
+                                                out.data_ptr(), out.stride(0), M, N, K,
+                                                relu_y.data_ptr(), relu_y.stride(0),
+                                                _stream(a.device)), "sv2n_gemm_f32x3_relu")
+            return out
+        out = project_planes(a, planes, w, transpose_w, bf16)
+        return torch.where(relu_y > 0, out, torch.zeros_like(out))
     if bf16:
         if planes is None:
             planes = weight_planes(w, transpose_w)

@@ -39,7 +39,9 @@ import torch
 from . import _lib, library  # noqa: F401  (library registers torch.ops.sv2n)
 from .layout import GraphLayout
 from .library import edge_order, fused_supported
-from .ops import _aligned, _require_device, resolve_precision
+from .ops import ACT_CODES, _aligned, _require_device, relu_mask_fusable, resolve_precision
+
+ACT_RELU = ACT_CODES["relu"]
 
 
 def _grad_buf(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -367,6 +369,7 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
     dy = dout.contiguous()
     daes = [None] * L
     dwf = torch.zeros_like(wf) if fused else None  # every layer writes its own columns
+    act_l = act  # the activation backward left to layer l's attention backward
     for l in range(L - 1, -1, -1):
         c = convs[l]
         Hc, C = c.heads, c.out_channels
@@ -387,7 +390,7 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
         else:
             dxs, dae, dbp = ops.gat_attn_bwd(
                 dy, ys[l], xs, pss[l], keeps[l], meta.kscales[l], layout.rowmask, use_edge,
-                B, n, Hc, C, c.concat, act, float(c.negative_slope), eo, post_u,
+                B, n, Hc, C, c.concat, act_l, float(c.negative_slope), eo, post_u,
                 meta.post_p[l] or 0.0)
         daes[l] = _opt(dae)
         gW = grad_of(c.lin_src.weight)
@@ -399,8 +402,16 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
             # att and bias grads), accumulated into the gradient buffers
             ops.gat_wgrad(xs_in[l], dxs, c.lin_src.weight, c.att_src, c.att_dst, dbp, Hc, C,
                           meta.bf16, gW, gas, gad, gb)
+        act_l = act
         if l > 0 or need_x0:
-            dy = ops.project(dxs, _opt(planes_t[l]), waugs[l], True, meta.bf16)  # dxs · Waug
+            # dxs · Waug; ahead of a ReLU layer on the n <= 32 path the GEMM
+            # stores dZ = relu'(y)·dy itself (sv2n_gemm_f32x3_relu) and that
+            # layer's attention backward runs with the identity (reads no y)
+            relu_y = None
+            if l > 0 and act == ACT_RELU and not fused and not layout.tiled and \
+                    relu_mask_fusable(dxs, _opt(planes_t[l]), meta.bf16):
+                relu_y, act_l = ys[l - 1], 0
+            dy = ops.project(dxs, _opt(planes_t[l]), waugs[l], True, meta.bf16, relu_y)
 
     if use_edge and ea is not None:
         # grads exist (zeros) even without edges, as in PyG

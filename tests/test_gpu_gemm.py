@@ -66,6 +66,34 @@ def test_split3_gemm_matches_f32_accuracy(dev, M, N, K, transpose):
     assert e3 < 1e-6 and e3 <= 2 * e32 + 1e-9, (e3, e32)
 
 
+@pytest.mark.parametrize("M,N,K", [(15360, 400, 208), (15360, 208, 400), (300, 144, 1024),
+                                   (129, 50, 36)])
+def test_split3_gemm_relu_mask_is_exact(dev, M, N, K):
+    """sv2n_gemm_f32x3_relu stores (y > 0) ? A·Bᵀ : 0: bit-identical to the
+    unmasked GEMM where y > 0, exact zeros elsewhere (ReLU's backward, as the
+    n <= 32 attention backward applies it: act_bwd<ACT_RELU>); y with exact
+    zeros, positives and negatives, and a row stride wider than N."""
+    from spotv2net_amd import _lib, ops
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(M + 7 * N + K)
+    a = torch.randn(M, K, generator=g).to(dev)
+    w = torch.randn(K, N, generator=g).to(dev)
+    planes = ops.weight_planes(w, True)
+    plain = ops.project_planes(a, planes, w, True)
+    yb = torch.randn(M, N + 8, generator=g)
+    yb[yb.abs() < 0.3] = 0.0
+    y = yb.to(dev)[:, :N]
+    got = ops.project_planes(a, planes, w, True, relu_y=y)
+    assert torch.equal(got, torch.where(y > 0, plain, torch.zeros_like(plain)))
+    out = torch.empty_like(plain)
+    st = _lib.stream_handle(dev)
+    # K % 4 != 0 is refused before any launch (the caller masks in the attention)
+    assert lib.sv2n_gemm_f32x3_relu(a.data_ptr(), K, planes.data_ptr(), out.data_ptr(), N, M, N,
+                                    K - 1, y.data_ptr(), y.stride(0), st) == -2
+    assert lib.sv2n_gemm_f32x3_relu(a.data_ptr(), K, planes.data_ptr(), out.data_ptr(), N, M, N,
+                                    K, None, 0, st) == -1
+
+
 def test_prep_fwd_all_matches_per_layer(dev):
     """sv2n_gat_prep_fwd_all (one launch, all layers) equals sv2n_gat_prep_fwd
     + sv2n_split3 (+ the transposed split) per layer, bit for bit."""

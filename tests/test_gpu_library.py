@@ -42,6 +42,10 @@ def test_opcheck_forward_ops(dev):
     pj = (d.x, planes[0], waugs[0], False, False)
     torch.library.opcheck(ops.project, pj, test_utils=UTILS)
     xs = ops.project(*pj)
+    # the ReLU-masked store (sv2n_gemm_f32x3_relu) behind the optional relu_y
+    ry = torch.randn(xs.shape, device=dev)
+    torch.library.opcheck(ops.project, pj + (ry,), test_utils=UTILS)
+    assert torch.equal(ops.project(*pj, ry), torch.where(ry > 0, xs, torch.zeros_like(xs)))
     assert aes[0].shape == (3 * 870, 2)  # canonical batch: edge-ordered logits
     att = (xs, aes[0], None, c0.bias, None, 1.0, 3, 30, 2, 8, True, 1, 0.2, True)
     torch.library.opcheck(ops.gat_attn_fwd, att, test_utils=UTILS)

@@ -28,7 +28,7 @@ KERNELS = {
     "edge_logits_fwd": "sv2n::k_edge_fwd<8, 8, false>",
     "edge_logits_bwd": "sv2n::k_edge_bwd<8, 8, false>",
     "gat_attn_fwd_l0": "sv2n::canon::k_fwd<1, true, false>",
-    "gat_attn_bwd_l0": "sv2n::canon::k_bwd<1, true, false, 2>",
+    "gat_attn_bwd_l0": "sv2n::canon::k_bwd<0, true, false, 3>",
 }
 
 
