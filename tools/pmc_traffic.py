@@ -23,7 +23,7 @@ from collections import defaultdict
 
 # bench.py kernel_table name -> rocprof kernel name prefix (the C2 instantiation)
 KERNELS = {
-    "gemm_l0_fwd": "sv2n::k_gemm3d<8, 1, 13, 2>",
+    "gemm_l0_fwd": "sv2n::k_gemm3d<8, 1, 13, 2, false>",
     "gemm_l0_dwT": "sv2n::k_gemm_tt3y<13, 2>",
     "edge_logits_fwd": "sv2n::k_edge_fwd<8, 8, false>",
     "edge_logits_bwd": "sv2n::k_edge_bwd<8, 8, false>",
@@ -35,8 +35,8 @@ KERNELS = {
 # C5 (tools/pmc_c5_traffic.sh): keys prefixed "c5:" in the same JSON
 KERNELS_C5 = {
     "gat_attn_fused_fwd_l0": "sv2n::fused::k_fattn_fwd<12, false, false>",
-    "gat_attn_fused_bwd_l0": "sv2n::fused::k_fattn_bwd<12, false, false>",
-    "gemm_l0_fwd": "sv2n::k_gemm3d<8, 1, 9, 2>",
+    "gat_attn_fused_bwd_l0": "sv2n::fused::k_fattn_bwd2<12, false, false>",
+    "gemm_l0_fwd": "sv2n::k_gemm3d<8, 1, 9, 2, false>",
 }
 
 
