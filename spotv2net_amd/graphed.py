@@ -179,8 +179,7 @@ class _Replay(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, entry: _Entry, layout: GraphLayout, *params):
-        entry.load_layout(layout)
-        entry.g_fwd.replay()
+        # the caller has already replayed entry.g_fwd (see forward below)
         entry.gen += 1
         entry.backwarded = False
         ctx.entry, ctx.gen = entry, entry.gen
@@ -286,4 +285,9 @@ def forward(model, data, x, edge_index, edge_attr, layout: GraphLayout) -> Optio
         return entry.out.clone()
     if entry.busy():
         return None
+    # replay first, then the autograd bookkeeping: Function.apply's argument
+    # processing is host time the GPU would otherwise wait through at the start
+    # of a synchronised step (the reference loop's loss.item() drains it)
+    entry.load_layout(layout)
+    entry.g_fwd.replay()
     return _Replay.apply(entry, layout, *ps)
