@@ -118,7 +118,9 @@ __global__ __launch_bounds__(256) void k_window_rows(
       dst[r] = tt * NP + v;
       a[r] = vol[base + (int64_t)u * n + v];
       w[r] = volvol[base + (int64_t)u * n + v];
-      d[r] = volvol[base + (int64_t)v * n + v];
+      // the diagonal is only read for the pairs (u, w > u): every diagonal
+      // element sits on its own 128-B line, so the rest are not fetched
+      d[r] = v > u ? volvol[base + (int64_t)v * n + v] : 0.f;
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r)
