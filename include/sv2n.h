@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 10
+#define SV2N_ABI_VERSION 11
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -500,6 +500,17 @@ int sv2n_window_gather(const float* vol, const float* volvol, int n, int64_t num
                        int64_t num_windows, int seq_length, int future_steps,
                        const uint16_t* canon, float* x, float* edge_attr, float* y,
                        hipStream_t stream);
+
+/* sv2n_window_gather with the series' diagonal given (ABI 11): diag [T][n],
+ * diag[t][v] = volvol[t][v][v] (contiguous fp32, built once per series), or
+ * NULL (read from volvol).  Same outputs bit for bit; the diagonal reads of
+ * the LDS row kernel become one 120-B run per matrix instead of one 128-B
+ * line per element. */
+int sv2n_window_gather_diag(const float* vol, const float* volvol, const float* diag, int n,
+                            int64_t num_matrices, const int64_t* starts, int64_t start_offset,
+                            int64_t num_windows, int seq_length, int future_steps,
+                            const uint16_t* canon, float* x, float* edge_attr, float* y,
+                            hipStream_t stream);
 
 #ifdef __cplusplus
 }

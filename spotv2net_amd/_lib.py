@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SV2N_LIB: an alternative build of the same library (diagnostic builds, e.g.
 # tools/stamps.py); default the in-tree one
 LIB_PATH = os.environ.get("SV2N_LIB") or os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p
@@ -108,6 +108,8 @@ _SIGNATURES = {
     "sv2n_head_fwd": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p]),
     "sv2n_window_gather": (_i32, [_p, _p, _i32, _i64, _p, _i64, _i64, _i32, _i32, _p, _p, _p, _p,
                                   _p]),
+    "sv2n_window_gather_diag": (_i32, [_p, _p, _p, _i32, _i64, _p, _i64, _i64, _i32, _i32, _p, _p,
+                                       _p, _p, _p]),
     "sv2n_head_bwd_workspace": (_i64, [_i64, _i32, _i32]),
     "sv2n_head_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _p, _p, _i64, _p]),
 }

@@ -78,11 +78,12 @@ __global__ __launch_bounds__(256) void k_window_gather(
 //   the edge rows of the upper pairs (u, w), w > u, and of their swapped
 //   copies (canonical order: both runs are contiguous, 3S floats per row)
 //   y[(b*n+u)*F .. +F)
-// 3 * S * (n+1) floats of LDS.
+// 3 * S * (n+1) floats of LDS.  diag (optional): diag[t][v] = volvol[t][v][v].
 __global__ __launch_bounds__(256) void k_window_rows(
     const float* __restrict__ vol, const float* __restrict__ volvol, int n, int64_t T,
-    const int64_t* __restrict__ starts, int64_t soff, int S, int F, float* __restrict__ x,
-    float* __restrict__ ea, float* __restrict__ y) {
+    const int64_t* __restrict__ starts, int64_t soff, int S, int F,
+    const float* __restrict__ diag, float* __restrict__ x, float* __restrict__ ea,
+    float* __restrict__ y) {
   extern __shared__ float lds[];
   const int NP = n + 1;
   float* sv = lds;             // [S][NP] vol[t][u][v]
@@ -118,9 +119,10 @@ __global__ __launch_bounds__(256) void k_window_rows(
       dst[r] = tt * NP + v;
       a[r] = vol[base + (int64_t)u * n + v];
       w[r] = volvol[base + (int64_t)u * n + v];
-      // the diagonal is only read for the pairs (u, w > u): every diagonal
-      // element sits on its own 128-B line, so the rest are not fetched
-      d[r] = v > u ? volvol[base + (int64_t)v * n + v] : 0.f;
+      // the diagonal is only read for the pairs (u, w > u); from the series'
+      // diagonal [T][n] when given (ABI 11: one line per matrix instead of
+      // one per element)
+      d[r] = v > u ? (diag ? diag[(st + tt) * n + v] : volvol[base + (int64_t)v * n + v]) : 0.f;
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r)
@@ -223,11 +225,12 @@ __global__ __launch_bounds__(256) void k_window_rows(
 
 using namespace sv2n;
 
-extern "C" int sv2n_window_gather(const float* vol, const float* volvol, int n,
-                                  int64_t num_matrices, const int64_t* starts,
-                                  int64_t start_offset, int64_t num_windows, int seq_length,
-                                  int future_steps, const uint16_t* canon, float* x,
-                                  float* edge_attr, float* y, hipStream_t stream) {
+extern "C" int sv2n_window_gather_diag(const float* vol, const float* volvol,
+                                       const float* diag, int n, int64_t num_matrices,
+                                       const int64_t* starts, int64_t start_offset,
+                                       int64_t num_windows, int seq_length, int future_steps,
+                                       const uint16_t* canon, float* x, float* edge_attr,
+                                       float* y, hipStream_t stream) {
   if (!vol || !volvol || !starts || !canon || !x || !edge_attr || !y) return SV2N_ERR_ARG;
   if (n < 2 || n > SV2N_MAX_N_TILED || num_windows < 1 || seq_length < 1 || future_steps < 1 ||
       num_matrices < 1)
@@ -239,7 +242,7 @@ extern "C" int sv2n_window_gather(const float* vol, const float* volvol, int n,
   if (lds <= 64 * 1024 && future_steps <= 256) {
     hipLaunchKernelGGL(k_window_rows, dim3((unsigned)(num_windows * n)), dim3(256), lds, stream,
                        vol, volvol, n, num_matrices, starts, start_offset, seq_length, future_steps,
-                       x, edge_attr, y);
+                       diag, x, edge_attr, y);
     return (int)hipGetLastError();
   }
   const int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);
@@ -247,4 +250,14 @@ extern "C" int sv2n_window_gather(const float* vol, const float* volvol, int n,
                      n, num_matrices, starts, start_offset, num_windows, seq_length, future_steps,
                      canon, x, edge_attr, y);
   return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_window_gather(const float* vol, const float* volvol, int n,
+                                  int64_t num_matrices, const int64_t* starts,
+                                  int64_t start_offset, int64_t num_windows, int seq_length,
+                                  int future_steps, const uint16_t* canon, float* x,
+                                  float* edge_attr, float* y, hipStream_t stream) {
+  return sv2n_window_gather_diag(vol, volvol, nullptr, n, num_matrices, starts, start_offset,
+                                 num_windows, seq_length, future_steps, canon, x, edge_attr, y,
+                                 stream);
 }

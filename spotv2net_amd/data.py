@@ -231,6 +231,10 @@ class WindowDataset:
         self._up_s, self._up_t = self._src[:P], self._tgt[:P]
         self._arS = torch.arange(seq_length, device=dev)
         self._arF = torch.arange(self.future_steps, device=dev)
+        # the series' diagonal volvol[t][v][v] as one [T][n] copy, built once:
+        # the device window kernel reads it in runs instead of a line per element
+        self.diag = torch.diagonal(volvol, dim1=1, dim2=2).contiguous() \
+            if volvol.dtype == torch.float32 else None
 
     def empty_batch(self, batch_size: int) -> Batch:
         """Static device buffers of one batch of ``batch_size`` windows (the
@@ -265,7 +269,7 @@ class WindowDataset:
             torch.ops.sv2n.window_gather(self.vol.contiguous(), self.volvol.contiguous(),
                                          idx if idx.dtype == torch.long else idx.long(), S, Fs,
                                          canonical_table(n, self.vol.device), out.x,
-                                         out.edge_attr, out.y_x, self.cut)
+                                         out.edge_attr, out.y_x, self.cut, self.diag)
             return
         st = self.starts.index_select(0, idx)
         tidx = st.view(B, 1) + self._arS.view(1, S)                               # [B, S]

@@ -87,7 +87,7 @@ _SCHEMAS = {
                  "float eps, float weight_decay) -> ()",
     "window_gather": "(Tensor vol, Tensor volvol, Tensor starts, int seq_length, "
                      "int future_steps, Tensor canon, Tensor(a!) x, Tensor(b!) edge_attr, "
-                     "Tensor(c!) y, int start_offset=0) -> ()",
+                     "Tensor(c!) y, int start_offset=0, Tensor? diag=None) -> ()",
 }
 for _name, _schema in _SCHEMAS.items():
     LIB.define(_name + _schema)
@@ -774,7 +774,7 @@ def _adam_step_fake(param, grad, exp_avg, exp_avg_sq, step, ticket, lr, beta1, b
 
 @_impl("window_gather")
 def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y,
-                   start_offset=0):
+                   start_offset=0, diag=None):
     lib = _lib.load()
     _f32(vol, volvol, x, edge_attr, y)
     _need(vol.is_contiguous() and volvol.is_contiguous(), "series must be contiguous")
@@ -787,16 +787,20 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
     _need(volvol.shape == vol.shape and vol.dim() == 3, "series shapes")
     # windows outside the series come back as NaN (checked in the kernel:
     # the starts live on the device, so no host round trip here)
-    _lib.check(lib.sv2n_window_gather(vol.data_ptr(), volvol.data_ptr(), vol.shape[1],
-                                      vol.shape[0], starts.data_ptr(), start_offset,
-                                      starts.numel(), seq_length, future_steps,
-                                      canon.data_ptr(), x.data_ptr(), edge_attr.data_ptr(),
-                                      y.data_ptr(), _st(vol)), "sv2n_window_gather")
+    if diag is not None:  # the series' diagonal, diag[t][v] = volvol[t][v][v]
+        _f32(diag)
+        _need(diag.is_contiguous() and diag.shape == vol.shape[:2], "diag must be [T][n]")
+    _lib.check(lib.sv2n_window_gather_diag(vol.data_ptr(), volvol.data_ptr(), _p(diag),
+                                           vol.shape[1], vol.shape[0], starts.data_ptr(),
+                                           start_offset, starts.numel(), seq_length,
+                                           future_steps, canon.data_ptr(), x.data_ptr(),
+                                           edge_attr.data_ptr(), y.data_ptr(), _st(vol)),
+               "sv2n_window_gather_diag")
 
 
 @_fake("window_gather")
 def _window_gather_fake(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y,
-                        start_offset=0):
+                        start_offset=0, diag=None):
     return None
 
 

@@ -214,3 +214,29 @@ def test_window_gather_out_of_range_windows_are_nan(dev, n, S, Fs):
     for b, j in k.items():
         assert torch.equal(x[b * n:(b + 1) * n], want.x[j * n:(j + 1) * n])
         assert torch.equal(ea[b * E0:(b + 1) * E0], want.edge_attr[j * E0:(j + 1) * E0])
+
+
+@pytest.mark.parametrize("n,S,Fs", [(30, 42, 1), (7, 3, 2)])
+def test_window_gather_diag_matches_volvol_path(dev, n, S, Fs):
+    """sv2n_window_gather_diag (ABI 11) with the series' diagonal given is bit-exact
+    with the kernel reading the diagonal from volvol, in-range and NaN windows alike."""
+    from spotv2net_amd import WindowDataset
+    from spotv2net_amd.data import synthetic_series
+    from spotv2net_amd.layout import canonical_table
+    T = S + Fs + 50
+    V, W = synthetic_series(T, n, seed=11)
+    ds = WindowDataset(V.to(dev), W.to(dev), S, cut=2, future_steps=Fs)
+    assert ds.diag is not None and ds.diag.shape == (T, n)
+    starts = torch.tensor([0, 5, -4, T, 17, T - S - Fs - 2], device=dev)
+    B, E0 = starts.numel(), n * (n - 1)
+    outs = []
+    for diag in (None, ds.diag):
+        x = torch.empty(B * n, n * S, device=dev)
+        ea = torch.empty(B * E0, 3 * S, device=dev)
+        y = torch.empty(B * n * Fs, device=dev)
+        torch.ops.sv2n.window_gather(ds.vol, ds.volvol, starts, S, Fs, canonical_table(n, dev),
+                                     x, ea, y, 2, diag)
+        outs.append((x, ea, y))
+    for a, b in zip(*outs):
+        assert torch.equal(a.isnan(), b.isnan())
+        assert torch.equal(a.nan_to_num(), b.nan_to_num())

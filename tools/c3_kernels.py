@@ -29,6 +29,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--no-diag", action="store_true",
+                    help="window gather reading the diagonal from volvol (no [T][n] copy)")
     args = ap.parse_args()
     from spotv2net_amd import GATModel, WindowDataset, ops
     from spotv2net_amd.data import synthetic_series
@@ -46,6 +48,8 @@ def main():
     out["prep_fwd_all"] = timeit(lambda: torch.ops.sv2n.gat_prep(*prep_args), args.reps, stream)
     V, W = synthetic_series(10556, 30, seed=1234, device=dev)
     ds = WindowDataset(V, W, 42, cut=8357)
+    if args.no_diag:
+        ds.diag = None
     b = ds.empty_batch(128)
     idx = torch.randperm(len(ds))[:128].to(dev)
     out["window_gather"] = timeit(lambda: ds.fill(b, idx), args.reps, stream)
