@@ -84,12 +84,31 @@ def time_replays(fn, k, sync_group=True):
     return time.perf_counter() - t0
 
 
+def _coll_device(dev):
+    """Where a collective's tensors live: the GPU under nccl (RCCL), the host
+    under gloo."""
+    return dev if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
 def max_over_ranks(x: float, dev) -> float:
     if not dist.is_initialized():
         return x
-    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    t = torch.tensor([x], device=_coll_device(dev), dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def replicas_identical(flat: torch.Tensor, dev) -> bool:
+    """Every rank's parameters bit for bit equal: the elementwise MAX and MIN
+    over ranks of the parameters' int32 bit patterns both equal this rank's."""
+    bits = flat.detach().view(torch.int32).to(_coll_device(dev))
+    hi, lo = bits.clone(), bits.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    ok = torch.tensor([int(torch.equal(hi, bits) and torch.equal(lo, bits))],
+                      device=_coll_device(dev), dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return bool(ok.item())
 
 
 # --------------------------------------------------------------------------
@@ -541,37 +560,64 @@ def step_roofline(cfg, train_gps: float, fwd_gps: float, dtype: str) -> dict:
             "fwd_frac": round(fwd_gps / fwd_bound, 4), "train_frac": round(train_gps / train_bound, 4)}
 
 
-def reference_loop_rate(dev, cfg, data, args, world, canonical: bool = True) -> float:
-    """5_train_SpotV2Net.py:142-160 as written, eager Python: a NEW batch object
-    with a new edge_index every step, model(data), nn.MSELoss, zero_grad,
-    backward, torch.optim.Adam(fused) step and the per-step loss.item() sync.
-    The batch carries what sv2n ``collate`` attaches to a batch of the
-    reference's graphs: ``nodes_per_graph`` and, ``canonical``, the verified
-    canonical edge order (False: the same batch without it, analysed on the
-    device every step, block-layout kernels).  GATModel replays its forward
-    and backward as hipGraphs from the second step on (graphed.py).  Inputs
-    stay device-resident (the DataLoader's CPU collation and H2D copy are not
-    on the GPU path)."""
-    from spotv2net_amd import Batch
+def _ref_model(dev, cfg, args, world):
+    """The model as the reference loop sees it: GATModel, wrapped in
+    DistributedDataParallel at N > 1 (its gradient all-reduce is what makes
+    the loop data-parallel; GATModel returns its gradients to autograd)."""
     model = build_model(dev, cfg).set_precision(args.precision)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    if world > 1:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        model = DDP(model, device_ids=[dev.index], broadcast_buffers=False)
+    return model
+
+
+def reference_loop_rate(dev, cfg, batches, args, world, canonical: bool = True,
+                        fused_adam: bool = False, steps=None) -> float:
+    """5_train_SpotV2Net.py:127, :142-160 as written, eager Python:
+    ``torch.optim.Adam(model.parameters(), lr)`` (``fused_adam``: the one-word
+    change ``fused=True``), per step a NEW batch object with a new edge_index,
+    ``data = data.to(device)``, ``model(data)``, ``nn.MSELoss``, ``zero_grad``,
+    ``backward``, ``step`` and the per-step ``loss.item()`` sync.
+
+    ``batches``: the loader's batches, cycled.  Device-resident batches make
+    ``.to(device)`` a no-op (the data already in HBM, as ``value`` assumes);
+    host batches make it the reference's H2D copy of every batch (pageable
+    memory, as its DataLoader yields without ``pin_memory``).  The batches
+    carry what sv2n ``collate`` attaches to a batch of the reference's graphs:
+    ``nodes_per_graph`` and, ``canonical``, the verified canonical edge order
+    (False: the same batches without it, analysed on the device every step,
+    block-layout kernels).  GATModel replays its forward and backward as
+    hipGraphs from the second call of a signature on (graphed.py).  At N > 1
+    the model is wrapped in DDP (one gradient all-reduce per step)."""
+    from spotv2net_amd import Batch
+    model = _ref_model(dev, cfg, args, world)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True) if fused_adam \
+        else torch.optim.Adam(model.parameters(), lr=1e-3)
     crit = torch.nn.MSELoss()
     extra = {"canonical_edges": True} if canonical else {}
+    loader = [Batch(x=b.x, edge_index=b.edge_index, edge_attr=b.edge_attr, y_x=b.y_x,
+                    batch=b.batch, ptr=b.ptr, nodes_per_graph=cfg["n"], **extra)
+              for b in batches]
+    it = [0]
 
     def step():
-        b = Batch(x=data.x, edge_index=data.edge_index.clone(), edge_attr=data.edge_attr,
-                  y_x=data.y_x, batch=data.batch, ptr=data.ptr, nodes_per_graph=cfg["n"],
-                  **extra)
-        loss = crit(model(b), b.y_x)
+        src = loader[it[0] % len(loader)]
+        it[0] += 1
+        data = src.to(dev)
+        if data.edge_index is src.edge_index:   # device-resident: a DataLoader still
+            data.edge_index = src.edge_index.clone()   # yields a new edge_index tensor
+        y_x_hat = model(data)
+        loss = crit(y_x_hat, data.y_x)
         opt.zero_grad()
         loss.backward()
         opt.step()
         return loss.item()
 
+    steps = steps or args.steps
     for _ in range(max(3, args.warmup)):
         step()
-    el = max_over_ranks(time_replays(step, args.steps), dev)
-    return world * args.batch * args.steps / el
+    el = max_over_ranks(time_replays(step, steps), dev)
+    return world * args.batch * steps / el
 
 
 def run_c3_loop(args, dev, cfg) -> dict:
@@ -610,7 +656,7 @@ def run_c3_loop(args, dev, cfg) -> dict:
     return {"windows": len(ds), "n_train": f.n_train, "n_test": f.n_test, "runs": out}
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -630,17 +676,26 @@ def main():
     ap.add_argument("--warmup-epochs", type=int, default=1, help="c3: untimed epochs")
     ap.add_argument("--no-compare", action="store_true",
                     help="c3: skip the run in the other precision")
-    args = ap.parse_args()
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process group at N > 1: nccl (= RCCL over xGMI, one GPU per rank) "
+                         "or gloo (host-staged; e.g. several ranks sharing one GPU)")
+    args = ap.parse_args(argv)
     if args.precision is None:
         args.precision = "bf16" if args.config == "c3" else "f32"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":
+        # ranks may share a GPU (the -m gpu test runs two on the box's one card)
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from spotv2net_amd import synthetic_batch
     from spotv2net_amd.train import ForwardStep, TrainStep, broadcast_params_
@@ -663,10 +718,26 @@ def main():
     value = world * args.batch * args.steps / el
     loss = float(step.loss.item())
 
-    ref_loop = ref_loop_block = None
+    replicas_ok = replicas_identical(step.flat_params, dev) if world > 1 else None
+
+    ref = {}
     if not args.no_ref_loop:
-        ref_loop = reference_loop_rate(dev, cfg, data, args, world)
-        ref_loop_block = reference_loop_rate(dev, cfg, data, args, world, canonical=False)
+        # the loader's batches: two distinct device-resident ones, alternating
+        # (new contents every step at recycled addresses)
+        dev_batches = [data, synthetic_batch(args.batch, cfg["S"], n=cfg["n"],
+                                             seed=5678 + rank, device=dev)]
+        ref["ref_loop_graphs_per_s"] = reference_loop_rate(dev, cfg, dev_batches, args, world)
+        ref["ref_loop_fused_adam_graphs_per_s"] = reference_loop_rate(
+            dev, cfg, dev_batches, args, world, fused_adam=True)
+        ref["ref_loop_block_layout_graphs_per_s"] = reference_loop_rate(
+            dev, cfg, dev_batches, args, world, canonical=False)
+        del dev_batches
+        # literal: host batches, the H2D copy of each inside the step
+        host_batches = [synthetic_batch(args.batch, cfg["S"], n=cfg["n"], seed=9100 + 10 * rank + i)
+                        for i in range(3)]
+        ref["ref_loop_literal_graphs_per_s"] = reference_loop_rate(
+            dev, cfg, host_batches, args, world, steps=min(args.steps, 20))
+        del host_batches
     model.eval()
     fstep = ForwardStep(model, data, use_graph=not args.no_graph)
     for _ in range(max(1, args.warmup)):
@@ -711,9 +782,15 @@ def main():
                        "graphs_per_gpu": args.batch, "global_batch": args.batch * world,
                        "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
             "fwd_graphs_per_s": round(fwd_value, 1),
-            "ref_loop_graphs_per_s": round(ref_loop, 1) if ref_loop else None,
-            "ref_loop_block_layout_graphs_per_s": round(ref_loop_block, 1) if ref_loop_block
-            else None,
+            **{k: round(v, 1) for k, v in ref.items()},
+            "ref_loop_is": "5_train_SpotV2Net.py:142-160 unchanged (new batch per step, "
+                           "data.to(device), MSELoss, zero_grad, backward, torch.optim.Adam, "
+                           "loss.item()); DDP-wrapped at N > 1. ref_loop: two device-resident "
+                           "batches alternating, default Adam; fused_adam: Adam(fused=True); "
+                           "block_layout: no canonical mark; literal: pageable host batches, "
+                           "the H2D copy inside the step",
+            "replicas_bit_identical": replicas_ok,
+            "backend": args.backend if world > 1 else None,
             "step_roofline": step_roofline(cfg, value, fwd_value, args.precision),
             "final_loss": loss,
             "roofline": roof,

@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 11
+#define SV2N_ABI_VERSION 12
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -493,8 +493,9 @@ int sv2n_block_rowmask_checked(const int64_t* edge_index, int64_t num_edges, int
  *             [2*S+t] volvol[t][g][g]
  *   y         [B*n*F]         y[(b*n+v)*F+k] = vol[st_b+S+k][v][v]
  * vol / volvol: [T][n][n] fp32 series, T = num_matrices.  A window outside
- * the series (st_b < 0 or st_b + S + F > T) reads nothing and its
- * x / edge_attr / y rows are written as NaN (ABI 8). */
+ * the series (starts[b] < 0, st_b < 0 or st_b + S + F > T) reads nothing and
+ * its x / edge_attr / y rows are written as NaN (ABI 8; a negative starts[b]
+ * since ABI 12, so a negative batch index never reads before the offset). */
 int sv2n_window_gather(const float* vol, const float* volvol, int n, int64_t num_matrices,
                        const int64_t* starts, int64_t start_offset,
                        int64_t num_windows, int seq_length, int future_steps,

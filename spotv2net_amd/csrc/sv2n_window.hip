@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k_window_gather(
       const int64_t b = row / n;
       const int v = (int)(row - b * n);
       const int c = j / S, t = j - c * S;
-      const int64_t st = starts[b] + soff;
+      const int64_t st = starts[b] < 0 ? -1 : starts[b] + soff;  // a negative index is out of range
       x[i] = (st >= 0 && st + S + F <= T) ? vol[(st + t) * nn + v * n + c] : qnan;
     } else if (i < nx + ne) {
       const int64_t k0 = i - nx;
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void k_window_gather(
       } else {
         r = c = (kind == 1) ? s : g;
       }
-      const int64_t st = starts[b] + soff;
+      const int64_t st = starts[b] < 0 ? -1 : starts[b] + soff;  // a negative index is out of range
       ea[k0] = (st >= 0 && st + S + F <= T) ? volvol[(st + t) * nn + r * n + c] : qnan;
     } else {
       const int64_t k0 = i - nx - ne;
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void k_window_gather(
       const int k = (int)(k0 - row * F);
       const int64_t b = row / n;
       const int v = (int)(row - b * n);
-      const int64_t st = starts[b] + soff;
+      const int64_t st = starts[b] < 0 ? -1 : starts[b] + soff;  // a negative index is out of range
       y[k0] = (st >= 0 && st + S + F <= T) ? vol[(st + S + k) * nn + v * n + v] : qnan;
     }
   }
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void k_window_rows(
   const int64_t b = blockIdx.x / n;
   const int t = threadIdx.x;
   const int64_t nn = (int64_t)n * n;
-  const int64_t st = starts[b] + soff;
+  const int64_t st = starts[b] < 0 ? -1 : starts[b] + soff;  // a negative index is out of range
   const int E0 = n * (n - 1), P = E0 / 2;
   if (st < 0 || st + S + F > T) {  // window outside the series: NaN rows, no reads
     const float qnan = __builtin_nanf("");

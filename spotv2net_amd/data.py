@@ -256,14 +256,18 @@ class WindowDataset:
         """Gather the windows ``self.starts[idx]`` into ``out``'s buffers
         (from ``empty_batch(idx.numel())``), on the device, with no host
         synchronisation or host->device copy: capturable into a hipGraph.
-        Same values as ``batch(idx)``."""
+        Same values as ``batch(idx)`` for ``idx`` in ``[0, len(self))``; an
+        index outside that range (negative ones included: no Python-style
+        wrap-around) gives NaN rows on the device path, the device-side error
+        that needs no host round trip."""
         B, n, S, Fs = idx.numel(), self.n, self.S, self.future_steps
         P = self._up_s.numel()
         if self.vol.is_cuda and self.vol.dtype == torch.float32 and \
                 self.volvol.dtype == torch.float32:
             # one sv2n::window_gather launch (include/sv2n.h sv2n_window_gather):
             # starts[idx] = cut + idx, added in the kernel (no gather launch);
-            # an index past the windows names matrices past the series: NaN rows
+            # an index past the windows names matrices past the series, a
+            # negative one is refused by the kernel: NaN rows either way
             from . import library  # noqa: F401
             from .layout import canonical_table
             torch.ops.sv2n.window_gather(self.vol.contiguous(), self.volvol.contiguous(),

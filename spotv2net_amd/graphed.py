@@ -178,11 +178,17 @@ class _Replay(torch.autograd.Function):
     the flat gradient buffer (fresh tensors for AccumulateGrad)."""
 
     @staticmethod
-    def forward(ctx, entry: _Entry, layout: GraphLayout, *params):
+    def forward(ctx, entry: _Entry, layout: GraphLayout, inputs, *params):
         # the caller has already replayed entry.g_fwd (see forward below)
         entry.gen += 1
         entry.backwarded = False
         ctx.entry, ctx.gen = entry, entry.gen
+        # the backward graph reads x / edge_attr in place (layer 0's weight
+        # gradient, the edge-gradient pass): hold them until backward, as the
+        # eager node's saved tensors do, and remember their versions so an
+        # in-place write in between raises as it would eagerly
+        ctx.inputs = inputs
+        ctx.versions = tuple(t._version for t in inputs)
         entry.ctx_ref = weakref.ref(ctx)
         return entry.out.clone()
 
@@ -194,6 +200,12 @@ class _Replay(torch.autograd.Function):
                 "spotv2net_amd: the graph-replayed forward this backward belongs to was "
                 "overwritten by a later forward (retain_graph with interleaved forwards); set "
                 "model.graph_replay = False for this pattern")
+        for t, v in zip(ctx.inputs, ctx.versions):
+            if t._version != v:
+                raise RuntimeError(
+                    "spotv2net_amd: one of the variables needed for gradient computation has "
+                    f"been modified by an inplace operation (input version {t._version}, "
+                    f"expected {v})")
         entry.dout.copy_(dout.reshape(entry.dout.shape))
         if entry.g_bwd is None:
             entry.capture_bwd()
@@ -204,7 +216,7 @@ class _Replay(torch.autograd.Function):
         for slot, used, shape in entry.grad_shapes:
             g = next(parts) if slot else None
             grads.append(g.view(shape) if used else None)
-        return (None, None) + tuple(grads)
+        return (None, None, None) + tuple(grads)
 
 
 class GraphCache:
@@ -258,7 +270,8 @@ def forward(model, data, x, edge_index, edge_attr, layout: GraphLayout) -> Optio
     ps = _params(model)
     needs = tuple(p.requires_grad for p in ps)
     train_graph = torch.is_grad_enabled() and any(needs)
-    key = (model.training, train_graph, model.precision, torch.is_autocast_enabled("cuda"),
+    precision = resolve_precision(model.precision)
+    key = (model.training, train_graph, precision, torch.is_autocast_enabled("cuda"),
            model._act_code, model.dropout, tuple(c.dropout for c in model.gat_layers),
            _tsig(x), _tsig(edge_attr), _layout_sig(layout), needs,
            tuple(p.data_ptr() for p in ps))
@@ -273,7 +286,7 @@ def forward(model, data, x, edge_index, edge_attr, layout: GraphLayout) -> Optio
         _require_params(ps)
         entry = _Entry(model, layout, train_graph)
         entry.load_layout(layout)
-        entry.capture_fwd(x, edge_attr, resolve_precision(model.precision))
+        entry.capture_fwd(x, edge_attr, precision)
         cache.entries[key] = entry
         while len(cache.entries) > MAX_ENTRIES:
             cache.entries.popitem(last=False)
@@ -290,4 +303,5 @@ def forward(model, data, x, edge_index, edge_attr, layout: GraphLayout) -> Optio
     # of a synchronised step (the reference loop's loss.item() drains it)
     entry.load_layout(layout)
     entry.g_fwd.replay()
-    return _Replay.apply(entry, layout, *ps)
+    inputs = (x,) if edge_attr is None else (x, edge_attr)
+    return _Replay.apply(entry, layout, inputs, *ps)

@@ -462,13 +462,12 @@ class Fit:
             self.step(self._train_shape[b])   # adds its loss to _tot_train
             nb += 1
         nt = 0
+        self._tot_test.zero_()   # an empty test split reports 0, not the last epoch's sum
         self.model.eval()
         test_idx = torch.arange(self.n_train, self.n_train + self.n_test, device=dev)
         for k in range(0, self.n_test, self.bs):
             b = min(self.bs, self.n_test - k)
-            fs = self._eval_step(b)
-            if nt == 0:
-                self._tot_test.zero_()
+            fs = self._eval_step(b)   # its capture restores _tot_test after warming up
             self._idx[b].copy_(test_idx[k:k + b])
             fs()                               # adds its loss to _tot_test
             nt += 1

@@ -185,3 +185,137 @@ def test_inference_replay_and_autograd_grad(dev):
     g2 = torch.autograd.grad(m2(_fresh(d)).square().sum(), list(m2.parameters()))
     for a, b in zip(g1, g2):
         assert torch.equal(a, b)
+
+
+# ---------------------------------------------------------------------------
+# the DataLoader pattern: a different host batch every step, moved with
+# .to(device) (5_train_SpotV2Net.py:142-147), so the replayed graphs see new
+# contents at allocator-recycled, alternating addresses
+# ---------------------------------------------------------------------------
+def _host_batches(k, B=12, S=4, seed=40, canonical=False):
+    from spotv2net_amd import synthetic_batch
+    out = []
+    for i in range(k):
+        b = synthetic_batch(B, S, seed=seed + i)      # host tensors, distinct contents
+        if canonical:
+            b.canonical_edges = True
+        out.append(b)
+    return out
+
+
+def _loader_loop(model, host, steps, dev, scale_up=None):
+    """5_train_SpotV2Net.py:127, :142-160 as written: default torch.optim.Adam,
+    ``data = data.to(device)``, the optional scale_up rebinding, MSELoss,
+    zero_grad, backward, step, loss.item()."""
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    crit = torch.nn.MSELoss()
+    losses, ptrs = [], set()
+    for k in range(steps):
+        data = host[k % len(host)]
+        data = data.to(dev)
+        if scale_up:
+            data.x = data.x * scale_up
+            data.edge_attr = data.edge_attr * scale_up
+            data.y_x = data.y_x * scale_up
+        ptrs.add((data.x.data_ptr(), data.edge_attr.data_ptr()))
+        y_x_hat = model(data)
+        loss = crit(y_x_hat, data.y_x)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    return losses, ptrs
+
+
+@pytest.mark.parametrize("scale_up,canonical", [(None, True), (None, False), (2.5, True)])
+def test_dataloader_pattern_replay_equals_eager(dev, scale_up, canonical):
+    """8 steps over 3 distinct host batches, each moved with .to(device):
+    with graph replay on, losses and parameters equal the eager loop's bit for
+    bit, and at least one captured entry is replayed at an address a later
+    batch reuses (a stale read would show up as a loss difference)."""
+    host = _host_batches(3, canonical=canonical)
+    m1 = _model(dev, seed=21)
+    m2 = copy.deepcopy(m1)
+    m2.graph_replay = False
+    l1, p1 = _loader_loop(m1, host, 8, dev, scale_up)
+    l2, _ = _loader_loop(m2, host, 8, dev, scale_up)
+    assert l1 == l2
+    assert len(set(l1)) == len(l1)   # every step saw different data
+    for (n, p), (_, q) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(p, q), n
+    # the allocator recycles addresses: fewer distinct input addresses than steps,
+    # so entries were replayed on new contents
+    assert len(p1) < 8
+    assert any(e.g_bwd is not None for e in m1._graph_cache.entries.values())
+
+
+def test_inplace_refilled_batch_replay_equals_eager(dev):
+    """One device batch whose contents are overwritten in place between steps
+    (same addresses every step, e.g. a static prefetch buffer): every replay
+    reads the new contents."""
+    from spotv2net_amd import synthetic_batch
+    host = _host_batches(4, seed=60)
+    res = []
+    for replay in (True, False):
+        m = _model(dev, seed=22)
+        m.graph_replay = replay
+        buf = synthetic_batch(12, 4, seed=0, device=dev)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        losses = []
+        for k in range(7):
+            src = host[k % 4]
+            buf.x.copy_(src.x)
+            buf.edge_attr.copy_(src.edge_attr)
+            buf.y_x.copy_(src.y_x)
+            loss = torch.nn.functional.mse_loss(m(_fresh(buf)), buf.y_x)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+        res.append((losses, [p.detach().clone() for p in m.parameters()]))
+    assert res[0][0] == res[1][0]
+    assert len(set(res[0][0])) == len(res[0][0])
+    for p, q in zip(res[0][1], res[1][1]):
+        assert torch.equal(p, q)
+
+
+def test_replayed_inputs_kept_alive_until_backward(dev):
+    """The backward graph reads x / edge_attr in place: a batch dropped
+    between forward and backward stays alive (the allocator cannot hand its
+    memory to the next batch), so the gradients equal eager ones."""
+    host = _host_batches(2, seed=80)
+    m1 = _model(dev, seed=23)
+    m2 = copy.deepcopy(m1)
+    m2.graph_replay = False
+    grads = []
+    for m in (m1, m2):
+        for k in range(3):   # capture + replay this signature
+            m(host[0].to(dev)).square().sum().backward()
+        m.zero_grad()
+        out = m(host[0].to(dev))          # the batch has no other reference
+        junk = [host[1].to(dev) for _ in range(3)]   # allocations that could reuse it
+        for j in junk:
+            j.x.fill_(7.0)
+            j.edge_attr.fill_(-3.0)
+        out.square().sum().backward()
+        grads.append([p.grad.clone() for p in m.parameters()])
+        del junk
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
+def test_inplace_write_between_forward_and_backward_raises(dev):
+    """Writing a replayed forward's x in place before its backward raises, as
+    the eager node's saved-tensor version check does."""
+    from spotv2net_amd import synthetic_batch
+    d = synthetic_batch(8, 4, seed=31, device=dev)
+    for replay in (True, False):
+        m = _model(dev, seed=24)
+        m.graph_replay = replay
+        for _ in range(3):
+            m(_fresh(d)).sum().backward()
+        out = m(_fresh(d))
+        d.x.add_(1.0)
+        with pytest.raises(RuntimeError, match="inplace"):
+            out.sum().backward()
+        d.x.sub_(1.0)

@@ -216,6 +216,30 @@ def test_window_gather_out_of_range_windows_are_nan(dev, n, S, Fs):
         assert torch.equal(ea[b * E0:(b + 1) * E0], want.edge_attr[j * E0:(j + 1) * E0])
 
 
+@pytest.mark.parametrize("n,S,Fs", [(30, 42, 1), (30, 180, 1)])
+def test_negative_window_index_is_nan_with_cut(dev, n, S, Fs):
+    """WindowDataset.fill with a cut: a negative batch index is out of range
+    (NaN rows), not a window cut + idx read from before the split (ABI 12),
+    on both kernels; the in-range indices of the same launch are unchanged."""
+    from spotv2net_amd import WindowDataset
+    from spotv2net_amd.data import synthetic_series
+    V, W = synthetic_series(S + Fs + 40, n, seed=17)
+    ds = WindowDataset(V.to(dev), W.to(dev), S, cut=9, future_steps=Fs)
+    idx = torch.tensor([2, -1, 0, -9, len(ds) - 1, len(ds)], device=dev)
+    got = ds.empty_batch(idx.numel())
+    ds.fill(got, idx)
+    want = ds.batch(torch.tensor([2, 0, len(ds) - 1]))
+    E0 = n * (n - 1)
+    for b, j in {0: 0, 2: 1, 4: 2}.items():
+        assert torch.equal(got.x[b * n:(b + 1) * n], want.x[j * n:(j + 1) * n])
+        assert torch.equal(got.edge_attr[b * E0:(b + 1) * E0], want.edge_attr[j * E0:(j + 1) * E0])
+        assert torch.equal(got.y_x[b * n:(b + 1) * n], want.y_x[j * n:(j + 1) * n])
+    for b in (1, 3, 5):
+        assert torch.isnan(got.x[b * n:(b + 1) * n]).all(), b
+        assert torch.isnan(got.edge_attr[b * E0:(b + 1) * E0]).all(), b
+        assert torch.isnan(got.y_x[b * n:(b + 1) * n]).all(), b
+
+
 @pytest.mark.parametrize("n,S,Fs", [(30, 42, 1), (7, 3, 2)])
 def test_window_gather_diag_matches_volvol_path(dev, n, S, Fs):
     """sv2n_window_gather_diag (ABI 11) with the series' diagonal given is bit-exact
