@@ -192,14 +192,18 @@ def kernel_table(model, data, reps=50):
         lib.sv2n_gemm_f32_slabs(0, 0, x0.data_ptr(), x0.stride(0), dxs0.data_ptr(),
                                 dxs0.stride(0), Fd, Nd, N0, slabs.data_ptr(), slabs.numel(), sh)
 
-    M0, N0c, K0 = N0, W[0].shape[0], x0.shape[1]
+    # algorithmic work: the H·C projection columns plus the node
+    # logits (4·n·H·C per graph), not the GEMM's padded / augmented columns
+    M0, K0 = N0, x0.shape[1]
+    HC0 = conv0.heads * conv0.out_channels
+    N0c = W[0].shape[0]
     # (fn, bound, algorithmic flops, algorithmic bytes, peak for the arithmetic used)
     rows = {
-        "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * N0c * K0,
-                        4.0 * (M0 * K0 + N0c * K0 + M0 * N0c), BF16X3_PEAK_TFLOPS),
-        # bf16x3 weight-gradient kernel (k_gemm_tt3y)
-        "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * N0c * K0,
-                        4.0 * (M0 * K0 + M0 * N0c + N0c * K0), BF16X3_PEAK_TFLOPS),
+        "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * HC0 * K0 + 4.0 * M0 * HC0,
+                        4.0 * (M0 * K0 + HC0 * K0 + M0 * HC0), BF16X3_PEAK_TFLOPS),
+        # bf16x3 weight-gradient kernel (k_gemm_tt3y): dW = xᵀ·dxs over the H·C columns
+        "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * HC0 * K0,
+                        4.0 * (M0 * K0 + M0 * N0c + HC0 * K0), BF16X3_PEAK_TFLOPS),
         "edge_logits_fwd": (edge_fwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS),
                             None),
         "edge_logits_bwd": (edge_bwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS),
@@ -321,14 +325,15 @@ def kernel_table_tiled(model, data, cfg, reps=10):
 
     attn_fwd()  # the backward reads the training forward's outputs
     eab, xsb, rowb, stb = 4.0 * E * D, 4.0 * N0 * ldx, 4.0 * N0 * HC, 4.0 * N0 * 4 * H
-    M0, Nc, K0 = N0, W0.shape[0], x0.shape[1]
+    M0, K0 = N0, x0.shape[1]
+    Nc = HC   # algorithmic columns, not the augmented / padded ones
     # (fn, bound, algorithmic flops, algorithmic bytes, peak)
     rows = {
         "gat_attn_fused_fwd_l0": (attn_fwd, "hbm", 0.0, eab + xsb + 2 * rowb + stb, None),
         "gat_attn_fused_bwd_l0": (attn_bwd, "hbm", 0.0, eab + 2 * xsb + 3 * rowb + stb, None),
-        "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * Nc * K0, 4.0 * (M0 * K0 + Nc * K0 + M0 * Nc),
-                        BF16X3_PEAK_TFLOPS),
-        "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * Nd * K0, 4.0 * (M0 * K0 + M0 * Nd + Nd * K0),
+        "gemm_l0_fwd": (gemm_fwd, "mfma", 2.0 * M0 * Nc * K0 + 4.0 * M0 * Nc,
+                        4.0 * (M0 * K0 + Nc * K0 + M0 * Nc), BF16X3_PEAK_TFLOPS),
+        "gemm_l0_dwT": (gemm_dwt, "mfma", 2.0 * M0 * Nc * K0, 4.0 * (M0 * K0 + M0 * Nd + Nc * K0),
                         BF16X3_PEAK_TFLOPS),
     }
     return time_rows(rows, stream, reps, order=["gemm_l0_fwd", "gat_attn_fused_fwd_l0",
@@ -405,7 +410,7 @@ def kernel_table_c3(model, cfg, precision, reps=20):
                               dbp2.data_ptr(), B, n, H, C, 0, 1, 0.2, sh)
 
     peak = BF16_MFMA_PEAK_TFLOPS if bf16 else BF16X3_PEAK_TFLOPS
-    gflop = 2.0 * N * ldx * F
+    gflop = 2.0 * N * HC * F + 4.0 * N * HC   # algorithmic: H·C columns
     rows = {
         "gemm_fwd": (gemm_fwd, "mfma", gflop, 4.0 * (N * F + N * ldx) + (2 if bf16 else 6) * ldx * F,
                      peak),

@@ -167,6 +167,33 @@ int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* xs, int ldx,
  * its backward products dX (a_kmajor=1, b_kmajor=0) and dWᵀ (0, 0).
  * workspace: sv2n_gemm_f32_workspace(M,N,K) floats (split-K partial slabs;
  * 0 => may be NULL). */
+/* sv2n_gat_attn_bwd with the edge-logit weight gradient of EVERY layer fused
+ * in (ABI 12; replaces sv2n_edge_logits_bwd for canonical batches, reference
+ * GATConv lin_edge / att_edge backward, utils/models.py:146): the workgroup
+ * of graph g keeps this layer's d-logits in LDS (none are written), reads
+ * the other layers' d-logits layer_dae[l] ([E][heads] canonical edge order,
+ * as sv2n_gat_attn_bwd writes them; entry `layer` unused) and streams the
+ * graph's edge_attr rows once:
+ *   edge_partial[g][d][k] = Σ_{e of g} edge_attr[e][d] · dae_l(k)[e][h(k)],
+ * k = l·heads + h < num_layers·heads <= hl_pad (columns past that: 0).
+ * Sum the partials in graph order with sv2n_edge_partials_reduce to get the
+ * [edge_dim][hl_pad] gradient sv2n_edge_logits_bwd returns.  Canonical
+ * complete graphs only; sv2n_gat_attn_bwd_edge_supported says whether the
+ * shape runs (all heads in one workgroup, hl_pad <= 8, even edge_dim <= 128).
+ * edge_attr 16-B aligned; layer_dae is a HOST array of device pointers. */
+int sv2n_gat_attn_bwd_edge_supported(int64_t num_graphs, int n, int heads, int channels,
+                                     int edge_dim, int hl_pad);
+int sv2n_gat_attn_bwd_edge(const float* dy, const float* y, const float* xs, int ldx,
+                           const float* psave, const uint8_t* keep, float keep_scale,
+                           const float* post_u, float post_p, float* dxs, float* dbias_partial,
+                           const float* edge_attr, int edge_dim, const float* const* layer_dae,
+                           int num_layers, int layer, int hl_pad, float* edge_partial,
+                           int64_t num_graphs, int n, int heads, int channels, int concat, int act,
+                           float negative_slope, hipStream_t stream);
+/* out[o] = Σ_p partial[p][o], p = 0 .. num_parts-1 in order (deterministic). */
+int sv2n_edge_partials_reduce(const float* partial, int64_t num_parts, int64_t width, float* out,
+                              hipStream_t stream);
+
 int64_t sv2n_gemm_f32_workspace(int64_t M, int64_t N, int64_t K);
 int sv2n_gemm_f32(int a_kmajor, int b_kmajor, const float* A, int64_t lda,
                   const float* B, int64_t ldb, float* C, int64_t ldc,

@@ -56,6 +56,13 @@ _SIGNATURES = {
                                  _i32, _i32, _i32, _i32, _i32, _f32, _p]),
     "sv2n_gat_attn_bwd": (_i32, [_p, _p, _p, _i32, _p, _p, _f32, _p, _f32, _p, _p, _p, _i32, _p,
                                  _i64, _i32, _i32, _i32, _i32, _i32, _f32, _p]),
+    "sv2n_gat_attn_bwd_edge_supported": (_i32, [_i64, _i32, _i32, _i32, _i32, _i32]),
+    # dy y xs ldx psave keep keep_scale post_u post_p dxs dbp ea D layer_dae L layer hlp part
+    # B n H C concat act slope stream
+    "sv2n_gat_attn_bwd_edge": (_i32, [_p, _p, _p, _i32, _p, _p, _f32, _p, _f32, _p, _p, _p, _i32,
+                                      _p, _i32, _i32, _i32, _p, _i64, _i32, _i32, _i32, _i32,
+                                      _i32, _f32, _p]),
+    "sv2n_edge_partials_reduce": (_i32, [_p, _i64, _i64, _p, _p]),
     "sv2n_gat_attn_tiled_workspace": (_i64, [_i64, _i32, _i32, _i32, _i32]),
     "sv2n_gat_attn_tiled_fwd": (_i32, [_p, _i32, _p, _i64, _p, _p, _p, _p, _f32, _p, _p, _i64,
                                        _i64, _i32, _i32, _i32, _i32, _i32, _f32, _p]),

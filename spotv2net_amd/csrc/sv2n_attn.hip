@@ -19,7 +19,9 @@ void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const f
 void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, const float* xs,
                     int ldx, const float* psave, const uint8_t* keep, float keep_scale,
                     const float* post_u, float post_p, const uint32_t* rowmask, float* dxs, float* dae, int ae_edge_order,
-                    float* dbias, int n, int H, int C, int concat, int act, float slope);
+                    float* dbias, int n, int H, int C, int concat, int act, float slope,
+                    const EdgeTail& et);
+bool attn_canon_edge_tail_ok(int64_t B, int n, int H, int C, int D, int hlp);
 }  // namespace sv2n
 
 using namespace sv2n;
@@ -61,6 +63,49 @@ extern "C" int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* x
   attn_canon_bwd(num_graphs, stream, dy, y, xs, ldx, psave, keep, keep_scale, post_u, post_p,
                  rowmask, dxs,
                  dae, ae_edge_order, dbias_partial, n, heads, channels, concat, act,
-                 negative_slope);
+                 negative_slope, EdgeTail{});
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_gat_attn_bwd_edge_supported(int64_t num_graphs, int n, int heads, int channels,
+                                                int edge_dim, int hl_pad) {
+  if (num_graphs <= 0 || channels <= 0 || heads < 1 || heads > SV2N_MAX_HEADS) return 0;
+  return attn_canon_edge_tail_ok(num_graphs, n, heads, channels, edge_dim, hl_pad) ? 1 : 0;
+}
+
+extern "C" int sv2n_gat_attn_bwd_edge(const float* dy, const float* y, const float* xs, int ldx,
+                                      const float* psave, const uint8_t* keep, float keep_scale,
+                                      const float* post_u, float post_p, float* dxs,
+                                      float* dbias_partial, const float* edge_attr, int edge_dim,
+                                      const float* const* layer_dae, int num_layers, int layer,
+                                      int hl_pad, float* edge_partial, int64_t num_graphs, int n,
+                                      int heads, int channels, int concat, int act,
+                                      float negative_slope, hipStream_t stream) {
+  if (!dy || !y || !xs || !psave || !dxs || !dbias_partial || !edge_attr || !edge_partial ||
+      !layer_dae)
+    return SV2N_ERR_ARG;
+  if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
+  if (post_u && !(post_p >= 0.f && post_p < 1.f)) return SV2N_ERR_ARG;
+  if (num_layers < 1 || num_layers > SV2N_MAX_LAYERS || layer < 0 || layer >= num_layers ||
+      num_layers * heads > hl_pad)
+    return SV2N_ERR_SHAPE;
+  if (!attn_canon_edge_tail_ok(num_graphs, n, heads, channels, edge_dim, hl_pad))
+    return SV2N_ERR_SHAPE;
+  if ((uintptr_t)edge_attr % 16) return SV2N_ERR_ALIGN;
+  EdgeTail et{};
+  et.ea = edge_attr;
+  for (int l = 0; l < num_layers; ++l) {
+    if (l == layer) continue;
+    if (!layer_dae[l]) return SV2N_ERR_ARG;
+    et.dae[l] = layer_dae[l];
+  }
+  et.part = edge_partial;
+  et.D = edge_dim;
+  et.L = num_layers;
+  et.own = layer;
+  et.hlp = hl_pad;
+  attn_canon_bwd(num_graphs, stream, dy, y, xs, ldx, psave, keep, keep_scale, post_u, post_p,
+                 nullptr, dxs, nullptr, 1, dbias_partial, n, heads, channels, concat, act,
+                 negative_slope, et);
   return (int)hipGetLastError();
 }

@@ -358,11 +358,127 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 //      G in registers until then.
 // ---------------------------------------------------------------------------
 constexpr int CS = 36;  // chunk row stride (floats): 16-B rows, conflict-free b128 row reads
+constexpr int AREA = 4 * 2 * 32 * CS;  // the four waves' chunk areas (floats)
 constexpr int DS = 33;  // dl row stride (floats): conflict-free column sums
 constexpr int PB = 32;  // P_d row stride: column reads only (conflict-free at any stride)
 
 __host__ __device__ inline int canon_bwd_tail_floats(int HS) {  // sDL .. sDec
   return HS * 32 * DS + 2 * HS * 32 + 32 + (32 * 31 / 2 + 1) / 2;
+}
+
+// ---------------------------------------------------------------------------
+// Edge-gradient tail (EdgeTail.ea != nullptr; canonical batches, one split per
+// graph): the weight gradient of the folded edge logits of EVERY layer,
+//   part[g][d][k] = Σ_{e of graph g} edge_attr[e][d] · dAE[e][k],
+// k = l·H + h over the hl_pad columns of the edge pass (sv2n_edge.hip), with
+// this layer's d-logits taken from LDS (never written to HBM) and the other
+// layers' from their [E][H] edge-order buffers.  The graph's edge rows are
+// streamed once; the caller sums the per-graph partials in graph order
+// (k_reduce_partials).  This replaces the separate edge-gradient pass over
+// edge_attr (k_edge_bwd) and its d-logit write / read for this layer.
+// LDS: the tail region moves to the end of the chunk areas so that the
+// d-logit table sE[E0][8] can span sP and the start of the areas; the wave
+// partials reuse sE after the stream.
+// ---------------------------------------------------------------------------
+
+__host__ __device__ inline int canon_bwd_tail_off(bool edge, int HS) {
+  return edge ? ((AREA - canon_bwd_tail_floats(HS)) & ~3) : 0;
+}
+
+// The tail proper (every thread of the workgroup; sDL / sSh / sDec complete).
+__device__ __forceinline__ void edge_grad_tail(const EdgeTail& et, int64_t g, int n, int H,
+                                               const float* sDL, const float* sSh,
+                                               const uint16_t* sDec, float* smem) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int E0 = n * (n - 1), P = E0 / 2, D = et.D;
+  float* sE = smem;  // [E0][ET_COLS]
+  // this layer's d-logits (dl + the self-loop share of row ti), PyG's per-edge
+  // gradient of the folded edge logit
+  for (int p = t; p < P; p += THREADS) {
+    const uint32_t uw = sDec[p];
+    const int u = uw >> 8, w = uw & 0xff;
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const int ti = side ? u : w, tj = side ? w : u, e = side ? P + p : p;
+      for (int h = 0; h < H; ++h)
+        sE[e * ET_COLS + et.own * H + h] = sDL[(h * 32 + ti) * DS + tj] + sSh[h * 32 + ti];
+    }
+  }
+  // the other layers' columns (coalesced [E0][H] runs) and the zero padding
+  for (int l = 0; l < et.L; ++l) {
+    if (l == et.own) continue;
+    const rsrc_t rd = make_rsrc(et.dae[l] + g * E0 * H, (uint32_t)(E0 * H) * 4u);
+    for (int k = t; k < E0 * H; k += THREADS) {
+      const int e = k / H, h = k - e * H;
+      sE[e * ET_COLS + l * H + h] = bld(rd, k * 4);
+    }
+  }
+  for (int k = t; k < E0 * (ET_COLS - et.L * H); k += THREADS) {
+    const int w = ET_COLS - et.L * H, e = k / w;
+    sE[e * ET_COLS + et.L * H + (k - e * w)] = 0.f;
+  }
+  __syncthreads();
+  // stream the graph's edge rows: wave w takes edges w, w + 4, ...; lane l the
+  // columns d = 2l, 2l + 1 (8-B loads: a row is one wave-instruction); two
+  // register sets of U rows in flight
+  constexpr int U = 8;
+  const int d0 = 2 * lane;
+  const bool dv = d0 < D;
+  const rsrc_t rea = make_rsrc(et.ea + g * E0 * D, (uint32_t)(E0 * D) * 4u);
+  float a0[ET_COLS], a1[ET_COLS];
+#pragma unroll
+  for (int c = 0; c < ET_COLS; ++c) a0[c] = a1[c] = 0.f;
+  u32x2 va[U], vb[U];
+  auto load = [&](u32x2 (&v)[U], int e0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + 4 * u;
+      v[u] = bld2_u32(rea, (dv && e < E0) ? (e * D + d0) * 4 : OOB);
+    }
+  };
+  auto fma_rows = [&](const u32x2 (&v)[U], int e0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + 4 * u;
+      if (e < E0) {  // wave-uniform
+        const f32x4 k0 = *reinterpret_cast<const f32x4*>(sE + e * ET_COLS);
+        const f32x4 k1 = *reinterpret_cast<const f32x4*>(sE + e * ET_COLS + 4);
+        const float x0 = __uint_as_float(v[u][0]), x1 = __uint_as_float(v[u][1]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          a0[c] = fmaf(x0, k0[c], a0[c]);
+          a1[c] = fmaf(x1, k0[c], a1[c]);
+          a0[4 + c] = fmaf(x0, k1[c], a0[4 + c]);
+          a1[4 + c] = fmaf(x1, k1[c], a1[4 + c]);
+        }
+      }
+    }
+  };
+  int e0 = wave;
+  load(va, e0);
+  for (; e0 < E0; e0 += 8 * U) {
+    load(vb, e0 + 4 * U);
+    fma_rows(va, e0);
+    load(va, e0 + 8 * U);
+    fma_rows(vb, e0 + 4 * U);
+  }
+  __syncthreads();  // every wave is done with sE: it takes the wave partials
+  float* sR = smem;  // [4][ET_COLS][128]
+#pragma unroll
+  for (int c = 0; c < ET_COLS; ++c) {
+    sR[(wave * ET_COLS + c) * 128 + d0] = a0[c];
+    sR[(wave * ET_COLS + c) * 128 + d0 + 1] = a1[c];
+  }
+  __syncthreads();
+  const int O = D * et.hlp;
+  const rsrc_t rp = make_rsrc(et.part + g * O, (uint32_t)O * 4u);
+  for (int o = t; o < O; o += THREADS) {
+    const int d = o / et.hlp, c = o - d * et.hlp;
+    float s = sR[c * 128 + d];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) s += sR[(w * ET_COLS + c) * 128 + d];
+    bst(rp, o * 4, s);
+  }
 }
 
 template <int ACT, bool CONCAT, bool KEEP, int DEPTH>
@@ -372,11 +488,12 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     const float* __restrict__ post_u, float post_p, float post_scale,
     const uint32_t* __restrict__ rowmask, float* __restrict__ dxs, float* __restrict__ dae,
     int ae_edge_order, float* __restrict__ dbias_part, int n, int H, int C, float slope, int S,
-    int HS, int WPH, int64_t B) {
+    int HS, int WPH, int64_t B, EdgeTail et) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sP = smem;
   float* sArea = sP + HS * 32 * PB;
-  float* sDL = sArea;  // after the chunk loop
+  const bool etail = et.ea != nullptr;  // uniform
+  float* sDL = sArea + canon_bwd_tail_off(etail, HS);  // after the chunk loop
   float* sSh = sDL + HS * 32 * DS;
   float* sDad = sSh + HS * 32;
   uint32_t* sRB = reinterpret_cast<uint32_t*>(sDad + HS * 32);  // source bits of row i
@@ -636,7 +753,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   }
   if (nhw > 0 && sub == 0) softmax_bwd(grp, G);  // pr still holds this head's P
   if (t < 32) sRB[t] = rbits;
-  if (dae && ae_edge_order && t < n) {  // row u of the pair table
+  if ((dae || etail) && ae_edge_order && t < n) {  // row u of the pair table
     const int base = (t * (2 * n - 1 - t)) >> 1;
     for (int w = t + 1; w < n; ++w) sDec[base + w - t - 1] = (uint16_t)((t << 8) | w);
   }
@@ -714,6 +831,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       const int j = q & 31, c2 = q >> 5;
       bst(rdx, j < n ? (j * ldx + HC + 2 * H + c2) * 4 : OOB, 0.f);
     }
+  if (etail) edge_grad_tail(et, g, n, H, sDL, sSh, sDec, smem);
   SV2N_STAMP(12, SV2N_T());
   SV2N_STAMP(13, SV2N_RT());
 }
@@ -774,7 +892,8 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
                              const float* xs, int ldx, const float* psave, const uint8_t* keep,
                              float keep_scale, const float* post_u, float post_p,
                              const uint32_t* rowmask, float* dxs, float* dae,
-                             int ae_edge_order, float* dbias, int n, int H, int C, float slope) {
+                             int ae_edge_order, float* dbias, int n, int H, int C, float slope,
+                             const EdgeTail& et) {
   const CanonBwdPlan pl = canon_bwd_plan(B, H, C);
   const size_t lds = attn_canon_bwd_lds(pl.HS);
   const unsigned grid = canon_grid(B, pl.S);
@@ -787,7 +906,7 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
     hipLaunchKernelGGL(kern, dim3(grid), dim3(canon::THREADS), lds, st, dy, y, xs, ldx, psave,
                        keep, keep_scale, post_u, post_p,
                        post_u ? (float)(1.0 / (1.0 - (double)post_p)) : 1.f, rowmask, dxs, dae,
-                       ae_edge_order, dbias, n, H, C, slope, pl.S, pl.HS, pl.WPH, B);
+                       ae_edge_order, dbias, n, H, C, slope, pl.S, pl.HS, pl.WPH, B, et);
   };
   const int nch = (C + 31) >> 5;
   const bool resident = grid <= 2 * CANON_CUS;
@@ -803,14 +922,27 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
     launch(canon::k_bwd<ACT, CONCAT, KEEP, 1>);
 }
 
+// Whether the edge-gradient tail runs for this shape (canonical complete
+// graphs, all heads in one workgroup, hl_pad <= 8 columns, even D <= 128 with
+// 8-B aligned rows; the d-logit table and the moved tail fit the LDS).
+bool attn_canon_edge_tail_ok(int64_t B, int n, int H, int C, int D, int hlp) {
+  const CanonBwdPlan pl = canon_bwd_plan(B, H, C);
+  if (pl.S != 1 || n < 2 || n > 32 || hlp > ET_COLS || hlp < H || D < 1 || D > 128 ||
+      (D & 1))
+    return false;
+  const int E0 = n * (n - 1);
+  const int room = pl.HS * 32 * canon::PB + canon::canon_bwd_tail_off(true, pl.HS);
+  return E0 * ET_COLS <= room && 4 * ET_COLS * 128 <= room;
+}
+
 void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, const float* xs,
                     int ldx, const float* psave, const uint8_t* keep, float keep_scale,
                     const float* post_u, float post_p, const uint32_t* rowmask, float* dxs,
                     float* dae, int ae_edge_order, float* dbias, int n, int H, int C, int concat,
-                    int act, float slope) {
+                    int act, float slope, const EdgeTail& et) {
 #define SV2N_CB(A, CC, K)                                                                      \
   launch_canon_bwd<A, CC, K>(B, st, dy, y, xs, ldx, psave, keep, keep_scale, post_u, post_p,   \
-                             rowmask, dxs, dae, ae_edge_order, dbias, n, H, C, slope)
+                             rowmask, dxs, dae, ae_edge_order, dbias, n, H, C, slope, et)
 #define SV2N_CB_ACT(CC, K)                 \
   switch (act) {                           \
     case 0: SV2N_CB(0, CC, K); break;      \

@@ -190,6 +190,17 @@ __device__ __forceinline__ bool last_block_ticket2(unsigned* cnt, unsigned nbloc
   return *s_flag != 0;
 }
 
+// Edge-gradient tail of the n <= 32 attention backward (sv2n_attn_canon.hip,
+// sv2n_gat_attn_bwd_edge): the edge pass's hl_pad columns it carries, and its
+// arguments (ea == nullptr: off).
+constexpr int ET_COLS = 8;
+struct EdgeTail {
+  const float* ea;                     // [B·E0][D] edge_attr (canonical order)
+  const float* dae[SV2N_MAX_LAYERS];   // other layers' d-logits [B·E0][H] (own: unused)
+  float* part;                         // [B][D][hlp] per-graph partials
+  int D, L, own, hlp;                  // own: this layer's index (columns own·H ..)
+};
+
 // rows i of graph g: bit j set <=> edge j->i present (self loop excluded)
 __device__ __forceinline__ uint32_t row_bits(const uint32_t* rowmask, int64_t row, int n, int i) {
   if (rowmask) return rowmask[row] & ~(1u << i);
@@ -283,10 +294,13 @@ __device__ __forceinline__ f32x4 bld4(rsrc_t r, int off) {
 __device__ __forceinline__ u32x4 bld4_u32(rsrc_t r, int off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x2 bld2_u32(rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+}
 __device__ __forceinline__ void bst(rsrc_t r, int off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
 }
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void bst2(rsrc_t r, int off, float a, float b) {
   __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(a), __float_as_uint(b)}, r, off, 0,
                                         0);

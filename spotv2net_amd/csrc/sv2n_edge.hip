@@ -845,6 +845,15 @@ extern "C" int sv2n_edge_logits_bwd(const float* edge_attr, int64_t num_edges, i
                        hl_pad, false, stream);
 }
 
+extern "C" int sv2n_edge_partials_reduce(const float* partial, int64_t num_parts, int64_t width,
+                                         float* out, hipStream_t stream) {
+  if (!partial || !out || num_parts <= 0 || width <= 0) return SV2N_ERR_ARG;
+  if (num_parts * width * 4 > 0x7fffffff) return SV2N_ERR_SHAPE;
+  hipLaunchKernelGGL(k_reduce_partials, dim3((unsigned)((width + 15) / 16)), dim3(256), 0, stream,
+                     partial, (int)num_parts, (int)width, out);
+  return (int)hipGetLastError();
+}
+
 extern "C" int sv2n_edge_logits_fwd_planes(const float* edge_attr, int64_t num_edges,
                                            int edge_dim, const float* wfold, int hl_pad,
                                            float* const* ae_layers, int num_layers, int heads,

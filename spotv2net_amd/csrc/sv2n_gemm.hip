@@ -19,6 +19,7 @@
 #include "sv2n_gemm_kernel.h"
 #include "sv2n_gemm3_kernel.h"
 #include "sv2n_gemm_tt.h"
+#include "sv2n_gemm_bw.h"
 
 namespace sv2n {
 
@@ -586,15 +587,36 @@ static void launch_wgrad_bf16(const GemmPlan& p, hipStream_t st, const float* x,
 }
 
 // the same product transposed, dWaug = dxsᵀ·x [ldx][F] (operands swapped):
-// the epilogue (k_wgrad_epi_t) then works along rows of gW
+// the epilogue (k_wgrad_epi_t) then works along rows of gW.  Round 4: the
+// large-tile kernel k_gemm_bw<256, 128, TN> (sv2n_gemm_bw.h; 256 x 128 tiles,
+// K slices of multiples of 64 aiming at one round of ~240 workgroups)
+constexpr int BWT_BM = 256, BWT_BN = 128;
+static GemmPlan plan_wgrad_bw(int64_t ldx, int64_t F, int64_t K) {
+  GemmPlan p{};
+  const int64_t tiles = ((ldx + BWT_BM - 1) / BWT_BM) * ((F + BWT_BN - 1) / BWT_BN);
+  int64_t sk = std::max<int64_t>(1, (240 + tiles / 2) / tiles);
+  sk = std::min<int64_t>(sk, std::max<int64_t>(1, K / 512));
+  sk = std::min<int64_t>(sk, 8);
+  int64_t ks = (K + sk - 1) / sk;
+  ks = (ks + 63) / 64 * 64;
+  p.splitk = (int)((K + ks - 1) / ks);
+  p.kslice = ks;
+  return p;
+}
 static void launch_wgrad_bf16_t(const GemmPlan& p, hipStream_t st, const float* x, int64_t ld_x,
                                 const float* dxs, int64_t ldx, int64_t F, int64_t K, float* out) {
-  using Cfg = GemmTTCfg<TT_BM, TT_BN, 1>;
-  constexpr size_t lds = Cfg::LDS;
-  const dim3 grid((unsigned)((ldx + TT_BM - 1) / TT_BM), (unsigned)((F + TT_BN - 1) / TT_BN),
-                  (unsigned)p.splitk);
-  hipLaunchKernelGGL((k_gemm_tt<TT_BM, TT_BN, 1>), grid, dim3(256), lds, st, dxs, ldx, x, ld_x,
-                     out, F, ldx, F, K, p.kslice);
+  using Cfg = GemmBWCfg<BWT_BM, BWT_BN, true, true, true>;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)k_gemm_bw<BWT_BM, BWT_BN, true, true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
+    return true;
+  }();
+  (void)attr;
+  const int nm = (int)((ldx + BWT_BM - 1) / BWT_BM), nn = (int)((F + BWT_BN - 1) / BWT_BN);
+  const dim3 grid((unsigned)(((nm + 7) / 8) * 8 * nn), 1, (unsigned)p.splitk);
+  hipLaunchKernelGGL((k_gemm_bw<BWT_BM, BWT_BN, true, true, true>), grid, dim3(Cfg::THREADS),
+                     Cfg::LDS, st, (const void*)dxs, ldx, (const void*)x, ld_x, out, F, ldx, F, K,
+                     p.kslice, nm, nn);
 }
 
 static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* dxs, int ldx,
@@ -620,7 +642,8 @@ extern "C" int64_t sv2n_gat_wgrad_node_bf16_workspace(int64_t num_nodes, int in_
                                                       int heads, int channels) {
   if (num_nodes <= 0 || in_features <= 0 || ldx <= 0 || heads <= 0 || channels <= 0) return 0;
   const GemmPlan p = plan_gemm_bf16t(in_features, ldx, num_nodes);
-  return (int64_t)in_features * ldx * (p.splitk > 1 ? 1 + p.splitk : 1);
+  const int sk = std::max(p.splitk, plan_wgrad_bw(ldx, in_features, num_nodes).splitk);
+  return (int64_t)in_features * ldx * (sk > 1 ? 1 + sk : 1);
 }
 
 extern "C" int sv2n_gat_wgrad_node_bf16(const float* x, int64_t ld_x, const float* dxs, int ldx,
@@ -665,9 +688,10 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
     if (num_nodes * std::max<int64_t>(ld_x, ldx) * 4 > 0x7fffffff) return SV2N_ERR_SHAPE;
     const GemmPlan p = plan_gemm_bf16t(F, ldx, num_nodes);
     if ((F & 3) == 0 && gW) {
-      // dWaug [ldx][F] as p.splitk slabs, summed by the epilogue launch itself
-      float* S = p.splitk > 1 ? slabs : T;
-      launch_wgrad_bf16_t(p, stream, x, ld_x, dxs, ldx, F, num_nodes, S);
+      // dWaug [ldx][F] as pt.splitk slabs, summed by the epilogue launch itself
+      const GemmPlan pt = plan_wgrad_bw(ldx, F, num_nodes);
+      float* S = pt.splitk > 1 ? slabs : T;
+      launch_wgrad_bf16_t(pt, stream, x, ld_x, dxs, ldx, F, num_nodes, S);
       const int nfc = (F / 4 + 63) / 64, nrow = (HC + WT_RB - 1) / WT_RB;
       const int natt = (g_att_src || g_att_dst) ? (HC + ATT_RB - 1) / ATT_RB : 0;
       size_t lds = 0;
@@ -684,7 +708,7 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
       }
       const int nbias = bias ? (bias_len + 15) / 16 : 0;
       hipLaunchKernelGGL(k_wgrad_epi_t, dim3((unsigned)(natt + nrow * nfc + nbias)), dim3(256),
-                         lds, stream, S, p.splitk, ldx, W, att_src, att_dst, H, C, F, gW,
+                         lds, stream, S, pt.splitk, ldx, W, att_src, att_dst, H, C, F, gW,
                          g_att_src, g_att_dst, nrow, nfc, natt, dbias_partial, num_parts,
                          bias_len, g_bias);
       return (int)hipGetLastError();

@@ -7,6 +7,7 @@
 #include "sv2n_common.h"
 #include "sv2n_gemm3_kernel.h"
 #include "sv2n_gemm_bf16.h"
+#include "sv2n_gemm_bw.h"
 
 #include <algorithm>
 
@@ -114,6 +115,23 @@ extern "C" int sv2n_gemm_bf16(const float* A, int64_t lda, const uint16_t* Bp, f
   if (((uintptr_t)A & 15) || (lda & 3) || ((uintptr_t)Bp & 15)) return SV2N_ERR_ALIGN;
   const int64_t Kp = sv2n_split3_kpad(K);
   const unsigned short* B = reinterpret_cast<const unsigned short*>(Bp);
+  if (K % 4 == 0 && (lda & 3) == 0 && M >= 1024 && N >= 384) {
+    // large-tile kernel (sv2n_gemm_bw.h): 256 x 192 tiles of 8 waves (round 4;
+    // the 128 x 128 k_gemm_bf16nt below was L2-bound on the C3 projection)
+    using Cfg = GemmBWCfg<256, 192, false, true, false>;
+    static bool attr_bw = [] {
+      (void)hipFuncSetAttribute((const void*)k_gemm_bw<256, 192, false, true, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
+      return true;
+    }();
+    (void)attr_bw;
+    const int nm = (int)((M + 255) / 256), nn = (int)((N + 191) / 192);
+    hipLaunchKernelGGL((k_gemm_bw<256, 192, false, true, false>),
+                       dim3((unsigned)(((nm + 7) / 8) * 8 * nn)), dim3(Cfg::THREADS), Cfg::LDS,
+                       stream, (const void*)A, lda, (const void*)B, Kp, C, ldc, M, N, K,
+                       (int64_t)K, nm, nn);
+    return (int)hipGetLastError();
+  }
   if (K % 4 == 0) {  // k_gemm_bf16nt (sv2n_gemm_bf16.h)
     static bool attr = [] {
       (void)hipFuncSetAttribute((const void*)k_gemm_bf16nt,

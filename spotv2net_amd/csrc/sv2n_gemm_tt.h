@@ -393,11 +393,15 @@ struct GemmTT3YCfg {
   static_assert(16 * MT * W::BK / 4 % 64 == 0, "wave A staging tiles the lanes");
 };
 
-template <int NT, int MT>
+// BPL = true: B arrives pre-split as three bf16 planes [3][K][ldb] (plane
+// stride bplane elements; the producer, the layer's attention backward,
+// splits every element once), so only A is split here.
+template <int NT, int MT, bool BPL = false>
 __global__ __launch_bounds__(512) void k_gemm_tt3y(const float* __restrict__ A, int64_t lda,
                                                    const float* __restrict__ B, int64_t ldb,
                                                    float* __restrict__ part, int64_t M, int64_t N,
-                                                   int64_t K, int64_t kslice, int nz) {
+                                                   int64_t K, int64_t kslice, int nz,
+                                                   int64_t bplane = 0) {
   using Cfg = GemmTT3WCfg<NT, MT>;
   constexpr int BK = Cfg::BK, BN = Cfg::BN, SA = Cfg::SA, SB = Cfg::SB;
   constexpr int PA = Cfg::PA, PB = Cfg::PB, BV = Cfg::BV, BVN = Cfg::BVN;
@@ -422,10 +426,12 @@ __global__ __launch_bounds__(512) void k_gemm_tt3y(const float* __restrict__ A, 
   const int64_t kbeg = (int64_t)bz * kslice, kend = min(K, kbeg + kslice);
   float* C = part + (int64_t)bz * M * N;
   const rsrc_t ra = make_rsrc(A, (uint32_t)min<int64_t>(K * lda * 4, 0x7fffffff));
-  const rsrc_t rb = make_rsrc(B, (uint32_t)min<int64_t>(K * ldb * 4, 0x7fffffff));
+  const rsrc_t rb = make_rsrc(B, (uint32_t)min<int64_t>(BPL ? 3 * bplane * 2 : K * ldb * 4,
+                                                       0x7fffffff));
   const int wrow = WR * wave;  // first A row (in the block) of this wave
 
-  f32x4 va[AVW], vb[BV];
+  f32x4 va[AVW], vb[BPL ? 1 : BV];
+  u32x2 vp[BPL ? BV : 1][3];
   auto load_a = [&](int64_t k0) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < AVW; ++s) {
@@ -441,7 +447,14 @@ __global__ __launch_bounds__(512) void k_gemm_tt3y(const float* __restrict__ A, 
       const int idx = min(t + 512 * s, BVN - 1);
       const int r = idx / (BN / 4), c4 = idx - r * (BN / 4);
       const int64_t k = k0 + r, n = n0 + 4 * c4;
-      vb[s] = bld4(rb, (k < kend && n < N) ? (int)((k * ldb + n) * 4) : OOB);
+      if constexpr (BPL) {
+        const int off = (k < kend && n < N) ? (int)((k * ldb + n) * 2) : OOB;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          vp[s][p] = bld2_u32(rb, off == OOB ? OOB : off + (int)(p * bplane * 2));
+      } else {
+        vb[s] = bld4(rb, (k < kend && n < N) ? (int)((k * ldb + n) * 4) : OOB);
+      }
     }
   };
   auto put = [&](unsigned short* dst, int plane, int stride, int r, int c, const f32x4& v)
@@ -462,7 +475,13 @@ __global__ __launch_bounds__(512) void k_gemm_tt3y(const float* __restrict__ A, 
     } else {
       const int idx = min(t + 512 * (i - AVW), BVN - 1);
       const int r = idx / (BN / 4), c4 = idx - r * (BN / 4);
-      put(sb, PB, SB, r, 4 * c4, vb[i - AVW]);
+      if constexpr (BPL) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          *reinterpret_cast<u32x2*>(sb + p * PB + r * SB + 4 * c4) = vp[i - AVW][p];
+      } else {
+        put(sb, PB, SB, r, 4 * c4, vb[i - AVW]);
+      }
     }
   };
 

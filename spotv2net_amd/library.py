@@ -69,6 +69,11 @@ _SCHEMAS = {
                  "Tensor(b!)? g_att_src, Tensor(c!)? g_att_dst, Tensor(d!)? g_bias) -> ()",
     "edge_logits_bwd": "(Tensor edge_attr, Tensor? edge_index, Tensor canon, Tensor[] dae, "
                        "int heads, int num_graphs, int n, int hl_pad, bool planes) -> Tensor",
+    "gat_attn_bwd_edge": "(Tensor dy, Tensor y, Tensor xs, Tensor psave, Tensor? keep, "
+                         "float keep_scale, Tensor edge_attr, Tensor?[] dae, int layer, "
+                         "int hl_pad, int num_graphs, int n, int heads, int channels, "
+                         "bool concat, int act, float slope, Tensor? post_u=None, "
+                         "float post_p=0.0) -> (Tensor, Tensor, Tensor)",
     "prep_bwd_edge": "(Tensor dwfold, int col0, Tensor W_edge, Tensor att_edge, int heads, "
                      "int channels, Tensor(a!)? gW_edge, Tensor(b!)? g_att_edge) -> ()",
     "prep_bwd_edge_all": "(Tensor dwfold, int[] col0, Tensor[] W_edge, Tensor[] att_edge, "
@@ -559,6 +564,62 @@ def _gat_attn_bwd_fake(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num
     return (torch.empty_like(xs),
             xs.new_empty(_dae_shape(edge_order, num_graphs, n, heads) if with_ae else (0,)),
             xs.new_empty((num_graphs, _oc(heads, channels, concat))))
+
+
+def attn_bwd_edge_supported(num_graphs: int, n: int, heads: int, channels: int, edge_dim: int,
+                            hl_pad: int) -> bool:
+    """Whether sv2n_gat_attn_bwd_edge runs this shape (include/sv2n.h)."""
+    return bool(_lib.load().sv2n_gat_attn_bwd_edge_supported(num_graphs, n, heads, channels,
+                                                             edge_dim, hl_pad))
+
+
+@_impl("gat_attn_bwd_edge")
+def _gat_attn_bwd_edge(dy, y, xs, psave, keep, keep_scale, edge_attr, dae, layer, hl_pad,
+                       num_graphs, n, heads, channels, concat, act, slope, post_u=None,
+                       post_p=0.0):
+    """gat_attn_bwd of canonical complete graphs with the edge-logit weight
+    gradient of every layer fused in (sv2n_gat_attn_bwd_edge, then the
+    graph-order sum sv2n_edge_partials_reduce): returns dxs, the bias partials
+    and the [edge_dim][hl_pad] gradient edge_logits_bwd would return."""
+    lib = _lib.load()
+    _f32(dy, y, xs, psave, post_u, edge_attr)
+    N, OC = num_graphs * n, _oc(heads, channels, concat)
+    E0 = n * (n - 1)
+    _rows(xs, N, heads * channels + 2 * heads, "xs")
+    _dense(dy, y, psave, keep, post_u, edge_attr, *[d for d in dae if d is not None])
+    _need(dy.numel() == N * OC and y.numel() == N * OC, "dy / y shape")
+    _need(post_u is None or (post_u.numel() == N * OC and 0.0 <= post_p < 1.0), "post_u / post_p")
+    _need(psave.numel() == num_graphs * heads * 1024, "psave shape")
+    _need(keep is None or keep.numel() == num_graphs * heads * 1024, "keep shape")
+    _need(edge_attr.dim() == 2 and edge_attr.shape[0] == num_graphs * E0, "edge_attr rows")
+    L = len(dae)
+    _need(0 <= layer < L and all((d is None) == (k == layer) for k, d in enumerate(dae)),
+          "dae: one tensor per other layer, None for this one")
+    _need(all(d.numel() == num_graphs * E0 * heads for d in dae if d is not None), "dae shape")
+    D = edge_attr.shape[1]
+    dev = xs.device
+    dxs = torch.empty_like(xs)
+    dbp = torch.empty(num_graphs, OC, device=dev)
+    part = torch.empty(num_graphs, D * hl_pad, device=dev)
+    dwf = torch.empty(D, hl_pad, device=dev)
+    ptrs = _lib.ptr_array([0 if d is None else d.data_ptr() for d in dae])
+    st = _st(xs)
+    _lib.check(lib.sv2n_gat_attn_bwd_edge(
+        dy.data_ptr(), y.data_ptr(), xs.data_ptr(), xs.stride(0), psave.data_ptr(), _p(keep),
+        keep_scale, _p(post_u), post_p, dxs.data_ptr(), dbp.data_ptr(), edge_attr.data_ptr(), D,
+        ptrs, L, layer, hl_pad, part.data_ptr(), num_graphs, n, heads, channels, int(concat), act,
+        slope, st), "sv2n_gat_attn_bwd_edge")
+    _lib.check(lib.sv2n_edge_partials_reduce(part.data_ptr(), num_graphs, D * hl_pad,
+                                             dwf.data_ptr(), st), "sv2n_edge_partials_reduce")
+    return dxs, dbp, dwf
+
+
+@_fake("gat_attn_bwd_edge")
+def _gat_attn_bwd_edge_fake(dy, y, xs, psave, keep, keep_scale, edge_attr, dae, layer, hl_pad,
+                            num_graphs, n, heads, channels, concat, act, slope, post_u=None,
+                            post_p=0.0):
+    return (torch.empty_like(xs), xs.new_empty((num_graphs, _oc(heads, channels, concat))),
+            xs.new_empty((edge_attr.shape[1], hl_pad)))
 
 
 @_impl("gat_attn_tiled_bwd")

@@ -10,10 +10,11 @@ keys, so reference checkpoints load and 5_train_SpotV2Net.py runs unchanged.
 The GAT layers run as ONE fused autograd node (``stack.gat_stack``):
 * one edge pass computes the folded edge logits of EVERY layer
   (edge_attr is the same tensor for all layers, utils/models.py:145-146);
-* per layer: projection GEMM (f32 MFMA) -> fused attention kernel with the
-  model's activation in its epilogue, then the inter-layer dropout
-  (utils/models.py:147-148); the final ``nn.Linear`` (:150) keeps its module
-  and parameters but runs on the sv2n head kernels.
+* per layer: projection GEMM (f32-accurate "bf16x3" split on bf16 MFMA, or
+  one bf16 product per pair in bf16 mode) -> fused attention kernel with the
+  model's activation and the inter-layer dropout (utils/models.py:147-148) in
+  its epilogue; the final ``nn.Linear`` (:150) keeps its module and
+  parameters but runs on the sv2n head kernels.
 Documented deviation: an unknown activation raises ValueError instead of
 printing and calling ``sys.exit()`` (utils/models.py:131-133).
 """

@@ -153,7 +153,8 @@ def _hp(L: int, H: int) -> int:
 # "auto" (the rule in _use_fused), "on" (whenever the kernels take the shape) or
 # "off" (always edge pass + planes): an A/B switch for tests and measurements
 EDGE_FUSED = os.environ.get("SV2N_EDGE_FUSED", "auto")
-LAST_PATH = {"attention": None}  # which attention path the last forward took (tests)
+LAST_PATH = {"attention": None,   # which attention path the last forward took (tests)
+             "edge_tail": None}   # whether the last backward fused the edge gradient
 
 
 def _overlap_edge(training: bool) -> bool:
@@ -194,6 +195,25 @@ def _use_fused(layout: GraphLayout, convs, D: int, num_edges: int) -> bool:
 
 def _opt(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return None if t is None or t.numel() == 0 else t
+
+
+# A/B switch for tests and measurements: "auto" (fuse where the kernel takes
+# the shape) or "off" (always the separate edge-gradient pass)
+EDGE_TAIL = os.environ.get("SV2N_EDGE_TAIL", "auto")
+
+
+def _edge_tail_ok(layout: GraphLayout, convs, ea, hp: int) -> bool:
+    """Layer 0's n <= 32 attention backward can carry the edge gradient of
+    every layer (sv2n_gat_attn_bwd_edge_supported; equal head counts, the
+    other layers' d-logits in edge order)."""
+    if EDGE_TAIL == "off" or layout.kind == "block" or ea.dim() != 2:
+        return False
+    H = convs[0].heads
+    if any(c.heads != H for c in convs) or len(convs) * H > hp:
+        return False
+    from .library import attn_bwd_edge_supported
+    return attn_bwd_edge_supported(layout.num_graphs, layout.n, H, convs[0].out_channels,
+                                   ea.size(1), hp) and ea.data_ptr() % 16 == 0
 
 
 class _StackMeta:
@@ -370,6 +390,14 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
     daes = [None] * L
     dwf = torch.zeros_like(wf) if fused else None  # every layer writes its own columns
     act_l = act  # the activation backward left to layer l's attention backward
+    # canonical complete graphs: layer 0's attention backward also computes the
+    # edge-logit weight gradient of every layer (sv2n_gat_attn_bwd_edge), so
+    # edge_attr is streamed there and no separate edge-gradient pass runs
+    need_edge = use_edge and ea is not None and ea.size(0) > 0 and any(
+        grad_of(c.lin_edge.weight) is not None or grad_of(c.att_edge) is not None for c in convs)
+    edge_tail = bool(need_edge and not fused and not layout.tiled and eo and
+                     _edge_tail_ok(layout, convs, ea, hp))
+    LAST_PATH["edge_tail"] = edge_tail
     for l in range(L - 1, -1, -1):
         c = convs[l]
         Hc, C = c.heads, c.out_channels
@@ -387,6 +415,12 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
                 dy, ys[l], xs, pss[l], layout.num_edges, layout.eid, keeps[l],
                 meta.kscales[l], layout.rowmask, B, n, Hc, C, c.concat, act,
                 float(c.negative_slope))
+        elif edge_tail and l == 0:
+            dxs, dbp, dwf = ops.gat_attn_bwd_edge(
+                dy, ys[l], xs, pss[l], keeps[l], meta.kscales[l], ea,
+                [None] + [_opt(d) for d in daes[1:]], 0, hp, B, n, Hc, C, c.concat, act_l,
+                float(c.negative_slope), post_u, meta.post_p[l] or 0.0)
+            dae = None
         else:
             dxs, dae, dbp = ops.gat_attn_bwd(
                 dy, ys[l], xs, pss[l], keeps[l], meta.kscales[l], layout.rowmask, use_edge,
@@ -418,7 +452,7 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
         need_e = [(grad_of(c.lin_edge.weight), grad_of(c.att_edge)) for c in convs]
         if ea.size(0) > 0 and any(a is not None or b is not None for a, b in need_e):
             ei = layout.edge_index if layout.kind == "block" else None
-            if not fused:
+            if not fused and not edge_tail:
                 dwf = ops.edge_logits_bwd(ea, ei, layout.canon, daes, H, B, n, hp,
                                           layout.tiled)
             if all(a is not None and b is not None for a, b in need_e):

@@ -26,7 +26,8 @@ def _rel_to_abs_sum(got, a, b):
     return ((got.double() - ref).abs() / absum.clamp_min(1e-30)).max().item()
 
 
-@pytest.mark.parametrize("M,N,K", [(3840, 3012, 1260), (15360, 408, 1260), (97, 37, 72)])
+@pytest.mark.parametrize("M,N,K", [(3840, 3012, 1260), (15360, 408, 1260), (97, 37, 72),
+                                   (1100, 389, 332)])
 def test_gemm_bf16_is_exact_bf16_products(dev, M, N, K):
     from spotv2net_amd import _lib
     from spotv2net_amd.ops import weight_planes
@@ -55,7 +56,7 @@ def test_project_planes_bf16_unaligned_rows(dev):
 
 
 @pytest.mark.parametrize("F,H,C,nodes", [(1260, 6, 500, 3840), (1260, 4, 100, 15360),
-                                         (72, 3, 21, 300), (70, 3, 21, 300)])
+                                         (72, 3, 21, 300), (70, 3, 21, 300), (332, 5, 77, 1010)])
 def test_wgrad_bf16_equals_f32_on_rounded_operands(dev, F, H, C, nodes):
     """sv2n_gat_wgrad_node_bf16 == sv2n_gat_wgrad_node (exact f32) fed the
     bf16-rounded x and dxs: the bf16 GEMM's products are exact, so only the

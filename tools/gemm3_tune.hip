@@ -96,7 +96,8 @@ void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short
   using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
   const size_t lds = Cfg::LDS;
   if (lds > 160 * 1024) return;
-  auto kern = DV ? k_gemm3d<NW, MT, NT, AP> : CV ? k_gemm3c<NW, MT, NT, BK, AP, ABL, PD> : k_gemm3b<NW, MT, NT, BK, AP>;
+  static_assert(DV, "k_gemm3d only (the product's projection kernel)");
+  auto kern = k_gemm3d<NW, MT, NT, AP, false>;
   if (lds > 65536)
     CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   const int nm = (int)((sh.M + Cfg::BM - 1) / Cfg::BM), nn = (int)((sh.N + Cfg::BN - 1) / Cfg::BN);
@@ -104,7 +105,7 @@ void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short
   CK(hipMemset(C, 0, sizeof(float) * sh.M * sh.N));
   auto f = [&]() {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(Cfg::THREADS), lds, st, A, sh.K, Bp, Kp, sh.N * Kp,
-                       C, sh.N, sh.M, sh.N, sh.K, nm, nn);
+                       C, sh.N, sh.M, sh.N, sh.K, nm, nn, (const float*)nullptr, (int64_t)0);
   };
   f();
   CK(hipGetLastError());
@@ -203,15 +204,14 @@ int main() {
       printf("  f32 MFMA NT13     %8.1f us %7.1f TF          max|err| %.2e  max err/Σ|ab| %.2e\n", us,
              2.0 * M * N * K / us / 1e6, maxabs, maxrel);
     }
-    run3<8, 1, 13, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3<8, 1, 7, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3<8, 1, 9, 64, 1>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 13, 32, 3, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 7, 64, 2, true>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<8, 1, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<8, 1, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<8, 2, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<8, 1, 9, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    // round 4: three A register sets; four waves of two row tiles (one wave per SIMD)
+    run3b<8, 1, 13, 32, 3, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<4, 2, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<4, 2, 13, 32, 3, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(S)); CK(hipFree(Bp));
   }
   return 0;
