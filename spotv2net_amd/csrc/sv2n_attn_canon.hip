@@ -863,14 +863,16 @@ static int canon_fwd_splits(int64_t B, int H, int C, bool concat) {
 struct CanonBwdPlan {
   int S, HS, WPH;
 };
-static CanonBwdPlan canon_bwd_plan(int64_t B, int H, int C) {
+// single: the fewest splits (the edge-gradient tail needs a whole graph per
+// workgroup, whatever B)
+static CanonBwdPlan canon_bwd_plan(int64_t B, int H, int C, bool single = false) {
   const int nch = (C + 31) >> 5;
   int S = 1;
   for (int s = 1; s <= H; ++s) {
     const int hs = (H + s - 1) / s;
     if (hs > 4 || (H + hs - 1) / hs != s) continue;  // one head per wave; no empty split
     S = s;
-    if (B * s >= CANON_FILL) break;
+    if (single || B * s >= CANON_FILL) break;
   }
   const int HS = (H + S - 1) / S;
   const int WPH = max(1, min(4 / HS, nch));
@@ -894,7 +896,7 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
                              const uint32_t* rowmask, float* dxs, float* dae,
                              int ae_edge_order, float* dbias, int n, int H, int C, float slope,
                              const EdgeTail& et) {
-  const CanonBwdPlan pl = canon_bwd_plan(B, H, C);
+  const CanonBwdPlan pl = canon_bwd_plan(B, H, C, et.ea != nullptr);
   const size_t lds = attn_canon_bwd_lds(pl.HS);
   const unsigned grid = canon_grid(B, pl.S);
   // two chunks in flight per wave when every workgroup is resident at 2 waves
@@ -926,7 +928,7 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
 // graphs, all heads in one workgroup, hl_pad <= 8 columns, even D <= 128 with
 // 8-B aligned rows; the d-logit table and the moved tail fit the LDS).
 bool attn_canon_edge_tail_ok(int64_t B, int n, int H, int C, int D, int hlp) {
-  const CanonBwdPlan pl = canon_bwd_plan(B, H, C);
+  const CanonBwdPlan pl = canon_bwd_plan(B, H, C, true);
   if (pl.S != 1 || n < 2 || n > 32 || hlp > ET_COLS || hlp < H || D < 1 || D > 128 ||
       (D & 1))
     return false;

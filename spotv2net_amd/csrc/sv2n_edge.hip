@@ -567,6 +567,204 @@ __global__ __launch_bounds__(256) void k_edge_bwd_mfma(const float* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// Canonical batches with wide edge rows (C2 / C3: D = 126), round 4: both
+// passes as HBM streams whose inner products run on v_mfma_f32_16x16x4_f32
+// (exact f32 products, f32 accumulation), so LDS carries each edge row at
+// most once (the kernels above re-read every staged value 8-16 times from
+// LDS: thread tiles of 4 d x 4 columns, W̃ broadcasts).  A wave owns tiles
+// of MX_TE = 16 consecutive edges (grid-stride over tiles, adjacent waves on
+// adjacent tiles); the next tile's loads are in flight while one is computed.
+//
+// forward:  logits[e][k] = Σ_d ea[e][d]·W̃[d][k]   (M = 16 edges, N = 16 >= HL
+//   columns, K = d).  The MFMA A operand puts 16 rows on 4 lanes each, so the
+//   tile (16·D contiguous floats) is loaded flat instead (dwordx2, 512
+//   contiguous bytes per instruction; D even, so no float2 straddles a row)
+//   into the wave's [17][132] LDS image (row 16 takes the lanes past the
+//   tile; row i starts at bank 4i, so a half-wave's 32 b64 reads hit 64
+//   distinct banks) and read back with ds_read_b64: MFMA (s, c) pairs lane
+//   group g with d = 8s + 2g + c.  W̃ lives in 2·NS registers per lane.
+// backward: partial[d][k] = Σ_e ea[e][d]·dAE[e][k]   (M = d, N = columns,
+//   K = edges).  K step q takes edges 4g + q of the tile; M tile m holds
+//   d = 32·(m/2) + 2i + (m&1), so lane (i, g) loads the A operands of M tiles
+//   m, m + 1 as one float2 straight from HBM: an instruction reads 4 rows x
+//   128 contiguous bytes, no LDS image at all.  dAE comes from the layers'
+//   [E][H] buffers (4 dwords per lane per tile).  The wave accumulators are
+//   summed in wave order through LDS into one [D][hl_pad] partial per
+//   workgroup (k_reduce_partials finishes).
+// ---------------------------------------------------------------------------
+constexpr int MX_TE = 16, MX_PF = 132, MX_WAVES = 4;
+// backward: tiles in flight per wave.  Round 4 A/B (C2 traced step, one box):
+// 1 tile (95 VGPRs, 5 waves / SIMD) 52.0 us, 2 tiles (150 VGPRs, 3 waves /
+// SIMD) 53.4 us; the round-3 LDS-tile kernel took 56.7 us in the same place.
+constexpr int MX_DEPTH = 1;
+
+// per lane: this column's output / input row pointer (column li = l·H + h)
+template <typename T, typename P>
+__device__ __forceinline__ T* mx_col_ptr(const P& lp, int li, int L, int H) {
+  T* r = nullptr;
+#pragma unroll
+  for (int l = 0; l < SV2N_MAX_LAYERS; ++l)
+    if (l < L && li >= l * H && li < (l + 1) * H) r = lp.p[l] + (li - l * H);
+  return r;
+}
+
+// the tile's rows as a buffer (nothing past E or past the last tile)
+__device__ __forceinline__ rsrc_t mx_tile_rsrc(const float* ea, int64_t t, int64_t ntiles,
+                                               int64_t E, int D) {
+  const int64_t e0 = t * MX_TE;
+  const int64_t rows = t < ntiles ? min((int64_t)MX_TE, E - e0) : 0;
+  return make_rsrc(ea + (t < ntiles ? e0 * D : 0), (uint32_t)(rows * D * 4));
+}
+
+template <int NS>
+__global__ __launch_bounds__(256, 4) void k_edge_fwd_mx(const float* __restrict__ ea, int64_t E,
+                                                        int D, const float* __restrict__ wf,
+                                                        int hlp, LayerPtrs ae, int L, int H) {
+  __shared__ __attribute__((aligned(16))) float s_img[MX_WAVES][(MX_TE + 1) * MX_PF];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int HL = L * H;
+  float* img = s_img[wave];
+  // columns D .. 8·NS of the 16 rows are read as operands: zero them once
+  for (int k = lane; k < MX_TE * (8 * NS - D); k += 64) {
+    const int r = k / (8 * NS - D);
+    img[r * MX_PF + D + (k - r * (8 * NS - D))] = 0.f;
+  }
+  float wb[NS][2];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int d = 8 * s + 2 * g + c;
+      wb[s][c] = (d < D && li < HL) ? wf[d * hlp + li] : 0.f;
+    }
+  float* outp = li < HL ? mx_col_ptr<float>(ae, li, L, H) : nullptr;
+  // flat piece j of a tile: floats f = 128j + 2·lane -> tile byte offset, image offset
+  int goff[NS], loff[NS];
+  const int nf = MX_TE * D;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int f = 128 * j + 2 * lane;
+    const int r = f / D;
+    goff[j] = f < nf ? 4 * f : OOB;
+    loff[j] = f < nf ? r * MX_PF + (f - r * D) : MX_TE * MX_PF + 2 * (lane & 31);
+  }
+  const int64_t ntiles = (E + MX_TE - 1) / MX_TE;
+  const int64_t stride = (int64_t)gridDim.x * MX_WAVES;
+  int64_t tile = (int64_t)blockIdx.x * MX_WAVES + wave;
+  u32x2 v[NS];
+  {
+    const rsrc_t r = mx_tile_rsrc(ea, tile, ntiles, E, D);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) v[j] = bld2_u32(r, goff[j]);
+  }
+  for (; tile < ntiles; tile += stride) {
+#pragma unroll
+    for (int j = 0; j < NS; ++j) *reinterpret_cast<u32x2*>(img + loff[j]) = v[j];
+    {
+      const rsrc_t r = mx_tile_rsrc(ea, tile + stride, ntiles, E, D);  // next tile in flight
+#pragma unroll
+      for (int j = 0; j < NS; ++j) v[j] = bld2_u32(r, goff[j]);
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const float2 a = *reinterpret_cast<const float2*>(img + li * MX_PF + 8 * s + 2 * g);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wb[s][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wb[s][1], acc, 0, 0, 0);
+    }
+    if (outp) {
+      const int64_t e0 = tile * MX_TE + 4 * g;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (e0 + r < E) outp[(e0 + r) * H] = acc[r];
+    }
+  }
+}
+
+// DEPTH tiles in flight per wave (register sets used in rotation)
+template <int NS, int DEPTH>
+__global__ __launch_bounds__(256, 4) void k_edge_bwd_mx(const float* __restrict__ ea,
+                                                                  int64_t E, int D,
+                                                                  LayerCPtrs dae, int L, int H,
+                                                                  int hlp,
+                                                                  float* __restrict__ partial) {
+  constexpr int NM = NS / 2, NP = NM / 2;  // M tiles of 16 d; float2 pieces per row
+  __shared__ __attribute__((aligned(16))) float s_red[MX_WAVES * 8 * NS * 16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int HL = L * H;
+  const float* inp = li < HL ? mx_col_ptr<const float>(dae, li, L, H) : nullptr;
+  const int64_t ntiles = (E + MX_TE - 1) / MX_TE;
+  const int64_t stride = (int64_t)gridDim.x * MX_WAVES;
+  f32x4 acc[NM];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x2 v[DEPTH][4][NP];
+  float b[DEPTH][4];
+  // lane (li, g): row 4g + q, columns 32·mm + 2li (+1); the row / column step
+  // goes in the wave-uniform soffset, the last piece past D reads nothing
+  const int vo = ((4 * g) * D + 2 * li) * 4;
+  const int vo_last = 32 * (NP - 1) + 2 * li < D ? vo : OOB;
+  auto load = [&](u32x2 (&w)[4][NP], float (&bb)[4], int64_t t) __attribute__((always_inline)) {
+    const rsrc_t r = mx_tile_rsrc(ea, t, ntiles, E, D);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int mm = 0; mm < NP; ++mm)
+        w[q][mm] = __builtin_amdgcn_raw_buffer_load_b64(r, mm == NP - 1 ? vo_last : vo,
+                                                        (q * D + 32 * mm) * 4, 0);
+    // this lane's column for edges 4g + q of the tile (0 past E / past HL;
+    // per-lane pointers, so plain masked global loads, not a descriptor)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t e = t * MX_TE + 4 * g + q;
+      bb[q] = (inp && e < E) ? inp[e * H] : 0.f;
+    }
+  };
+  int64_t tile = (int64_t)blockIdx.x * MX_WAVES + wave;
+#pragma unroll
+  for (int k = 0; k < DEPTH; ++k) load(v[k], b[k], tile + k * stride);
+  for (; tile < ntiles; tile += DEPTH * stride) {
+#pragma unroll
+    for (int k = 0; k < DEPTH; ++k) {
+      const int64_t t = tile + k * stride;
+      if (t >= ntiles) break;  // wave-uniform
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int mm = 0; mm < NP; ++mm) {
+          acc[2 * mm] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(v[k][q][mm][0]),
+                                                              b[k][q], acc[2 * mm], 0, 0, 0);
+          acc[2 * mm + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              __uint_as_float(v[k][q][mm][1]), b[k][q], acc[2 * mm + 1], 0, 0, 0);
+        }
+      load(v[k], b[k], t + DEPTH * stride);  // the tile DEPTH ahead (or nothing)
+    }
+  }
+  // wave partials -> LDS [wave][8NS][16], summed in wave order
+#pragma unroll
+  for (int m = 0; m < NM; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int d = 32 * (m >> 1) + 2 * (4 * g + r) + (m & 1);
+      s_red[(wave * 8 * NS + d) * 16 + li] = acc[m][r];
+    }
+  __syncthreads();
+  float* pb = partial + (int64_t)blockIdx.x * D * hlp;
+  for (int o = threadIdx.x; o < D * hlp; o += 256) {
+    const int d = o / hlp, k = o - d * hlp;
+    float sm = 0.f;
+    if (k < 16) {
+      sm = s_red[d * 16 + k];
+#pragma unroll
+      for (int w = 1; w < MX_WAVES; ++w) sm += s_red[(w * 8 * NS + d) * 16 + k];
+    }
+    pb[o] = sm;
+  }
+}
+
 // eid[t*n + j] = e for every non-self edge s->t, j = s - g*n (caller fills -1)
 __global__ void k_block_eid(const int64_t* __restrict__ ei, int64_t E, int64_t N, int n,
                             int32_t* __restrict__ eid) {
@@ -590,6 +788,16 @@ static constexpr int EDGE_FWD_GRID = 1024;
 // backward within noise of these; the backward's bounds its workspace)
 static constexpr int EDGE_SMALL_FWD_GRID = 4096;
 static constexpr int EDGE_SMALL_BWD_GRID = 1024;
+// MFMA streaming kernels (k_edge_fwd_mx / k_edge_bwd_mx): 4 workgroups of 4
+// waves per CU (~36 KB LDS each)
+static constexpr int EDGE_MX_GRID = 1024;
+
+// canonical edge order (no edge_index, no planes), even D up to 128 (float2
+// pieces never straddle a row), at most 16 logit columns (one MFMA N tile)
+static bool edge_mx_ok(bool planes, const int64_t* edge_index, int edge_dim, int hl) {
+  return !planes && !edge_index && edge_dim > EDGE_SMALL_D && (edge_dim & 1) == 0 &&
+         edge_dim <= 128 && hl <= 16;
+}
 
 #define SV2N_SMALL_DISPATCH(KERNEL, GRID, ...)                                              \
   {                                                                                         \
@@ -702,6 +910,21 @@ static int edge_fwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
                   : edge_fwd_small<false>(edge_attr, num_edges, edge_dim, edge_index, canon, E0,
                                           wfold, hl_pad, lp, num_layers, heads, num_graphs, n,
                                           stream);
+  if (edge_mx_ok(planes, edge_index, edge_dim, num_layers * heads)) {
+    const int64_t waves = (num_edges + MX_TE - 1) / MX_TE;
+    const dim3 grid((unsigned)std::min<int64_t>((waves + MX_WAVES - 1) / MX_WAVES, EDGE_MX_GRID));
+#define SV2N_MXF(NS)                                                                          \
+  hipLaunchKernelGGL((k_edge_fwd_mx<NS>), grid, dim3(256), 0, stream, edge_attr, num_edges,    \
+                     edge_dim, wfold, hl_pad, lp, num_layers, heads);
+    switch ((edge_dim + 31) / 32) {
+      case 1: SV2N_MXF(4) break;
+      case 2: SV2N_MXF(8) break;
+      case 3: SV2N_MXF(12) break;
+      default: SV2N_MXF(16) break;
+    }
+#undef SV2N_MXF
+    return (int)hipGetLastError();
+  }
   const int64_t nchunks = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
   constexpr int fwd_grid = EDGE_FWD_GRID;
   const unsigned grid = (unsigned)std::min<int64_t>(nchunks, fwd_grid);
@@ -745,8 +968,9 @@ static int edge_fwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
 }
 
 extern "C" int64_t sv2n_edge_logits_bwd_workspace(int edge_dim, int hl_pad) {
-  return (int64_t)(edge_dim <= EDGE_SMALL_D ? EDGE_SMALL_BWD_GRID : EDGE_BWD_GRID) * edge_dim *
-         hl_pad;
+  return (int64_t)std::max(EDGE_MX_GRID, edge_dim <= EDGE_SMALL_D ? EDGE_SMALL_BWD_GRID
+                                                                    : EDGE_BWD_GRID) *
+         edge_dim * hl_pad;
 }
 
 static int edge_bwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim,
@@ -778,6 +1002,20 @@ static int edge_bwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
                   : edge_bwd_small<false>(edge_attr, num_edges, edge_dim, edge_index, canon, E0,
                                           lp, num_layers, heads, num_graphs, n, workspace,
                                           workspace_floats, dwfold, hl_pad, stream);
+  if (num_edges > 0 && edge_mx_ok(planes, edge_index, edge_dim, num_layers * heads)) {
+    const int64_t waves = (num_edges + MX_TE - 1) / MX_TE;
+    const int grid = (int)std::min<int64_t>((waves + MX_WAVES - 1) / MX_WAVES, EDGE_MX_GRID);
+    if (workspace_floats < (int64_t)grid * O) return SV2N_ERR_WORKSPACE;
+    switch ((edge_dim + 31) / 32) {
+      case 1: hipLaunchKernelGGL((k_edge_bwd_mx<4, MX_DEPTH>), dim3(grid), dim3(256), 0, stream, edge_attr, num_edges, edge_dim, lp, num_layers, heads, hl_pad, workspace); break;
+      case 2: hipLaunchKernelGGL((k_edge_bwd_mx<8, MX_DEPTH>), dim3(grid), dim3(256), 0, stream, edge_attr, num_edges, edge_dim, lp, num_layers, heads, hl_pad, workspace); break;
+      case 3: hipLaunchKernelGGL((k_edge_bwd_mx<12, MX_DEPTH>), dim3(grid), dim3(256), 0, stream, edge_attr, num_edges, edge_dim, lp, num_layers, heads, hl_pad, workspace); break;
+      default: hipLaunchKernelGGL((k_edge_bwd_mx<16, MX_DEPTH>), dim3(grid), dim3(256), 0, stream, edge_attr, num_edges, edge_dim, lp, num_layers, heads, hl_pad, workspace); break;
+    }
+    hipLaunchKernelGGL(k_reduce_partials, dim3((O + 15) / 16), dim3(256), 0, stream, workspace,
+                       grid, O, dwfold);
+    return (int)hipGetLastError();
+  }
   const int64_t nchunks = (num_edges + EDGE_CHUNK - 1) / EDGE_CHUNK;
   constexpr int bwd_grid = EDGE_BWD_GRID;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(bwd_grid, nchunks));

@@ -588,9 +588,11 @@ static void launch_wgrad_bf16(const GemmPlan& p, hipStream_t st, const float* x,
 
 // the same product transposed, dWaug = dxsᵀ·x [ldx][F] (operands swapped):
 // the epilogue (k_wgrad_epi_t) then works along rows of gW.  Round 4: the
-// large-tile kernel k_gemm_bw<256, 128, TN> (sv2n_gemm_bw.h; 256 x 128 tiles,
-// K slices of multiples of 64 aiming at one round of ~240 workgroups)
-constexpr int BWT_BM = 256, BWT_BN = 128;
+// large-tile kernel k_gemm_bw<128, 256, TN> (sv2n_gemm_bw.h; K slices of
+// multiples of 64 aiming at one round of ~240 workgroups).  C3 shape (M 3012,
+// N 1260, K 3840, tools/gemm_bw_tune.hip): 128 x 256 split 2 68.3 us, the
+// round-3 k_gemm_tt<128, 128, 1> 75.1, 256 x 128 117.6, 256 x 192 247.7
+constexpr int BWT_BM = 128, BWT_BN = 256;
 static GemmPlan plan_wgrad_bw(int64_t ldx, int64_t F, int64_t K) {
   GemmPlan p{};
   const int64_t tiles = ((ldx + BWT_BM - 1) / BWT_BM) * ((F + BWT_BN - 1) / BWT_BN);

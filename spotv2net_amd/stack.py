@@ -197,16 +197,21 @@ def _opt(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return None if t is None or t.numel() == 0 else t
 
 
-# A/B switch for tests and measurements: "auto" (fuse where the kernel takes
-# the shape) or "off" (always the separate edge-gradient pass)
-EDGE_TAIL = os.environ.get("SV2N_EDGE_TAIL", "auto")
+# "on": layer 0's attention backward also computes the edge-logit weight
+# gradient wherever the kernel takes the shape; "off" (default): the separate
+# MFMA edge-gradient pass.  Round 4, C2 traced step on one MI355X: the fused
+# tail made layer 0's backward 28 -> 78-80 us against 52 + 5.7 us for the
+# separate pass and its reduce, but the next step's edge forward then misses
+# the Infinity Cache (43 -> 48 us): step span 543.0 (on) vs 530.6-539.3 us
+# (off, `profiles/r04_c2_edge_ab.txt`).
+EDGE_TAIL = os.environ.get("SV2N_EDGE_TAIL", "off")
 
 
 def _edge_tail_ok(layout: GraphLayout, convs, ea, hp: int) -> bool:
     """Layer 0's n <= 32 attention backward can carry the edge gradient of
     every layer (sv2n_gat_attn_bwd_edge_supported; equal head counts, the
     other layers' d-logits in edge order)."""
-    if EDGE_TAIL == "off" or layout.kind == "block" or ea.dim() != 2:
+    if EDGE_TAIL != "on" or layout.kind == "block" or ea.dim() != 2:
         return False
     H = convs[0].heads
     if any(c.heads != H for c in convs) or len(convs) * H > hp:

@@ -149,6 +149,9 @@ int main() {
     run_bw<256, 128, false, true, false>("bw A fp32, B bf16", st, A, K, Bb, Kp, C, M, N, K, 1, ref, fl);
     run_bw<256, 128, false, false, false>("bw A bf16, B bf16", st, Ab, Kp, Bb, Kp, C, M, N, K, 1, ref, fl);
     run_bw<128, 256, false, true, false>("bw A fp32, B bf16", st, A, K, Bb, Kp, C, M, N, K, 1, ref, fl);
+    run_bw<192, 256, false, true, false>("bw A fp32, B bf16", st, A, K, Bb, Kp, C, M, N, K, 1, ref, fl);
+    run_bw<256, 256, false, true, false>("bw A fp32, B bf16", st, A, K, Bb, Kp, C, M, N, K, 1, ref, fl);
+    run_bw<256, 256, false, false, false>("bw A bf16, B bf16", st, Ab, Kp, Bb, Kp, C, M, N, K, 1, ref, fl);
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(Ab)); CK(hipFree(Bb));
   }
   // ---- weight gradient (TN): dWaug[o][f] = Σ_n dxs[n][o] x[n][f]: M 3012, N 1260, K 3840 ----
@@ -185,17 +188,18 @@ int main() {
       printf("  %-28s %8.1f us %7.1f TF  (2 slabs, no check)\n", "round-3 k_gemm_tt<128,128,1>", us,
              fl / us / 1e6);
     }
-    run_bw<256, 192, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 1, ref, fl);
-    run_bw<256, 128, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 1, ref, fl);
-    run_bw<256, 128, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 2, ref, fl);
+    run_bw<128, 256, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 1, ref, fl);
     run_bw<128, 256, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 2, ref, fl);
-    run_bw<192, 128, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 1, ref, fl);
-    run_bw<256, 192, true, true, false>("bw A fp32, B bf16", st, A, ldA, Bb, ldBb, C, M, N, K, 1, ref, fl);
-    run_bw<256, 192, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 1, ref, fl);
-    run_bw<256, 192, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 3, ref, fl);
-    run_bw<256, 192, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 3, ref, fl);
+    run_bw<128, 256, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 3, ref, fl);
+    run_bw<128, 128, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 1, ref, fl);
+    run_bw<128, 128, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 2, ref, fl);
+    run_bw<128, 192, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 2, ref, fl);
+    run_bw<128, 256, true, false, true>("bw A bf16, B fp32", st, Ab, ldAb, B, ldB, C, M, N, K, 2, ref, fl);
+    run_bw<128, 256, true, true, false>("bw A fp32, B bf16", st, A, ldA, Bb, ldBb, C, M, N, K, 2, ref, fl);
+    run_bw<128, 256, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 1, ref, fl);
+    run_bw<128, 256, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
     run_bw<128, 128, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 1, ref, fl);
-    run_bw<256, 128, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
+    run_bw<128, 128, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(Ab)); CK(hipFree(Bb));
   }
   return 0;
