@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 12
+#define SV2N_ABI_VERSION 13
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -142,6 +142,36 @@ int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, int ae_edge_ord
                       int64_t num_graphs, int n, int heads, int channels, int concat,
                       int act, float negative_slope, hipStream_t stream);
 
+/* sv2n_gat_attn_fwd for the model's LAST GAT layer with GATModel.linear
+ * (out_features 1, utils/models.py:120/:150) and the training loss
+ * nn.MSELoss (5_train_SpotV2Net.py:125/:154, upstream gradient 1) fused in
+ * (ABI 13): per graph, out_i = Σ_oc drop(y)[i][oc]·head_weight[oc] +
+ * head_bias[0], diff_i = out_i - target_i, and the forward writes
+ *   dz     [N][OC]  = act'(2/N·diff_i·head_weight[oc]·m)  (m: the post-dropout
+ *          mask·scale, 1 without post_u) — the gradient the layer's backward
+ *          starts from, so call sv2n_gat_attn_bwd on it with act = 0
+ *          (identity) and no post_u; the layer output itself is not stored;
+ *   loss[0] = mean(diff²);
+ *   g_head_weight[oc] += Σ_i 2/N·diff_i·drop(y)[i][oc], g_head_bias[0] +=
+ *          Σ_i 2/N·diff_i (either may be NULL).
+ * Two launches (the attention, then a fixed-order sum of per-graph partials
+ * in workspace: sv2n_gat_attn_fwd_head_mse_workspace floats).  Runs when
+ * sv2n_gat_attn_fwd_head_mse_supported: one workgroup per graph (the batch
+ * fills the chip, or few work items), OC <= 512.  Replaces the separate
+ * sv2n_head_mse_train launch of a training step. */
+int sv2n_gat_attn_fwd_head_mse_supported(int64_t num_graphs, int n, int heads, int channels,
+                                         int concat);
+int64_t sv2n_gat_attn_fwd_head_mse_workspace(int64_t num_graphs, int heads, int channels,
+                                             int concat);
+int sv2n_gat_attn_fwd_head_mse(const float* xs, int ldx, const float* ae, int ae_edge_order,
+                               const uint32_t* rowmask, const float* bias, const uint8_t* keep,
+                               float keep_scale, float* dz, float* psave, const float* post_u,
+                               float post_p, const float* head_weight, const float* head_bias,
+                               const float* target, float* loss, float* g_head_weight,
+                               float* g_head_bias, float* workspace, int64_t workspace_floats,
+                               int64_t num_graphs, int n, int heads, int channels, int concat,
+                               int act, float negative_slope, hipStream_t stream);
+
 /* Backward of sv2n_gat_attn_fwd.
  *   dy, y   [N][OC] (OC = concat ? H*C : C); y is the forward output.
  *   dxs     [N][ldx] gradient w.r.t. xs (all ldx columns written; padding 0).
@@ -159,14 +189,6 @@ int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* xs, int ldx,
                       int64_t num_graphs, int n, int heads, int channels, int concat,
                       int act, float negative_slope, hipStream_t stream);
 
-/* C[M][N] = Σ_k A(m,k)·B(n,k), f32 in / f32 accumulate on MFMA (exact f32).
- *   A(m,k) = A[m*lda+k] if a_kmajor else A[k*lda+m]
- *   B(n,k) = B[n*ldb+k] if b_kmajor else B[k*ldb+n]
- *   C[m*ldc+n] is overwritten.
- * Replaces the lin_src projection GEMM (row a6: a_kmajor = b_kmajor = 1) and
- * its backward products dX (a_kmajor=1, b_kmajor=0) and dWᵀ (0, 0).
- * workspace: sv2n_gemm_f32_workspace(M,N,K) floats (split-K partial slabs;
- * 0 => may be NULL). */
 /* sv2n_gat_attn_bwd with the edge-logit weight gradient of EVERY layer fused
  * in (ABI 12; replaces sv2n_edge_logits_bwd for canonical batches, reference
  * GATConv lin_edge / att_edge backward, utils/models.py:146): the workgroup
@@ -194,6 +216,14 @@ int sv2n_gat_attn_bwd_edge(const float* dy, const float* y, const float* xs, int
 int sv2n_edge_partials_reduce(const float* partial, int64_t num_parts, int64_t width, float* out,
                               hipStream_t stream);
 
+/* C[M][N] = Σ_k A(m,k)·B(n,k), f32 in / f32 accumulate on MFMA (exact f32).
+ *   A(m,k) = A[m*lda+k] if a_kmajor else A[k*lda+m]
+ *   B(n,k) = B[n*ldb+k] if b_kmajor else B[k*ldb+n]
+ *   C[m*ldc+n] is overwritten.
+ * Replaces the lin_src projection GEMM (row a6: a_kmajor = b_kmajor = 1) and
+ * its backward products dX (a_kmajor=1, b_kmajor=0) and dWᵀ (0, 0).
+ * workspace: sv2n_gemm_f32_workspace(M,N,K) floats (split-K partial slabs;
+ * 0 => may be NULL). */
 int64_t sv2n_gemm_f32_workspace(int64_t M, int64_t N, int64_t K);
 int sv2n_gemm_f32(int a_kmajor, int b_kmajor, const float* A, int64_t lda,
                   const float* B, int64_t ldb, float* C, int64_t ldc,

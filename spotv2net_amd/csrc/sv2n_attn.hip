@@ -15,7 +15,8 @@ void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const f
                     int ae_edge_order, const uint32_t* rowmask, const float* bias,
                     const uint8_t* keep, float keep_scale, float* y, float* psave,
                     const float* post_u, float post_p, float* post_out, int n, int H, int C,
-                    int concat, int act, float slope);
+                    int concat, int act, float slope, const HeadFuse& hf);
+bool attn_canon_head_ok(int64_t B, int n, int H, int C, bool concat);
 void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, const float* xs,
                     int ldx, const float* psave, const uint8_t* keep, float keep_scale,
                     const float* post_u, float post_p, const uint32_t* rowmask, float* dxs, float* dae, int ae_edge_order,
@@ -46,7 +47,50 @@ extern "C" int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, int 
   if (post_u && (!post_out || !(post_p >= 0.f && post_p < 1.f))) return SV2N_ERR_ARG;
   attn_canon_fwd(num_graphs, stream, xs, ldx, ae, ae_edge_order, rowmask, bias, keep,
                  keep_scale, y, psave, post_u, post_p, post_out, n, heads, channels, concat, act,
-                 negative_slope);
+                 negative_slope, HeadFuse{});
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_gat_attn_fwd_head_mse_supported(int64_t num_graphs, int n, int heads,
+                                                    int channels, int concat) {
+  if (num_graphs <= 0 || channels <= 0 || heads < 1 || heads > SV2N_MAX_HEADS) return 0;
+  return attn_canon_head_ok(num_graphs, n, heads, channels, concat != 0) ? 1 : 0;
+}
+
+extern "C" int64_t sv2n_gat_attn_fwd_head_mse_workspace(int64_t num_graphs, int heads,
+                                                        int channels, int concat) {
+  if (num_graphs <= 0 || heads < 1 || channels < 1) return 0;
+  return num_graphs * ((concat ? heads * channels : channels) + 2);
+}
+
+extern "C" int sv2n_gat_attn_fwd_head_mse(
+    const float* xs, int ldx, const float* ae, int ae_edge_order, const uint32_t* rowmask,
+    const float* bias, const uint8_t* keep, float keep_scale, float* dz, float* psave,
+    const float* post_u, float post_p, const float* head_weight, const float* head_bias,
+    const float* target, float* loss, float* g_head_weight, float* g_head_bias,
+    float* workspace, int64_t workspace_floats, int64_t num_graphs, int n, int heads,
+    int channels, int concat, int act, float negative_slope, hipStream_t stream) {
+  if (!xs || !dz || !psave || !head_weight || !target || !loss || !workspace)
+    return SV2N_ERR_ARG;
+  if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
+  if (ae_edge_order && (rowmask || n < 2)) return SV2N_ERR_ARG;
+  if (post_u && !(post_p >= 0.f && post_p < 1.f)) return SV2N_ERR_ARG;
+  if (!attn_canon_head_ok(num_graphs, n, heads, channels, concat != 0)) return SV2N_ERR_SHAPE;
+  if (workspace_floats <
+      sv2n_gat_attn_fwd_head_mse_workspace(num_graphs, heads, channels, concat))
+    return SV2N_ERR_WORKSPACE;
+  HeadFuse hf{};
+  hf.w = head_weight;
+  hf.b = head_bias;
+  hf.target = target;
+  hf.part = workspace;
+  hf.inv_n2 = (float)(2.0 / ((double)num_graphs * n));
+  hf.gw = g_head_weight;
+  hf.gb = g_head_bias;
+  hf.loss = loss;
+  attn_canon_fwd(num_graphs, stream, xs, ldx, ae, ae_edge_order, rowmask, bias, keep,
+                 keep_scale, dz, psave, post_u, post_p, nullptr, n, heads, channels, concat, act,
+                 negative_slope, hf);
   return (int)hipGetLastError();
 }
 

@@ -74,13 +74,22 @@ __device__ __forceinline__ bool graph_split(int64_t B, int S, int64_t& g, int& s
   return g < B;
 }
 
-template <int ACT, bool CONCAT, bool KEEP>
+// HEAD (one workgroup per graph, the model's last GAT layer): the output head
+// and the MSE loss of the training step are fused in (HeadFuse).  The layer
+// output a = act(z) goes to LDS sY[32][OC + 1] instead of HBM; after a
+// barrier, per row i: out_i = Σ_oc m·a·w[oc] + b (m the post-dropout factor),
+// dout_i = 2/(B·n)·(out_i − target_i); then y receives dZ = act'(dout_i·w·m)
+// (what the backward's activation step would produce, so the layer's
+// backward runs with the identity and reads no y) and the graph's partials
+// Σ_i dout_i·m·a (head weight), Σ_i dout_i (head bias), Σ_i diff² (loss)
+// go to part[g] (k_head_fuse_finish sums them in graph order).
+template <int ACT, bool CONCAT, bool KEEP, bool HEAD = false>
 __global__ __launch_bounds__(THREADS) void k_fwd(
     const float* __restrict__ xs, int ldx, const float* __restrict__ ae, int ae_edge_order,
     const uint32_t* __restrict__ rowmask, const float* __restrict__ bias, const uint8_t* __restrict__ keep, float keep_scale,
     float* __restrict__ y, float* __restrict__ psave, const float* __restrict__ post_u,
     float post_p, float post_scale, float* __restrict__ post_out, int n, int H, int C, float slope,
-    int S, int64_t B) {
+    int S, int64_t B, HeadFuse hf) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sP = smem;
   float* sAS = sP + H * 32 * PS;
@@ -281,6 +290,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const float invH = 1.f / (float)H;
+  float* sY = sAE + ((nae + 3) & ~3);  // HEAD: the layer output [32][OC + 1]
   float uv[16];  // post-dropout draws of the work item's outputs (loaded at its first sub-item)
   auto run = [&](int q, const float (&b)[16]) {
     int h, tc;
@@ -308,9 +318,15 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       for (int r = 0; r < 16; ++r) {
         const float z = (CONCAT ? acc[r] : acc[r] * invH) + bv;
         const float a = act_fwd<ACT>(z);
-        bst_s(ry, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4, a);
-        if (post)
-          bst_s(ro, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4, uv[r] >= post_p ? a * post_scale : 0.f);
+        if constexpr (HEAD) {
+          const int row = crow(r, half);
+          if (cv && row < n) sY[row * (OC + 1) + oc] = a;
+        } else {
+          bst_s(ry, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4, a);
+          if (post)
+            bst_s(ro, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4,
+                  uv[r] >= post_p ? a * post_scale : 0.f);
+        }
         acc[r] = 0.f;
       }
     }
@@ -325,10 +341,105 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       }
     }
   }
+  if constexpr (HEAD) {
+    const int OC1 = OC + 1;
+    float* sD = sY + 32 * OC1;  // dout per row
+    float* sL = sD + 32;        // diff² per row
+    const rsrc_t rw = make_rsrc(hf.w, (uint32_t)OC * 4u);
+    // post-dropout factor of (row, oc): the forward's mask and scale
+    auto mfac = [&](int row, int oc) {
+      return post ? (bld(ru, (row * OC + oc) * 4) >= post_p ? post_scale : 0.f) : 1.f;
+    };
+    __syncthreads();  // sY complete
+    {  // head output and residual: 8 threads per row, columns sub, sub + 8, ...
+      const int row = t >> 3, sub = t & 7;
+      float sacc = 0.f;
+      if (row < n)
+        for (int oc = sub; oc < OC; oc += 8)
+          sacc = fmaf(sY[row * OC1 + oc] * mfac(row, oc), bld(rw, oc * 4), sacc);
+      sacc += __shfl_xor(sacc, 1, 64);
+      sacc += __shfl_xor(sacc, 2, 64);
+      sacc += __shfl_xor(sacc, 4, 64);
+      if (sub == 0) {
+        float dv = 0.f, lv = 0.f;
+        if (row < n) {
+          const float out = sacc + (hf.b ? hf.b[0] : 0.f);
+          const float diff = out - hf.target[g * n + row];
+          dv = diff * hf.inv_n2;
+          lv = diff * diff;
+        }
+        sD[row] = dv;
+        sL[row] = lv;
+      }
+    }
+    __syncthreads();
+    // dZ in y's place (coalesced rows)
+    const rsrc_t rz = make_rsrc(y + (int64_t)g * n * OC, (uint32_t)(n * OC) * 4u);
+    for (int k = t; k < n * OC; k += THREADS) {
+      const int row = k / OC, oc = k - row * OC;
+      const float a = sY[row * OC1 + oc];
+      bst(rz, k * 4, act_bwd<ACT>(sD[row] * bld(rw, oc * 4) * mfac(row, oc), a));
+    }
+    // the graph's partials, rows summed in order
+    float* pg = hf.part + (int64_t)g * (OC + 2);
+    for (int oc = t; oc < OC; oc += THREADS) {
+      float sacc = 0.f;
+      for (int row = 0; row < n; ++row)
+        sacc = fmaf(sD[row], sY[row * OC1 + oc] * mfac(row, oc), sacc);
+      pg[oc] = sacc;
+    }
+    if (t == THREADS - 1) {
+      float sd = 0.f, sl = 0.f;
+      for (int row = 0; row < n; ++row) {
+        sd += sD[row];
+        sl += sL[row];
+      }
+      pg[OC] = sd;
+      pg[OC + 1] = sl;
+    }
+  }
   SV2N_STAMP(5, SV2N_T());
   SV2N_STAMP(6, SV2N_RT());
 }
 
+
+// Sums k_fwd<HEAD>'s per-graph partials part[B][OC + 2] in graph order:
+// g_w[o] += Σ_g part[g][o] (o < OC), g_b[0] += Σ_g part[g][OC], loss[0] =
+// Σ_g part[g][OC + 1] / (B·n).  Block: 16 columns x 16 graph groups.
+__global__ __launch_bounds__(256) void k_head_fuse_finish(const float* __restrict__ part,
+                                                          int64_t B, int OC, float inv_n,
+                                                          float* __restrict__ g_w,
+                                                          float* __restrict__ g_b,
+                                                          float* __restrict__ loss) {
+  __shared__ float s_red[16][17];
+  const int lo = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int o = blockIdx.x * 16 + lo, O = OC + 2;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (o < O) {
+    int64_t b = grp;
+    for (; b + 48 < B; b += 64) {
+      a0 += part[b * O + o];
+      a1 += part[(b + 16) * O + o];
+      a2 += part[(b + 32) * O + o];
+      a3 += part[(b + 48) * O + o];
+    }
+    for (; b < B; b += 16) a0 += part[b * O + o];
+  }
+  s_red[grp][lo] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (grp == 0 && o < O) {
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sm += s_red[k][lo];
+    if (o < OC) {
+      if (g_w) g_w[o] += sm;
+    } else if (o == OC) {
+      if (g_b) g_b[0] += sm;
+    } else {
+      loss[0] = sm * inv_n;
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------
 // backward: S workgroups per graph (graph_split), split s owning heads
@@ -961,38 +1072,56 @@ void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, 
 #undef SV2N_CB
 }
 
-size_t attn_canon_fwd_lds(int n, int H, bool has_ae, bool edge_order) {
+// HEAD: + the layer output [32][OC + 1] and two [32] row vectors
+size_t attn_canon_fwd_lds(int n, int H, bool has_ae, bool edge_order, int head_oc) {
   const int nae = has_ae ? (edge_order ? n * (n - 1) : n * n) * H : 0;
   return sizeof(float) * ((size_t)H * 32 * canon::PS + 2 * (size_t)H * 32 +
-                          (size_t)((nae + 3) & ~3));
+                          (size_t)((nae + 3) & ~3) +
+                          (head_oc > 0 ? (size_t)32 * (head_oc + 1) + 64 : 0));
 }
 
-template <int ACT, bool CONCAT, bool KEEP>
+// the output head fuses into the layer's forward when one workgroup runs each
+// graph (its rows and columns all in one place) and the layer output fits LDS
+bool attn_canon_head_ok(int64_t B, int n, int H, int C, bool concat) {
+  const int OC = concat ? H * C : C;
+  return n >= 1 && n <= 32 && canon_fwd_splits(B, H, C, concat) == 1 && OC <= 512;
+}
+
+template <int ACT, bool CONCAT, bool KEEP, bool HEAD>
 static void launch_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
                              int ae_edge_order, const uint32_t* rowmask, const float* bias,
                              const uint8_t* keep, float keep_scale, float* y, float* psave,
                              const float* post_u, float post_p, float* post_out, int n, int H,
-                             int C, float slope) {
-  const size_t lds = attn_canon_fwd_lds(n, H, ae != nullptr, ae_edge_order != 0);
+                             int C, float slope, const HeadFuse& hf) {
+  const size_t lds = attn_canon_fwd_lds(n, H, ae != nullptr, ae_edge_order != 0,
+                                        HEAD ? (CONCAT ? H * C : C) : 0);
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)canon::k_fwd<ACT, CONCAT, KEEP>,
+    (void)hipFuncSetAttribute((const void*)canon::k_fwd<ACT, CONCAT, KEEP, HEAD>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  const int S = canon_fwd_splits(B, H, C, CONCAT);
-  hipLaunchKernelGGL((canon::k_fwd<ACT, CONCAT, KEEP>), dim3(canon_grid(B, S)),
+  const int S = HEAD ? 1 : canon_fwd_splits(B, H, C, CONCAT);
+  hipLaunchKernelGGL((canon::k_fwd<ACT, CONCAT, KEEP, HEAD>), dim3(canon_grid(B, S)),
                      dim3(canon::THREADS), lds, st, xs, ldx, ae, ae_edge_order, rowmask, bias, keep,
                      keep_scale, y, psave, post_u, post_p,
                      post_u ? (float)(1.0 / (1.0 - (double)post_p)) : 1.f, post_out, n, H, C,
-                     slope, S, B);
+                     slope, S, B, hf);
 }
 
 void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const float* ae,
                     int ae_edge_order, const uint32_t* rowmask, const float* bias,
                     const uint8_t* keep, float keep_scale, float* y, float* psave,
                     const float* post_u, float post_p, float* post_out, int n, int H, int C,
-                    int concat, int act, float slope) {
-#define SV2N_CF(A, CC, K)                                                                     \
-  launch_canon_fwd<A, CC, K>(B, st, xs, ldx, ae, ae_edge_order, rowmask, bias, keep, keep_scale, \
-                             y, psave, post_u, post_p, post_out, n, H, C, slope)
+                    int concat, int act, float slope, const HeadFuse& hf) {
+#define SV2N_CF(A, CC, K)                                                                      \
+  {                                                                                            \
+    if (hf.w)                                                                                  \
+      launch_canon_fwd<A, CC, K, true>(B, st, xs, ldx, ae, ae_edge_order, rowmask, bias, keep, \
+                                       keep_scale, y, psave, post_u, post_p, post_out, n, H,   \
+                                       C, slope, hf);                                          \
+    else                                                                                       \
+      launch_canon_fwd<A, CC, K, false>(B, st, xs, ldx, ae, ae_edge_order, rowmask, bias,      \
+                                        keep, keep_scale, y, psave, post_u, post_p, post_out,  \
+                                        n, H, C, slope, hf);                                   \
+  }
 #define SV2N_CF_ACT(CC, K)                 \
   switch (act) {                           \
     case 0: SV2N_CF(0, CC, K); break;      \
@@ -1007,6 +1136,12 @@ void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const f
   }
 #undef SV2N_CF_ACT
 #undef SV2N_CF
+  if (hf.w) {
+    const int OC = concat ? H * C : C;
+    hipLaunchKernelGGL(canon::k_head_fuse_finish, dim3((unsigned)((OC + 2 + 15) / 16)),
+                       dim3(256), 0, st, hf.part, B, OC, 0.5f * hf.inv_n2, hf.gw, hf.gb,
+                       hf.loss);
+  }
 }
 
 }  // namespace sv2n

@@ -190,6 +190,19 @@ __device__ __forceinline__ bool last_block_ticket2(unsigned* cnt, unsigned nbloc
   return *s_flag != 0;
 }
 
+// Output head + MSE fused into the last layer's n <= 32 attention forward
+// (sv2n_gat_attn_fwd_head_mse): w == nullptr: off.
+struct HeadFuse {
+  const float* w;       // [OC] GATModel.linear.weight (out_features 1)
+  const float* b;       // [1] its bias, or NULL
+  const float* target;  // [B·n]
+  float* part;          // [B][OC + 2] per-graph partials: Σ dout·y per column, Σ dout, Σ diff²
+  float inv_n2;         // 2 / (B·n): d mean((out - target)²) / d out
+  float* gw;            // host side (k_head_fuse_finish): [OC] += Σ_g, or NULL
+  float* gb;            // [1] += Σ_g, or NULL
+  float* loss;          // [1] = mean((out - target)²)
+};
+
 // Edge-gradient tail of the n <= 32 attention backward (sv2n_attn_canon.hip,
 // sv2n_gat_attn_bwd_edge): the edge pass's hl_pad columns it carries, and its
 // arguments (ea == nullptr: off).

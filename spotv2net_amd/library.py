@@ -44,6 +44,12 @@ _SCHEMAS = {
                          "float keep_scale, Tensor post_u, float post_p, int num_graphs, int n, "
                          "int heads, int channels, bool concat, int act, float slope, "
                          "bool edge_order=False) -> (Tensor, Tensor, Tensor)",
+    "gat_attn_fwd_head_mse": "(Tensor xs, Tensor? ae, Tensor? rowmask, Tensor? bias, Tensor? keep, "
+                             "float keep_scale, Tensor? post_u, float post_p, Tensor head_weight, "
+                             "Tensor? head_bias, Tensor target, Tensor(a!)? g_head_weight, "
+                             "Tensor(b!)? g_head_bias, int num_graphs, int n, int heads, "
+                             "int channels, bool concat, int act, float slope, "
+                             "bool edge_order=False) -> (Tensor, Tensor, Tensor)",
     "gat_attn_tiled_fwd": "(Tensor xs, Tensor? ae, int num_edges, Tensor? eid, Tensor? rowmask, "
                           "Tensor? bias, Tensor? keep, float keep_scale, int num_graphs, int n, "
                           "int heads, int channels, bool concat, int act, float slope) -> Tensor",
@@ -407,6 +413,59 @@ def _gat_attn_fwd_post_fake(xs, ae, rowmask, bias, keep, keep_scale, post_u, pos
     oc = _oc(heads, channels, concat)
     return (xs.new_empty((num_graphs * n, oc)), xs.new_empty((num_graphs, heads, 32, 32)),
             xs.new_empty((num_graphs * n, oc)))
+
+
+def attn_fwd_head_mse_supported(num_graphs: int, n: int, heads: int, channels: int,
+                                concat: bool) -> bool:
+    """Whether sv2n_gat_attn_fwd_head_mse runs this layer shape (include/sv2n.h)."""
+    return bool(_lib.load().sv2n_gat_attn_fwd_head_mse_supported(num_graphs, n, heads, channels,
+                                                                 int(concat)))
+
+
+@_impl("gat_attn_fwd_head_mse")
+def _gat_attn_fwd_head_mse(xs, ae, rowmask, bias, keep, keep_scale, post_u, post_p, head_weight,
+                           head_bias, target, g_head_weight, g_head_bias, num_graphs, n, heads,
+                           channels, concat, act, slope, edge_order=False):
+    """The last layer's attention with GATModel.linear (out_features 1) and the
+    MSE loss fused in: returns (dz, psave, loss) — dz the gradient the layer's
+    backward starts from (identity activation, no post dropout) — and
+    accumulates the head's parameter gradients."""
+    lib = _lib.load()
+    _f32(xs, ae, bias, post_u, head_weight, head_bias, target)
+    N, OC = num_graphs * n, _oc(heads, channels, concat)
+    _rows(xs, N, heads * channels + 2 * heads, "xs")
+    _dense(ae, rowmask, bias, keep, post_u, head_weight, head_bias, target, g_head_weight,
+           g_head_bias)
+    _need(ae is None or ae.numel() == num_graphs * n * (n - int(edge_order)) * heads, "ae shape")
+    _need(not edge_order or rowmask is None, "edge-ordered ae needs complete graphs")
+    _need(bias is None or bias.numel() == OC, "bias shape")
+    _need(keep is None or keep.numel() == num_graphs * heads * 1024, "keep shape")
+    _need(rowmask is None or rowmask.numel() >= N, "rowmask shape")
+    _need(post_u is None or (post_u.numel() == N * OC and 0.0 <= post_p < 1.0), "post_u / post_p")
+    _need(head_weight.numel() == OC and (head_bias is None or head_bias.numel() == 1),
+          "head shape (out_features 1)")
+    _need(target.numel() == N, f"target has {target.numel()} elements, expected {N}")
+    dz = torch.empty(N, OC, device=xs.device)
+    ps = torch.empty(num_graphs, heads, 32, 32, device=xs.device)
+    loss = torch.empty((), device=xs.device)
+    ws_n = lib.sv2n_gat_attn_fwd_head_mse_workspace(num_graphs, heads, channels, int(concat))
+    ws = torch.empty(ws_n, device=xs.device)
+    _lib.check(lib.sv2n_gat_attn_fwd_head_mse(
+        xs.data_ptr(), xs.stride(0), _p(ae), int(edge_order), _p(rowmask), _p(bias), _p(keep),
+        keep_scale, dz.data_ptr(), ps.data_ptr(), _p(post_u), post_p, head_weight.data_ptr(),
+        _p(head_bias), target.data_ptr(), loss.data_ptr(), _p(g_head_weight), _p(g_head_bias),
+        ws.data_ptr(), ws_n, num_graphs, n, heads, channels, int(concat), act, slope, _st(xs)),
+        "sv2n_gat_attn_fwd_head_mse")
+    return dz, ps, loss
+
+
+@_fake("gat_attn_fwd_head_mse")
+def _gat_attn_fwd_head_mse_fake(xs, ae, rowmask, bias, keep, keep_scale, post_u, post_p,
+                                head_weight, head_bias, target, g_head_weight, g_head_bias,
+                                num_graphs, n, heads, channels, concat, act, slope,
+                                edge_order=False):
+    return (xs.new_empty((num_graphs * n, _oc(heads, channels, concat))),
+            xs.new_empty((num_graphs, heads, 32, 32)), xs.new_empty(()))
 
 
 @_impl("gat_attn_tiled_fwd")

@@ -29,7 +29,7 @@ from torch import nn
 from . import graphed, ops
 from .conv import GATConv
 from .layout import GraphLayout, analyze_edge_index, declare_canonical
-from .stack import gat_stack, head_mse_loss, linear_head
+from .stack import gat_stack, gat_train_head_mse, head_mse_loss, linear_head
 
 
 def _equal_sizes_on_host(data) -> Optional[int]:
@@ -132,6 +132,18 @@ class GATModel(nn.Module):
             layout = _layout_of(data, x, edge_index)
         return gat_stack(x, edge_attr, tuple(self.gat_layers), layout, self._act_code,
                          float(self.dropout or 0.0), self.training, self.precision)
+
+    def _train_head_mse(self, data, target: torch.Tensor) -> Optional[torch.Tensor]:
+        """``train.TrainStep``'s forward + backward with the output head and
+        the MSE loss fused into the last GAT layer (stack.gat_train_head_mse):
+        the loss, with every gradient accumulated into ``p.grad``; None when
+        the model / batch does not take that path."""
+        if self.standardize or not self.training:
+            return None
+        layout = _layout_of(data, data.x, data.edge_index)
+        return gat_train_head_mse(data.x, data.edge_attr, tuple(self.gat_layers), layout,
+                                  self._act_code, float(self.dropout or 0.0), self.linear, target,
+                                  self.precision)
 
     def set_precision(self, precision: Optional[str]) -> "GATModel":
         """"bf16": projection / weight-gradient GEMMs on bf16 operands with

@@ -223,20 +223,33 @@ def _edge_tail_ok(layout: GraphLayout, convs, ea, hp: int) -> bool:
 
 class _StackMeta:
     """What the backward needs besides the saved tensors (stack_forward)."""
-    __slots__ = ("dims", "bf16", "feid", "kscales", "post_p")
+    __slots__ = ("dims", "bf16", "feid", "kscales", "post_p", "head_dz")
 
-    def __init__(self, dims, bf16, feid, kscales, post_p=None):
+    def __init__(self, dims, bf16, feid, kscales, post_p=None, head_dz=None):
         self.dims, self.bf16, self.feid, self.kscales = dims, bf16, feid, kscales
         # per layer: the post-layer dropout probability when its draws (not a
         # mask) are saved, i.e. the attention kernels apply it themselves
         self.post_p = post_p or [None] * len(kscales)
+        # the output head + MSE ran inside the last layer's forward: the
+        # gradient its backward starts from (identity activation)
+        self.head_dz = head_dz
+
+
+# "on": the training step fuses GATModel.linear + MSE into the last layer's
+# attention forward where the kernel takes the shape (gat_train_head_mse);
+# "off": the separate head + loss launch (A/B switch for tests and measurements)
+HEAD_FUSE = os.environ.get("SV2N_HEAD_FUSE", "on")
 
 
 def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropout: float,
-                  training: bool, precision: str, need_saved: bool):
+                  training: bool, precision: str, need_saved: bool, head=None):
     """The fused stack's forward launches (module docstring); returns the
     output, the tensors the backward reads and a ``_StackMeta``.  Capturable:
-    no host synchronisation, every buffer from the caching allocator."""
+    no host synchronisation, every buffer from the caching allocator.
+    ``head`` = (linear, target, g_weight, g_bias): the last layer also runs
+    the output head and the MSE loss (sv2n::gat_attn_fwd_head_mse, the caller
+    checked ``head_mse_fusable``); the output is then the loss and
+    ``meta.head_dz`` the last layer's incoming gradient."""
     ops = torch.ops.sv2n
     dev = x.device
     L = len(convs)
@@ -330,7 +343,17 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
                                        c.concat, act, float(c.negative_slope))
             ps = aes[l]
         post_u = None
-        if not (fused or tiled) and training and 0.0 < post_dropout < 1.0:
+        if head is not None and l == L - 1:
+            lin, target, ghw, ghb = head
+            if training and 0.0 < post_dropout < 1.0:
+                post_u = torch.rand(N, Hc * C if c.concat else C, device=dev)
+            y, ps, out = ops.gat_attn_fwd_head_mse(
+                xs, aes[l], layout.rowmask, c.bias, keep, kscale, post_u,
+                float(post_dropout) if post_u is not None else 0.0, lin.weight.view(-1), lin.bias,
+                target.reshape(-1), ghw, ghb, B, n, Hc, C, c.concat, act,
+                float(c.negative_slope), eo)
+            post_u = None  # applied: y is the layer's incoming gradient dz
+        elif not (fused or tiled) and training and 0.0 < post_dropout < 1.0:
             # the post-layer dropout (utils/models.py:148) fused into the
             # attention's store: torch draws the uniforms (same stream as
             # rand_like(y) >= p), the kernel masks, scales and writes both y
@@ -342,11 +365,12 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
         elif not (fused or tiled):
             y, ps = ops.gat_attn_fwd(xs, aes[l], layout.rowmask, c.bias, keep, kscale, B, n,
                                      Hc, C, c.concat, act, float(c.negative_slope), eo)
-        if post_u is None:
+        head_last = head is not None and l == L - 1
+        if post_u is None and not head_last:
             out = y
         dmask = post_u
         post_p.append(float(post_dropout) if post_u is not None else None)
-        if post_u is None and training and post_dropout > 0.0:
+        if post_u is None and training and post_dropout > 0.0 and not head_last:
             if post_dropout >= 1.0:
                 dmask = torch.zeros_like(y)
             else:
@@ -364,7 +388,8 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
 
     meta = _StackMeta((L, act, use_edge, hp, H, eo, fused), bf16, feid,
                       [(1.0 / (1.0 - c.dropout)) if (training and 0.0 < c.dropout < 1.0) else
-                       (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs], post_p)
+                       (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs], post_p,
+                      saved_y[-1] if head is not None else None)
     saved = [ea, wf if fused else None, *saved_x, *saved_xs, *saved_y, *saved_p, *saved_st,
              *saved_keep, *saved_drop, *waugs, *planes_t]
     return xin, saved, meta
@@ -394,7 +419,9 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
     dy = dout.contiguous()
     daes = [None] * L
     dwf = torch.zeros_like(wf) if fused else None  # every layer writes its own columns
-    act_l = act  # the activation backward left to layer l's attention backward
+    # the activation backward left to layer l's attention backward (none when
+    # the fused head's forward already produced the last layer's dZ)
+    act_l = 0 if meta.head_dz is not None else act
     # canonical complete graphs: layer 0's attention backward also computes the
     # edge-logit weight gradient of every layer (sv2n_gat_attn_bwd_edge), so
     # edge_attr is streamed there and no separate edge-gradient pass runs
@@ -495,6 +522,49 @@ class _GATStack(torch.autograd.Function):
         dx0 = stack_backward(ctx.saved_tensors, ctx.meta, ctx.convs, ctx.layout, dout,
                              ctx.needs_input_grad[0], grad_of)
         return (dx0, None, None, None, None, None, None, None) + grad_of.returned()
+
+
+def head_mse_fusable(convs, layout: GraphLayout, linear: torch.nn.Linear,
+                     post_dropout: float) -> bool:
+    """Whether the training step can run GATModel.linear + MSE inside the last
+    layer's attention forward (sv2n_gat_attn_fwd_head_mse_supported: the
+    n <= 32 path with one workgroup per graph, out_features 1)."""
+    from .library import attn_fwd_head_mse_supported
+    last = convs[-1]
+    return (HEAD_FUSE == "on" and not layout.tiled and linear.out_features == 1
+            and post_dropout < 1.0 and last.in_channels > 0
+            and attn_fwd_head_mse_supported(layout.num_graphs, layout.n, last.heads,
+                                            last.out_channels, last.concat))
+
+
+def gat_train_head_mse(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs: Sequence,
+                       layout: GraphLayout, act: int, post_dropout: float, linear: torch.nn.Linear,
+                       target: torch.Tensor, precision: Optional[str] = None):
+    """One training forward + backward with the upstream loss gradient 1
+    (5_train_SpotV2Net.py:150-158: ``loss = MSELoss()(model(data), y);
+    loss.backward()``) with the output head and the loss fused into the last
+    layer's attention forward: parameter gradients ACCUMULATE into ``p.grad``
+    (direct mode, as ``train.TrainStep`` keeps them); returns the loss, or
+    None when the shape does not fuse (the caller takes the unfused path).
+    No autograd graph is built; capturable."""
+    if not head_mse_fusable(convs, layout, linear, post_dropout):
+        return None
+    precision = resolve_precision(precision)
+    params = [p for c in convs for p in layer_params(c)]
+    _require_params(params + [linear.weight, linear.bias])
+    _require_device(x, edge_attr, target)
+    if edge_attr is not None and edge_attr.requires_grad:
+        raise NotImplementedError("gradients w.r.t. edge_attr are not supported")
+    grad_of = _GradTargets(params, [p.requires_grad for p in params], True, x.device)
+    ghw = _grad_buf(linear.weight) if linear.weight.requires_grad else None
+    ghb = _grad_buf(linear.bias) if linear.bias is not None and linear.bias.requires_grad \
+        else None
+    with torch.no_grad():
+        loss, saved, meta = stack_forward(x, edge_attr, tuple(convs), layout, int(act),
+                                          float(post_dropout), True, precision, True,
+                                          head=(linear, target, ghw, ghb))
+        stack_backward(saved, meta, tuple(convs), layout, meta.head_dz, False, grad_of)
+    return layout.poison(loss).reshape(())
 
 
 def _require_params(params) -> None:

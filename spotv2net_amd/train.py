@@ -205,8 +205,15 @@ class TrainStep:
         # it directly (no per-parameter AccumulateGrad launches)
         with direct_grad_accumulation():
             if self._fused_mse:
-                # head + loss forward AND backward in one launch (the upstream
-                # gradient of the loss is 1), then the GAT stack's backward
+                # the output head and the loss inside the last GAT layer's
+                # attention forward (stack.gat_train_head_mse) ...
+                loss = self.model._train_head_mse(sh.data, sh.data.y_x)
+                if loss is not None:
+                    sh.loss = loss.detach()
+                    self._accumulate(sh)
+                    return
+                # ... or head + loss forward AND backward in one launch (the
+                # upstream gradient of the loss is 1), then the stack's backward
                 h = self.model._hidden(sh.data)
                 res = head_mse_train(h, self.model.linear, sh.data.y_x)
                 if res is not None:

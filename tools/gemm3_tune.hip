@@ -212,6 +212,10 @@ int main() {
     run3b<8, 1, 13, 32, 3, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<4, 2, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<4, 2, 13, 32, 3, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    // round 4: more, smaller workgroups (240 -> 480-960 per launch at C2 sizes)
+    run3b<4, 1, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 4, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 5, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(S)); CK(hipFree(Bp));
   }
   return 0;
