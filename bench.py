@@ -365,10 +365,19 @@ def kernel_table_c3(model, cfg, precision, reps=20):
     planes = ops.weight_planes(W, False)
     xs = torch.empty(N, ldx, device=dev)
 
+    # bf16 mode as the step runs it: the projection also exports bf16(x)
+    # (sv2n_gemm_bf16_export), the weight gradient reads bf16 x and bf16 dxs
+    # (sv2n_gat_wgrad_node_bf16b), the attention backward writes bf16 dxs
+    kb = (F + 63) // 64 * 64
+    xb = torch.empty(N, kb, device=dev, dtype=torch.bfloat16)
+
     def gemm_fwd():
-        (lib.sv2n_gemm_bf16 if bf16 else lib.sv2n_gemm_f32x3)(
-            x.data_ptr(), x.stride(0), planes.data_ptr(), xs.data_ptr(), xs.stride(0), N, ldx, F,
-            sh)
+        if bf16:
+            lib.sv2n_gemm_bf16_export(x.data_ptr(), x.stride(0), planes.data_ptr(), xs.data_ptr(),
+                                      xs.stride(0), N, ldx, F, xb.data_ptr(), kb, sh)
+        else:
+            lib.sv2n_gemm_f32x3(x.data_ptr(), x.stride(0), planes.data_ptr(), xs.data_ptr(),
+                                xs.stride(0), N, ldx, F, sh)
 
     gemm_fwd()
     dxs = torch.randn(N, ldx, device=dev) * 1e-3
@@ -382,11 +391,23 @@ def kernel_table_c3(model, cfg, precision, reps=20):
     ws_n = ws_fn(N, F, ldx, H, C)
     ws = torch.empty(ws_n, device=dev)
 
+    ldb = (ldx + 7) // 8 * 8
+    dxb = dxs.new_zeros(N, ldb).to(torch.bfloat16)
+    dxb[:, :ldx] = dxs.to(torch.bfloat16)
+
     def wgrad():
-        (lib.sv2n_gat_wgrad_node_bf16 if bf16 else lib.sv2n_gat_wgrad_node)(
-            x.data_ptr(), x.stride(0), dxs.data_ptr(), ldx, N, F, conv.lin_src.weight.data_ptr(),
-            att_s.data_ptr(), att_d.data_ptr(), H, C, dbp.data_ptr(), B, C, gW.data_ptr(),
-            ga.data_ptr(), gd.data_ptr(), gb.data_ptr(), ws.data_ptr(), ws_n, sh)
+        if bf16:
+            lib.sv2n_gat_wgrad_node_bf16b(
+                xb.data_ptr(), kb, dxb.data_ptr(), ldb, N, F, ldx,
+                conv.lin_src.weight.data_ptr(), att_s.data_ptr(), att_d.data_ptr(), H, C,
+                dbp.data_ptr(), B, C, gW.data_ptr(), ga.data_ptr(), gd.data_ptr(), gb.data_ptr(),
+                ws.data_ptr(), ws_n, sh)
+        else:
+            lib.sv2n_gat_wgrad_node(
+                x.data_ptr(), x.stride(0), dxs.data_ptr(), ldx, N, F,
+                conv.lin_src.weight.data_ptr(), att_s.data_ptr(), att_d.data_ptr(), H, C,
+                dbp.data_ptr(), B, C, gW.data_ptr(), ga.data_ptr(), gd.data_ptr(), gb.data_ptr(),
+                ws.data_ptr(), ws_n, sh)
 
     E = data.edge_attr.shape[0]
     ae = torch.randn(E, H, device=dev)
@@ -404,17 +425,29 @@ def kernel_table_c3(model, cfg, precision, reps=20):
     dae = torch.empty_like(ae)
     dbp2 = torch.empty(B, C, device=dev)
 
+    dxb2 = torch.empty_like(dxb)
+
     def attn_bwd():
-        lib.sv2n_gat_attn_bwd(dy.data_ptr(), y.data_ptr(), xs.data_ptr(), ldx, ps.data_ptr(),
-                              None, 1.0, None, 0.0, None, dxs2.data_ptr(), dae.data_ptr(), 1,
-                              dbp2.data_ptr(), B, n, H, C, 0, 1, 0.2, sh)
+        if bf16:
+            lib.sv2n_gat_attn_bwd_bf16dx(dy.data_ptr(), y.data_ptr(), xs.data_ptr(), ldx,
+                                         ps.data_ptr(), None, 1.0, None, 0.0, None,
+                                         dxb2.data_ptr(), ldb, dae.data_ptr(), 1, dbp2.data_ptr(),
+                                         B, n, H, C, 0, 1, 0.2, sh)
+        else:
+            lib.sv2n_gat_attn_bwd(dy.data_ptr(), y.data_ptr(), xs.data_ptr(), ldx, ps.data_ptr(),
+                                  None, 1.0, None, 0.0, None, dxs2.data_ptr(), dae.data_ptr(), 1,
+                                  dbp2.data_ptr(), B, n, H, C, 0, 1, 0.2, sh)
 
     peak = BF16_MFMA_PEAK_TFLOPS if bf16 else BF16X3_PEAK_TFLOPS
     gflop = 2.0 * N * HC * F + 4.0 * N * HC   # algorithmic: H·C columns
     rows = {
-        "gemm_fwd": (gemm_fwd, "mfma", gflop, 4.0 * (N * F + N * ldx) + (2 if bf16 else 6) * ldx * F,
-                     peak),
-        "wgrad_node": (wgrad, "mfma", gflop, 4.0 * (N * F + N * ldx + 3 * HC * F), peak),
+        # bf16: x read (fp32) and written once more as bf16
+        "gemm_fwd": (gemm_fwd, "mfma", gflop, 4.0 * (N * F + N * ldx) + (2 if bf16 else 6) * ldx * F
+                     + (2.0 * N * kb if bf16 else 0.0), peak),
+        # bf16: both operands bf16 in memory; gW (and the fold's W) read and written
+        "wgrad_node": (wgrad, "mfma", gflop,
+                       (2.0 * (N * kb + N * ldb) if bf16 else 4.0 * (N * F + N * ldx))
+                       + 4.0 * 3 * HC * F, peak),
         "gat_attn_fwd": (attn_fwd, "hbm", 2.0 * B * n * n * HC,
                          4.0 * (xs.numel() + ae.numel() + y.numel() + ps.numel()), None),
         "gat_attn_bwd": (attn_bwd, "hbm", 4.0 * B * n * n * HC,
@@ -822,7 +855,8 @@ def main_c3(args, dev, cfg):
     roof, table = None, {}
     if not args.no_kernel_table:
         table = kernel_table_c3(build_model(dev, cfg), cfg, args.precision)
-        _, roof = roofline_entry(table)
+        kname, roof = roofline_entry(table)
+        roof["traffic"] = load_traffic(f"c3_{args.precision}:" + kname)
     if not args.no_cpu_baseline:
         model = build_model(dev, cfg)
         cpu = cpu_baseline(model, cfg, min(args.cpu_batch, 16))

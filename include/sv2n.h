@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 13
+#define SV2N_ABI_VERSION 14
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -189,6 +189,19 @@ int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* xs, int ldx,
                       int64_t num_graphs, int n, int heads, int channels, int concat,
                       int act, float negative_slope, hipStream_t stream);
 
+/* sv2n_gat_attn_bwd writing dxs as bf16 (round to nearest even) into
+ * dxs_bf16 [N][ld_dxs] (ld_dxs >= ldx, % 8 == 0, 16-B aligned; columns past
+ * ldx zero) instead of fp32 (ABI 14): the bf16 execution mode's
+ * weight-gradient operand (sv2n_gat_wgrad_node_bf16b), rounded exactly as
+ * that GEMM's staging would round the fp32 dxs. */
+int sv2n_gat_attn_bwd_bf16dx(const float* dy, const float* y, const float* xs, int ldx,
+                             const float* psave, const uint8_t* keep, float keep_scale,
+                             const float* post_u, float post_p, const uint32_t* rowmask,
+                             uint16_t* dxs_bf16, int ld_dxs, float* dae, int ae_edge_order,
+                             float* dbias_partial, int64_t num_graphs, int n, int heads,
+                             int channels, int concat, int act, float negative_slope,
+                             hipStream_t stream);
+
 /* sv2n_gat_attn_bwd with the edge-logit weight gradient of EVERY layer fused
  * in (ABI 12; replaces sv2n_edge_logits_bwd for canonical batches, reference
  * GATConv lin_edge / att_edge backward, utils/models.py:146): the workgroup
@@ -262,6 +275,13 @@ int sv2n_gemm_f32x3_relu(const float* A, int64_t lda, const uint16_t* Bp, float*
  * sv2n_split3 planes of B (= bf16_rn(B), [N][Kp]); planes 1-2 are not read. */
 int sv2n_gemm_bf16(const float* A, int64_t lda, const uint16_t* Bp, float* C, int64_t ldc,
                    int64_t M, int64_t N, int64_t K, hipStream_t stream);
+/* sv2n_gemm_bf16 that also leaves bf16(A) in a_bf16 [M][ld_ab] (ld_ab >=
+ * K rounded up to 64, % 8 == 0, 16-B aligned; zero past K): written by the
+ * GEMM's own operand staging on the large-tile path (ABI 14), for the
+ * weight-gradient GEMM of the same layer (sv2n_gat_wgrad_node_bf16b). */
+int sv2n_gemm_bf16_export(const float* A, int64_t lda, const uint16_t* Bp, float* C,
+                          int64_t ldc, int64_t M, int64_t N, int64_t K, uint16_t* a_bf16,
+                          int64_t ld_ab, hipStream_t stream);
 
 /* Weight preparation for one GAT layer (replaces, per step, PyG's separate
  * (x_src*att_src).sum(-1) / (x_dst*att_dst).sum(-1) and lin_edge·att_edge
@@ -351,6 +371,19 @@ int sv2n_gat_wgrad_node_bf16(const float* x, int64_t ld_x, const float* dxs, int
                              const float* dbias_partial, int num_parts, int bias_len, float* gW,
                              float* g_att_src, float* g_att_dst, float* g_bias, float* workspace,
                              int64_t workspace_floats, hipStream_t stream);
+
+/* sv2n_gat_wgrad_node_bf16 on operands already in bf16 (ABI 14): x_bf16
+ * [num_nodes][ld_xb] (sv2n_gemm_bf16_export of the layer's projection) and
+ * dxs_bf16 [num_nodes][ld_db] (sv2n_gat_attn_bwd_bf16dx); ld % 8 == 0, 16-B
+ * aligned, in_features % 4 == 0, gW required.  Same results as
+ * sv2n_gat_wgrad_node_bf16 on the fp32 operands; same workspace. */
+int sv2n_gat_wgrad_node_bf16b(const uint16_t* x_bf16, int64_t ld_xb, const uint16_t* dxs_bf16,
+                              int64_t ld_db, int64_t num_nodes, int in_features, int ldx,
+                              const float* W, const float* att_src, const float* att_dst,
+                              int heads, int channels, const float* dbias_partial, int num_parts,
+                              int bias_len, float* gW, float* g_att_src, float* g_att_dst,
+                              float* g_bias, float* workspace, int64_t workspace_floats,
+                              hipStream_t stream);
 
 /* Backward of the edge fold: ACCUMULATE gW_edge[h*C+c][d] += dwfold[d][col0+h]·att_edge[h*C+c]
  * and g_att_edge[h*C+c] += Σ_d W_edge[h*C+c][d]·dwfold[d][col0+h]. */

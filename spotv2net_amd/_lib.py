@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SV2N_LIB: an alternative build of the same library (diagnostic builds, e.g.
 # tools/stamps.py); default the in-tree one
 LIB_PATH = os.environ.get("SV2N_LIB") or os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p
@@ -56,6 +56,11 @@ _SIGNATURES = {
                                  _i32, _i32, _i32, _i32, _i32, _f32, _p]),
     "sv2n_gat_attn_bwd": (_i32, [_p, _p, _p, _i32, _p, _p, _f32, _p, _f32, _p, _p, _p, _i32, _p,
                                  _i64, _i32, _i32, _i32, _i32, _i32, _f32, _p]),
+    # dy y xs ldx psave keep keep_scale post_u post_p rowmask dxb ld dae eo dbp B n H C concat
+    # act slope stream
+    "sv2n_gat_attn_bwd_bf16dx": (_i32, [_p, _p, _p, _i32, _p, _p, _f32, _p, _f32, _p, _p, _i32,
+                                        _p, _i32, _p, _i64, _i32, _i32, _i32, _i32, _i32, _f32,
+                                        _p]),
     "sv2n_gat_attn_fwd_head_mse_supported": (_i32, [_i64, _i32, _i32, _i32, _i32]),
     "sv2n_gat_attn_fwd_head_mse_workspace": (_i64, [_i64, _i32, _i32, _i32]),
     # xs ldx ae eo rowmask bias keep keep_scale dz psave post_u post_p hw hb target loss
@@ -91,6 +96,7 @@ _SIGNATURES = {
     "sv2n_gemm_f32x3": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "sv2n_gemm_f32x3_relu": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "sv2n_gemm_bf16": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "sv2n_gemm_bf16_export": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "sv2n_gemm_f32_workspace": (_i64, [_i64, _i64, _i64]),
     "sv2n_gemm_f32_slabs_count": (_i32, [_i64, _i64, _i64]),
     "sv2n_gemm_f32_slabs": (_i32, [_i32, _i32, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
@@ -107,6 +113,8 @@ _SIGNATURES = {
     "sv2n_gat_wgrad_node_bf16_workspace": (_i64, [_i64, _i32, _i32, _i32, _i32]),
     "sv2n_gat_wgrad_node_bf16": (_i32, [_p, _i64, _p, _i32, _i64, _i32, _p, _p, _p, _i32, _i32,
                                         _p, _i32, _i32, _p, _p, _p, _p, _p, _i64, _p]),
+    "sv2n_gat_wgrad_node_bf16b": (_i32, [_p, _i64, _p, _i64, _i64, _i32, _i32, _p, _p, _p, _i32,
+                                         _i32, _p, _i32, _i32, _p, _p, _p, _p, _p, _i64, _p]),
     "sv2n_gat_prep_bwd_node": (_i32, [_p, _i32, _p, _p, _p, _i32, _i32, _i32, _p, _i32, _i32, _p,
                                       _p, _p, _p, _p, _i64, _p]),
     "sv2n_gat_prep_bwd_edge": (_i32, [_p, _i32, _i32, _p, _p, _i32, _i32, _i32, _p, _p, _p]),

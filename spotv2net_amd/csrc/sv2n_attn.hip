@@ -21,7 +21,7 @@ void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, 
                     int ldx, const float* psave, const uint8_t* keep, float keep_scale,
                     const float* post_u, float post_p, const uint32_t* rowmask, float* dxs, float* dae, int ae_edge_order,
                     float* dbias, int n, int H, int C, int concat, int act, float slope,
-                    const EdgeTail& et);
+                    const EdgeTail& et, unsigned short* dxb = nullptr, int ldb = 0);
 bool attn_canon_edge_tail_ok(int64_t B, int n, int H, int C, int D, int hlp);
 }  // namespace sv2n
 
@@ -108,6 +108,27 @@ extern "C" int sv2n_gat_attn_bwd(const float* dy, const float* y, const float* x
                  rowmask, dxs,
                  dae, ae_edge_order, dbias_partial, n, heads, channels, concat, act,
                  negative_slope, EdgeTail{});
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_gat_attn_bwd_bf16dx(const float* dy, const float* y, const float* xs,
+                                        int ldx, const float* psave, const uint8_t* keep,
+                                        float keep_scale, const float* post_u, float post_p,
+                                        const uint32_t* rowmask, uint16_t* dxs_bf16, int ld_dxs,
+                                        float* dae, int ae_edge_order, float* dbias_partial,
+                                        int64_t num_graphs, int n, int heads, int channels,
+                                        int concat, int act, float negative_slope,
+                                        hipStream_t stream) {
+  if (!dy || !y || !xs || !psave || !dxs_bf16 || !dbias_partial) return SV2N_ERR_ARG;
+  if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
+  if (ld_dxs < ldx || (ld_dxs & 7)) return SV2N_ERR_SHAPE;
+  if ((uintptr_t)dxs_bf16 & 15) return SV2N_ERR_ALIGN;
+  if (post_u && !(post_p >= 0.f && post_p < 1.f)) return SV2N_ERR_ARG;
+  if (ae_edge_order && (rowmask || n < 2)) return SV2N_ERR_ARG;
+  attn_canon_bwd(num_graphs, stream, dy, y, xs, ldx, psave, keep, keep_scale, post_u, post_p,
+                 rowmask, nullptr, dae, ae_edge_order, dbias_partial, n, heads, channels, concat,
+                 act, negative_slope, EdgeTail{}, reinterpret_cast<unsigned short*>(dxs_bf16),
+                 ld_dxs);
   return (int)hipGetLastError();
 }
 

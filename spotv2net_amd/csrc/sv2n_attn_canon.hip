@@ -46,6 +46,18 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 // row of accumulator register r in lane half hf (32x32 MFMA C/D layout)
 __device__ __forceinline__ int crow(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
 
+// f32 -> bf16 bits, round to nearest even (v_cvt_pk_bf16_f32, as the bf16
+// GEMMs' operand staging)
+__device__ __forceinline__ unsigned short to_bf16(float x) {
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 v = {x, 0.f};
+  return (unsigned short)(__builtin_bit_cast(unsigned, __builtin_convertvector(v, b2)) & 0xffffu);
+}
+__device__ __forceinline__ void bst16_s(rsrc_t r, int voff, int soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b16(to_bf16(v), r, voff, soff, 0);
+}
+
 // dword buffer load / store with a wave-uniform scalar offset
 __device__ __forceinline__ float bld_s(rsrc_t r, int voff, int soff) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
@@ -411,21 +423,23 @@ __global__ __launch_bounds__(256) void k_head_fuse_finish(const float* __restric
                                                           float* __restrict__ g_w,
                                                           float* __restrict__ g_b,
                                                           float* __restrict__ loss) {
+  constexpr int U = 32;  // loads in flight per thread and round
   __shared__ float s_red[16][17];
   const int lo = threadIdx.x & 15, grp = threadIdx.x >> 4;
   const int o = blockIdx.x * 16 + lo, O = OC + 2;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  if (o < O) {
-    int64_t b = grp;
-    for (; b + 48 < B; b += 64) {
-      a0 += part[b * O + o];
-      a1 += part[(b + 16) * O + o];
-      a2 += part[(b + 32) * O + o];
-      a3 += part[(b + 48) * O + o];
+  const rsrc_t rp = make_rsrc(part, (uint32_t)(B * O) * 4u);
+  float a = 0.f;
+  for (int64_t b0 = 0; b0 < B; b0 += 16 * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t b = b0 + grp + 16 * u;
+      v[u] = bld(rp, (o < O && b < B) ? (int)(b * O + o) * 4 : OOB);
     }
-    for (; b < B; b += 16) a0 += part[b * O + o];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a += v[u];
   }
-  s_red[grp][lo] = (a0 + a1) + (a2 + a3);
+  s_red[grp][lo] = a;
   __syncthreads();
   if (grp == 0 && o < O) {
     float sm = 0.f;
@@ -599,7 +613,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     const float* __restrict__ post_u, float post_p, float post_scale,
     const uint32_t* __restrict__ rowmask, float* __restrict__ dxs, float* __restrict__ dae,
     int ae_edge_order, float* __restrict__ dbias_part, int n, int H, int C, float slope, int S,
-    int HS, int WPH, int64_t B, EdgeTail et) {
+    int HS, int WPH, int64_t B, EdgeTail et, unsigned short* __restrict__ dxb, int ldb) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sP = smem;
   float* sArea = sP + HS * 32 * PB;
@@ -622,7 +636,18 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   const float invH = 1.f / (float)H;
   const int h0 = split * HS, nhs = min(HS, H - h0);  // this split's heads
   const rsrc_t rx = make_rsrc(xs + g * n * ldx, (uint32_t)(n * ldx) * 4u);
-  const rsrc_t rdx = make_rsrc(dxs + g * n * ldx, (uint32_t)(n * ldx) * 4u);
+  // dxb != NULL (uniform): dxs goes out as bf16 [N][ldb] instead (the bf16
+  // weight-gradient GEMM's operand, rounded as its staging would)
+  const bool bfo = dxb != nullptr;
+  const rsrc_t rdx = make_rsrc(bfo ? nullptr : dxs + g * n * ldx, bfo ? 0u : (uint32_t)(n * ldx) * 4u);
+  const rsrc_t rdb16 = make_rsrc(bfo ? dxb + g * n * ldb : nullptr, bfo ? (uint32_t)(n * ldb) * 2u : 0u);
+  auto put = [&](int j, int col, float v) __attribute__((always_inline)) {  // dxs[j][col]
+    if (bfo)
+      __builtin_amdgcn_raw_buffer_store_b16(to_bf16(v), rdb16, j < n ? (j * ldb + col) * 2 : OOB,
+                                            0, 0);
+    else
+      bst(rdx, j < n ? (j * ldx + col) * 4 : OOB, v);
+  };
   const rsrc_t rdy = make_rsrc(dy + g * n * OC, (uint32_t)(n * OC) * 4u);
   const rsrc_t ryy = make_rsrc(y + g * n * OC, (uint32_t)(n * OC) * 4u);
   const rsrc_t rps = make_rsrc(psave + g * H * 1024, (uint32_t)H * 4096u);
@@ -831,7 +856,12 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 #pragma unroll
       for (int kk = 0; kk < 16; ++kk)
         D = __builtin_amdgcn_mfma_f32_32x32x2f32(pcol[kk * PB], zcol[kk * CS], D, 0, 0, 0);
-      {
+      if (bfo) {
+        const int voff = l32 < cw ? (4 * half * ldb + h * C + c0 + l32) * 2 : OOB;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          bst16_s(rdb16, voff, ((r & 3) + 8 * (r >> 2)) * ldb * 2, CONCAT ? D[r] : D[r] * invH);
+      } else {
         const int voff = l32 < cw ? (4 * half * ldx + h * C + c0 + l32) * 4 : OOB;
 #pragma unroll
         for (int r = 0; r < 16; ++r)
@@ -930,17 +960,17 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 #pragma unroll
     for (int r = 0; r < 16; ++r) v += col[r * DS];
     v += __shfl_xor(v, 1, 64);
-    bst(rdx, (part == 0 && j < n) ? (j * ldx + HC + h0 + hl) * 4 : OOB, v);
+    if (part == 0) put(j, HC + h0 + hl, v);
   }
   for (int q = t; q < 32 * nhs; q += THREADS) {
     const int j = q & 31, hl = q >> 5;
-    bst(rdx, j < n ? (j * ldx + HC + H + h0 + hl) * 4 : OOB, sDad[hl * 32 + j]);
+    put(j, HC + H + h0 + hl, sDad[hl * 32 + j]);
   }
-  const int npad = ldx - HC - 2 * H;
+  const int npad = (bfo ? ldb : ldx) - HC - 2 * H;
   if (split == 0)
     for (int q = t; q < 32 * npad; q += THREADS) {
       const int j = q & 31, c2 = q >> 5;
-      bst(rdx, j < n ? (j * ldx + HC + 2 * H + c2) * 4 : OOB, 0.f);
+      put(j, HC + 2 * H + c2, 0.f);
     }
   if (etail) edge_grad_tail(et, g, n, H, sDL, sSh, sDec, smem);
   SV2N_STAMP(12, SV2N_T());
@@ -1006,7 +1036,7 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
                              float keep_scale, const float* post_u, float post_p,
                              const uint32_t* rowmask, float* dxs, float* dae,
                              int ae_edge_order, float* dbias, int n, int H, int C, float slope,
-                             const EdgeTail& et) {
+                             const EdgeTail& et, unsigned short* dxb, int ldb) {
   const CanonBwdPlan pl = canon_bwd_plan(B, H, C, et.ea != nullptr);
   const size_t lds = attn_canon_bwd_lds(pl.HS);
   const unsigned grid = canon_grid(B, pl.S);
@@ -1019,7 +1049,8 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
     hipLaunchKernelGGL(kern, dim3(grid), dim3(canon::THREADS), lds, st, dy, y, xs, ldx, psave,
                        keep, keep_scale, post_u, post_p,
                        post_u ? (float)(1.0 / (1.0 - (double)post_p)) : 1.f, rowmask, dxs, dae,
-                       ae_edge_order, dbias, n, H, C, slope, pl.S, pl.HS, pl.WPH, B, et);
+                       ae_edge_order, dbias, n, H, C, slope, pl.S, pl.HS, pl.WPH, B, et, dxb,
+                       ldb);
   };
   const int nch = (C + 31) >> 5;
   const bool resident = grid <= 2 * CANON_CUS;
@@ -1052,10 +1083,11 @@ void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, 
                     int ldx, const float* psave, const uint8_t* keep, float keep_scale,
                     const float* post_u, float post_p, const uint32_t* rowmask, float* dxs,
                     float* dae, int ae_edge_order, float* dbias, int n, int H, int C, int concat,
-                    int act, float slope, const EdgeTail& et) {
+                    int act, float slope, const EdgeTail& et, unsigned short* dxb, int ldb) {
 #define SV2N_CB(A, CC, K)                                                                      \
   launch_canon_bwd<A, CC, K>(B, st, dy, y, xs, ldx, psave, keep, keep_scale, post_u, post_p,   \
-                             rowmask, dxs, dae, ae_edge_order, dbias, n, H, C, slope, et)
+                             rowmask, dxs, dae, ae_edge_order, dbias, n, H, C, slope, et, dxb, \
+                             ldb)
 #define SV2N_CB_ACT(CC, K)                 \
   switch (act) {                           \
     case 0: SV2N_CB(0, CC, K); break;      \

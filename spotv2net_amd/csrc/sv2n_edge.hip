@@ -320,25 +320,28 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
 }
 
 // out[o] = Σ_b partial[b][o] in a fixed order: a block owns 16 outputs, 16
-// row groups each sum every 16th partial with 8 buffer loads in flight per
-// round (out-of-range offsets read 0), then combine through LDS.
+// row groups each sum every 16th partial with 32 buffer loads in flight per
+// round (out-of-range offsets read 0; round 4: 8 in flight took 5.7 us for
+// the 1,024 partials of the C2 edge gradient, a chain of memory round trips),
+// then combine through LDS.
 __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ partial,
                                                          int nparts, int O,
                                                          float* __restrict__ out) {
+  constexpr int U = 32;
   __shared__ float s_red[16][17];
   const int lo = threadIdx.x & 15, grp = threadIdx.x >> 4;
   const int o = blockIdx.x * 16 + lo;
   const rsrc_t rp = make_rsrc(partial, (uint32_t)nparts * (uint32_t)O * 4u);
   float a = 0.f;
-  for (int b0 = 0; b0 < nparts; b0 += 16 * 8) {
-    float v[8];
+  for (int b0 = 0; b0 < nparts; b0 += 16 * U) {
+    float v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int b = b0 + grp + 16 * u;
       v[u] = bld(rp, (o < O && b < nparts) ? (b * O + o) * 4 : OOB);
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) a += v[u];
+    for (int u = 0; u < U; ++u) a += v[u];
   }
   s_red[grp][lo] = a;
   __syncthreads();

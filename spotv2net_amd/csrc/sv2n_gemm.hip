@@ -20,6 +20,7 @@
 #include "sv2n_gemm3_kernel.h"
 #include "sv2n_gemm_tt.h"
 #include "sv2n_gemm_bw.h"
+#include <algorithm>
 
 namespace sv2n {
 
@@ -593,9 +594,13 @@ static void launch_wgrad_bf16(const GemmPlan& p, hipStream_t st, const float* x,
 // N 1260, K 3840, tools/gemm_bw_tune.hip): 128 x 256 split 2 68.3 us, the
 // round-3 k_gemm_tt<128, 128, 1> 75.1, 256 x 128 117.6, 256 x 192 247.7
 constexpr int BWT_BM = 128, BWT_BN = 256;
-static GemmPlan plan_wgrad_bw(int64_t ldx, int64_t F, int64_t K) {
+// both operands already bf16 in memory (sv2n_gat_wgrad_node_bf16b): 128 x 128
+// tiles, split 2 on the C3 shape (48.6 us; 128 x 256: 51.1)
+constexpr int BWB_BM = 128, BWB_BN = 128;
+static GemmPlan plan_wgrad_bw(int64_t ldx, int64_t F, int64_t K, int BM = BWT_BM,
+                              int BN = BWT_BN) {
   GemmPlan p{};
-  const int64_t tiles = ((ldx + BWT_BM - 1) / BWT_BM) * ((F + BWT_BN - 1) / BWT_BN);
+  const int64_t tiles = ((ldx + BM - 1) / BM) * ((F + BN - 1) / BN);
   int64_t sk = std::max<int64_t>(1, (240 + tiles / 2) / tiles);
   sk = std::min<int64_t>(sk, std::max<int64_t>(1, K / 512));
   sk = std::min<int64_t>(sk, 8);
@@ -621,12 +626,38 @@ static void launch_wgrad_bf16_t(const GemmPlan& p, hipStream_t st, const float* 
                      p.kslice, nm, nn);
 }
 
+static void launch_wgrad_bf16b(const GemmPlan& p, hipStream_t st, const unsigned short* xb,
+                               int64_t ld_xb, const unsigned short* db, int64_t ld_db,
+                               int64_t ldx, int64_t F, int64_t K, float* out) {
+  using Cfg = GemmBWCfg<BWB_BM, BWB_BN, true, false, false>;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)k_gemm_bw<BWB_BM, BWB_BN, true, false, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
+    return true;
+  }();
+  (void)attr;
+  const int nm = (int)((ldx + BWB_BM - 1) / BWB_BM), nn = (int)((F + BWB_BN - 1) / BWB_BN);
+  const dim3 grid((unsigned)(((nm + 7) / 8) * 8 * nn), 1, (unsigned)p.splitk);
+  hipLaunchKernelGGL((k_gemm_bw<BWB_BM, BWB_BN, true, false, false>), grid, dim3(Cfg::THREADS),
+                     Cfg::LDS, st, (const void*)db, ld_db, (const void*)xb, ld_xb, out, F, ldx, F,
+                     K, p.kslice, nm, nn);
+}
+
+// bf16 operands in memory (precision 1 with xb / db set): x_bf16 [K][ld_xb],
+// dxs_bf16 [K][ld_db]
+struct Bf16Ops {
+  const unsigned short* xb;
+  int64_t ld_xb;
+  const unsigned short* db;
+  int64_t ld_db;
+};
+
 static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* dxs, int ldx,
                       int64_t num_nodes, int in_features, const float* W, const float* att_src,
                       const float* att_dst, int heads, int channels, const float* dbias_partial,
                       int num_parts, int bias_len, float* gW, float* g_att_src, float* g_att_dst,
                       float* g_bias, float* workspace, int64_t workspace_floats,
-                      hipStream_t stream);
+                      hipStream_t stream, const Bf16Ops& bo = Bf16Ops{});
 
 extern "C" int sv2n_gat_wgrad_node(const float* x, int64_t ld_x, const float* dxs, int ldx,
                                    int64_t num_nodes, int in_features, const float* W,
@@ -644,8 +675,29 @@ extern "C" int64_t sv2n_gat_wgrad_node_bf16_workspace(int64_t num_nodes, int in_
                                                       int heads, int channels) {
   if (num_nodes <= 0 || in_features <= 0 || ldx <= 0 || heads <= 0 || channels <= 0) return 0;
   const GemmPlan p = plan_gemm_bf16t(in_features, ldx, num_nodes);
-  const int sk = std::max(p.splitk, plan_wgrad_bw(ldx, in_features, num_nodes).splitk);
+  const int sk = std::max({p.splitk, plan_wgrad_bw(ldx, in_features, num_nodes).splitk,
+                           plan_wgrad_bw(ldx, in_features, num_nodes, BWB_BM, BWB_BN).splitk});
   return (int64_t)in_features * ldx * (sk > 1 ? 1 + sk : 1);
+}
+
+extern "C" int sv2n_gat_wgrad_node_bf16b(const uint16_t* x_bf16, int64_t ld_xb,
+                                         const uint16_t* dxs_bf16, int64_t ld_db,
+                                         int64_t num_nodes, int in_features, int ldx,
+                                         const float* W, const float* att_src,
+                                         const float* att_dst, int heads, int channels,
+                                         const float* dbias_partial, int num_parts, int bias_len,
+                                         float* gW, float* g_att_src, float* g_att_dst,
+                                         float* g_bias, float* workspace,
+                                         int64_t workspace_floats, hipStream_t stream) {
+  if (!x_bf16 || !dxs_bf16) return SV2N_ERR_ARG;
+  if (ld_xb < in_features || ld_db < ldx || (ld_xb & 7) || (ld_db & 7)) return SV2N_ERR_SHAPE;
+  if (((uintptr_t)x_bf16 & 15) || ((uintptr_t)dxs_bf16 & 15)) return SV2N_ERR_ALIGN;
+  if (!gW) return SV2N_ERR_ARG;  // the bf16-operand form always produces the weight gradient
+  const Bf16Ops bo{reinterpret_cast<const unsigned short*>(x_bf16), ld_xb,
+                   reinterpret_cast<const unsigned short*>(dxs_bf16), ld_db};
+  return wgrad_node(1, nullptr, in_features, nullptr, ldx, num_nodes, in_features, W, att_src,
+                    att_dst, heads, channels, dbias_partial, num_parts, bias_len, gW, g_att_src,
+                    g_att_dst, g_bias, workspace, workspace_floats, stream, bo);
 }
 
 extern "C" int sv2n_gat_wgrad_node_bf16(const float* x, int64_t ld_x, const float* dxs, int ldx,
@@ -665,12 +717,13 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
                       const float* att_dst, int heads, int channels, const float* dbias_partial,
                       int num_parts, int bias_len, float* gW, float* g_att_src, float* g_att_dst,
                       float* g_bias, float* workspace, int64_t workspace_floats,
-                      hipStream_t stream) {
+                      hipStream_t stream, const Bf16Ops& bo) {
   const bool weights = gW || g_att_src || g_att_dst;
+  const bool bfin = bo.xb != nullptr;
   const int F = in_features, H = heads, C = channels, HC = heads * channels;
   if (H < 1 || C < 1 || F < 1 || num_nodes < 1) return SV2N_ERR_ARG;
   if (H > SV2N_MAX_HEADS || ldx < HC + 2 * H) return SV2N_ERR_SHAPE;
-  if (weights && (!x || !dxs || !W || !att_src || !att_dst)) return SV2N_ERR_ARG;
+  if (weights && ((!bfin && (!x || !dxs)) || !W || !att_src || !att_dst)) return SV2N_ERR_ARG;
   if (weights && ld_x < F) return SV2N_ERR_SHAPE;
   if ((int64_t)F * ldx >= (int64_t)1 << 29 || (int64_t)HC * F >= (int64_t)1 << 29)
     return SV2N_ERR_SHAPE;  // 32-bit buffer offsets
@@ -684,16 +737,21 @@ static int wgrad_node(int precision, const float* x, int64_t ld_x, const float* 
   float* slabs = T + (int64_t)F * ldx;
   if (weights && precision) {
     // bf16 operands: both k-strided, rounded while staged (k_gemm_tt, NP = 1)
-    if (((uintptr_t)x & 15) || (ld_x & 3) || ((uintptr_t)dxs & 15) || (ldx & 3) || F < 4 ||
-        ldx < 4)
+    if (!bfin && (((uintptr_t)x & 15) || (ld_x & 3) || ((uintptr_t)dxs & 15) || (ldx & 3) ||
+                  F < 4 || ldx < 4))
       return SV2N_ERR_ALIGN;
     if (num_nodes * std::max<int64_t>(ld_x, ldx) * 4 > 0x7fffffff) return SV2N_ERR_SHAPE;
+    if (bfin && ((F & 3) != 0 || !gW)) return SV2N_ERR_SHAPE;
     const GemmPlan p = plan_gemm_bf16t(F, ldx, num_nodes);
     if ((F & 3) == 0 && gW) {
       // dWaug [ldx][F] as pt.splitk slabs, summed by the epilogue launch itself
-      const GemmPlan pt = plan_wgrad_bw(ldx, F, num_nodes);
+      const GemmPlan pt = bfin ? plan_wgrad_bw(ldx, F, num_nodes, BWB_BM, BWB_BN)
+                               : plan_wgrad_bw(ldx, F, num_nodes);
       float* S = pt.splitk > 1 ? slabs : T;
-      launch_wgrad_bf16_t(pt, stream, x, ld_x, dxs, ldx, F, num_nodes, S);
+      if (bfin)
+        launch_wgrad_bf16b(pt, stream, bo.xb, bo.ld_xb, bo.db, bo.ld_db, ldx, F, num_nodes, S);
+      else
+        launch_wgrad_bf16_t(pt, stream, x, ld_x, dxs, ldx, F, num_nodes, S);
       const int nfc = (F / 4 + 63) / 64, nrow = (HC + WT_RB - 1) / WT_RB;
       const int natt = (g_att_src || g_att_dst) ? (HC + ATT_RB - 1) / ATT_RB : 0;
       size_t lds = 0;

@@ -109,12 +109,42 @@ static int launch_gemm_bf16(hipStream_t st, const float* A, int64_t lda, const u
 
 using namespace sv2n;
 
+// a[m][k] -> bf16 (RNE) into ab [M][ld_ab], zero for K <= k < ld_ab
+__global__ __launch_bounds__(256) void k_to_bf16(const float* __restrict__ a, int64_t lda,
+                                                 int64_t M, int64_t K,
+                                                 unsigned short* __restrict__ ab, int64_t ld_ab) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * ld_ab) return;
+  const int64_t m = i / ld_ab, k = i - m * ld_ab;
+  ab[i] = k < K ? (unsigned short)(bf16_pk(a[m * lda + k], 0.f) & 0xffffu) : (unsigned short)0;
+}
+
+static int gemm_bf16(const float* A, int64_t lda, const uint16_t* Bp, float* C, int64_t ldc,
+                     int64_t M, int64_t N, int64_t K, uint16_t* a_bf16, int64_t ld_ab,
+                     hipStream_t stream);
+
 extern "C" int sv2n_gemm_bf16(const float* A, int64_t lda, const uint16_t* Bp, float* C,
                               int64_t ldc, int64_t M, int64_t N, int64_t K, hipStream_t stream) {
+  return gemm_bf16(A, lda, Bp, C, ldc, M, N, K, nullptr, 0, stream);
+}
+
+extern "C" int sv2n_gemm_bf16_export(const float* A, int64_t lda, const uint16_t* Bp, float* C,
+                                     int64_t ldc, int64_t M, int64_t N, int64_t K,
+                                     uint16_t* a_bf16, int64_t ld_ab, hipStream_t stream) {
+  if (!a_bf16) return SV2N_ERR_ARG;
+  if (ld_ab < (K + 63) / 64 * 64 || (ld_ab & 7)) return SV2N_ERR_SHAPE;
+  if ((uintptr_t)a_bf16 & 15) return SV2N_ERR_ALIGN;
+  return gemm_bf16(A, lda, Bp, C, ldc, M, N, K, a_bf16, ld_ab, stream);
+}
+
+static int gemm_bf16(const float* A, int64_t lda, const uint16_t* Bp, float* C, int64_t ldc,
+                     int64_t M, int64_t N, int64_t K, uint16_t* a_bf16, int64_t ld_ab,
+                     hipStream_t stream) {
   if (!A || !Bp || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldc < N) return SV2N_ERR_ARG;
   if (((uintptr_t)A & 15) || (lda & 3) || ((uintptr_t)Bp & 15)) return SV2N_ERR_ALIGN;
   const int64_t Kp = sv2n_split3_kpad(K);
   const unsigned short* B = reinterpret_cast<const unsigned short*>(Bp);
+  unsigned short* Aex = reinterpret_cast<unsigned short*>(a_bf16);
   if (K % 4 == 0 && (lda & 3) == 0 && M >= 1024 && N >= 384) {
     // large-tile kernel (sv2n_gemm_bw.h): 256 x 192 tiles of 8 waves (round 4;
     // the 128 x 128 k_gemm_bf16nt below was L2-bound on the C3 projection)
@@ -129,8 +159,12 @@ extern "C" int sv2n_gemm_bf16(const float* A, int64_t lda, const uint16_t* Bp, f
     hipLaunchKernelGGL((k_gemm_bw<256, 192, false, true, false>),
                        dim3((unsigned)(((nm + 7) / 8) * 8 * nn)), dim3(Cfg::THREADS), Cfg::LDS,
                        stream, (const void*)A, lda, (const void*)B, Kp, C, ldc, M, N, K,
-                       (int64_t)K, nm, nn);
+                       (int64_t)K, nm, nn, Aex, ld_ab);
     return (int)hipGetLastError();
+  }
+  if (Aex) {  // the other kernels: a separate rounding pass
+    hipLaunchKernelGGL(k_to_bf16, dim3((unsigned)((M * ld_ab + 255) / 256)), dim3(256), 0, stream,
+                       A, lda, M, K, Aex, ld_ab);
   }
   if (K % 4 == 0) {  // k_gemm_bf16nt (sv2n_gemm_bf16.h)
     static bool attr = [] {

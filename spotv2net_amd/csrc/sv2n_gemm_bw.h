@@ -59,7 +59,9 @@ struct GemmBWCfg {
 template <bool F32>
 struct Piece {
   u32x4 v;
-  __device__ __forceinline__ void load(rsrc_t r, int off) { v = bld4_u32(r, off); }
+  __device__ __forceinline__ void load(rsrc_t r, int off, int soff) {
+    v = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0);
+  }
   __device__ __forceinline__ void put(unsigned short* p) const {
     if constexpr (F32) {
       u32x2 w;
@@ -77,7 +79,8 @@ __global__ __launch_bounds__(512) void k_gemm_bw(const void* __restrict__ Av, in
                                                  const void* __restrict__ Bv, int64_t ldb,
                                                  float* __restrict__ C, int64_t ldc, int64_t M,
                                                  int64_t N, int64_t K, int64_t kslice, int nm,
-                                                 int nn) {
+                                                 int nn, unsigned short* __restrict__ Aex = nullptr,
+                                                 int64_t ldex = 0) {
   using Cfg = GemmBWCfg<BM, BN, KO, AF, BF>;
   constexpr int BK = Cfg::BK, TM = Cfg::TM, TN = Cfg::TN, SA = Cfg::SA, SB = Cfg::SB;
   constexpr int IA = Cfg::IA, STAGE = Cfg::STAGE, TH = Cfg::THREADS;
@@ -101,66 +104,85 @@ __global__ __launch_bounds__(512) void k_gemm_bw(const void* __restrict__ Av, in
   const rsrc_t rb = make_rsrc(Bv, (uint32_t)min<int64_t>(bbytes, 0x7fffffff));
 
   // piece i of a tile: KO = false — row i / (BK / P), k-chunk i % (BK / P);
-  // KO = true — k-row i / (R / P), column chunk i % (R / P)
+  // KO = true — k-row i / (R / P), column chunk i % (R / P).  Everything but
+  // the K-step is fixed per thread: the k-independent byte offset (vo), the
+  // row / column bound (ok), the k offset inside a step (kk) and the LDS
+  // offset (lo) are computed once; a step adds its k0 through the wave-uniform
+  // scalar offset (round 4: the per-step 64-bit index arithmetic made the
+  // bf16 weight-gradient GEMM issue ~4,200 VALU per wave against ~890 MFMA).
   Piece<AF> pa[RA];
   Piece<BF> pb[RB];
+  int a_vo[RA], a_kk[RA], a_lo[RA], a_r[RA], a_c[RA];
+  bool a_ok[RA];
+#pragma unroll
+  for (int s = 0; s < RA; ++s) {
+    const int i = min(t + TH * s, Cfg::NA - 1);
+    if constexpr (!KO) {
+      const int r = i / (BK / PA), c = (i - r * (BK / PA)) * PA;
+      a_vo[s] = (int)(((m0 + r) * lda + c) * EA);
+      a_ok[s] = m0 + r < M;
+      a_kk[s] = c;
+      a_r[s] = r;
+      a_c[s] = c;
+      a_lo[s] = r * SA + c;
+    } else {
+      const int r = i / (BM / PA), c = (i - r * (BM / PA)) * PA;
+      a_vo[s] = (int)((r * lda + m0 + c) * EA);
+      a_ok[s] = m0 + c < lda;
+      a_kk[s] = r;
+      a_r[s] = r;
+      a_c[s] = c;
+      a_lo[s] = r * SA + c;
+    }
+  }
+  int b_vo[RB], b_kk[RB], b_lo[RB];
+  bool b_ok[RB];
+#pragma unroll
+  for (int s = 0; s < RB; ++s) {
+    const int i = min(t + TH * s, Cfg::NB - 1);
+    if constexpr (!KO) {
+      const int r = i / (BK / PB), c = (i - r * (BK / PB)) * PB;
+      b_vo[s] = (int)(((n0 + r) * ldb + c) * EB);
+      b_ok[s] = n0 + r < N;
+      b_kk[s] = c;
+      b_lo[s] = r * SB + c;
+    } else {
+      const int r = i / (BN / PB), c = (i - r * (BN / PB)) * PB;
+      b_vo[s] = (int)((r * ldb + n0 + c) * EB);
+      b_ok[s] = n0 + c < ldb;
+      b_kk[s] = r;
+      b_lo[s] = r * SB + c;
+    }
+  }
   auto load = [&](int64_t k0) __attribute__((always_inline)) {
+    const int kr = (int)(kend - k0);  // k offsets >= kr are past the slice
+    const int sa_off = (int)(KO ? k0 * lda * EA : k0 * EA);
+    const int sb_off = (int)(KO ? k0 * ldb * EB : k0 * EB);
 #pragma unroll
-    for (int s = 0; s < RA; ++s) {
-      const int i = min(t + TH * s, Cfg::NA - 1);
-      int off;
-      if constexpr (!KO) {
-        const int r = i / (BK / PA), c = (i - r * (BK / PA)) * PA;
-        const int64_t m = m0 + r, k = k0 + c;
-        off = (m < M && k < kend) ? (int)((m * lda + k) * EA) : OOB;
-      } else {
-        const int r = i / (BM / PA), c = (i - r * (BM / PA)) * PA;
-        const int64_t k = k0 + r, m = m0 + c;
-        off = (k < kend && m < lda) ? (int)((k * lda + m) * EA) : OOB;
-      }
-      pa[s].load(ra, off);
-    }
+    for (int s = 0; s < RA; ++s)
+      pa[s].load(ra, (a_ok[s] && a_kk[s] < kr) ? a_vo[s] : OOB, sa_off);
 #pragma unroll
-    for (int s = 0; s < RB; ++s) {
-      const int i = min(t + TH * s, Cfg::NB - 1);
-      int off;
-      if constexpr (!KO) {
-        const int r = i / (BK / PB), c = (i - r * (BK / PB)) * PB;
-        const int64_t n = n0 + r, k = k0 + c;
-        off = (n < N && k < kend) ? (int)((n * ldb + k) * EB) : OOB;
-      } else {
-        const int r = i / (BN / PB), c = (i - r * (BN / PB)) * PB;
-        const int64_t k = k0 + r, n = n0 + c;
-        off = (k < kend && n < ldb) ? (int)((k * ldb + n) * EB) : OOB;
-      }
-      pb[s].load(rb, off);
-    }
+    for (int s = 0; s < RB; ++s)
+      pb[s].load(rb, (b_ok[s] && b_kk[s] < kr) ? b_vo[s] : OOB, sb_off);
   };
+  // Aex (NT, fp32 A only): the column-tile-0 workgroups also store the
+  // bf16-rounded A tile to Aex [M][ldex] (columns up to the K-step end, zero
+  // past K), a bf16 copy of the operand for a later bf16 GEMM
+  const bool ex = !KO && AF && Aex != nullptr && nb == 0;
   // (surplus pieces repeat the last one: same value, same address)
-  auto store = [&](unsigned short* st) __attribute__((always_inline)) {
+  auto store = [&](unsigned short* st, int64_t k0) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < RA; ++s) {
-      const int i = min(t + TH * s, Cfg::NA - 1);
-      if constexpr (!KO) {
-        const int r = i / (BK / PA), c = (i - r * (BK / PA)) * PA;
-        pa[s].put(st + r * SA + c);
-      } else {
-        const int r = i / (BM / PA), c = (i - r * (BM / PA)) * PA;
-        pa[s].put(st + r * SA + c);
+      pa[s].put(st + a_lo[s]);
+      if constexpr (!KO && AF) {
+        if (ex && a_ok[s] && k0 + a_c[s] < ldex)
+          *reinterpret_cast<u32x2*>(Aex + (m0 + a_r[s]) * ldex + k0 + a_c[s]) =
+              *reinterpret_cast<const u32x2*>(st + a_lo[s]);
       }
     }
     unsigned short* sb = st + IA;
 #pragma unroll
-    for (int s = 0; s < RB; ++s) {
-      const int i = min(t + TH * s, Cfg::NB - 1);
-      if constexpr (!KO) {
-        const int r = i / (BK / PB), c = (i - r * (BK / PB)) * PB;
-        pb[s].put(sb + r * SB + c);
-      } else {
-        const int r = i / (BN / PB), c = (i - r * (BN / PB)) * PB;
-        pb[s].put(sb + r * SB + c);
-      }
-    }
+    for (int s = 0; s < RB; ++s) pb[s].put(sb + b_lo[s]);
   };
 
   f32x4 acc[TM][TN];
@@ -207,12 +229,13 @@ __global__ __launch_bounds__(512) void k_gemm_bw(const void* __restrict__ Av, in
   const int nk = (int)((kend - kbeg + BK - 1) / BK);
   if (nk > 0) {
     load(kbeg);
-    store(lds);
+    store(lds, kbeg);
     if (nk > 1) load(kbeg + BK);
     __syncthreads();
     for (int s = 0; s < nk; ++s) {
       if (s + 1 < nk) {
-        store(lds + ((s + 1) & 1) * STAGE);  // that stage was last read in step s - 1
+        // that stage was last read in step s - 1
+        store(lds + ((s + 1) & 1) * STAGE, kbeg + (int64_t)(s + 1) * BK);
         if (s + 2 < nk) load(kbeg + (int64_t)(s + 2) * BK);
       }
       compute(lds + (s & 1) * STAGE);

@@ -50,6 +50,15 @@ _SCHEMAS = {
                              "Tensor(b!)? g_head_bias, int num_graphs, int n, int heads, "
                              "int channels, bool concat, int act, float slope, "
                              "bool edge_order=False) -> (Tensor, Tensor, Tensor)",
+    "project_bf16_export": "(Tensor a, Tensor planes, Tensor w) -> (Tensor, Tensor)",
+    "gat_attn_bwd_bf16dx": "(Tensor dy, Tensor y, Tensor xs, Tensor psave, Tensor? keep, "
+                           "float keep_scale, Tensor? rowmask, bool with_ae, int num_graphs, "
+                           "int n, int heads, int channels, bool concat, int act, float slope, "
+                           "bool edge_order=False, Tensor? post_u=None, float post_p=0.0) "
+                           "-> (Tensor, Tensor, Tensor)",
+    "gat_wgrad_bf16b": "(Tensor x_b, Tensor dxs_b, Tensor W, Tensor att_src, Tensor att_dst, "
+                       "Tensor dbias_partial, int heads, int channels, Tensor(a!) gW, "
+                       "Tensor(b!)? g_att_src, Tensor(c!)? g_att_dst, Tensor(d!)? g_bias) -> ()",
     "gat_attn_tiled_fwd": "(Tensor xs, Tensor? ae, int num_edges, Tensor? eid, Tensor? rowmask, "
                           "Tensor? bias, Tensor? keep, float keep_scale, int num_graphs, int n, "
                           "int heads, int channels, bool concat, int act, float slope) -> Tensor",
@@ -351,6 +360,35 @@ def _project_fake(a, planes, w, transpose_w, bf16, relu_y=None):
     return a.new_empty((a.shape[0], N))
 
 
+def _pad_to(k: int, m: int) -> int:
+    return (k + m - 1) // m * m
+
+
+@_impl("project_bf16_export")
+def _project_bf16_export(a, planes, w):
+    """The bf16-mode projection a·wᵀ (sv2n_gemm_bf16) that also returns bf16(a)
+    [M][round_up(K, 64)] (zero past K), written by the GEMM's own operand
+    staging (sv2n_gemm_bf16_export): the layer's weight-gradient operand."""
+    lib = _lib.load()
+    _f32(a, w)
+    M, K = a.shape
+    N = w.shape[0]
+    _need(a.stride(1) == 1 and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0,
+          "a: 16-B aligned rows")
+    out = torch.empty(M, N, device=a.device, dtype=torch.float32)
+    ab = torch.empty(M, _pad_to(K, 64), device=a.device, dtype=torch.bfloat16)
+    _lib.check(lib.sv2n_gemm_bf16_export(a.data_ptr(), a.stride(0), planes.data_ptr(),
+                                         out.data_ptr(), out.stride(0), M, N, K, ab.data_ptr(),
+                                         ab.stride(0), _st(a)), "sv2n_gemm_bf16_export")
+    return out, ab
+
+
+@_fake("project_bf16_export")
+def _project_bf16_export_fake(a, planes, w):
+    return (a.new_empty((a.shape[0], w.shape[0])),
+            a.new_empty((a.shape[0], _pad_to(a.shape[1], 64)), dtype=torch.bfloat16))
+
+
 # --------------------------------------------------------------------------
 # fused attention (sv2n_gat_attn_* and the tiled forms)
 # --------------------------------------------------------------------------
@@ -623,6 +661,78 @@ def _gat_attn_bwd_fake(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num
     return (torch.empty_like(xs),
             xs.new_empty(_dae_shape(edge_order, num_graphs, n, heads) if with_ae else (0,)),
             xs.new_empty((num_graphs, _oc(heads, channels, concat))))
+
+
+@_impl("gat_attn_bwd_bf16dx")
+def _gat_attn_bwd_bf16dx(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_graphs, n,
+                         heads, channels, concat, act, slope, edge_order=False, post_u=None,
+                         post_p=0.0):
+    """gat_attn_bwd returning dxs as bf16 [N][round_up(ldx, 8)] (columns past
+    ldx zero; sv2n_gat_attn_bwd_bf16dx): the bf16 weight-gradient operand."""
+    lib = _lib.load()
+    _f32(dy, y, xs, psave, post_u)
+    N, OC = num_graphs * n, _oc(heads, channels, concat)
+    _rows(xs, N, heads * channels + 2 * heads, "xs")
+    _dense(dy, y, psave, keep, rowmask, post_u)
+    _need(dy.numel() == N * OC and y.numel() == N * OC, "dy / y shape")
+    _need(post_u is None or (post_u.numel() == N * OC and 0.0 <= post_p < 1.0), "post_u / post_p")
+    _need(psave.numel() == num_graphs * heads * 1024, "psave shape")
+    _need(keep is None or keep.numel() == num_graphs * heads * 1024, "keep shape")
+    _need(not edge_order or rowmask is None, "edge-ordered ae needs complete graphs")
+    dev = xs.device
+    ldx = xs.stride(0)
+    dxb = torch.empty(N, _pad_to(ldx, 8), device=dev, dtype=torch.bfloat16)
+    dae = torch.empty(_dae_shape(edge_order, num_graphs, n, heads), device=dev) if with_ae else \
+        torch.empty(0, device=dev)
+    dbp = torch.empty(num_graphs, OC, device=dev)
+    _lib.check(lib.sv2n_gat_attn_bwd_bf16dx(
+        dy.data_ptr(), y.data_ptr(), xs.data_ptr(), ldx, psave.data_ptr(), _p(keep), keep_scale,
+        _p(post_u), post_p, _p(rowmask), dxb.data_ptr(), dxb.stride(0), _p(dae), int(edge_order),
+        dbp.data_ptr(), num_graphs, n, heads, channels, int(concat), act, slope, _st(xs)),
+        "sv2n_gat_attn_bwd_bf16dx")
+    return dxb, dae, dbp
+
+
+@_fake("gat_attn_bwd_bf16dx")
+def _gat_attn_bwd_bf16dx_fake(dy, y, xs, psave, keep, keep_scale, rowmask, with_ae, num_graphs,
+                              n, heads, channels, concat, act, slope, edge_order=False,
+                              post_u=None, post_p=0.0):
+    return (xs.new_empty((xs.shape[0], _pad_to(xs.stride(0), 8)), dtype=torch.bfloat16),
+            xs.new_empty(_dae_shape(edge_order, num_graphs, n, heads) if with_ae else (0,)),
+            xs.new_empty((num_graphs, _oc(heads, channels, concat))))
+
+
+@_impl("gat_wgrad_bf16b")
+def _gat_wgrad_bf16b(x_b, dxs_b, W, att_src, att_dst, dbias_partial, heads, channels, gW,
+                     g_att_src, g_att_dst, g_bias):
+    """gat_wgrad in the bf16 mode on operands already in bf16: x_b from
+    project_bf16_export, dxs_b from gat_attn_bwd_bf16dx
+    (sv2n_gat_wgrad_node_bf16b)."""
+    lib = _lib.load()
+    _f32(W, att_src, att_dst, dbias_partial, gW, g_att_src, g_att_dst, g_bias)
+    _dense(x_b, dxs_b, W, att_src, att_dst, dbias_partial, gW, g_att_src, g_att_dst, g_bias)
+    _need(x_b.dtype == torch.bfloat16 and dxs_b.dtype == torch.bfloat16, "bf16 operands")
+    N = x_b.shape[0]
+    HC = heads * channels
+    F = W.shape[1]
+    ldx = (HC + 2 * heads + 3) // 4 * 4
+    _need(W.shape[0] == HC and dxs_b.shape[0] == N and dxs_b.shape[1] >= ldx and
+          x_b.shape[1] >= F, "W / x_b / dxs_b shapes")
+    _need(gW.shape == W.shape, "gW shape")
+    ws_n = lib.sv2n_gat_wgrad_node_bf16_workspace(N, F, ldx, heads, channels)
+    ws = torch.empty(max(ws_n, 1), device=x_b.device)
+    B, OC = dbias_partial.shape
+    _lib.check(lib.sv2n_gat_wgrad_node_bf16b(
+        x_b.data_ptr(), x_b.stride(0), dxs_b.data_ptr(), dxs_b.stride(0), N, F, ldx,
+        W.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), heads, channels,
+        dbias_partial.data_ptr(), B, OC, gW.data_ptr(), _p(g_att_src), _p(g_att_dst),
+        _p(g_bias), ws.data_ptr(), ws_n, _st(x_b)), "sv2n_gat_wgrad_node_bf16b")
+
+
+@_fake("gat_wgrad_bf16b")
+def _gat_wgrad_bf16b_fake(x_b, dxs_b, W, att_src, att_dst, dbias_partial, heads, channels, gW,
+                          g_att_src, g_att_dst, g_bias):
+    return None
 
 
 def attn_bwd_edge_supported(num_graphs: int, n: int, heads: int, channels: int, edge_dim: int,

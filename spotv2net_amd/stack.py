@@ -235,6 +235,11 @@ class _StackMeta:
         self.head_dz = head_dz
 
 
+# "on": in the bf16 mode, layer 0 (input without gradient) keeps bf16 copies of
+# its weight-gradient operands (_bf16_export_ok); "off": fp32 operands rounded
+# inside the GEMM (A/B switch for tests and measurements)
+BF16_OPERANDS = os.environ.get("SV2N_BF16_OPERANDS", "on")
+
 # "on": the training step fuses GATModel.linear + MSE into the last layer's
 # attention forward where the kernel takes the shape (gat_train_head_mse);
 # "off": the separate head + loss launch (A/B switch for tests and measurements)
@@ -309,6 +314,7 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
 
     # 3) layers
     xin = _aligned(x)
+    xb0 = None  # bf16(x) of layer 0 (bf16 mode, x without grad)
     saved_x, saved_xs, saved_y, saved_p, saved_keep, saved_drop = [], [], [], [], [], []
     saved_st = []
     post_p = []
@@ -317,7 +323,13 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
         F = c.in_channels
         if xin.size(1) != F:
             raise ValueError(f"layer {l}: expected {F} input features, got {xin.size(1)}")
-        xs = ops.project(xin, planes[l], waugs[l], False, bf16)  # x · Waugᵀ
+        if l == 0 and _bf16_export_ok(bf16, training and need_saved and not need_t[0], xin, c,
+                                      fused or tiled):
+            # bf16 mode: the projection also leaves bf16(x) for the layer's
+            # weight-gradient GEMM (sv2n_gemm_bf16_export)
+            xs, xb0 = ops.project_bf16_export(xin, planes[l], waugs[l])
+        else:
+            xs = ops.project(xin, planes[l], waugs[l], False, bf16)  # x · Waugᵀ
         if overlap is not None:
             overlap[0].wait_stream(overlap[1])
             overlap = None
@@ -391,7 +403,7 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
                        (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs], post_p,
                       saved_y[-1] if head is not None else None)
     saved = [ea, wf if fused else None, *saved_x, *saved_xs, *saved_y, *saved_p, *saved_st,
-             *saved_keep, *saved_drop, *waugs, *planes_t]
+             *saved_keep, *saved_drop, *waugs, *planes_t, xb0]
     return xin, saved, meta
 
 
@@ -412,7 +424,8 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
     keeps = sv[k:k + L]; k += L
     drops = sv[k:k + L]; k += L
     waugs = sv[k:k + L]; k += L
-    planes_t = sv[k:k + L]
+    planes_t = sv[k:k + L]; k += L
+    xb0 = sv[k]  # bf16(x) of layer 0, or None
     dev = dout.device
     B, n, N = layout.num_graphs, layout.n, layout.num_nodes
 
@@ -447,6 +460,20 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
                 dy, ys[l], xs, pss[l], layout.num_edges, layout.eid, keeps[l],
                 meta.kscales[l], layout.rowmask, B, n, Hc, C, c.concat, act,
                 float(c.negative_slope))
+        elif l == 0 and xb0 is not None and not need_x0 and not edge_tail and \
+                grad_of(c.lin_src.weight) is not None:
+            # bf16 mode: dxs as bf16 straight from the attention backward, both
+            # weight-gradient operands bf16 in memory (the GEMM rounds fp32
+            # operands the same way while staging them)
+            dxb, dae, dbp = ops.gat_attn_bwd_bf16dx(
+                dy, ys[l], xs, pss[l], keeps[l], meta.kscales[l], layout.rowmask, use_edge,
+                B, n, Hc, C, c.concat, act_l, float(c.negative_slope), eo, post_u,
+                meta.post_p[l] or 0.0)
+            daes[l] = _opt(dae)
+            ops.gat_wgrad_bf16b(xb0, dxb, c.lin_src.weight, c.att_src, c.att_dst, dbp, Hc, C,
+                                grad_of(c.lin_src.weight), grad_of(c.att_src),
+                                grad_of(c.att_dst), grad_of(c.bias))
+            continue  # layer 0 without dx (x needs no gradient): nothing else to do
         elif edge_tail and l == 0:
             dxs, dbp, dwf = ops.gat_attn_bwd_edge(
                 dy, ys[l], xs, pss[l], keeps[l], meta.kscales[l], ea,
@@ -522,6 +549,16 @@ class _GATStack(torch.autograd.Function):
         dx0 = stack_backward(ctx.saved_tensors, ctx.meta, ctx.convs, ctx.layout, dout,
                              ctx.needs_input_grad[0], grad_of)
         return (dx0, None, None, None, None, None, None, None) + grad_of.returned()
+
+
+def _bf16_export_ok(bf16: bool, want: bool, xin: torch.Tensor, conv, other_path: bool) -> bool:
+    """Layer 0 in the bf16 mode whose input needs no gradient: its projection
+    exports bf16(x) and its backward runs on bf16 operands end to end
+    (sv2n_gemm_bf16_export, sv2n_gat_attn_bwd_bf16dx, sv2n_gat_wgrad_node_bf16b)."""
+    return (bf16 and want and BF16_OPERANDS == "on" and not other_path
+            and conv.lin_src.weight.requires_grad
+            and xin.size(1) % 4 == 0 and xin.stride(1) == 1 and xin.stride(0) % 4 == 0
+            and xin.data_ptr() % 16 == 0)
 
 
 def head_mse_fusable(convs, layout: GraphLayout, linear: torch.nn.Linear,

@@ -97,7 +97,7 @@ void run_bw(const char* tag, hipStream_t st, const void* A, int64_t lda, const v
   CK(hipMemset(C, 0, sizeof(float) * M * N * nz));
   auto f = [&]() {
     hipLaunchKernelGGL(kern, grid, dim3(Cfg::THREADS), Cfg::LDS, st, A, lda, B, ldb, C, N, M, N,
-                       K, ks, nm, nn);
+                       K, ks, nm, nn, (unsigned short*)nullptr, (int64_t)0);
   };
   const double us = timeit(st, f);
   double err = -1;

@@ -24,11 +24,12 @@ from collections import defaultdict
 # bench.py kernel_table name -> rocprof kernel name prefix (the C2 instantiation)
 KERNELS = {
     "gemm_l0_fwd": "sv2n::k_gemm3d<8, 1, 13, 2, false>",
-    "gemm_l0_dwT": "sv2n::k_gemm_tt3y<13, 2>",
-    "edge_logits_fwd": "sv2n::k_edge_fwd<8, 8, false>",
-    "edge_logits_bwd": "sv2n::k_edge_bwd<8, 8, false>",
-    "gat_attn_fwd_l0": "sv2n::canon::k_fwd<1, true, false>",
+    "gemm_l0_dwT": "sv2n::k_gemm_tt3y<13, 2, false>",
+    "edge_logits_fwd": "sv2n::k_edge_fwd_mx<16>",
+    "edge_logits_bwd": "sv2n::k_edge_bwd_mx<16, 1>",
+    "gat_attn_fwd_l0": "sv2n::canon::k_fwd<1, true, false, false>",
     "gat_attn_bwd_l0": "sv2n::canon::k_bwd<0, true, false, 3>",
+    "gat_attn_fwd_l1_head": "sv2n::canon::k_fwd<1, false, false, true>",
 }
 
 
@@ -37,6 +38,17 @@ KERNELS_C5 = {
     "gat_attn_fused_fwd_l0": "sv2n::fused::k_fattn_fwd<12, false, false>",
     "gat_attn_fused_bwd_l0": "sv2n::fused::k_fattn_bwd2<12, false, false>",
     "gemm_l0_fwd": "sv2n::k_gemm3d<8, 1, 9, 2, false>",
+}
+
+# C3 bf16 loop (tools/r4_pmc.sh): keys "c3_bf16:..."; a list sums its kernels
+# (the weight-gradient node is the GEMM and its epilogue launch)
+KERNELS_C3 = {
+    "gemm_fwd": "sv2n::k_gemm_bw<256, 192, false, true, false>",
+    "wgrad_node": ["sv2n::k_gemm_bw<128, 128, true, false, false>", "sv2n::k_wgrad_epi_t"],
+    "gat_attn_fwd": "sv2n::canon::k_fwd<1, false, false, false>",
+    "gat_attn_bwd": "sv2n::canon::k_bwd<1, false, false, 1>",
+    "window_gather": "sv2n::k_window_rows",
+    "head_mse_train": "sv2n::k_head_mse_train_w<1, 8>",
 }
 
 
@@ -57,6 +69,11 @@ def per_kernel(path, counter):
 
 
 def find(table, prefix):
+    if isinstance(prefix, list):
+        parts = [find(table, p) for p in prefix]
+        if any(p is None for p in parts):
+            return None
+        return (sum(p[0] for p in parts), min(p[1] for p in parts))
     for k, v in table.items():
         if prefix + "(" in k:
             return v
@@ -68,7 +85,7 @@ def main():
     ap.add_argument("fetch")
     ap.add_argument("write")
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
-    ap.add_argument("--config", default="c2", choices=("c2", "c5"))
+    ap.add_argument("--config", default="c2", choices=("c2", "c5", "c3_bf16"))
     a = ap.parse_args()
     fetch = per_kernel(a.fetch, "FETCH_SIZE")
     write = per_kernel(a.write, "WRITE_SIZE")
@@ -81,15 +98,17 @@ def main():
                     "gfx950 FETCH_SIZE halving corrected per MI355X_MICROARCH.md; mean over "
                     "the dispatches of the profiled C2 train/forward steps (keys 'c5:...': "
                     "the C5 steps)")
-    table = KERNELS if a.config == "c2" else {"c5:" + k: v for k, v in KERNELS_C5.items()}
+    table = KERNELS if a.config == "c2" else \
+        {a.config + ":" + k: v for k, v in (KERNELS_C5 if a.config == "c5" else KERNELS_C3).items()}
     for key, prefix in table.items():
         f, w = find(fetch, prefix), find(write, prefix)
         if f is None or w is None:
             continue
         fb, wb = 2.0 * f[0] * 1024.0, w[0] * 1024.0
-        out[key] = {"kernel": prefix, "fetch_bytes": round(fb), "write_bytes": round(wb),
+        out[key] = {"kernel": " + ".join(prefix) if isinstance(prefix, list) else prefix,
+                    "fetch_bytes": round(fb), "write_bytes": round(wb),
                     "hbm_bytes_per_launch": round(fb + wb), "dispatches": f[1]}
-        print(f"{key:18s} read {fb / 1e6:9.2f} MB  write {wb / 1e6:8.2f} MB  ({f[1]} dispatches)")
+        print(f"{key:26s} read {fb / 1e6:9.2f} MB  write {wb / 1e6:8.2f} MB  ({f[1]} dispatches)")
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
     print("wrote", a.out)
