@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 14
+#define SV2N_ABI_VERSION 16
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -154,8 +154,12 @@ int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, int ae_edge_ord
  *   loss[0] = mean(diff²);
  *   g_head_weight[oc] += Σ_i 2/N·diff_i·drop(y)[i][oc], g_head_bias[0] +=
  *          Σ_i 2/N·diff_i (either may be NULL).
- * Two launches (the attention, then a fixed-order sum of per-graph partials
- * in workspace: sv2n_gat_attn_fwd_head_mse_workspace floats).  Runs when
+ *   loss_sum[0] += loss[0] when loss_sum is not NULL (ABI 16: a running
+ *          epoch sum with no separate add launch).
+ * One launch: the per-graph partials are summed in graph order inside it
+ * (two-level tickets).  workspace: sv2n_gat_attn_fwd_head_mse_workspace
+ * floats, 16-B aligned; its first SV2N_TICKET_WORDS are ticket counters that
+ * must be zero before the first call (every call leaves them zero).  Runs when
  * sv2n_gat_attn_fwd_head_mse_supported: one workgroup per graph (the batch
  * fills the chip, or few work items), OC <= 512.  Replaces the separate
  * sv2n_head_mse_train launch of a training step. */
@@ -167,8 +171,9 @@ int sv2n_gat_attn_fwd_head_mse(const float* xs, int ldx, const float* ae, int ae
                                const uint32_t* rowmask, const float* bias, const uint8_t* keep,
                                float keep_scale, float* dz, float* psave, const float* post_u,
                                float post_p, const float* head_weight, const float* head_bias,
-                               const float* target, float* loss, float* g_head_weight,
-                               float* g_head_bias, float* workspace, int64_t workspace_floats,
+                               const float* target, float* loss, float* loss_sum,
+                               float* g_head_weight, float* g_head_bias, float* workspace,
+                               int64_t workspace_floats,
                                int64_t num_graphs, int n, int heads, int channels, int concat,
                                int act, float negative_slope, hipStream_t stream);
 
@@ -282,6 +287,12 @@ int sv2n_gemm_bf16(const float* A, int64_t lda, const uint16_t* Bp, float* C, in
 int sv2n_gemm_bf16_export(const float* A, int64_t lda, const uint16_t* Bp, float* C,
                           int64_t ldc, int64_t M, int64_t N, int64_t K, uint16_t* a_bf16,
                           int64_t ld_ab, hipStream_t stream);
+/* sv2n_gemm_bf16 with A already bf16 [M][lda] (lda % 8 == 0, 16-B aligned;
+ * e.g. sv2n_window_gather_bf16x's x_bf16), ABI 15: the same products, no
+ * rounding pass.  Large-tile shapes only (M >= 1024, N >= 384), else
+ * SV2N_ERR_SHAPE. */
+int sv2n_gemm_bf16_a16(const uint16_t* A, int64_t lda, const uint16_t* Bp, float* C,
+                       int64_t ldc, int64_t M, int64_t N, int64_t K, hipStream_t stream);
 
 /* Weight preparation for one GAT layer (replaces, per step, PyG's separate
  * (x_src*att_src).sum(-1) / (x_dst*att_dst).sum(-1) and lin_edge·att_edge
@@ -445,8 +456,8 @@ int sv2n_head_bwd(const float* x, int64_t num_rows, int in_features, const float
 int64_t sv2n_head_mse_workspace(int64_t num_rows, int in_features, int out_features);
 int sv2n_head_mse_fwd(const float* x, int64_t num_rows, int in_features, const float* weight,
                       const float* bias, int out_features, const float* target, float* yhat,
-                      float* diff, float* loss, float* workspace, int64_t workspace_floats,
-                      hipStream_t stream);
+                      float* diff, float* loss, float* loss_sum, float* workspace,
+                      int64_t workspace_floats, hipStream_t stream);
 int sv2n_head_mse_bwd(const float* x, int64_t num_rows, int in_features, const float* weight,
                       int out_features, const float* diff, const float* grad_loss, float* dx,
                       float* g_weight, float* g_bias, float* workspace,
@@ -456,13 +467,15 @@ int sv2n_head_mse_bwd(const float* x, int64_t num_rows, int in_features, const f
  * upstream loss gradient is 1 (loss.backward()): loss[0] = mean(diff²), dx =
  * 2/(rows·out)·diff·weight, and g_weight / g_bias ACCUMULATE Σ 2/(rows·out)·
  * diff ⊗ [x, 1] (either may be NULL).  Equals sv2n_head_mse_fwd followed by
- * sv2n_head_mse_bwd with grad_loss = 1.  workspace:
+ * sv2n_head_mse_bwd with grad_loss = 1.  loss_sum (ABI 16; also in
+ * sv2n_head_mse_fwd): when not NULL, loss_sum[0] += loss[0] in the same
+ * launch (an epoch's running sum without an add launch).  workspace:
  * sv2n_head_mse_train_workspace(...) floats, same counter rule. */
 int64_t sv2n_head_mse_train_workspace(int64_t num_rows, int in_features, int out_features);
 int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_features, const float* weight,
                         const float* bias, int out_features, const float* target, float* loss,
-                        float* dx, float* g_weight, float* g_bias, float* workspace,
-                        int64_t workspace_floats, hipStream_t stream);
+                        float* loss_sum, float* dx, float* g_weight, float* g_bias,
+                        float* workspace, int64_t workspace_floats, hipStream_t stream);
 
 /* Fused attention for dense-block graphs of 32 < n <= 256 nodes (any n <= 256
  * works; n <= 32 is faster on sv2n_gat_attn_fwd/bwd).  Same semantics and
@@ -602,6 +615,18 @@ int sv2n_window_gather_diag(const float* vol, const float* volvol, const float* 
                             int64_t num_windows, int seq_length, int future_steps,
                             const uint16_t* canon, float* x, float* edge_attr, float* y,
                             hipStream_t stream);
+/* sv2n_window_gather_diag that also writes bf16(x) (round to nearest even)
+ * into x_bf16 [num_windows·n][ld_xb] (ld_xb >= n·seq_length, % 4 == 0, zero
+ * past n·seq_length; NaN rows for windows outside the series) — the bf16
+ * execution mode's projection operand (sv2n_gemm_bf16_a16) and its weight
+ * gradient's (sv2n_gat_wgrad_node_bf16b) straight from the data builder
+ * (ABI 15).  Row-kernel shapes only (n·seq_length % 4 == 0, 3·S·(n+1) floats
+ * of LDS <= 64 KiB, future_steps <= 256); else SV2N_ERR_SHAPE. */
+int sv2n_window_gather_bf16x(const float* vol, const float* volvol, const float* diag, int n,
+                             int64_t num_matrices, const int64_t* starts, int64_t start_offset,
+                             int64_t num_windows, int seq_length, int future_steps,
+                             const uint16_t* canon, float* x, uint16_t* x_bf16, int64_t ld_xb,
+                             float* edge_attr, float* y, hipStream_t stream);
 
 #ifdef __cplusplus
 }

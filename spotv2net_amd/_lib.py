@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SV2N_LIB: an alternative build of the same library (diagnostic builds, e.g.
 # tools/stamps.py); default the in-tree one
 LIB_PATH = os.environ.get("SV2N_LIB") or os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 14
+ABI_VERSION = 16
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p
@@ -66,8 +66,8 @@ _SIGNATURES = {
     # xs ldx ae eo rowmask bias keep keep_scale dz psave post_u post_p hw hb target loss
     # ghw ghb ws ws_n B n H C concat act slope stream
     "sv2n_gat_attn_fwd_head_mse": (_i32, [_p, _i32, _p, _i32, _p, _p, _p, _f32, _p, _p, _p, _f32,
-                                          _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _i32,
-                                          _i32, _i32, _i32, _f32, _p]),
+                                          _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32,
+                                          _i32, _i32, _i32, _i32, _f32, _p]),
     "sv2n_gat_attn_bwd_edge_supported": (_i32, [_i64, _i32, _i32, _i32, _i32, _i32]),
     # dy y xs ldx psave keep keep_scale post_u post_p dxs dbp ea D layer_dae L layer hlp part
     # B n H C concat act slope stream
@@ -97,6 +97,7 @@ _SIGNATURES = {
     "sv2n_gemm_f32x3_relu": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "sv2n_gemm_bf16": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "sv2n_gemm_bf16_export": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
+    "sv2n_gemm_bf16_a16": (_i32, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "sv2n_gemm_f32_workspace": (_i64, [_i64, _i64, _i64]),
     "sv2n_gemm_f32_slabs_count": (_i32, [_i64, _i64, _i64]),
     "sv2n_gemm_f32_slabs": (_i32, [_i32, _i32, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
@@ -124,14 +125,17 @@ _SIGNATURES = {
                                   _p]),
     "sv2n_head_mse_workspace": (_i64, [_i64, _i32, _i32]),
     "sv2n_head_mse_train_workspace": (_i64, [_i64, _i32, _i32]),
-    "sv2n_head_mse_train": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _i64, _p]),
-    "sv2n_head_mse_fwd": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _i64, _p]),
+    "sv2n_head_mse_train": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _i64,
+                                   _p]),
+    "sv2n_head_mse_fwd": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "sv2n_head_mse_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "sv2n_head_fwd": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p]),
     "sv2n_window_gather": (_i32, [_p, _p, _i32, _i64, _p, _i64, _i64, _i32, _i32, _p, _p, _p, _p,
                                   _p]),
     "sv2n_window_gather_diag": (_i32, [_p, _p, _p, _i32, _i64, _p, _i64, _i64, _i32, _i32, _p, _p,
                                        _p, _p, _p]),
+    "sv2n_window_gather_bf16x": (_i32, [_p, _p, _p, _i32, _i64, _p, _i64, _i64, _i32, _i32, _p,
+                                        _p, _p, _i64, _p, _p, _p]),
     "sv2n_head_bwd_workspace": (_i64, [_i64, _i32, _i32]),
     "sv2n_head_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _p, _p, _i64, _p]),
 }

@@ -60,18 +60,20 @@ extern "C" int sv2n_gat_attn_fwd_head_mse_supported(int64_t num_graphs, int n, i
 extern "C" int64_t sv2n_gat_attn_fwd_head_mse_workspace(int64_t num_graphs, int heads,
                                                         int channels, int concat) {
   if (num_graphs <= 0 || heads < 1 || channels < 1) return 0;
-  return num_graphs * ((concat ? heads * channels : channels) + 2);
+  // tickets | 8 group slabs | per-graph partials
+  return SV2N_TICKET_WORDS + (num_graphs + 8) * ((concat ? heads * channels : channels) + 2);
 }
 
 extern "C" int sv2n_gat_attn_fwd_head_mse(
     const float* xs, int ldx, const float* ae, int ae_edge_order, const uint32_t* rowmask,
     const float* bias, const uint8_t* keep, float keep_scale, float* dz, float* psave,
     const float* post_u, float post_p, const float* head_weight, const float* head_bias,
-    const float* target, float* loss, float* g_head_weight, float* g_head_bias,
+    const float* target, float* loss, float* loss_sum, float* g_head_weight, float* g_head_bias,
     float* workspace, int64_t workspace_floats, int64_t num_graphs, int n, int heads,
     int channels, int concat, int act, float negative_slope, hipStream_t stream) {
   if (!xs || !dz || !psave || !head_weight || !target || !loss || !workspace)
     return SV2N_ERR_ARG;
+  if ((uintptr_t)workspace & 15) return SV2N_ERR_ALIGN;
   if (int rc = check_attn_args(num_graphs, n, heads, channels, ldx, act)) return rc;
   if (ae_edge_order && (rowmask || n < 2)) return SV2N_ERR_ARG;
   if (post_u && !(post_p >= 0.f && post_p < 1.f)) return SV2N_ERR_ARG;
@@ -83,11 +85,15 @@ extern "C" int sv2n_gat_attn_fwd_head_mse(
   hf.w = head_weight;
   hf.b = head_bias;
   hf.target = target;
-  hf.part = workspace;
+  const int O2 = (concat ? heads * channels : channels) + 2;
+  hf.cnt = reinterpret_cast<unsigned*>(workspace);
+  hf.gslab = workspace + SV2N_TICKET_WORDS;
+  hf.part = hf.gslab + 8 * O2;
   hf.inv_n2 = (float)(2.0 / ((double)num_graphs * n));
   hf.gw = g_head_weight;
   hf.gb = g_head_bias;
   hf.loss = loss;
+  hf.loss_sum = loss_sum;
   attn_canon_fwd(num_graphs, stream, xs, ldx, ae, ae_edge_order, rowmask, bias, keep,
                  keep_scale, dz, psave, post_u, post_p, nullptr, n, heads, channels, concat, act,
                  negative_slope, hf);

@@ -137,6 +137,28 @@ extern "C" int sv2n_gemm_bf16_export(const float* A, int64_t lda, const uint16_t
   return gemm_bf16(A, lda, Bp, C, ldc, M, N, K, a_bf16, ld_ab, stream);
 }
 
+extern "C" int sv2n_gemm_bf16_a16(const uint16_t* A, int64_t lda, const uint16_t* Bp, float* C,
+                                  int64_t ldc, int64_t M, int64_t N, int64_t K,
+                                  hipStream_t stream) {
+  if (!A || !Bp || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldc < N) return SV2N_ERR_ARG;
+  if (((uintptr_t)A & 15) || (lda & 7) || ((uintptr_t)Bp & 15)) return SV2N_ERR_ALIGN;
+  if (M < 1024 || N < 384) return SV2N_ERR_SHAPE;  // the large-tile kernel's shapes
+  const int64_t Kp = sv2n_split3_kpad(K);
+  using Cfg = GemmBWCfg<256, 192, false, false, false>;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)k_gemm_bw<256, 192, false, false, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
+    return true;
+  }();
+  (void)attr;
+  const int nm = (int)((M + 255) / 256), nn = (int)((N + 191) / 192);
+  hipLaunchKernelGGL((k_gemm_bw<256, 192, false, false, false>),
+                     dim3((unsigned)(((nm + 7) / 8) * 8 * nn)), dim3(Cfg::THREADS), Cfg::LDS,
+                     stream, (const void*)A, lda, (const void*)Bp, Kp, C, ldc, M, N, K,
+                     (int64_t)K, nm, nn, (unsigned short*)nullptr, (int64_t)0);
+  return (int)hipGetLastError();
+}
+
 static int gemm_bf16(const float* A, int64_t lda, const uint16_t* Bp, float* C, int64_t ldc,
                      int64_t M, int64_t N, int64_t K, uint16_t* a_bf16, int64_t ld_ab,
                      hipStream_t stream) {

@@ -158,8 +158,8 @@ template <int OUT>
 __global__ __launch_bounds__(256) void k_head_mse_fwd(
     const float* __restrict__ x, int64_t N, int C, const float* __restrict__ W,
     const float* __restrict__ b, const float* __restrict__ target, float* __restrict__ yhat,
-    float* __restrict__ diff, float* __restrict__ ws, float* __restrict__ loss, float inv_count,
-    int R) {
+    float* __restrict__ diff, float* __restrict__ ws, float* __restrict__ loss,
+    float* __restrict__ loss_sum, float inv_count, int R) {
   extern __shared__ __attribute__((aligned(16))) float sx[];  // [R][C+1] | sw [OUT][C]
   __shared__ float s_part[256 * OUT];
   __shared__ float s_red[256];
@@ -201,7 +201,10 @@ __global__ __launch_bounds__(256) void k_head_mse_fwd(
       if (t < s) s_red[t] += s_red[t + s];
       __syncthreads();
     }
-    if (t == 0) loss[0] = s_red[0] * inv_count;
+    if (t == 0) {
+      loss[0] = s_red[0] * inv_count;
+      if (loss_sum) loss_sum[0] += s_red[0] * inv_count;
+    }
   }
 }
 
@@ -333,7 +336,7 @@ __global__ __launch_bounds__(256) void k_head_mse_train(
     const float* __restrict__ x, int64_t N, int C, const float* __restrict__ W,
     const float* __restrict__ b, const float* __restrict__ target, float* __restrict__ dx,
     float* __restrict__ ws, float* __restrict__ gW, float* __restrict__ gb,
-    float* __restrict__ loss, float inv_count, float scale, int R) {
+    float* __restrict__ loss, float* __restrict__ loss_sum, float inv_count, float scale, int R) {
   extern __shared__ __attribute__((aligned(16))) float sx[];  // [R][C+1] | sw [OUT][C]
   __shared__ float s_part[256 * OUT];
   __shared__ float sd[HEAD_ROWS][HEAD_MAX_OUT];
@@ -439,6 +442,7 @@ __global__ __launch_bounds__(256) void k_head_mse_train(
         const int oc = base + t;
         if (oc == tot) {
           loss[0] = s * inv_count;
+          if (loss_sum) loss_sum[0] += s * inv_count;
         } else {
           const int o = oc / CP, c = oc - o * CP;
           if (c < C) {
@@ -472,7 +476,8 @@ __global__ __launch_bounds__(256) void k_head_mse_train_w(
     const float* __restrict__ x, int64_t N, int C, const float* __restrict__ W,
     const float* __restrict__ b, const float* __restrict__ target, float* __restrict__ dx,
     float* __restrict__ ws, float* __restrict__ gW, float* __restrict__ gb,
-    float* __restrict__ loss, float inv_count, float scale, int RW) {
+    float* __restrict__ loss, float* __restrict__ loss_sum, float inv_count, float scale,
+    int RW) {
   constexpr int RB = KC >= 8 ? 4 : (KC >= 4 ? 8 : 16);  // rows in flight per wave
   extern __shared__ __attribute__((aligned(16))) float s_w4[];  // [4][stride] wave partials
   __shared__ int s_flag;
@@ -580,6 +585,7 @@ __global__ __launch_bounds__(256) void k_head_mse_train_w(
     const float s = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
     if (oc == OUT * CP) {
       loss[0] = s * inv_count;
+      if (loss_sum) loss_sum[0] += s * inv_count;
     } else {
       const int o = oc / CP, c = oc - o * CP;
       if (c < C) {
@@ -695,7 +701,8 @@ extern "C" int64_t sv2n_head_mse_workspace(int64_t num_rows, int in_features, in
 extern "C" int sv2n_head_mse_fwd(const float* x, int64_t num_rows, int in_features,
                                  const float* weight, const float* bias, int out_features,
                                  const float* target, float* yhat, float* diff, float* loss,
-                                 float* workspace, int64_t workspace_floats, hipStream_t stream) {
+                                 float* loss_sum, float* workspace, int64_t workspace_floats,
+                                 hipStream_t stream) {
   const int out_ch = out_features;
   if (!x || !weight || !target || !diff || !loss || !workspace) return SV2N_ERR_ARG;
   if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
@@ -707,7 +714,8 @@ extern "C" int sv2n_head_mse_fwd(const float* x, int64_t num_rows, int in_featur
   const size_t lds = head_lds_bytes(in_features, out_ch, num_rows);
   const float inv_count = 1.f / (float)(num_rows * out_ch);
   SV2N_HEAD_DISPATCH(k_head_mse_fwd, dim3(grid), dim3(256), lds, stream, x, num_rows,
-                     in_features, weight, bias, target, yhat, diff, workspace, loss, inv_count, R)
+                     in_features, weight, bias, target, yhat, diff, workspace, loss, loss_sum,
+                     inv_count, R)
   return (int)hipGetLastError();
 }
 
@@ -731,9 +739,9 @@ extern "C" int64_t sv2n_head_mse_train_workspace(int64_t num_rows, int in_featur
 
 extern "C" int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_features,
                                    const float* weight, const float* bias, int out_features,
-                                   const float* target, float* loss, float* dx, float* g_weight,
-                                   float* g_bias, float* workspace, int64_t workspace_floats,
-                                   hipStream_t stream) {
+                                   const float* target, float* loss, float* loss_sum, float* dx,
+                                   float* g_weight, float* g_bias, float* workspace,
+                                   int64_t workspace_floats, hipStream_t stream) {
   const int out_ch = out_features;
   if (!x || !weight || !target || !loss || !dx || !workspace) return SV2N_ERR_ARG;
   if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
@@ -750,7 +758,7 @@ extern "C" int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_feat
   if (out_ch == O && kc == K) {                                                                 \
     hipLaunchKernelGGL((k_head_mse_train_w<O, K>), dim3(grid), dim3(256), lds, stream, x,      \
                        num_rows, C, weight, bias, target, dx, workspace, g_weight, g_bias, loss, \
-                       inv_count, scale, RW);                                                   \
+                       loss_sum, inv_count, scale, RW);                                         \
     return (int)hipGetLastError();                                                              \
   }
     SV2N_HW(1, 1) SV2N_HW(1, 2) SV2N_HW(1, 4) SV2N_HW(1, 8) SV2N_HW(1, 16)
@@ -764,6 +772,6 @@ extern "C" int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_feat
   const size_t lds = head_lds_bytes(in_features, out_ch, num_rows);
   SV2N_HEAD_DISPATCH(k_head_mse_train, dim3(grid), dim3(256), lds, stream, x, num_rows,
                      in_features, weight, bias, target, dx, workspace, g_weight, g_bias, loss,
-                     inv_count, scale, R)
+                     loss_sum, inv_count, scale, R)
   return (int)hipGetLastError();
 }

@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void k_window_rows(
     const float* __restrict__ vol, const float* __restrict__ volvol, int n, int64_t T,
     const int64_t* __restrict__ starts, int64_t soff, int S, int F,
     const float* __restrict__ diag, float* __restrict__ x, float* __restrict__ ea,
-    float* __restrict__ y) {
+    float* __restrict__ y, unsigned short* __restrict__ xb, int64_t ldxb) {
   extern __shared__ float lds[];
   const int NP = n + 1;
   float* sv = lds;             // [S][NP] vol[t][u][v]
@@ -100,6 +100,9 @@ __global__ __launch_bounds__(256) void k_window_rows(
     if (t < F) y[(b * n + u) * F + t] = qnan;
     float* xr = x + (b * n + u) * (int64_t)n * S;
     for (int j = t; j < n * S; j += 256) xr[j] = qnan;
+    if (xb)
+      for (int j = t; j < ldxb; j += 256)
+        xb[(b * n + u) * ldxb + j] = j < n * S ? (unsigned short)0x7fc0 : (unsigned short)0;
     const int m = n - 1 - u, e0 = u * (2 * n - u - 1) / 2, RW = 3 * S;
     float* up = ea + (b * E0 + e0) * (int64_t)RW;
     float* lo = ea + (b * E0 + P + e0) * (int64_t)RW;
@@ -138,6 +141,7 @@ __global__ __launch_bounds__(256) void k_window_rows(
   float* xr = x + (b * n + u) * (int64_t)n * S;
   const int nxr = n * S;
   if ((nxr & 3) == 0 && (((uintptr_t)xr) & 15) == 0) {
+    unsigned short* xbr = xb ? xb + (b * n + u) * ldxb : nullptr;
     for (int j4 = t; j4 < nxr / 4; j4 += 256) {
       f32x4 v;
 #pragma unroll
@@ -146,7 +150,13 @@ __global__ __launch_bounds__(256) void k_window_rows(
         v[k] = sv[tt * NP + c];
       }
       *reinterpret_cast<f32x4*>(xr + 4 * j4) = v;
+      if (xbr) {  // bf16(x) beside it (round to nearest even, as the GEMMs' staging)
+        typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<b4*>(xbr + 4 * j4) = __builtin_convertvector(v, b4);
+      }
     }
+    if (xbr)
+      for (int j = nxr + t; j < ldxb; j += 256) xbr[j] = 0;
   } else {
     for (int j = t; j < nxr; j += 256) {
       const int c = j / S, tt = j - c * S;
@@ -225,6 +235,30 @@ __global__ __launch_bounds__(256) void k_window_rows(
 
 using namespace sv2n;
 
+extern "C" int sv2n_window_gather_bf16x(const float* vol, const float* volvol,
+                                        const float* diag, int n, int64_t num_matrices,
+                                        const int64_t* starts, int64_t start_offset,
+                                        int64_t num_windows, int seq_length, int future_steps,
+                                        const uint16_t* canon, float* x, uint16_t* x_bf16,
+                                        int64_t ld_xb, float* edge_attr, float* y,
+                                        hipStream_t stream) {
+  if (!vol || !volvol || !starts || !canon || !x || !x_bf16 || !edge_attr || !y)
+    return SV2N_ERR_ARG;
+  if (n < 2 || n > SV2N_MAX_N_TILED || num_windows < 1 || seq_length < 1 || future_steps < 1 ||
+      num_matrices < 1)
+    return SV2N_ERR_SHAPE;
+  const size_t lds = sizeof(float) * 3 * (size_t)seq_length * (n + 1);
+  // the row kernel's 16-B x path only (n·S % 4 == 0, 16-B aligned x rows)
+  if (lds > 64 * 1024 || future_steps > 256 || ((int64_t)n * seq_length) % 4 ||
+      ld_xb < (int64_t)n * seq_length || (ld_xb & 3) || ((uintptr_t)x & 15) ||
+      ((uintptr_t)x_bf16 & 7))
+    return SV2N_ERR_SHAPE;
+  hipLaunchKernelGGL(k_window_rows, dim3((unsigned)(num_windows * n)), dim3(256), lds, stream,
+                     vol, volvol, n, num_matrices, starts, start_offset, seq_length, future_steps,
+                     diag, x, edge_attr, y, reinterpret_cast<unsigned short*>(x_bf16), ld_xb);
+  return (int)hipGetLastError();
+}
+
 extern "C" int sv2n_window_gather_diag(const float* vol, const float* volvol,
                                        const float* diag, int n, int64_t num_matrices,
                                        const int64_t* starts, int64_t start_offset,
@@ -242,7 +276,7 @@ extern "C" int sv2n_window_gather_diag(const float* vol, const float* volvol,
   if (lds <= 64 * 1024 && future_steps <= 256) {
     hipLaunchKernelGGL(k_window_rows, dim3((unsigned)(num_windows * n)), dim3(256), lds, stream,
                        vol, volvol, n, num_matrices, starts, start_offset, seq_length, future_steps,
-                       diag, x, edge_attr, y);
+                       diag, x, edge_attr, y, (unsigned short*)nullptr, (int64_t)0);
     return (int)hipGetLastError();
   }
   const int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);

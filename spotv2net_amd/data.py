@@ -62,6 +62,17 @@ class Data:
         return f"{self.__class__.__name__}({', '.join(parts)})"
 
 
+def bf16_twin(data) -> Optional[torch.Tensor]:
+    """bf16(data.x) [N][K rounded up to 64] when the batch carries one written
+    together with x (``WindowDataset.empty_batch(bf16_x=True)``) and x is
+    still that tensor, unmodified by torch ops; else None."""
+    xb = getattr(data, "_x_bf16", None)
+    x = getattr(data, "x", None)
+    if xb is None or x is None or getattr(data, "_x_bf16_of", None) != (x.data_ptr(), x._version):
+        return None
+    return xb
+
+
 class Batch(Data):
     """A disjoint union of graphs (PyG ``Batch`` layout)."""
 
@@ -236,10 +247,13 @@ class WindowDataset:
         self.diag = torch.diagonal(volvol, dim1=1, dim2=2).contiguous() \
             if volvol.dtype == torch.float32 else None
 
-    def empty_batch(self, batch_size: int) -> Batch:
+    def empty_batch(self, batch_size: int, bf16_x: bool = False) -> Batch:
         """Static device buffers of one batch of ``batch_size`` windows (the
         layout of ``batch``), for ``fill``: a hipGraph-captured train step
-        reads the same tensors every replay."""
+        reads the same tensors every replay.  ``bf16_x``: ``fill`` also
+        writes bf16(x) (round to nearest even) beside x, which the bf16
+        execution mode's layer-0 GEMMs read instead of rounding x themselves
+        (``bf16_twin``)."""
         B, n, S = batch_size, self.n, self.S
         E0 = n * (n - 1)
         dev = self.vol.device
@@ -250,6 +264,12 @@ class WindowDataset:
                   batch=torch.arange(B, device=dev).repeat_interleave(n),
                   ptr=torch.arange(B + 1, device=dev) * n)
         b.nodes_per_graph = n
+        if bf16_x and dev.type == "cuda":
+            from .library import window_bf16x_supported
+            if window_bf16x_supported(n, S, self.future_steps):
+                b._x_bf16 = torch.zeros(B * n, (n * S + 63) // 64 * 64, device=dev,
+                                        dtype=torch.bfloat16)
+                b._x_bf16_of = (b.x.data_ptr(), b.x._version)
         return b
 
     def fill(self, out: Batch, idx: torch.Tensor) -> None:
@@ -270,10 +290,11 @@ class WindowDataset:
             # negative one is refused by the kernel: NaN rows either way
             from . import library  # noqa: F401
             from .layout import canonical_table
+            xb = bf16_twin(out)
             torch.ops.sv2n.window_gather(self.vol.contiguous(), self.volvol.contiguous(),
                                          idx if idx.dtype == torch.long else idx.long(), S, Fs,
                                          canonical_table(n, self.vol.device), out.x,
-                                         out.edge_attr, out.y_x, self.cut, self.diag)
+                                         out.edge_attr, out.y_x, self.cut, self.diag, xb)
             return
         st = self.starts.index_select(0, idx)
         tidx = st.view(B, 1) + self._arS.view(1, S)                               # [B, S]

@@ -49,7 +49,8 @@ _SCHEMAS = {
                              "Tensor? head_bias, Tensor target, Tensor(a!)? g_head_weight, "
                              "Tensor(b!)? g_head_bias, int num_graphs, int n, int heads, "
                              "int channels, bool concat, int act, float slope, "
-                             "bool edge_order=False) -> (Tensor, Tensor, Tensor)",
+                             "bool edge_order=False, Tensor(c!)? loss_sum=None) "
+                             "-> (Tensor, Tensor, Tensor)",
     "project_bf16_export": "(Tensor a, Tensor planes, Tensor w) -> (Tensor, Tensor)",
     "gat_attn_bwd_bf16dx": "(Tensor dy, Tensor y, Tensor xs, Tensor psave, Tensor? keep, "
                            "float keep_scale, Tensor? rowmask, bool with_ae, int num_graphs, "
@@ -97,9 +98,11 @@ _SCHEMAS = {
     "head_fwd": "(Tensor x, Tensor weight, Tensor? bias) -> Tensor",
     "head_bwd": "(Tensor x, Tensor weight, Tensor dout, Tensor(a!)? g_weight, "
                 "Tensor(b!)? g_bias) -> Tensor",
-    "head_mse_fwd": "(Tensor x, Tensor weight, Tensor? bias, Tensor target) -> (Tensor, Tensor)",
+    "head_mse_fwd": "(Tensor x, Tensor weight, Tensor? bias, Tensor target, "
+                    "Tensor(a!)? loss_sum=None) -> (Tensor, Tensor)",
     "head_mse_train": "(Tensor x, Tensor weight, Tensor? bias, Tensor target, "
-                      "Tensor(a!)? g_weight, Tensor(b!)? g_bias) -> (Tensor, Tensor)",
+                      "Tensor(a!)? g_weight, Tensor(b!)? g_bias, Tensor(c!)? loss_sum=None) "
+                      "-> (Tensor, Tensor)",
     "head_mse_bwd": "(Tensor x, Tensor weight, Tensor diff, Tensor grad_loss, "
                     "Tensor(a!)? g_weight, Tensor(b!)? g_bias) -> Tensor",
     "adam_step": "(Tensor(a!) param, Tensor(b!) grad, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "
@@ -107,7 +110,9 @@ _SCHEMAS = {
                  "float eps, float weight_decay) -> ()",
     "window_gather": "(Tensor vol, Tensor volvol, Tensor starts, int seq_length, "
                      "int future_steps, Tensor canon, Tensor(a!) x, Tensor(b!) edge_attr, "
-                     "Tensor(c!) y, int start_offset=0, Tensor? diag=None) -> ()",
+                     "Tensor(c!) y, int start_offset=0, Tensor? diag=None, "
+                     "Tensor(d!)? x_bf16=None) -> ()",
+    "project_a16": "(Tensor a_bf16, int k, Tensor planes, Tensor w) -> Tensor",
 }
 for _name, _schema in _SCHEMAS.items():
     LIB.define(_name + _schema)
@@ -463,7 +468,7 @@ def attn_fwd_head_mse_supported(num_graphs: int, n: int, heads: int, channels: i
 @_impl("gat_attn_fwd_head_mse")
 def _gat_attn_fwd_head_mse(xs, ae, rowmask, bias, keep, keep_scale, post_u, post_p, head_weight,
                            head_bias, target, g_head_weight, g_head_bias, num_graphs, n, heads,
-                           channels, concat, act, slope, edge_order=False):
+                           channels, concat, act, slope, edge_order=False, loss_sum=None):
     """The last layer's attention with GATModel.linear (out_features 1) and the
     MSE loss fused in: returns (dz, psave, loss) — dz the gradient the layer's
     backward starts from (identity activation, no post dropout) — and
@@ -486,14 +491,17 @@ def _gat_attn_fwd_head_mse(xs, ae, rowmask, bias, keep, keep_scale, post_u, post
     dz = torch.empty(N, OC, device=xs.device)
     ps = torch.empty(num_graphs, heads, 32, 32, device=xs.device)
     loss = torch.empty((), device=xs.device)
+    _need(loss_sum is None or (loss_sum.numel() == 1 and loss_sum.dtype == torch.float32),
+          "loss_sum: one float32")
     ws_n = lib.sv2n_gat_attn_fwd_head_mse_workspace(num_graphs, heads, channels, int(concat))
-    ws = torch.empty(ws_n, device=xs.device)
+    # first SV2N_TICKET_WORDS: ticket counters, zero between launches
+    ws = _lib.persistent_zeros("head_fuse", ws_n, xs.device)
     _lib.check(lib.sv2n_gat_attn_fwd_head_mse(
         xs.data_ptr(), xs.stride(0), _p(ae), int(edge_order), _p(rowmask), _p(bias), _p(keep),
         keep_scale, dz.data_ptr(), ps.data_ptr(), _p(post_u), post_p, head_weight.data_ptr(),
-        _p(head_bias), target.data_ptr(), loss.data_ptr(), _p(g_head_weight), _p(g_head_bias),
-        ws.data_ptr(), ws_n, num_graphs, n, heads, channels, int(concat), act, slope, _st(xs)),
-        "sv2n_gat_attn_fwd_head_mse")
+        _p(head_bias), target.data_ptr(), loss.data_ptr(), _p(loss_sum), _p(g_head_weight),
+        _p(g_head_bias), ws.data_ptr(), ws_n, num_graphs, n, heads, channels, int(concat), act,
+        slope, _st(xs)), "sv2n_gat_attn_fwd_head_mse")
     return dz, ps, loss
 
 
@@ -501,7 +509,7 @@ def _gat_attn_fwd_head_mse(xs, ae, rowmask, bias, keep, keep_scale, post_u, post
 def _gat_attn_fwd_head_mse_fake(xs, ae, rowmask, bias, keep, keep_scale, post_u, post_p,
                                 head_weight, head_bias, target, g_head_weight, g_head_bias,
                                 num_graphs, n, heads, channels, concat, act, slope,
-                                edge_order=False):
+                                edge_order=False, loss_sum=None):
     return (xs.new_empty((num_graphs * n, _oc(heads, channels, concat))),
             xs.new_empty((num_graphs, heads, 32, 32)), xs.new_empty(()))
 
@@ -907,7 +915,7 @@ def _head_bwd_fake(x, weight, dout, g_weight, g_bias):
 
 
 @_impl("head_mse_fwd")
-def _head_mse_fwd(x, weight, bias, target):
+def _head_mse_fwd(x, weight, bias, target, loss_sum=None):
     lib = _lib.load()
     _f32(x, weight, bias, target)
     _dense(x, weight, bias)
@@ -921,12 +929,13 @@ def _head_mse_fwd(x, weight, bias, target):
     ws = _lib.persistent_zeros("head", ws_n, x.device)
     _lib.check(lib.sv2n_head_mse_fwd(x.data_ptr(), N, C, weight.data_ptr(), _p(bias), O,
                                      target.data_ptr(), None, diff.data_ptr(), loss.data_ptr(),
-                                     ws.data_ptr(), ws_n, _st(x)), "sv2n_head_mse_fwd")
+                                     _p(loss_sum), ws.data_ptr(), ws_n, _st(x)),
+               "sv2n_head_mse_fwd")
     return loss, diff
 
 
 @_fake("head_mse_fwd")
-def _head_mse_fwd_fake(x, weight, bias, target):
+def _head_mse_fwd_fake(x, weight, bias, target, loss_sum=None):
     return x.new_empty(()), x.new_empty((x.shape[0] * weight.shape[0],))
 
 
@@ -953,7 +962,7 @@ def _head_mse_bwd_fake(x, weight, diff, grad_loss, g_weight, g_bias):
 
 
 @_impl("head_mse_train")
-def _head_mse_train(x, weight, bias, target, g_weight, g_bias):
+def _head_mse_train(x, weight, bias, target, g_weight, g_bias, loss_sum=None):
     """Head + MSE forward and backward in one launch (upstream loss gradient
     1): returns (loss, dx) and accumulates the head's parameter gradients."""
     lib = _lib.load()
@@ -968,14 +977,15 @@ def _head_mse_train(x, weight, bias, target, g_weight, g_bias):
     ws_n = lib.sv2n_head_mse_train_workspace(N, C, O)
     ws = _lib.persistent_zeros("head", ws_n, x.device)
     _lib.check(lib.sv2n_head_mse_train(x.data_ptr(), N, C, weight.data_ptr(), _p(bias), O,
-                                       target.data_ptr(), loss.data_ptr(), dx.data_ptr(),
+                                       target.data_ptr(), loss.data_ptr(), _p(loss_sum),
+                                       dx.data_ptr(),
                                        _p(g_weight), _p(g_bias), ws.data_ptr(), ws_n, _st(x)),
                "sv2n_head_mse_train")
     return loss, dx
 
 
 @_fake("head_mse_train")
-def _head_mse_train_fake(x, weight, bias, target, g_weight, g_bias):
+def _head_mse_train_fake(x, weight, bias, target, g_weight, g_bias, loss_sum=None):
     return x.new_empty(()), torch.empty_like(x)
 
 
@@ -1004,7 +1014,7 @@ def _adam_step_fake(param, grad, exp_avg, exp_avg_sq, step, ticket, lr, beta1, b
 
 @_impl("window_gather")
 def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y,
-                   start_offset=0, diag=None):
+                   start_offset=0, diag=None, x_bf16=None):
     lib = _lib.load()
     _f32(vol, volvol, x, edge_attr, y)
     _need(vol.is_contiguous() and volvol.is_contiguous(), "series must be contiguous")
@@ -1020,6 +1030,15 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
     if diag is not None:  # the series' diagonal, diag[t][v] = volvol[t][v][v]
         _f32(diag)
         _need(diag.is_contiguous() and diag.shape == vol.shape[:2], "diag must be [T][n]")
+    if x_bf16 is not None:  # bf16(x) beside x (sv2n_window_gather_bf16x)
+        _need(x_bf16.dtype == torch.bfloat16 and x_bf16.dim() == 2 and
+              x_bf16.shape[0] == x.shape[0] and x_bf16.stride(1) == 1, "x_bf16 layout")
+        _lib.check(lib.sv2n_window_gather_bf16x(
+            vol.data_ptr(), volvol.data_ptr(), _p(diag), vol.shape[1], vol.shape[0],
+            starts.data_ptr(), start_offset, starts.numel(), seq_length, future_steps,
+            canon.data_ptr(), x.data_ptr(), x_bf16.data_ptr(), x_bf16.stride(0),
+            edge_attr.data_ptr(), y.data_ptr(), _st(vol)), "sv2n_window_gather_bf16x")
+        return
     _lib.check(lib.sv2n_window_gather_diag(vol.data_ptr(), volvol.data_ptr(), _p(diag),
                                            vol.shape[1], vol.shape[0], starts.data_ptr(),
                                            start_offset, starts.numel(), seq_length,
@@ -1030,8 +1049,35 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
 
 @_fake("window_gather")
 def _window_gather_fake(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y,
-                        start_offset=0, diag=None):
+                        start_offset=0, diag=None, x_bf16=None):
     return None
+
+
+def window_bf16x_supported(n: int, seq_length: int, future_steps: int) -> bool:
+    """Whether sv2n_window_gather_bf16x takes the shape (include/sv2n.h)."""
+    return (n * seq_length) % 4 == 0 and 4 * 3 * seq_length * (n + 1) <= 64 * 1024 \
+        and future_steps <= 256
+
+
+@_impl("project_a16")
+def _project_a16(a_bf16, k, planes, w):
+    """The bf16-mode projection bf16(a)·wᵀ from a bf16 copy of a ([M][ld],
+    the first k columns; sv2n_gemm_bf16_a16)."""
+    lib = _lib.load()
+    _f32(w)
+    _need(a_bf16.dtype == torch.bfloat16 and a_bf16.stride(1) == 1, "a_bf16 layout")
+    M = a_bf16.shape[0]
+    N = w.shape[0]
+    out = torch.empty(M, N, device=a_bf16.device, dtype=torch.float32)
+    _lib.check(lib.sv2n_gemm_bf16_a16(a_bf16.data_ptr(), a_bf16.stride(0), planes.data_ptr(),
+                                      out.data_ptr(), out.stride(0), M, N, k, _st(a_bf16)),
+               "sv2n_gemm_bf16_a16")
+    return out
+
+
+@_fake("project_a16")
+def _project_a16_fake(a_bf16, k, planes, w):
+    return a_bf16.new_empty((a_bf16.shape[0], w.shape[0]), dtype=torch.float32)
 
 
 OPS = tuple(_SCHEMAS)

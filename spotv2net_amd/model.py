@@ -28,6 +28,7 @@ from torch import nn
 
 from . import graphed, ops
 from .conv import GATConv
+from .data import bf16_twin
 from .layout import GraphLayout, analyze_edge_index, declare_canonical
 from .stack import gat_stack, gat_train_head_mse, head_mse_loss, linear_head
 
@@ -131,9 +132,11 @@ class GATModel(nn.Module):
         if layout is None:
             layout = _layout_of(data, x, edge_index)
         return gat_stack(x, edge_attr, tuple(self.gat_layers), layout, self._act_code,
-                         float(self.dropout or 0.0), self.training, self.precision)
+                         float(self.dropout or 0.0), self.training, self.precision,
+                         None if self.standardize else bf16_twin(data))
 
-    def _train_head_mse(self, data, target: torch.Tensor) -> Optional[torch.Tensor]:
+    def _train_head_mse(self, data, target: torch.Tensor,
+                        loss_sum: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
         """``train.TrainStep``'s forward + backward with the output head and
         the MSE loss fused into the last GAT layer (stack.gat_train_head_mse):
         the loss, with every gradient accumulated into ``p.grad``; None when
@@ -143,7 +146,7 @@ class GATModel(nn.Module):
         layout = _layout_of(data, data.x, data.edge_index)
         return gat_train_head_mse(data.x, data.edge_attr, tuple(self.gat_layers), layout,
                                   self._act_code, float(self.dropout or 0.0), self.linear, target,
-                                  self.precision)
+                                  self.precision, bf16_twin(data), loss_sum)
 
     def set_precision(self, precision: Optional[str]) -> "GATModel":
         """"bf16": projection / weight-gradient GEMMs on bf16 operands with
@@ -163,10 +166,12 @@ class GATModel(nn.Module):
                 return out.view(-1)
         return linear_head(self._hidden(data, layout), self.linear).view(-1)
 
-    def mse_loss(self, data, target: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def mse_loss(self, data, target: Optional[torch.Tensor] = None,
+                 loss_sum: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``nn.MSELoss()(self(data), target)`` (reference
         5_train_SpotV2Net.py:125, :150-154; target defaults to ``data.y_x``)
-        with the output head and the loss fused into two kernel launches."""
+        with the output head and the loss fused into two kernel launches;
+        ``loss_sum``: a device scalar the loss is also added to (same launch)."""
         if target is None:
             target = data.y_x
-        return head_mse_loss(self._hidden(data), self.linear, target)
+        return head_mse_loss(self._hidden(data), self.linear, target, loss_sum)

@@ -247,14 +247,16 @@ HEAD_FUSE = os.environ.get("SV2N_HEAD_FUSE", "on")
 
 
 def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropout: float,
-                  training: bool, precision: str, need_saved: bool, head=None):
+                  training: bool, precision: str, need_saved: bool, head=None, x_bf16=None):
     """The fused stack's forward launches (module docstring); returns the
     output, the tensors the backward reads and a ``_StackMeta``.  Capturable:
     no host synchronisation, every buffer from the caching allocator.
-    ``head`` = (linear, target, g_weight, g_bias): the last layer also runs
+    ``head`` = (linear, target, g_weight, g_bias, loss_sum or None): the last layer also runs
     the output head and the MSE loss (sv2n::gat_attn_fwd_head_mse, the caller
     checked ``head_mse_fusable``); the output is then the loss and
-    ``meta.head_dz`` the last layer's incoming gradient."""
+    ``meta.head_dz`` the last layer's incoming gradient.  ``x_bf16``: bf16(x)
+    from the data builder (data.bf16_twin), read by the bf16 mode's layer-0
+    GEMMs instead of rounding x."""
     ops = torch.ops.sv2n
     dev = x.device
     L = len(convs)
@@ -323,8 +325,14 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
         F = c.in_channels
         if xin.size(1) != F:
             raise ValueError(f"layer {l}: expected {F} input features, got {xin.size(1)}")
-        if l == 0 and _bf16_export_ok(bf16, training and need_saved and not need_t[0], xin, c,
-                                      fused or tiled):
+        if l == 0 and bf16 and x_bf16 is not None and _a16_ok(x_bf16, xin, planes[l]):
+            # bf16 mode with bf16(x) from the data builder: no rounding pass
+            xs = ops.project_a16(x_bf16, F, planes[l], waugs[l])
+            if _bf16_export_ok(bf16, training and need_saved and not need_t[0], xin, c,
+                               fused or tiled):
+                xb0 = x_bf16
+        elif l == 0 and _bf16_export_ok(bf16, training and need_saved and not need_t[0], xin, c,
+                                        fused or tiled):
             # bf16 mode: the projection also leaves bf16(x) for the layer's
             # weight-gradient GEMM (sv2n_gemm_bf16_export)
             xs, xb0 = ops.project_bf16_export(xin, planes[l], waugs[l])
@@ -356,14 +364,14 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
             ps = aes[l]
         post_u = None
         if head is not None and l == L - 1:
-            lin, target, ghw, ghb = head
+            lin, target, ghw, ghb, lsum = head
             if training and 0.0 < post_dropout < 1.0:
                 post_u = torch.rand(N, Hc * C if c.concat else C, device=dev)
             y, ps, out = ops.gat_attn_fwd_head_mse(
                 xs, aes[l], layout.rowmask, c.bias, keep, kscale, post_u,
                 float(post_dropout) if post_u is not None else 0.0, lin.weight.view(-1), lin.bias,
                 target.reshape(-1), ghw, ghb, B, n, Hc, C, c.concat, act,
-                float(c.negative_slope), eo)
+                float(c.negative_slope), eo, lsum)
             post_u = None  # applied: y is the layer's incoming gradient dz
         elif not (fused or tiled) and training and 0.0 < post_dropout < 1.0:
             # the post-layer dropout (utils/models.py:148) fused into the
@@ -532,9 +540,10 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
 class _GATStack(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, edge_attr, convs, layout: GraphLayout, act: int, post_dropout: float,
-                training: bool, precision: str, *params):
+                training: bool, precision: str, x_bf16, *params):
         out, saved, meta = stack_forward(x, edge_attr, convs, layout, act, post_dropout, training,
-                                         precision, training or any(ctx.needs_input_grad))
+                                         precision, training or any(ctx.needs_input_grad),
+                                         x_bf16=x_bf16)
         ctx.convs = convs
         ctx.layout = layout
         ctx.direct = _direct_mode()
@@ -545,10 +554,19 @@ class _GATStack(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         params = [p for c in ctx.convs for p in layer_params(c)]
-        grad_of = _GradTargets(params, ctx.needs_input_grad[8:], ctx.direct, dout.device)
+        grad_of = _GradTargets(params, ctx.needs_input_grad[9:], ctx.direct, dout.device)
         dx0 = stack_backward(ctx.saved_tensors, ctx.meta, ctx.convs, ctx.layout, dout,
                              ctx.needs_input_grad[0], grad_of)
-        return (dx0, None, None, None, None, None, None, None) + grad_of.returned()
+        return (dx0, None, None, None, None, None, None, None, None) + grad_of.returned()
+
+
+def _a16_ok(x_bf16: torch.Tensor, xin: torch.Tensor, planes) -> bool:
+    """sv2n_gemm_bf16_a16 takes the layer-0 projection from the bf16 twin of x
+    (its large-tile shapes, 16-B rows of the twin)."""
+    return (BF16_OPERANDS == "on" and planes is not None and x_bf16.dtype == torch.bfloat16
+            and x_bf16.shape[0] == xin.shape[0] and x_bf16.shape[1] >= xin.shape[1]
+            and x_bf16.stride(1) == 1 and x_bf16.stride(0) % 8 == 0
+            and x_bf16.data_ptr() % 16 == 0 and xin.shape[0] >= 1024 and planes.shape[-2] >= 384)
 
 
 def _bf16_export_ok(bf16: bool, want: bool, xin: torch.Tensor, conv, other_path: bool) -> bool:
@@ -576,7 +594,9 @@ def head_mse_fusable(convs, layout: GraphLayout, linear: torch.nn.Linear,
 
 def gat_train_head_mse(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs: Sequence,
                        layout: GraphLayout, act: int, post_dropout: float, linear: torch.nn.Linear,
-                       target: torch.Tensor, precision: Optional[str] = None):
+                       target: torch.Tensor, precision: Optional[str] = None,
+                       x_bf16: Optional[torch.Tensor] = None,
+                       loss_sum: Optional[torch.Tensor] = None):
     """One training forward + backward with the upstream loss gradient 1
     (5_train_SpotV2Net.py:150-158: ``loss = MSELoss()(model(data), y);
     loss.backward()``) with the output head and the loss fused into the last
@@ -599,7 +619,8 @@ def gat_train_head_mse(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs
     with torch.no_grad():
         loss, saved, meta = stack_forward(x, edge_attr, tuple(convs), layout, int(act),
                                           float(post_dropout), True, precision, True,
-                                          head=(linear, target, ghw, ghb))
+                                          head=(linear, target, ghw, ghb, loss_sum),
+                                          x_bf16=x_bf16)
         stack_backward(saved, meta, tuple(convs), layout, meta.head_dz, False, grad_of)
     return layout.poison(loss).reshape(())
 
@@ -621,7 +642,8 @@ def _require_params(params) -> None:
 
 def gat_stack(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs: Sequence,
               layout: GraphLayout, act: int, post_dropout: float, training: bool,
-              precision: Optional[str] = None) -> torch.Tensor:
+              precision: Optional[str] = None,
+              x_bf16: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Run ``convs`` (GATConv modules) as one fused autograd node.
 
     ``precision``: "f32" (f32-accurate GEMMs, 1e-5 parity with PyG fp32) or
@@ -641,7 +663,7 @@ def gat_stack(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs: Sequenc
         if p.device != x.device:
             raise RuntimeError("parameters and data must be on the same device")
     out = _GATStack.apply(x, edge_attr, tuple(convs), layout, int(act), float(post_dropout),
-                          bool(training), precision, *params)
+                          bool(training), precision, x_bf16, *params)
     return layout.poison(out)  # NaN if a deferred layout check failed (layout.py)
 
 
@@ -674,9 +696,9 @@ class _HeadMSE(torch.autograd.Function):
     residual, loss) and sv2n::head_mse_bwd (dx and the head's parameter grads)."""
 
     @staticmethod
-    def forward(ctx, x, target, linear, weight, bias):
+    def forward(ctx, x, target, linear, weight, bias, loss_sum=None):
         x = _aligned(x)
-        loss, diff = torch.ops.sv2n.head_mse_fwd(x, weight, bias, target)
+        loss, diff = torch.ops.sv2n.head_mse_fwd(x, weight, bias, target, loss_sum)
         ctx.linear = linear
         ctx.direct = _direct_mode()
         ctx.save_for_backward(x, diff)
@@ -690,19 +712,27 @@ class _HeadMSE(torch.autograd.Function):
                                x.device)
         dx = torch.ops.sv2n.head_mse_bwd(x, lin.weight, diff, gloss, grad_of(lin.weight),
                                          grad_of(lin.bias))
-        return (dx if ctx.needs_input_grad[0] else None, None, None) + grad_of.returned()
+        return (dx if ctx.needs_input_grad[0] else None, None, None) + grad_of.returned() + \
+            (None,)
 
 
-def head_mse_loss(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tensor) -> torch.Tensor:
-    """mean((linear(x).view(-1) - target)²) with the head and the loss fused."""
+def head_mse_loss(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tensor,
+                  loss_sum: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """mean((linear(x).view(-1) - target)²) with the head and the loss fused.
+    ``loss_sum`` (a float32 device scalar): the loss is also added to it in
+    the same launch."""
     _require_params((linear.weight, linear.bias))
     _require_device(x, target)
     if not head_fits(linear.in_features, linear.out_features):
-        return torch.nn.functional.mse_loss(linear(x).view(-1), target)
-    return _HeadMSE.apply(x, target, linear, linear.weight, linear.bias)
+        loss = torch.nn.functional.mse_loss(linear(x).view(-1), target)
+        if loss_sum is not None:
+            loss_sum.add_(loss.detach())
+        return loss
+    return _HeadMSE.apply(x, target, linear, linear.weight, linear.bias, loss_sum)
 
 
-def head_mse_train(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tensor):
+def head_mse_train(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tensor,
+                   loss_sum: Optional[torch.Tensor] = None):
     """Training step's head + loss with the upstream loss gradient 1 (what
     ``loss.backward()`` gives): ONE launch returns ``(loss, dx)`` and
     accumulates ``linear``'s parameter gradients into their ``.grad`` — the
@@ -717,7 +747,7 @@ def head_mse_train(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tenso
     gb = _grad_buf(linear.bias) if linear.bias is not None else None
     return torch.ops.sv2n.head_mse_train(_aligned(x.detach()), linear.weight.detach(),
                                          None if linear.bias is None else linear.bias.detach(),
-                                         target, gw, gb)
+                                         target, gw, gb, loss_sum)
 
 
 def linear_head(x: torch.Tensor, linear: torch.nn.Linear) -> torch.Tensor:

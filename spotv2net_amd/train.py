@@ -207,20 +207,19 @@ class TrainStep:
             if self._fused_mse:
                 # the output head and the loss inside the last GAT layer's
                 # attention forward (stack.gat_train_head_mse) ...
-                loss = self.model._train_head_mse(sh.data, sh.data.y_x)
+                # (both add the loss to loss_sum in their own launch)
+                loss = self.model._train_head_mse(sh.data, sh.data.y_x, self.loss_sum)
                 if loss is not None:
                     sh.loss = loss.detach()
-                    self._accumulate(sh)
                     return
                 # ... or head + loss forward AND backward in one launch (the
                 # upstream gradient of the loss is 1), then the stack's backward
                 h = self.model._hidden(sh.data)
-                res = head_mse_train(h, self.model.linear, sh.data.y_x)
+                res = head_mse_train(h, self.model.linear, sh.data.y_x, self.loss_sum)
                 if res is not None:
                     loss, dh = res
                     torch.autograd.backward(h, dh)
                     sh.loss = loss.detach()
-                    self._accumulate(sh)
                     return
                 loss = self.model.mse_loss(sh.data)
             else:
@@ -438,7 +437,9 @@ class Fit:
     def _static(self, b: int):
         if b not in self._batch:
             self._idx[b] = torch.zeros(b, dtype=torch.long, device=self.dev)
-            self._batch[b] = self.ds.empty_batch(b)
+            # the bf16 mode's layer-0 GEMMs read bf16(x) from the gather
+            self._batch[b] = self.ds.empty_batch(
+                b, bf16_x=getattr(self.model, "precision", None) == "bf16")
             self.ds.fill(self._batch[b], self._idx[b])
         data, idx = self._batch[b], self._idx[b]
         return data, (lambda: self.ds.fill(data, idx))
@@ -448,9 +449,14 @@ class Fit:
             data, prep = self._static(b)
             was = self.model.training
             self.model.eval()
+            # the loss joins _tot_test inside the head launch; the warm-up and
+            # capture calls' additions are undone here
+            saved = self._tot_test.clone()
+            tot = self._tot_test
             self._eval[b] = ForwardStep(self.model, data, use_graph=self.use_graph,
-                                        fn=lambda m, d: m.mse_loss(d).reshape(()), prepare=prep,
-                                        out_sum=self._tot_test)
+                                        fn=lambda m, d: m.mse_loss(d, loss_sum=tot).reshape(()),
+                                        prepare=prep)
+            self._tot_test.copy_(saved)
             self.model.train(was)
         return self._eval[b]
 

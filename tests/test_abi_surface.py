@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     for name in names:
         assert hasattr(lib, name), f"libsv2n.so lacks {name}"
     assert set(names) == set(_lib.EXPORTED_SYMBOLS), "ctypes table and header disagree"
-    assert lib.sv2n_abi_version() == _lib.ABI_VERSION == 14
+    assert lib.sv2n_abi_version() == _lib.ABI_VERSION == 16
     assert b"invalid argument" in lib.sv2n_strerror(-1)
 
 
@@ -39,11 +39,11 @@ def test_argument_errors_without_gpu():
     assert lib.sv2n_edge_logits_bwd_workspace(126, 8) == 1024 * 126 * 8
     # the fused head forward: NULL operands / unsupported shapes, before any HIP call
     assert lib.sv2n_gat_attn_fwd_head_mse(None, 8, None, 0, None, None, None, 1.0, None, None,
-                                          None, 0.0, None, None, None, None, None, None, None, 0,
-                                          1, 30, 4, 8, 1, 1, 0.2, None) == -1
+                                          None, 0.0, None, None, None, None, None, None, None,
+                                          None, 0, 1, 30, 4, 8, 1, 1, 0.2, None) == -1
     assert lib.sv2n_gat_attn_fwd_head_mse_supported(512, 30, 4, 50, 0) == 1
     assert lib.sv2n_gat_attn_fwd_head_mse_supported(512, 40, 4, 50, 0) == 0  # n > 32
-    assert lib.sv2n_gat_attn_fwd_head_mse_workspace(512, 4, 50, 0) == 512 * 52
+    assert lib.sv2n_gat_attn_fwd_head_mse_workspace(512, 4, 50, 0) == 288 + (512 + 8) * 52
 
 
 def _ref_layer_dims(F, D, H, hidden, concat_heads):

@@ -88,3 +88,58 @@ def test_bf16_operand_path_matches_fp32_operands(dev, S, heads, hidden, B, dropo
         grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
     for name in grads[0]:
         assert_close(grads[0][name], grads[1][name], tol=2e-6, what=name)
+
+
+@pytest.mark.parametrize("n,S,Fs", [(30, 42, 1), (30, 4, 14)])
+def test_window_gather_bf16_twin(dev, n, S, Fs):
+    """WindowDataset.empty_batch(bf16_x=True): the gather writes bf16(x)
+    beside x (sv2n_window_gather_bf16x, ABI 15) — bit for bit x rounded to
+    nearest even, zero past n·S, NaN rows for windows outside the series —
+    and x, edge_attr, y_x as without it."""
+    from spotv2net_amd import WindowDataset
+    from spotv2net_amd.data import bf16_twin, synthetic_series
+    V, W = synthetic_series(S + Fs + 60, n, seed=n + S)
+    ds = WindowDataset(V.to(dev), W.to(dev), S, cut=3, future_steps=Fs)
+    idx = torch.randperm(len(ds), generator=torch.Generator().manual_seed(2))[:33].to(dev)
+    idx[5] = 10 ** 6   # past the series: NaN rows
+    a = ds.empty_batch(idx.numel(), bf16_x=True)
+    b = ds.empty_batch(idx.numel())
+    ds.fill(a, idx)
+    ds.fill(b, idx)
+    xb = bf16_twin(a)
+    assert xb is not None and bf16_twin(b) is None
+    for key in ("x", "edge_attr", "y_x"):
+        assert torch.equal(getattr(a, key).nan_to_num(7.0), getattr(b, key).nan_to_num(7.0)), key
+    K = n * S
+    assert torch.equal(xb[:, :K].float().nan_to_num(7.0), a.x.to(torch.bfloat16).float().nan_to_num(7.0))
+    assert not xb[:, K:].float().abs().any()
+    a.x.add_(0.0)   # an in-place write to x retires the twin
+    assert bf16_twin(a) is None
+
+
+def test_bf16_twin_step_is_bit_identical(dev):
+    """The C3 model in bf16 mode on a WindowDataset batch with and without the
+    bf16 twin of x: the same roundings feed the same GEMMs, so the output and
+    every gradient are bit-identical (project_a16 vs the exporting projection)."""
+    from spotv2net_amd import GATModel, WindowDataset
+    from spotv2net_amd.data import synthetic_series
+    S = 42
+    V, W = synthetic_series(S + 200, 30, seed=3)
+    ds = WindowDataset(V.to(dev), W.to(dev), S, cut=5)
+    idx = torch.arange(40, device=dev)
+    a, b = ds.empty_batch(40, bf16_x=True), ds.empty_batch(40)
+    ds.fill(a, idx)
+    ds.fill(b, idx)
+    torch.manual_seed(4)
+    m1 = GATModel(30 * S, 3 * S, 6, 1, [500], concat_heads=True).to(dev).set_precision("bf16")
+    m1.graph_replay = False
+    m2 = copy.deepcopy(m1)
+    outs = []
+    for m, d in ((m1, a), (m2, b)):
+        out = m(d)
+        torch.nn.functional.mse_loss(out, d.y_x).backward()
+        outs.append(out.detach())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    for (n1, p), (_, q) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(p.grad, q.grad), n1
