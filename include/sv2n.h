@@ -156,10 +156,9 @@ int sv2n_gat_attn_fwd(const float* xs, int ldx, const float* ae, int ae_edge_ord
  *          Σ_i 2/N·diff_i (either may be NULL).
  *   loss_sum[0] += loss[0] when loss_sum is not NULL (ABI 16: a running
  *          epoch sum with no separate add launch).
- * One launch: the per-graph partials are summed in graph order inside it
- * (two-level tickets).  workspace: sv2n_gat_attn_fwd_head_mse_workspace
- * floats, 16-B aligned; its first SV2N_TICKET_WORDS are ticket counters that
- * must be zero before the first call (every call leaves them zero).  Runs when
+ * Two launches (the attention, then a fixed-order sum of per-graph partials
+ * in workspace: sv2n_gat_attn_fwd_head_mse_workspace floats, 16-B aligned).
+ * Runs when
  * sv2n_gat_attn_fwd_head_mse_supported: one workgroup per graph (the batch
  * fills the chip, or few work items), OC <= 512.  Replaces the separate
  * sv2n_head_mse_train launch of a training step. */

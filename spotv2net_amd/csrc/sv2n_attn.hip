@@ -60,8 +60,7 @@ extern "C" int sv2n_gat_attn_fwd_head_mse_supported(int64_t num_graphs, int n, i
 extern "C" int64_t sv2n_gat_attn_fwd_head_mse_workspace(int64_t num_graphs, int heads,
                                                         int channels, int concat) {
   if (num_graphs <= 0 || heads < 1 || channels < 1) return 0;
-  // tickets | 8 group slabs | per-graph partials
-  return SV2N_TICKET_WORDS + (num_graphs + 8) * ((concat ? heads * channels : channels) + 2);
+  return num_graphs * ((concat ? heads * channels : channels) + 2);  // per-graph partials
 }
 
 extern "C" int sv2n_gat_attn_fwd_head_mse(
@@ -85,10 +84,7 @@ extern "C" int sv2n_gat_attn_fwd_head_mse(
   hf.w = head_weight;
   hf.b = head_bias;
   hf.target = target;
-  const int O2 = (concat ? heads * channels : channels) + 2;
-  hf.cnt = reinterpret_cast<unsigned*>(workspace);
-  hf.gslab = workspace + SV2N_TICKET_WORDS;
-  hf.part = hf.gslab + 8 * O2;
+  hf.part = workspace;
   hf.inv_n2 = (float)(2.0 / ((double)num_graphs * n));
   hf.gw = g_head_weight;
   hf.gb = g_head_bias;

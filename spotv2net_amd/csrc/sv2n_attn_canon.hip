@@ -94,9 +94,8 @@ __device__ __forceinline__ bool graph_split(int64_t B, int S, int64_t& g, int& s
 // (what the backward's activation step would produce, so the layer's
 // backward runs with the identity and reads no y) and the graph's partials
 // Σ_i dout_i·m·a (head weight), Σ_i dout_i (head bias), Σ_i diff² (loss)
-// go to part[g]; the launch then sums them in graph order in two levels
-// (group_last_sc1 / top_last_sc1), accumulates the head gradients and writes
-// the loss.
+// go to part[g] (k_head_fuse_finish sums them in graph order, accumulates
+// the head gradients and writes the loss).
 template <int ACT, bool CONCAT, bool KEEP, bool HEAD = false>
 __global__ __launch_bounds__(THREADS) void k_fwd(
     const float* __restrict__ xs, int ldx, const float* __restrict__ ae, int ae_edge_order,
@@ -394,14 +393,16 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       const float a = sY[row * OC1 + oc];
       bst(rz, k * 4, act_bwd<ACT>(sD[row] * bld(rw, oc * 4) * mfac(row, oc), a));
     }
-    // the graph's partials, rows summed in order, published write-through
-    const int O2 = OC + 2;
-    float* pg = hf.part + (int64_t)g * O2;
+    // the graph's partials, rows summed in order (k_head_fuse_finish sums
+    // them in graph order: round 4, summing them in this launch with two-level
+    // tickets made the C2 layer-1 forward 31.4 us against 24.9 + 4.9 for the
+    // forward and the separate finish launch)
+    float* pg = hf.part + (int64_t)g * (OC + 2);
     for (int oc = t; oc < OC; oc += THREADS) {
       float sacc = 0.f;
       for (int row = 0; row < n; ++row)
         sacc = fmaf(sD[row], sY[row * OC1 + oc] * mfac(row, oc), sacc);
-      st_sc1(pg + oc, sacc);
+      pg[oc] = sacc;
     }
     if (t == THREADS - 1) {
       float sd = 0.f, sl = 0.f;
@@ -409,53 +410,57 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
         sd += sD[row];
         sl += sL[row];
       }
-      st_sc1(pg + OC, sd);
-      st_sc1(pg + OC + 1, sl);
-    }
-    // two-level in-launch reduction (graph = block here): group q = g % 8
-    // sums graphs q, q + 8, ... in order, the last group finisher the 8 group
-    // sums in order (cdna_hip_programming.md §6 G16; no separate launch)
-    __shared__ int s_flag;
-    const unsigned nb = (unsigned)B;
-    if (group_last_sc1(hf.cnt, nb, &s_flag)) {
-      const unsigned q = (unsigned)(g & 7), members = (nb - q + 7u) / 8u;
-      for (int o = t; o < O2; o += THREADS) {
-        float sacc = 0.f;
-        for (unsigned m0 = 0; m0 < members; m0 += 16) {
-          float v[16];
-#pragma unroll
-          for (int u = 0; u < 16; ++u)
-            v[u] = m0 + u < members ? ld_sc1(hf.part + (int64_t)(q + 8u * (m0 + u)) * O2 + o)
-                                    : 0.f;
-#pragma unroll
-          for (int u = 0; u < 16; ++u) sacc += v[u];
-        }
-        st_sc1(hf.gslab + (int64_t)q * O2 + o, sacc);
-      }
-      if (top_last_sc1(hf.cnt, nb, &s_flag)) {
-        const int groups = nb < 8u ? (int)nb : 8;
-        for (int o = t; o < O2; o += THREADS) {
-          float v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = u < groups ? ld_sc1(hf.gslab + u * O2 + o) : 0.f;
-          const float sm = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-          if (o < OC) {
-            if (hf.gw) hf.gw[o] += sm;
-          } else if (o == OC) {
-            if (hf.gb) hf.gb[0] += sm;
-          } else {
-            const float l = sm * (0.5f * hf.inv_n2);
-            hf.loss[0] = l;
-            if (hf.loss_sum) hf.loss_sum[0] += l;
-          }
-        }
-      }
+      pg[OC] = sd;
+      pg[OC + 1] = sl;
     }
   }
   SV2N_STAMP(5, SV2N_T());
   SV2N_STAMP(6, SV2N_RT());
 }
 
+
+// Sums k_fwd<HEAD>'s per-graph partials part[B][OC + 2] in graph order:
+// g_w[o] += Σ_g part[g][o] (o < OC), g_b[0] += Σ_g part[g][OC], loss[0] =
+// Σ_g part[g][OC + 1] / (B·n) (and loss_sum[0] += loss[0]).  Block: 16
+// columns x 16 graph groups, 32 loads in flight per thread.
+__global__ __launch_bounds__(256) void k_head_fuse_finish(const float* __restrict__ part,
+                                                          int64_t B, int OC, float inv_n,
+                                                          float* __restrict__ g_w,
+                                                          float* __restrict__ g_b,
+                                                          float* __restrict__ loss,
+                                                          float* __restrict__ loss_sum) {
+  constexpr int U = 32;
+  __shared__ float s_red[16][17];
+  const int lo = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int o = blockIdx.x * 16 + lo, O = OC + 2;
+  const rsrc_t rp = make_rsrc(part, (uint32_t)(B * O) * 4u);
+  float a = 0.f;
+  for (int64_t b0 = 0; b0 < B; b0 += 16 * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t b = b0 + grp + 16 * u;
+      v[u] = bld(rp, (o < O && b < B) ? (int)(b * O + o) * 4 : OOB);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) a += v[u];
+  }
+  s_red[grp][lo] = a;
+  __syncthreads();
+  if (grp == 0 && o < O) {
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sm += s_red[k][lo];
+    if (o < OC) {
+      if (g_w) g_w[o] += sm;
+    } else if (o == OC) {
+      if (g_b) g_b[0] += sm;
+    } else {
+      loss[0] = sm * inv_n;
+      if (loss_sum) loss_sum[0] += sm * inv_n;
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------
 // backward: S workgroups per graph (graph_split), split s owning heads
@@ -1170,6 +1175,12 @@ void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const f
   }
 #undef SV2N_CF_ACT
 #undef SV2N_CF
+  if (hf.w) {
+    const int OC = concat ? H * C : C;
+    hipLaunchKernelGGL(canon::k_head_fuse_finish, dim3((unsigned)((OC + 2 + 15) / 16)),
+                       dim3(256), 0, st, hf.part, B, OC, 0.5f * hf.inv_n2, hf.gw, hf.gb,
+                       hf.loss, hf.loss_sum);
+  }
 }
 
 }  // namespace sv2n

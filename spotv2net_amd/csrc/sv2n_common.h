@@ -196,11 +196,9 @@ struct HeadFuse {
   const float* w;       // [OC] GATModel.linear.weight (out_features 1)
   const float* b;       // [1] its bias, or NULL
   const float* target;  // [B·n]
-  unsigned* cnt;        // SV2N_TICKET_WORDS two-level ticket counters (zero between launches)
   float* part;          // [B][OC + 2] per-graph partials: Σ dout·y per column, Σ dout, Σ diff²
-  float* gslab;         // [8][OC + 2] group sums
   float inv_n2;         // 2 / (B·n): d mean((out - target)²) / d out
-  float* gw;            // [OC] += Σ_g, or NULL
+  float* gw;            // host side (k_head_fuse_finish): [OC] += Σ_g, or NULL
   float* gb;            // [1] += Σ_g, or NULL
   float* loss;          // [1] = mean((out - target)²)
   float* loss_sum;      // [1] += loss, or NULL (a running sum the caller keeps)

@@ -494,8 +494,7 @@ def _gat_attn_fwd_head_mse(xs, ae, rowmask, bias, keep, keep_scale, post_u, post
     _need(loss_sum is None or (loss_sum.numel() == 1 and loss_sum.dtype == torch.float32),
           "loss_sum: one float32")
     ws_n = lib.sv2n_gat_attn_fwd_head_mse_workspace(num_graphs, heads, channels, int(concat))
-    # first SV2N_TICKET_WORDS: ticket counters, zero between launches
-    ws = _lib.persistent_zeros("head_fuse", ws_n, xs.device)
+    ws = torch.empty(ws_n, device=xs.device)
     _lib.check(lib.sv2n_gat_attn_fwd_head_mse(
         xs.data_ptr(), xs.stride(0), _p(ae), int(edge_order), _p(rowmask), _p(bias), _p(keep),
         keep_scale, dz.data_ptr(), ps.data_ptr(), _p(post_u), post_p, head_weight.data_ptr(),

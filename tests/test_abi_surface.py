@@ -43,7 +43,7 @@ def test_argument_errors_without_gpu():
                                           None, 0, 1, 30, 4, 8, 1, 1, 0.2, None) == -1
     assert lib.sv2n_gat_attn_fwd_head_mse_supported(512, 30, 4, 50, 0) == 1
     assert lib.sv2n_gat_attn_fwd_head_mse_supported(512, 40, 4, 50, 0) == 0  # n > 32
-    assert lib.sv2n_gat_attn_fwd_head_mse_workspace(512, 4, 50, 0) == 288 + (512 + 8) * 52
+    assert lib.sv2n_gat_attn_fwd_head_mse_workspace(512, 4, 50, 0) == 512 * 52
 
 
 def _ref_layer_dims(F, D, H, hidden, concat_heads):
