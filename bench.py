@@ -365,16 +365,18 @@ def kernel_table_c3(model, cfg, precision, reps=20):
     planes = ops.weight_planes(W, False)
     xs = torch.empty(N, ldx, device=dev)
 
-    # bf16 mode as the step runs it: the projection also exports bf16(x)
-    # (sv2n_gemm_bf16_export), the weight gradient reads bf16 x and bf16 dxs
-    # (sv2n_gat_wgrad_node_bf16b), the attention backward writes bf16 dxs
+    # bf16 mode as the C3 loop runs it: the window gather leaves bf16(x)
+    # beside x, the projection reads it (sv2n_gemm_bf16_a16), the weight
+    # gradient reads bf16 x and bf16 dxs (sv2n_gat_wgrad_node_bf16b), the
+    # attention backward writes bf16 dxs
     kb = (F + 63) // 64 * 64
-    xb = torch.empty(N, kb, device=dev, dtype=torch.bfloat16)
+    xb = torch.zeros(N, kb, device=dev, dtype=torch.bfloat16)
+    xb[:, :F] = x.to(torch.bfloat16)
 
     def gemm_fwd():
         if bf16:
-            lib.sv2n_gemm_bf16_export(x.data_ptr(), x.stride(0), planes.data_ptr(), xs.data_ptr(),
-                                      xs.stride(0), N, ldx, F, xb.data_ptr(), kb, sh)
+            lib.sv2n_gemm_bf16_a16(xb.data_ptr(), kb, planes.data_ptr(), xs.data_ptr(),
+                                   xs.stride(0), N, ldx, F, sh)
         else:
             lib.sv2n_gemm_f32x3(x.data_ptr(), x.stride(0), planes.data_ptr(), xs.data_ptr(),
                                 xs.stride(0), N, ldx, F, sh)
@@ -441,9 +443,9 @@ def kernel_table_c3(model, cfg, precision, reps=20):
     peak = BF16_MFMA_PEAK_TFLOPS if bf16 else BF16X3_PEAK_TFLOPS
     gflop = 2.0 * N * HC * F + 4.0 * N * HC   # algorithmic: H·C columns
     rows = {
-        # bf16: x read (fp32) and written once more as bf16
-        "gemm_fwd": (gemm_fwd, "mfma", gflop, 4.0 * (N * F + N * ldx) + (2 if bf16 else 6) * ldx * F
-                     + (2.0 * N * kb if bf16 else 0.0), peak),
+        # bf16: x read as its bf16 twin
+        "gemm_fwd": (gemm_fwd, "mfma", gflop, (2.0 * N * kb if bf16 else 4.0 * N * F)
+                     + 4.0 * N * ldx + (2 if bf16 else 6) * ldx * F, peak),
         # bf16: both operands bf16 in memory; gW (and the fold's W) read and written
         "wgrad_node": (wgrad, "mfma", gflop,
                        (2.0 * (N * kb + N * ldb) if bf16 else 4.0 * (N * F + N * ldx))
