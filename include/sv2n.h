@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 16
+#define SV2N_ABI_VERSION 17
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -428,6 +428,16 @@ int sv2n_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_av
 int sv2n_adam_f32_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                        float* step, uint32_t* counter, float lr, float beta1, float beta2,
                        float eps, float weight_decay, hipStream_t stream);
+
+/* Dropout uniforms for the captured training step (ABI 17; replaces the
+ * torch.rand draw behind F.dropout, reference utils/models.py:148, inside
+ * spotv2net_amd.train.TrainStep): u[i] = word i%4 of Philox4x32-10 with key
+ * = seed and counter = (i/4 low, i/4 high, salt, (uint32)*step), scaled as
+ * (word >> 8)·2^-24 in [0, 1).  *step is a device float (the optimizer's step
+ * count), so a graph replay draws new values with no host work; u 16-B
+ * aligned. */
+int sv2n_dropout_uniform(float* u, int64_t n, uint64_t seed, const float* step, uint32_t salt,
+                         hipStream_t stream);
 
 /* Output head (GATModel.linear, reference utils/models.py:120/:150):
  *   out[i][o] = Σ_c x[i][c]·weight[o][c] + bias[o]      x [rows][in], weight [out][in]

@@ -16,13 +16,15 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SV2N_LIB: an alternative build of the same library (diagnostic builds, e.g.
 # tools/stamps.py); default the in-tree one
 LIB_PATH = os.environ.get("SV2N_LIB") or os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p
 _i64 = ctypes.c_int64
 _i32 = ctypes.c_int
 _f32 = ctypes.c_float
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
 
 class PrepLayer(ctypes.Structure):
     """sv2n_prep_layer (include/sv2n.h)."""
@@ -123,6 +125,7 @@ _SIGNATURES = {
     "sv2n_adam_f32": (_i32, [_p, _p, _p, _p, _i64, _p, _f32, _f32, _f32, _f32, _f32, _p]),
     "sv2n_adam_f32_step": (_i32, [_p, _p, _p, _p, _i64, _p, _p, _f32, _f32, _f32, _f32, _f32,
                                   _p]),
+    "sv2n_dropout_uniform": (_i32, [_p, _i64, _u64, _p, _u32, _p]),
     "sv2n_head_mse_workspace": (_i64, [_i64, _i32, _i32]),
     "sv2n_head_mse_train_workspace": (_i64, [_i64, _i32, _i32]),
     "sv2n_head_mse_train": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _i64,

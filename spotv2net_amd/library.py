@@ -105,6 +105,7 @@ _SCHEMAS = {
                       "-> (Tensor, Tensor)",
     "head_mse_bwd": "(Tensor x, Tensor weight, Tensor diff, Tensor grad_loss, "
                     "Tensor(a!)? g_weight, Tensor(b!)? g_bias) -> Tensor",
+    "dropout_uniform": "(int rows, int cols, Tensor step, int seed, int salt) -> Tensor",
     "adam_step": "(Tensor(a!) param, Tensor(b!) grad, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "
                  "Tensor(e!) step, Tensor(f!) ticket, float lr, float beta1, float beta2, "
                  "float eps, float weight_decay) -> ()",
@@ -1003,6 +1004,27 @@ def _adam_step(param, grad, exp_avg, exp_avg_sq, step, ticket, lr, beta1, beta2,
                                       exp_avg_sq.data_ptr(), param.numel(), step.data_ptr(),
                                       ticket.data_ptr(), lr, beta1, beta2, eps, weight_decay,
                                       _st(param)), "sv2n_adam_f32_step")
+
+
+@_impl("dropout_uniform")
+def _dropout_uniform(rows, cols, step, seed, salt):
+    """[rows][cols] uniforms in [0, 1) from Philox4x32-10 keyed by ``seed``
+    with the device step count ``step`` (float32 scalar) and ``salt`` in the
+    counter (sv2n_dropout_uniform): a captured step draws fresh values on
+    every replay without a torch random op in the graph."""
+    lib = _lib.load()
+    _need(step.is_cuda and step.dtype == torch.float32 and step.numel() >= 1,
+          "step must be a device float32 scalar")
+    u = torch.empty(rows, cols, device=step.device)
+    _lib.check(lib.sv2n_dropout_uniform(u.data_ptr(), u.numel(), seed & 0xFFFFFFFFFFFFFFFF,
+                                        step.data_ptr(), salt & 0xFFFFFFFF, _st(step)),
+               "sv2n_dropout_uniform")
+    return u
+
+
+@_fake("dropout_uniform")
+def _dropout_uniform_fake(rows, cols, step, seed, salt):
+    return step.new_empty(rows, cols)
 
 
 @_fake("adam_step")

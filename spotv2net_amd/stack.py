@@ -87,6 +87,29 @@ def _direct_mode() -> bool:
     return getattr(_mode, "direct", False)
 
 
+@contextlib.contextmanager
+def device_dropout(seed: int, step: torch.Tensor):
+    """Within this context the post-layer dropout of the n <= 32 attention
+    (utils/models.py:148) draws its uniforms from sv2n::dropout_uniform keyed
+    by (``seed``, the device step count ``step``, layer) instead of torch's
+    generator, so a captured step holds no torch random op (whose replays
+    each launch two generator-state fills).  ``train.TrainStep`` uses it with
+    its Adam step counter; outside it every draw is torch.rand."""
+    prev = getattr(_mode, "drop_rng", None)
+    _mode.drop_rng = (int(seed), step)
+    try:
+        yield
+    finally:
+        _mode.drop_rng = prev
+
+
+def _post_uniforms(rows: int, cols: int, layer: int, dev) -> torch.Tensor:
+    rng = getattr(_mode, "drop_rng", None)
+    if rng is None:
+        return torch.rand(rows, cols, device=dev)
+    return torch.ops.sv2n.dropout_uniform(rows, cols, rng[1], rng[0], layer)
+
+
 class _GradTargets:
     """Where a fused node's kernels accumulate parameter gradients, and what
     its backward returns for the parameters (see module docstring)."""
@@ -366,7 +389,7 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
         if head is not None and l == L - 1:
             lin, target, ghw, ghb, lsum = head
             if training and 0.0 < post_dropout < 1.0:
-                post_u = torch.rand(N, Hc * C if c.concat else C, device=dev)
+                post_u = _post_uniforms(N, Hc * C if c.concat else C, l, dev)
             y, ps, out = ops.gat_attn_fwd_head_mse(
                 xs, aes[l], layout.rowmask, c.bias, keep, kscale, post_u,
                 float(post_dropout) if post_u is not None else 0.0, lin.weight.view(-1), lin.bias,
@@ -376,9 +399,10 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
         elif not (fused or tiled) and training and 0.0 < post_dropout < 1.0:
             # the post-layer dropout (utils/models.py:148) fused into the
             # attention's store: torch draws the uniforms (same stream as
-            # rand_like(y) >= p), the kernel masks, scales and writes both y
-            # (for the activation's backward) and the layer output
-            post_u = torch.rand(N, Hc * C if c.concat else C, device=dev)
+            # rand_like(y) >= p; device_dropout: sv2n::dropout_uniform), the
+            # kernel masks, scales and writes both y (for the activation's
+            # backward) and the layer output
+            post_u = _post_uniforms(N, Hc * C if c.concat else C, l, dev)
             y, ps, out = ops.gat_attn_fwd_post(xs, aes[l], layout.rowmask, c.bias, keep, kscale,
                                                post_u, float(post_dropout), B, n, Hc, C,
                                                c.concat, act, float(c.negative_slope), eo)

@@ -159,7 +159,8 @@ class TrainStep:
                  loss_fn: Callable = torch.nn.functional.mse_loss, use_graph: bool = True,
                  group=None, warmup: int = 3, optimizer: str = "sv2n",
                  prepare: Optional[Callable[[], None]] = None,
-                 loss_sum: Optional[torch.Tensor] = None):
+                 loss_sum: Optional[torch.Tensor] = None, device_rng: bool = True,
+                 dropout_seed: Optional[int] = None):
         self.model = model
         self.loss_sum = loss_sum
         self.loss_fn = loss_fn
@@ -170,6 +171,11 @@ class TrainStep:
         self.flat = flatten_grads(self.params)
         self.opt = FlatAdam(self.flat_params, self.flat, lr) if optimizer == "sv2n" \
             else make_adam(self.params, lr)
+        # post-layer dropout uniforms keyed by (seed, Adam's device step
+        # count, layer) (stack.device_dropout): no torch random op in the
+        # captured step; device_rng=False keeps torch's generator
+        self.device_rng = device_rng and isinstance(self.opt, FlatAdam)
+        self.dropout_seed = int(torch.initial_seed() if dropout_seed is None else dropout_seed)
         self.distributed = dist.is_available() and dist.is_initialized() and \
             dist.get_world_size(group) > 1
         self.use_graph = use_graph
@@ -196,6 +202,13 @@ class TrainStep:
 
     # -- eager pieces -------------------------------------------------------
     def _fwd_bwd(self, sh: _Shape) -> None:
+        from .stack import device_dropout
+        if not self.device_rng:
+            return self._fwd_bwd_inner(sh)
+        with device_dropout(self.dropout_seed, self.opt.step_t):
+            return self._fwd_bwd_inner(sh)
+
+    def _fwd_bwd_inner(self, sh: _Shape) -> None:
         from .stack import direct_grad_accumulation, head_mse_train
         if sh.prepare is not None:
             sh.prepare()
@@ -424,9 +437,10 @@ class Fit:
         for b in sizes:
             data, prep = self._static(b)
             if self.step is None:
+                # a step_hook seeds torch's generator per step: its draws stay torch's
                 self.step = TrainStep(model, data, lr=lr, use_graph=self.use_graph,
                                       optimizer=optimizer, prepare=prep,
-                                      loss_sum=self._tot_train)
+                                      loss_sum=self._tot_train, device_rng=step_hook is None)
                 self._train_shape[b] = 0
             else:
                 self._train_shape[b] = self.step.add_shape(data, prep)

@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     for name in names:
         assert hasattr(lib, name), f"libsv2n.so lacks {name}"
     assert set(names) == set(_lib.EXPORTED_SYMBOLS), "ctypes table and header disagree"
-    assert lib.sv2n_abi_version() == _lib.ABI_VERSION == 16
+    assert lib.sv2n_abi_version() == _lib.ABI_VERSION == 17
     assert b"invalid argument" in lib.sv2n_strerror(-1)
 
 
@@ -44,6 +44,8 @@ def test_argument_errors_without_gpu():
     assert lib.sv2n_gat_attn_fwd_head_mse_supported(512, 30, 4, 50, 0) == 1
     assert lib.sv2n_gat_attn_fwd_head_mse_supported(512, 40, 4, 50, 0) == 0  # n > 32
     assert lib.sv2n_gat_attn_fwd_head_mse_workspace(512, 4, 50, 0) == 512 * 52
+    # the device dropout generator: NULL output / step
+    assert lib.sv2n_dropout_uniform(None, 16, 1, None, 0, None) == -1
 
 
 def _ref_layer_dims(F, D, H, hidden, concat_heads):
