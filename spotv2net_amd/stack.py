@@ -229,11 +229,6 @@ def _opt(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 # (off, `profiles/r04_c2_edge_ab.txt`).
 EDGE_TAIL = os.environ.get("SV2N_EDGE_TAIL", "off")
 
-# "on": the training step's edge-gradient pass (HBM-bound) runs on a side
-# stream beside layer 0's weight-gradient GEMM (MFMA/VALU-bound), joined before
-# the edge-fold launch; "off": in order on the launch stream (A/B switch)
-EDGE_BWD_SIDE = os.environ.get("SV2N_EDGE_BWD_SIDE", "off")
-
 
 def _edge_tail_ok(layout: GraphLayout, convs, ea, hp: int) -> bool:
     """Layer 0's n <= 32 attention backward can carry the edge gradient of
@@ -480,21 +475,6 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
     edge_tail = bool(need_edge and not fused and not layout.tiled and eo and
                      _edge_tail_ok(layout, convs, ea, hp))
     LAST_PATH["edge_tail"] = edge_tail
-    side_join = None  # (main, side) once the edge-gradient pass runs on the side stream
-
-    def edge_bwd_beside():
-        # every layer's dAE exists once layer 0's attention backward has run
-        nonlocal dwf, side_join
-        main = torch.cuda.current_stream(dev)
-        side = _side_stream(dev)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            dwf = ops.edge_logits_bwd(ea, None, layout.canon, daes, H, B, n, hp, False)
-        dwf.record_stream(main)
-        side_join = (main, side)
-
-    side_edge = bool(EDGE_BWD_SIDE == "on" and need_edge and not fused and not layout.tiled
-                     and not edge_tail and layout.kind != "block" and dev.type == "cuda")
     for l in range(L - 1, -1, -1):
         c = convs[l]
         Hc, C = c.heads, c.out_channels
@@ -522,8 +502,6 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
                 B, n, Hc, C, c.concat, act_l, float(c.negative_slope), eo, post_u,
                 meta.post_p[l] or 0.0)
             daes[l] = _opt(dae)
-            if side_edge:
-                edge_bwd_beside()
             ops.gat_wgrad_bf16b(xb0, dxb, c.lin_src.weight, c.att_src, c.att_dst, dbp, Hc, C,
                                 grad_of(c.lin_src.weight), grad_of(c.att_src),
                                 grad_of(c.att_dst), grad_of(c.bias))
@@ -540,8 +518,6 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
                 B, n, Hc, C, c.concat, act_l, float(c.negative_slope), eo, post_u,
                 meta.post_p[l] or 0.0)
         daes[l] = _opt(dae)
-        if side_edge and l == 0:
-            edge_bwd_beside()
         gW = grad_of(c.lin_src.weight)
         gas = grad_of(c.att_src)
         gad = grad_of(c.att_dst)
@@ -567,9 +543,7 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
         need_e = [(grad_of(c.lin_edge.weight), grad_of(c.att_edge)) for c in convs]
         if ea.size(0) > 0 and any(a is not None or b is not None for a, b in need_e):
             ei = layout.edge_index if layout.kind == "block" else None
-            if side_join is not None:
-                side_join[0].wait_stream(side_join[1])
-            elif not fused and not edge_tail:
+            if not fused and not edge_tail:
                 dwf = ops.edge_logits_bwd(ea, ei, layout.canon, daes, H, B, n, hp,
                                           layout.tiled)
             if all(a is not None and b is not None for a, b in need_e):
