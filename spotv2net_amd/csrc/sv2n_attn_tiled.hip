@@ -117,11 +117,14 @@ __device__ __forceinline__ int canon_logit_id(int upb, int i, int j, int n) {
   const int id = j > i ? upb + j : tri_off(n, j) - j - 1 + i;
   return (i < n && j < n && j != i) ? id : -1;
 }
-// the same through an edge-id map row (erow = (g*n + i)*n)
+// the same through an edge-id map row (erow = (g*n + i)*n).  The load is
+// unconditional (a branch per element costs an exec-masked region); a row
+// past n (the padding rows of a graph's last target block, which for the
+// last graph lie past the end of the map) reads element 0 instead.
 __device__ __forceinline__ int eid_logit_id(const int32_t* __restrict__ eid, int64_t erow, int i,
                                             int j, int n) {
   const bool ok = i < n && j < n && j != i;
-  const int e = eid[erow + (ok ? j : 0)];
+  const int e = eid[ok ? erow + j : 0];
   return ok ? e : -1;
 }
 
@@ -181,7 +184,8 @@ __device__ __forceinline__ void row_softmax(RowSoft& S, float (&e)[16], const La
     for (int k = 0; k < 16; ++k) {
       const int j = src_of(q, k);
       const bool in = i < n && j < n && j != i;
-      const uint32_t w = rowmask ? rowmask[grow * W + (in ? (j >> 5) : 0)] : ~0u;
+      // rows past n (last graph: past the end of the mask) read word 0
+      const uint32_t w = rowmask ? rowmask[in ? grow * W + (j >> 5) : 0] : ~0u;
       pres |= ((in && ((w >> (j & 31)) & 1u)) ? 1u : 0u) << k;
     }
     valid = pres | (kd >= 0 ? (1u << kd) : 0u);
