@@ -758,6 +758,25 @@ def main(argv=None):
     value = world * args.batch * args.steps / el
     loss = float(step.loss.item())
 
+    # the batch's edge_attr is in the reference's covariance layout (written
+    # by window_batch, layout.mark_cov_var), so the step's edge passes read
+    # ≈ 1/6 of it; the same step over every edge row, for comparison
+    from spotv2net_amd import stack
+    cov_var = bool(stack.LAST_PATH.get("cov_var"))
+    value_generic = None
+    if cov_var:
+        old = stack.COV_VAR_EDGES
+        stack.COV_VAR_EDGES = "off"
+        try:
+            gstep = TrainStep(model, data, lr=1e-3, use_graph=not args.no_graph)
+            for _ in range(args.warmup):
+                gstep()
+            gel = max_over_ranks(time_replays(gstep, args.steps), dev)
+            value_generic = world * args.batch * args.steps / gel
+            del gstep
+        finally:
+            stack.COV_VAR_EDGES = old
+
     replicas_ok = replicas_identical(step.flat_params, dev) if world > 1 else None
 
     ref = {}
@@ -821,6 +840,10 @@ def main(argv=None):
             "config": {"workload": cfg["desc"], "name": args.config,
                        "graphs_per_gpu": args.batch, "global_batch": args.batch * world,
                        "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
+            "edge_features": ("reference covariance layout [cov | var_src | var_dst] per lag "
+                              "(utils/dataset.py:228-243), read as such by the edge passes"
+                              if cov_var else "generic rows"),
+            "value_generic_edges": (round(value_generic, 1) if value_generic else None),
             "fwd_graphs_per_s": round(fwd_value, 1),
             **{k: round(v, 1) for k, v in ref.items()},
             "ref_loop_is": "5_train_SpotV2Net.py:142-160 unchanged (new batch per step, "

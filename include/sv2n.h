@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 17
+#define SV2N_ABI_VERSION 18
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -428,6 +428,27 @@ int sv2n_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_av
 int sv2n_adam_f32_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                        float* step, uint32_t* counter, float lr, float beta1, float beta2,
                        float eps, float weight_decay, hipStream_t stream);
+
+/* Edge logits for edge features in the reference's covariance layout (ABI
+ * 18; utils/dataset.py:228-243 and :279-282): row s -> t of edge_attr is
+ * [cov_t'(s,t) | var_t'(s) | var_t'(t)] for t' < seq_length (edge_dim =
+ * 3·seq_length), cov the same for both directions, var a per-node series.
+ * Canonical complete graphs of n <= 32 nodes (canon as for
+ * sv2n_edge_logits_fwd), L·H <= 16 logit columns, seq_length <= 64.  The
+ * outputs are those of sv2n_edge_logits_fwd / _bwd (ae per layer [E][H] in
+ * edge order; dwfold [edge_dim][hl_pad]) computed from the covariance columns
+ * of the upper rows and one variance series per node: ≈ 1/6 of edge_attr is
+ * read.  The caller guarantees the layout (its builder wrote it); other
+ * edge_attr gives other logits.  The backward's workspace:
+ * sv2n_edge_logits_bwd_cv_workspace floats. */
+int sv2n_edge_logits_fwd_cv(const float* edge_attr, int64_t num_graphs, int n, int seq_length,
+                            const uint16_t* canon, const float* wfold, int hl_pad,
+                            float* const* ae_layers, int num_layers, int heads, hipStream_t stream);
+int64_t sv2n_edge_logits_bwd_cv_workspace(int seq_length, int hl_pad);
+int sv2n_edge_logits_bwd_cv(const float* edge_attr, int64_t num_graphs, int n, int seq_length,
+                            const uint16_t* canon, const float* const* dae_layers, int num_layers,
+                            int heads, float* workspace, int64_t workspace_floats, float* dwfold,
+                            int hl_pad, hipStream_t stream);
 
 /* Dropout uniforms for the captured training step (ABI 17; replaces the
  * torch.rand draw behind F.dropout, reference utils/models.py:148, inside

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SV2N_LIB: an alternative build of the same library (diagnostic builds, e.g.
 # tools/stamps.py); default the in-tree one
 LIB_PATH = os.environ.get("SV2N_LIB") or os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p
@@ -126,6 +126,10 @@ _SIGNATURES = {
     "sv2n_adam_f32_step": (_i32, [_p, _p, _p, _p, _i64, _p, _p, _f32, _f32, _f32, _f32, _f32,
                                   _p]),
     "sv2n_dropout_uniform": (_i32, [_p, _i64, _u64, _p, _u32, _p]),
+    "sv2n_edge_logits_fwd_cv": (_i32, [_p, _i64, _i32, _i32, _p, _p, _i32, _p, _i32, _i32, _p]),
+    "sv2n_edge_logits_bwd_cv_workspace": (_i64, [_i32, _i32]),
+    "sv2n_edge_logits_bwd_cv": (_i32, [_p, _i64, _i32, _i32, _p, _p, _i32, _i32, _p, _i64, _p,
+                                       _i32, _p]),
     "sv2n_head_mse_workspace": (_i64, [_i64, _i32, _i32]),
     "sv2n_head_mse_train_workspace": (_i64, [_i64, _i32, _i32]),
     "sv2n_head_mse_train": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _i64,

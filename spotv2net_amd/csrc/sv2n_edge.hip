@@ -780,6 +780,246 @@ __global__ void k_block_eid(const int64_t* __restrict__ ei, int64_t E, int64_t N
   eid[t * n + j] = (int32_t)e;
 }
 
+// ---------------------------------------------------------------------------
+// Edge features in the reference's covariance layout (utils/dataset.py:
+// 228-243, stacked over the window at :279-282): the row of edge s -> t is
+//   [cov_t'(s,t) | var_t'(s) | var_t'(t)]  for t' < S  (D = 3S),
+// with cov symmetric (both directions carry adj[min][max]) and var a node
+// quantity (the volvol diagonal).  Canonical complete graphs only (upper pairs
+// p = (u, v), u < v, row-major, source u -> target v; then the same pairs
+// swapped at P + p).  Every logit is then
+//   ae[u->v][c] = A[p][c] + Vs[u][c] + Vt[v][c],   ae[v->u][c] = A[p][c] + Vs[v][c] + Vt[u][c]
+//   A[p][c] = Σ cov_t'(p)·W̃[t'][c],  Vs[u][c] = Σ var_t'(u)·W̃[S+t'][c],  Vt: W̃[2S+t'][c]
+// so a graph's pass reads the covariance columns of its P upper rows and
+// one variance series per node (from the rows of pairs (0, u)): ≈ 1/6 of
+// its edge_attr bytes.  The backward is the transpose:
+//   dW̃[t'][c]    = Σ_p cov_t'(p)·(dae[p][c] + dae[P+p][c])
+//   dW̃[S+t'][c]  = Σ_u var_t'(u)·Σ_{source u} dae[e][c]
+//   dW̃[2S+t'][c] = Σ_u var_t'(u)·Σ_{target u} dae[e][c]
+// One 256-thread workgroup per graph (grid-stride); the backward accumulates
+// its graphs' dW̃ in registers and leaves one partial slab per workgroup
+// (k_reduce_partials sums them in order).  The caller vouches for the layout
+// (spotv2net_amd.layout.mark_cov_var: the builders that write it).
+// ---------------------------------------------------------------------------
+constexpr int CV_T = 256, CV_MAXN = 32, CV_MAXS = 64, CV_MAXC = 16, CV_PCH = 64;
+constexpr int CV_BWD_GRID = 256;
+
+// node u's variance series: the source columns of pair (0, 1) for u = 0, the
+// target columns of pair (0, u) (upper row u - 1) otherwise
+__device__ __forceinline__ const float* cv_var_row(const float* gea, int u, int S, int D) {
+  return u == 0 ? gea + S : gea + (int64_t)(u - 1) * D + 2 * S;
+}
+
+__device__ __forceinline__ float* cv_col(const LayerPtrs& lp, int c, int H) {
+  float* r = nullptr;
+#pragma unroll
+  for (int l = 0; l < SV2N_MAX_LAYERS; ++l)
+    if (c >= l * H && c < (l + 1) * H) r = lp.p[l] + (c - l * H);
+  return r;
+}
+__device__ __forceinline__ const float* cv_col(const LayerCPtrs& lp, int c, int H) {
+  const float* r = nullptr;
+#pragma unroll
+  for (int l = 0; l < SV2N_MAX_LAYERS; ++l)
+    if (c >= l * H && c < (l + 1) * H) r = lp.p[l] + (c - l * H);
+  return r;
+}
+
+// global -> LDS staging with 8 loads in flight per thread (a runtime-bounded
+// loop would wait on each load before issuing the next)
+template <typename LOAD, typename STORE>
+__device__ __forceinline__ void cv_stage(int total, int t, LOAD load, STORE store) {
+  for (int k0 = t; k0 < total; k0 += 8 * CV_T) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u * CV_T;
+      v[u] = k < total ? load(k) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u * CV_T;
+      if (k < total) store(k, v[u]);
+    }
+  }
+}
+
+// Forward: one workgroup per (graph, chunk of CV_PCH upper pairs), four
+// threads per pair.  A thread's covariance loads (t' = cq, cq + 4, ...) are
+// issued first and land while W̃ and the node variances are staged; the four
+// partial dot products of a pair are summed across its lanes (xor 1, 2).
+__global__ __launch_bounds__(CV_T) void k_edge_fwd_cv(const float* __restrict__ ea, int n, int S,
+                                                      const uint16_t* __restrict__ canon,
+                                                      const float* __restrict__ wf, int hlp,
+                                                      LayerPtrs ae, int L, int H) {
+  __shared__ __attribute__((aligned(16))) float sW[3 * CV_MAXS][CV_MAXC];
+  __shared__ float sVar[CV_MAXN][CV_MAXS + 1];
+  __shared__ float sVs[CV_MAXN][CV_MAXC], sVt[CV_MAXN][CV_MAXC];
+  const int t = threadIdx.x, D = 3 * S, HL = L * H, E0 = n * (n - 1), P = E0 / 2;
+  const int nch = (P + CV_PCH - 1) / CV_PCH;
+  const int64_t g = blockIdx.x / nch;
+  const int p0 = (int)(blockIdx.x - g * nch) * CV_PCH;
+  const int pl = t >> 2, cq = t & 3, p = p0 + pl;
+  const bool pv = p < P;
+  const float* gea = ea + g * E0 * D;
+  float x[CV_MAXS / 4];
+#pragma unroll
+  for (int k = 0; k < CV_MAXS / 4; ++k) {
+    const int tt = cq + 4 * k;
+    x[k] = (pv && tt < S) ? gea[(int64_t)p * D + tt] : 0.f;
+  }
+  cv_stage(D * CV_MAXC, t,
+           [&](int k) {
+             const int d = k / CV_MAXC, c = k - d * CV_MAXC;
+             return c < HL ? wf[d * hlp + c] : 0.f;
+           },
+           [&](int k, float v) { sW[k / CV_MAXC][k % CV_MAXC] = v; });
+  cv_stage(n * S, t, [&](int k) { return cv_var_row(gea, k / S, S, D)[k % S]; },
+           [&](int k, float v) { sVar[k / S][k % S] = v; });
+  __syncthreads();
+  for (int k = t; k < n * HL; k += CV_T) {
+    const int u = k / HL, c = k - u * HL;
+    float vs = 0.f, vt = 0.f;
+    for (int tt = 0; tt < S; ++tt) {
+      vs = fmaf(sVar[u][tt], sW[S + tt][c], vs);
+      vt = fmaf(sVar[u][tt], sW[2 * S + tt][c], vt);
+    }
+    sVs[u][c] = vs;
+    sVt[u][c] = vt;
+  }
+  float acc[CV_MAXC];
+#pragma unroll
+  for (int c = 0; c < CV_MAXC; ++c) acc[c] = 0.f;
+#pragma unroll
+  for (int k = 0; k < CV_MAXS / 4; ++k) {
+    const int tt = cq + 4 * k;
+    if (tt < S) {
+#pragma unroll
+      for (int c = 0; c < CV_MAXC; c += 4) {
+        const float4 w = *reinterpret_cast<const float4*>(&sW[tt][c]);
+        acc[c] = fmaf(x[k], w.x, acc[c]);
+        acc[c + 1] = fmaf(x[k], w.y, acc[c + 1]);
+        acc[c + 2] = fmaf(x[k], w.z, acc[c + 2]);
+        acc[c + 3] = fmaf(x[k], w.w, acc[c + 3]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CV_MAXC; ++c) {
+    acc[c] += __shfl_xor(acc[c], 1, 64);
+    acc[c] += __shfl_xor(acc[c], 2, 64);
+  }
+  __syncthreads();  // sVs / sVt
+  if (!pv) return;
+  const int pr = canon[p];  // (target << 8) | source of upper edge p
+  const int u = pr & 0xff, v = pr >> 8;
+  const int64_t eu = g * E0 + p, el = g * E0 + P + p;
+#pragma unroll
+  for (int i = 0; i < CV_MAXC / 4; ++i) {
+    const int c = cq + 4 * i;
+    float a = acc[0];
+#pragma unroll
+    for (int j = 1; j < CV_MAXC; ++j) a = (j == c) ? acc[j] : a;
+    if (c < HL) {
+      float* col = cv_col(ae, c, H);
+      col[eu * H] = a + sVs[u][c] + sVt[v][c];
+      col[el * H] = a + sVs[v][c] + sVt[u][c];
+    }
+  }
+}
+
+// dynamic LDS: sDae [E0][HL] (this graph's d-logits), then sCov [CV_PCH][S + 1]
+__global__ __launch_bounds__(CV_T) void k_edge_bwd_cv(const float* __restrict__ ea, int64_t B,
+                                                      int n, int S,
+                                                      const uint16_t* __restrict__ canon,
+                                                      LayerCPtrs dae, int L, int H, int hlp,
+                                                      float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float sVar[CV_MAXN][CV_MAXS + 1];
+  __shared__ float sDS[CV_MAXN][CV_MAXC], sDT[CV_MAXN][CV_MAXC];
+  const int t = threadIdx.x, D = 3 * S, HL = L * H, E0 = n * (n - 1), P = E0 / 2;
+  float* sDae = smem;
+  float* sCov = smem + E0 * HL;
+  const int NO = 3 * S * HL;  // outputs o: part q = o / (S·HL), t' and c within
+  float acc[(3 * CV_MAXS * CV_MAXC + CV_T - 1) / CV_T];
+  constexpr int NA = (3 * CV_MAXS * CV_MAXC + CV_T - 1) / CV_T;
+#pragma unroll
+  for (int j = 0; j < NA; ++j) acc[j] = 0.f;
+  for (int64_t g = blockIdx.x; g < B; g += gridDim.x) {
+    const float* gea = ea + g * E0 * D;
+    __syncthreads();
+    cv_stage(n * S, t, [&](int k) { return cv_var_row(gea, k / S, S, D)[k % S]; },
+             [&](int k, float v) { sVar[k / S][k % S] = v; });
+    cv_stage(E0 * HL, t,
+             [&](int k) { return cv_col(dae, k % HL, H)[(g * E0 + k / HL) * H]; },
+             [&](int k, float v) { sDae[k] = v; });
+    __syncthreads();
+    // per node: the d-logits of its outgoing (source) and incoming (target) edges
+    for (int k = t; k < n * HL; k += CV_T) {
+      const int u = k / HL, c = k - u * HL;
+      float ds = 0.f, dt = 0.f;
+      for (int w = 0; w < n; ++w) {
+        if (w == u) continue;
+        const int a = min(u, w), b = max(u, w);
+        const int p = a * n - a * (a + 1) / 2 + (b - a - 1);  // upper pair (a, b)
+        const int e_uw = u < w ? p : P + p;                  // u -> w
+        const int e_wu = u < w ? P + p : p;                  // w -> u
+        ds += sDae[e_uw * HL + c];
+        dt += sDae[e_wu * HL + c];
+      }
+      sDS[u][c] = ds;
+      sDT[u][c] = dt;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int o = t + CV_T * j;
+      if (o >= S * HL && o < NO) {
+        const int q = o / (S * HL), r = o - q * S * HL, tt = r / HL, c = r - tt * HL;
+        const float(*sN)[CV_MAXC] = q == 1 ? sDS : sDT;
+        float a = 0.f;
+        for (int u = 0; u < n; ++u) a = fmaf(sVar[u][tt], sN[u][c], a);
+        acc[j] += a;
+      }
+    }
+    // covariance part over chunks of upper rows staged in LDS (coalesced)
+    for (int p0 = 0; p0 < P; p0 += CV_PCH) {
+      const int np = min(CV_PCH, P - p0);
+      __syncthreads();
+      cv_stage(np * S, t,
+               [&](int k) { return gea[(int64_t)(p0 + k / S) * D + k % S]; },
+               [&](int k, float v) { sCov[(k / S) * (S + 1) + k % S] = v; });
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const int o = t + CV_T * j;
+        if (o < S * HL) {
+          const int tt = o / HL, c = o - tt * HL;
+          float a = 0.f;
+          for (int pp = 0; pp < np; ++pp)
+            a = fmaf(sCov[pp * (S + 1) + tt],
+                     sDae[(p0 + pp) * HL + c] + sDae[(P + p0 + pp) * HL + c], a);
+          acc[j] += a;
+        }
+      }
+    }
+  }
+  // this workgroup's slab: partial[blockIdx.x][d][hlp], padding columns zero
+  float* pb = partial + (int64_t)blockIdx.x * D * hlp;
+  for (int k = t; k < D * hlp; k += CV_T) {
+    const int c = k % hlp;
+    if (c >= HL) pb[k] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int o = t + CV_T * j;
+    if (o < NO) {
+      const int q = o / (S * HL), r = o - q * S * HL, tt = r / HL, c = r - tt * HL;
+      pb[(q * S + tt) * hlp + c] = acc[j];
+    }
+  }
+}
+
 }  // namespace sv2n
 
 // ============================ C-ABI ========================================
@@ -1144,5 +1384,67 @@ extern "C" int sv2n_block_rowmask_checked(const int64_t* edge_index, int64_t num
   hipLaunchKernelGGL(k_block_rowmask_checked, dim3((unsigned)((num_edges + 255) / 256)),
                      dim3(256), 0, stream, edge_index, num_edges, num_nodes, n, rowmask,
                      violations);
+  return (int)hipGetLastError();
+}
+
+// ---- covariance-layout edge features (k_edge_fwd_cv / k_edge_bwd_cv) ----
+static int cv_check(const float* ea, int64_t B, int n, int S, const uint16_t* canon, int L,
+                    int H, int hlp) {
+  if (!ea || !canon || B < 0 || L < 1 || L > SV2N_MAX_LAYERS || H < 1) return SV2N_ERR_ARG;
+  if (n < 2 || n > CV_MAXN || S < 1 || S > CV_MAXS || L * H > CV_MAXC || hlp < L * H)
+    return SV2N_ERR_SHAPE;
+  return 0;
+}
+
+extern "C" int sv2n_edge_logits_fwd_cv(const float* edge_attr, int64_t num_graphs, int n,
+                                       int seq_length, const uint16_t* canon, const float* wfold,
+                                       int hl_pad, float* const* ae_layers, int num_layers,
+                                       int heads, hipStream_t stream) {
+  if (int rc = cv_check(edge_attr, num_graphs, n, seq_length, canon, num_layers, heads, hl_pad))
+    return rc;
+  if (!wfold || !ae_layers) return SV2N_ERR_ARG;
+  if (num_graphs == 0) return 0;
+  LayerPtrs lp{};
+  for (int l = 0; l < num_layers; ++l) {
+    if (!ae_layers[l]) return SV2N_ERR_ARG;
+    lp.p[l] = ae_layers[l];
+  }
+  const int64_t P = (int64_t)n * (n - 1) / 2, nch = (P + CV_PCH - 1) / CV_PCH;
+  if (num_graphs * nch > 0x7fffffff) return SV2N_ERR_SHAPE;
+  hipLaunchKernelGGL(k_edge_fwd_cv, dim3((unsigned)(num_graphs * nch)), dim3(CV_T), 0, stream,
+                     edge_attr, n, seq_length, canon, wfold, hl_pad, lp, num_layers, heads);
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t sv2n_edge_logits_bwd_cv_workspace(int seq_length, int hl_pad) {
+  return (int64_t)CV_BWD_GRID * 3 * seq_length * hl_pad;
+}
+
+extern "C" int sv2n_edge_logits_bwd_cv(const float* edge_attr, int64_t num_graphs, int n,
+                                       int seq_length, const uint16_t* canon,
+                                       const float* const* dae_layers, int num_layers, int heads,
+                                       float* workspace, int64_t workspace_floats, float* dwfold,
+                                       int hl_pad, hipStream_t stream) {
+  if (int rc = cv_check(edge_attr, num_graphs, n, seq_length, canon, num_layers, heads, hl_pad))
+    return rc;
+  if (!dae_layers || !workspace || !dwfold) return SV2N_ERR_ARG;
+  if (workspace_floats < sv2n_edge_logits_bwd_cv_workspace(seq_length, hl_pad))
+    return SV2N_ERR_WORKSPACE;
+  LayerCPtrs lp{};
+  for (int l = 0; l < num_layers; ++l) {
+    if (!dae_layers[l]) return SV2N_ERR_ARG;
+    lp.p[l] = dae_layers[l];
+  }
+  const int D = 3 * seq_length, width = D * hl_pad;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(num_graphs, CV_BWD_GRID));
+  const size_t lds = sizeof(float) * ((size_t)n * (n - 1) * num_layers * heads +
+                                      (size_t)CV_PCH * (seq_length + 1));
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)k_edge_bwd_cv,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+  hipLaunchKernelGGL(k_edge_bwd_cv, dim3(grid), dim3(CV_T), lds, stream, edge_attr, num_graphs,
+                     n, seq_length, canon, lp, num_layers, heads, hl_pad, workspace);
+  hipLaunchKernelGGL(k_reduce_partials, dim3((unsigned)((width + 15) / 16)), dim3(256), 0, stream,
+                     workspace, grid, width, dwfold);
   return (int)hipGetLastError();
 }

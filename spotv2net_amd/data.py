@@ -22,7 +22,7 @@ from typing import Optional, Sequence
 
 import torch
 
-from .layout import canonical_edge_index, canonical_pairs, is_canonical_graph
+from .layout import canonical_edge_index, canonical_pairs, is_canonical_graph, mark_cov_var
 
 _FIELDS = ("x", "edge_index", "edge_attr", "y_x")
 
@@ -203,6 +203,7 @@ def window_batch(vol: torch.Tensor, volvol: torch.Tensor, starts: torch.Tensor,
     b = Batch(x=x.contiguous(), edge_index=ei, edge_attr=ea.contiguous(), y_x=y,
               batch=torch.arange(B, device=dev).repeat_interleave(n), ptr=ptr)
     b.nodes_per_graph = n
+    mark_cov_var(b.edge_attr, S)  # written above in the reference's covariance layout
     return b
 
 
@@ -295,6 +296,7 @@ class WindowDataset:
                                          idx if idx.dtype == torch.long else idx.long(), S, Fs,
                                          canonical_table(n, self.vol.device), out.x,
                                          out.edge_attr, out.y_x, self.cut, self.diag, xb)
+            mark_cov_var(out.edge_attr, S)
             return
         st = self.starts.index_select(0, idx)
         tidx = st.view(B, 1) + self._arS.view(1, S)                               # [B, S]
@@ -311,6 +313,7 @@ class WindowDataset:
         fidx = st.view(B, 1) + S + self._arF.view(1, Fs)                          # [B, F]
         yk = torch.diagonal(self.vol[fidx], dim1=2, dim2=3)                       # [B, F, n]
         out.y_x.view(B, n, Fs).copy_(yk.permute(0, 2, 1))
+        mark_cov_var(out.edge_attr, S)
 
     def __len__(self) -> int:
         return int(self.starts.numel())

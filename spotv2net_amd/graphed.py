@@ -41,7 +41,7 @@ from typing import Optional
 
 import torch
 
-from .layout import GraphLayout
+from .layout import GraphLayout, cov_var_seq_length
 from .ops import _aligned, resolve_precision
 from .stack import (_GradTargets, _direct_mode, _require_params, head_fits, layer_params,
                     stack_backward, stack_forward)
@@ -273,7 +273,7 @@ def forward(model, data, x, edge_index, edge_attr, layout: GraphLayout) -> Optio
     precision = resolve_precision(model.precision)
     key = (model.training, train_graph, precision, torch.is_autocast_enabled("cuda"),
            model._act_code, model.dropout, tuple(c.dropout for c in model.gat_layers),
-           _tsig(x), _tsig(edge_attr), _layout_sig(layout), needs,
+           _tsig(x), _tsig(edge_attr), cov_var_seq_length(edge_attr), _layout_sig(layout), needs,
            tuple(p.data_ptr() for p in ps))
     entry = cache.entries.get(key)
     if entry is None:

@@ -97,6 +97,27 @@ def canonical_pairs(n: int) -> tuple[list[int], list[int]]:
 _canon_cache: dict = {}
 
 
+def mark_cov_var(edge_attr: Optional[torch.Tensor], seq_length: int):
+    """Record that ``edge_attr`` holds edge features in the reference's
+    covariance layout (utils/dataset.py:228-243, :279-282: row s -> t is
+    [cov_t(s,t) | var_t(s) | var_t(t)], cov the same in both directions, var a
+    per-node series) for canonical complete graphs — stated by the builders
+    that write it (``window_batch``, ``WindowDataset``).  The edge passes then
+    read ≈ 1/6 of it (sv2n_edge_logits_fwd_cv / _bwd_cv).  The mark holds for
+    the tensor's current version: an in-place write drops it."""
+    if edge_attr is not None and edge_attr.dim() == 2 and edge_attr.size(1) == 3 * seq_length:
+        edge_attr._sv2n_cov_var = (int(seq_length), edge_attr._version)
+    return edge_attr
+
+
+def cov_var_seq_length(edge_attr: Optional[torch.Tensor]) -> Optional[int]:
+    """seq_length of a ``mark_cov_var`` tensor whose contents are unchanged since."""
+    m = getattr(edge_attr, "_sv2n_cov_var", None)
+    if m is None or m[1] != edge_attr._version:
+        return None
+    return m[0]
+
+
 def canonical_table(n: int, device: torch.device) -> torch.Tensor:
     key = ("table", n, str(device))
     if key not in _canon_cache:

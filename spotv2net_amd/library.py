@@ -85,6 +85,10 @@ _SCHEMAS = {
                  "Tensor(b!)? g_att_src, Tensor(c!)? g_att_dst, Tensor(d!)? g_bias) -> ()",
     "edge_logits_bwd": "(Tensor edge_attr, Tensor? edge_index, Tensor canon, Tensor[] dae, "
                        "int heads, int num_graphs, int n, int hl_pad, bool planes) -> Tensor",
+    "edge_logits_cv": "(Tensor edge_attr, Tensor wfold, Tensor canon, int num_layers, int heads, "
+                      "int num_graphs, int n) -> Tensor[]",
+    "edge_logits_bwd_cv": "(Tensor edge_attr, Tensor canon, Tensor[] dae, int heads, "
+                          "int num_graphs, int n, int hl_pad) -> Tensor",
     "gat_attn_bwd_edge": "(Tensor dy, Tensor y, Tensor xs, Tensor psave, Tensor? keep, "
                          "float keep_scale, Tensor edge_attr, Tensor?[] dae, int layer, "
                          "int hl_pad, int num_graphs, int n, int heads, int channels, "
@@ -311,6 +315,67 @@ def _edge_logits_bwd(edge_attr, edge_index, canon, dae, heads, num_graphs, n, hl
 @_fake("edge_logits_bwd")
 def _edge_logits_bwd_fake(edge_attr, edge_index, canon, dae, heads, num_graphs, n, hl_pad,
                           planes):
+    return edge_attr.new_empty((edge_attr.shape[1], hl_pad))
+
+
+def _cv_common(edge_attr, canon, num_graphs, n):
+    _dense(edge_attr, canon)
+    E, D = edge_attr.shape
+    _need(D % 3 == 0, "covariance-layout edge_attr has 3 x seq_length columns")
+    _need(E == num_graphs * n * (n - 1), "covariance layout: canonical complete graphs")
+    _need(canon.numel() == n * (n - 1), "canonical table shape")
+    return E, D
+
+
+@_impl("edge_logits_cv")
+def _edge_logits_cv(edge_attr, wfold, canon, num_layers, heads, num_graphs, n):
+    """sv2n_edge_logits_fwd_cv: edge_logits for edge features in the
+    reference's covariance layout (the caller vouches for it)."""
+    lib = _lib.load()
+    _f32(edge_attr, wfold)
+    E, D = _cv_common(edge_attr, canon, num_graphs, n)
+    _dense(wfold)
+    _need(wfold.shape[0] == D and num_layers * heads <= wfold.shape[1], "wfold shape")
+    outs = [torch.empty(E, heads, device=edge_attr.device) for _ in range(num_layers)]
+    if E == 0:
+        return outs
+    ptrs = _lib.ptr_array([o.data_ptr() for o in outs])
+    _lib.check(lib.sv2n_edge_logits_fwd_cv(edge_attr.data_ptr(), num_graphs, n, D // 3,
+                                           canon.data_ptr(), wfold.data_ptr(), wfold.shape[1],
+                                           ptrs, num_layers, heads, _st(edge_attr)),
+               "sv2n_edge_logits_fwd_cv")
+    return outs
+
+
+@_fake("edge_logits_cv")
+def _edge_logits_cv_fake(edge_attr, wfold, canon, num_layers, heads, num_graphs, n):
+    return [edge_attr.new_empty((edge_attr.shape[0], heads)) for _ in range(num_layers)]
+
+
+@_impl("edge_logits_bwd_cv")
+def _edge_logits_bwd_cv(edge_attr, canon, dae, heads, num_graphs, n, hl_pad):
+    lib = _lib.load()
+    _f32(edge_attr, *dae)
+    E, D = _cv_common(edge_attr, canon, num_graphs, n)
+    _dense(*dae)
+    for d in dae:
+        _need(d.numel() == heads * E, "dae shape")
+    dev = edge_attr.device
+    dwf = torch.empty(D, hl_pad, device=dev)
+    if E == 0:
+        return dwf.zero_()
+    ptrs = _lib.ptr_array([d.data_ptr() for d in dae])
+    ws_n = lib.sv2n_edge_logits_bwd_cv_workspace(D // 3, hl_pad)
+    ws = torch.empty(ws_n, device=dev)
+    _lib.check(lib.sv2n_edge_logits_bwd_cv(edge_attr.data_ptr(), num_graphs, n, D // 3,
+                                           canon.data_ptr(), ptrs, len(dae), heads, ws.data_ptr(),
+                                           ws_n, dwf.data_ptr(), hl_pad, _st(edge_attr)),
+               "sv2n_edge_logits_bwd_cv")
+    return dwf
+
+
+@_fake("edge_logits_bwd_cv")
+def _edge_logits_bwd_cv_fake(edge_attr, canon, dae, heads, num_graphs, n, hl_pad):
     return edge_attr.new_empty((edge_attr.shape[1], hl_pad))
 
 

@@ -37,7 +37,7 @@ from typing import Optional, Sequence
 import torch
 
 from . import _lib, library  # noqa: F401  (library registers torch.ops.sv2n)
-from .layout import GraphLayout
+from .layout import GraphLayout, cov_var_seq_length
 from .library import edge_order, fused_supported
 from .ops import ACT_CODES, _aligned, _require_device, relu_mask_fusable, resolve_precision
 
@@ -177,7 +177,8 @@ def _hp(L: int, H: int) -> int:
 # "off" (always edge pass + planes): an A/B switch for tests and measurements
 EDGE_FUSED = os.environ.get("SV2N_EDGE_FUSED", "auto")
 LAST_PATH = {"attention": None,   # which attention path the last forward took (tests)
-             "edge_tail": None}   # whether the last backward fused the edge gradient
+             "edge_tail": None,   # whether the last backward fused the edge gradient
+             "cov_var": None}     # whether the last forward took the covariance-layout passes
 
 
 def _overlap_edge(training: bool) -> bool:
@@ -229,6 +230,14 @@ def _opt(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 # (off, `profiles/r04_c2_edge_ab.txt`).
 EDGE_TAIL = os.environ.get("SV2N_EDGE_TAIL", "off")
 
+# "on": edge_attr marked as the reference's covariance layout (layout.mark_cov_var)
+# goes through the covariance-layout edge passes; "off": the generic passes
+# over every edge row (A/B switch for tests and measurements)
+COV_VAR_EDGES = os.environ.get("SV2N_COV_VAR_EDGES", "off")
+# the backward's covariance-layout pass (sv2n_edge_logits_bwd_cv); "off": the
+# generic edge-gradient pass over every row (faster today: see DESIGN.md §4)
+COV_VAR_BWD = os.environ.get("SV2N_COV_VAR_BWD", "off")
+
 
 def _edge_tail_ok(layout: GraphLayout, convs, ea, hp: int) -> bool:
     """Layer 0's n <= 32 attention backward can carry the edge gradient of
@@ -246,10 +255,12 @@ def _edge_tail_ok(layout: GraphLayout, convs, ea, hp: int) -> bool:
 
 class _StackMeta:
     """What the backward needs besides the saved tensors (stack_forward)."""
-    __slots__ = ("dims", "bf16", "feid", "kscales", "post_p", "head_dz")
+    __slots__ = ("dims", "bf16", "feid", "kscales", "post_p", "head_dz", "cv")
 
-    def __init__(self, dims, bf16, feid, kscales, post_p=None, head_dz=None):
+    def __init__(self, dims, bf16, feid, kscales, post_p=None, head_dz=None, cv=False):
         self.dims, self.bf16, self.feid, self.kscales = dims, bf16, feid, kscales
+        # the edge passes read edge_attr in its covariance layout (edge_logits_cv)
+        self.cv = cv
         # per layer: the post-layer dropout probability when its draws (not a
         # mask) are saved, i.e. the attention kernels apply it themselves
         self.post_p = post_p or [None] * len(kscales)
@@ -319,6 +330,20 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
     fused = bool(use_edge and _use_fused(layout, convs, ea.size(1), ea.size(0)))
     feid = layout.eid if (fused and layout.kind == "block") else None
     LAST_PATH["attention"] = "fused" if fused else ("tiled" if tiled else "small")
+    # edge features the builder wrote in the reference's covariance layout
+    # (layout.mark_cov_var): the edge passes read the covariance columns of the
+    # upper rows and one variance series per node (sv2n_edge_logits_fwd_cv)
+    s_cv = cov_var_seq_length(edge_attr) if use_edge else None
+    cv = bool(s_cv is not None and COV_VAR_EDGES == "on" and not fused and not tiled and
+              layout.kind == "canonical" and 2 <= n <= 32 and s_cv <= 64 and L * H <= 16 and
+              ea.size(1) == 3 * s_cv and ea.size(0) == B * n * (n - 1))
+    LAST_PATH["cov_var"] = cv
+
+    def edge_fwd():
+        if cv:
+            return list(ops.edge_logits_cv(ea, wf, layout.canon, L, H, B, n))
+        return list(ops.edge_logits(ea, wf, ei, layout.canon, L, H, B, n, tiled))
+
     overlap = None
     if use_edge and not fused:
         if _overlap_edge(need_saved) and dev.type == "cuda":
@@ -328,12 +353,12 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
             side = _side_stream(dev)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                aes = list(ops.edge_logits(ea, wf, ei, layout.canon, L, H, B, n, tiled))
+                aes = edge_fwd()
             for a in aes:
                 a.record_stream(main)
             overlap = (main, side)
         else:
-            aes = list(ops.edge_logits(ea, wf, ei, layout.canon, L, H, B, n, tiled))
+            aes = edge_fwd()
         if tiled and ea.size(0) == 0:
             aes = [None] * L
 
@@ -433,7 +458,7 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
     meta = _StackMeta((L, act, use_edge, hp, H, eo, fused), bf16, feid,
                       [(1.0 / (1.0 - c.dropout)) if (training and 0.0 < c.dropout < 1.0) else
                        (0.0 if training and c.dropout >= 1.0 else 1.0) for c in convs], post_p,
-                      saved_y[-1] if head is not None else None)
+                      saved_y[-1] if head is not None else None, cv)
     saved = [ea, wf if fused else None, *saved_x, *saved_xs, *saved_y, *saved_p, *saved_st,
              *saved_keep, *saved_drop, *waugs, *planes_t, xb0]
     return xin, saved, meta
@@ -472,7 +497,7 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
     # edge_attr is streamed there and no separate edge-gradient pass runs
     need_edge = use_edge and ea is not None and ea.size(0) > 0 and any(
         grad_of(c.lin_edge.weight) is not None or grad_of(c.att_edge) is not None for c in convs)
-    edge_tail = bool(need_edge and not fused and not layout.tiled and eo and
+    edge_tail = bool(need_edge and not fused and not layout.tiled and eo and not meta.cv and
                      _edge_tail_ok(layout, convs, ea, hp))
     LAST_PATH["edge_tail"] = edge_tail
     for l in range(L - 1, -1, -1):
@@ -543,7 +568,9 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
         need_e = [(grad_of(c.lin_edge.weight), grad_of(c.att_edge)) for c in convs]
         if ea.size(0) > 0 and any(a is not None or b is not None for a, b in need_e):
             ei = layout.edge_index if layout.kind == "block" else None
-            if not fused and not edge_tail:
+            if meta.cv and COV_VAR_BWD == "on":
+                dwf = ops.edge_logits_bwd_cv(ea, layout.canon, daes, H, B, n, hp)
+            elif not fused and not edge_tail:
                 dwf = ops.edge_logits_bwd(ea, ei, layout.canon, daes, H, B, n, hp,
                                           layout.tiled)
             if all(a is not None and b is not None for a, b in need_e):

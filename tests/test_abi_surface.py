@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     for name in names:
         assert hasattr(lib, name), f"libsv2n.so lacks {name}"
     assert set(names) == set(_lib.EXPORTED_SYMBOLS), "ctypes table and header disagree"
-    assert lib.sv2n_abi_version() == _lib.ABI_VERSION == 17
+    assert lib.sv2n_abi_version() == _lib.ABI_VERSION == 18
     assert b"invalid argument" in lib.sv2n_strerror(-1)
 
 
@@ -46,6 +46,9 @@ def test_argument_errors_without_gpu():
     assert lib.sv2n_gat_attn_fwd_head_mse_workspace(512, 4, 50, 0) == 512 * 52
     # the device dropout generator: NULL output / step
     assert lib.sv2n_dropout_uniform(None, 16, 1, None, 0, None) == -1
+    # covariance-layout edge passes: NULL / unsupported shapes
+    assert lib.sv2n_edge_logits_fwd_cv(None, 1, 30, 42, None, None, 16, None, 2, 4, None) == -1
+    assert lib.sv2n_edge_logits_bwd_cv_workspace(42, 16) == 256 * 126 * 16
 
 
 def _ref_layer_dims(F, D, H, hidden, concat_heads):

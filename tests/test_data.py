@@ -95,3 +95,16 @@ def test_collate_marks_canonical_batches():
     small = Data(x=torch.zeros(5, 60), edge_index=torch.zeros(2, 0, dtype=torch.long),
                  edge_attr=torch.zeros(0, 6), y_x=torch.zeros(5))
     assert not getattr(collate([gs[0], small]), "canonical_edges", False)
+
+
+def test_cov_var_mark_follows_the_tensor_version():
+    """layout.mark_cov_var holds for the tensor's current contents only."""
+    import torch
+    from spotv2net_amd.layout import cov_var_seq_length, mark_cov_var
+    ea = torch.zeros(6, 9)
+    assert cov_var_seq_length(ea) is None
+    mark_cov_var(ea, 3)
+    assert cov_var_seq_length(ea) == 3
+    ea[0, 0] = 1.0
+    assert cov_var_seq_length(ea) is None
+    assert cov_var_seq_length(mark_cov_var(torch.zeros(6, 8), 3)) is None  # not 3 x S columns

@@ -25,8 +25,9 @@ def _canonical(data, n=30):
 
 def _grads(model, data, tail, seed=0):
     from spotv2net_amd import stack
-    old = stack.EDGE_TAIL
+    old, old_cv = stack.EDGE_TAIL, stack.COV_VAR_EDGES
     stack.EDGE_TAIL = tail
+    stack.COV_VAR_EDGES = "off"  # the tail is an alternative to the generic edge-row passes
     try:
         model.zero_grad()
         torch.cuda.manual_seed(seed)
@@ -35,7 +36,7 @@ def _grads(model, data, tail, seed=0):
         torch.cuda.synchronize()
         used = stack.LAST_PATH["edge_tail"]
     finally:
-        stack.EDGE_TAIL = old
+        stack.EDGE_TAIL, stack.COV_VAR_EDGES = old, old_cv
     return {n: p.grad.detach().clone() for n, p in model.named_parameters()}, used
 
 
