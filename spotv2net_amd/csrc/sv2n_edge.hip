@@ -928,7 +928,14 @@ __global__ __launch_bounds__(CV_T) void k_edge_fwd_cv(const float* __restrict__ 
   }
 }
 
-// dynamic LDS: sDae [E0][HL] (this graph's d-logits), then sCov [CV_PCH][S + 1]
+// Backward: one workgroup per graph (grid-stride), 256 threads.  The node
+// variances and the graph's d-logits are staged together; the per-node sums
+// of outgoing / incoming d-logits give the two variance blocks; the
+// covariance block runs over chunks of upper rows (the next chunk's loads in
+// registers while this one is computed), NG = 256 / S thread groups taking
+// every NG-th pair, each thread one t' and all columns in registers.  Group
+// partials are added in group order at the end.
+// dynamic LDS: sDae [E0][HL], sCov [CV_PCH][S + 1], sRed [NG][S][CV_MAXC]
 __global__ __launch_bounds__(CV_T) void k_edge_bwd_cv(const float* __restrict__ ea, int64_t B,
                                                       int n, int S,
                                                       const uint16_t* __restrict__ canon,
@@ -936,87 +943,132 @@ __global__ __launch_bounds__(CV_T) void k_edge_bwd_cv(const float* __restrict__ 
                                                       float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float sVar[CV_MAXN][CV_MAXS + 1];
-  __shared__ float sDS[CV_MAXN][CV_MAXC], sDT[CV_MAXN][CV_MAXC];
+  __shared__ __attribute__((aligned(16))) float sDS[CV_MAXN][CV_MAXC];
+  __shared__ __attribute__((aligned(16))) float sDT[CV_MAXN][CV_MAXC];
   const int t = threadIdx.x, D = 3 * S, HL = L * H, E0 = n * (n - 1), P = E0 / 2;
-  float* sDae = smem;
-  float* sCov = smem + E0 * HL;
-  const int NO = 3 * S * HL;  // outputs o: part q = o / (S·HL), t' and c within
-  float acc[(3 * CV_MAXS * CV_MAXC + CV_T - 1) / CV_T];
-  constexpr int NA = (3 * CV_MAXS * CV_MAXC + CV_T - 1) / CV_T;
+  const int NG = CV_T / S;                  // thread groups of the covariance block
+  const int grp = t / S, tt = t - grp * S;  // this thread's group and t'
+  const bool cov_t = grp < NG;
+  float* sDae = smem;                                 // [E0][HL] (HL padded to 4)
+  const int HLP = (HL + 3) & ~3;
+  float* sCov = sDae + E0 * HLP;                      // [CV_PCH][S + 1]
+  float* sRed = sCov + CV_PCH * (S + 1);              // [NG][S][CV_MAXC]
+  float acc[CV_MAXC], accv[CV_MAXC];                  // covariance / variance rows
 #pragma unroll
-  for (int j = 0; j < NA; ++j) acc[j] = 0.f;
+  for (int c = 0; c < CV_MAXC; ++c) acc[c] = accv[c] = 0.f;
+  const int nch = (P + CV_PCH - 1) / CV_PCH;
   for (int64_t g = blockIdx.x; g < B; g += gridDim.x) {
     const float* gea = ea + g * E0 * D;
-    __syncthreads();
+    __syncthreads();  // the previous graph's LDS reads
     cv_stage(n * S, t, [&](int k) { return cv_var_row(gea, k / S, S, D)[k % S]; },
              [&](int k, float v) { sVar[k / S][k % S] = v; });
-    cv_stage(E0 * HL, t,
-             [&](int k) { return cv_col(dae, k % HL, H)[(g * E0 + k / HL) * H]; },
+    cv_stage(E0 * HLP, t,
+             [&](int k) {
+               const int c = k % HLP;
+               return c < HL ? cv_col(dae, c, H)[(g * E0 + k / HLP) * H] : 0.f;
+             },
              [&](int k, float v) { sDae[k] = v; });
+    // the first chunk's covariance columns in registers
+    constexpr int CR = (CV_PCH * (CV_MAXS + 1) + CV_T - 1) / CV_T;
+    float cr[CR];
+    auto load_chunk = [&](int p0) {
+      const int np = min(CV_PCH, P - p0);
+#pragma unroll
+      for (int u = 0; u < CR; ++u) {
+        const int k = t + u * CV_T;
+        cr[u] = k < np * S ? gea[(int64_t)(p0 + k / S) * D + k % S] : 0.f;
+      }
+    };
+    load_chunk(0);
     __syncthreads();
-    // per node: the d-logits of its outgoing (source) and incoming (target) edges
+    // per node: d-logits of its outgoing (source) and incoming (target) edges
     for (int k = t; k < n * HL; k += CV_T) {
       const int u = k / HL, c = k - u * HL;
       float ds = 0.f, dt = 0.f;
       for (int w = 0; w < n; ++w) {
         if (w == u) continue;
-        const int a = min(u, w), b = max(u, w);
-        const int p = a * n - a * (a + 1) / 2 + (b - a - 1);  // upper pair (a, b)
-        const int e_uw = u < w ? p : P + p;                  // u -> w
-        const int e_wu = u < w ? P + p : p;                  // w -> u
-        ds += sDae[e_uw * HL + c];
-        dt += sDae[e_wu * HL + c];
+        const int lo = min(u, w), hi = max(u, w);
+        const int p = lo * n - lo * (lo + 1) / 2 + (hi - lo - 1);  // upper pair (lo, hi)
+        ds += sDae[(u < w ? p : P + p) * HLP + c];
+        dt += sDae[(u < w ? P + p : p) * HLP + c];
       }
       sDS[u][c] = ds;
       sDT[u][c] = dt;
     }
-    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+      const int p0 = ch * CV_PCH, np = min(CV_PCH, P - p0);
 #pragma unroll
-    for (int j = 0; j < NA; ++j) {
-      const int o = t + CV_T * j;
-      if (o >= S * HL && o < NO) {
-        const int q = o / (S * HL), r = o - q * S * HL, tt = r / HL, c = r - tt * HL;
-        const float(*sN)[CV_MAXC] = q == 1 ? sDS : sDT;
-        float a = 0.f;
-        for (int u = 0; u < n; ++u) a = fmaf(sVar[u][tt], sN[u][c], a);
-        acc[j] += a;
+      for (int u = 0; u < CR; ++u) {
+        const int k = t + u * CV_T;
+        if (k < np * S) sCov[(k / S) * (S + 1) + k % S] = cr[u];
       }
-    }
-    // covariance part over chunks of upper rows staged in LDS (coalesced)
-    for (int p0 = 0; p0 < P; p0 += CV_PCH) {
-      const int np = min(CV_PCH, P - p0);
       __syncthreads();
-      cv_stage(np * S, t,
-               [&](int k) { return gea[(int64_t)(p0 + k / S) * D + k % S]; },
-               [&](int k, float v) { sCov[(k / S) * (S + 1) + k % S] = v; });
-      __syncthreads();
+      if (ch + 1 < nch) load_chunk(p0 + CV_PCH);  // in flight during this chunk
+      if (cov_t) {
+        for (int pp = grp; pp < np; pp += NG) {
+          const float x = sCov[pp * (S + 1) + tt];
+          const float* du = sDae + (p0 + pp) * HLP;
+          const float* dl = sDae + (P + p0 + pp) * HLP;
 #pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        const int o = t + CV_T * j;
-        if (o < S * HL) {
-          const int tt = o / HL, c = o - tt * HL;
-          float a = 0.f;
-          for (int pp = 0; pp < np; ++pp)
-            a = fmaf(sCov[pp * (S + 1) + tt],
-                     sDae[(p0 + pp) * HL + c] + sDae[(P + p0 + pp) * HL + c], a);
-          acc[j] += a;
+          for (int c = 0; c < CV_MAXC; c += 4) {
+            if (c < HL) {
+              const float4 a = *reinterpret_cast<const float4*>(du + c);
+              const float4 b = *reinterpret_cast<const float4*>(dl + c);
+              acc[c] = fmaf(x, a.x + b.x, acc[c]);
+              acc[c + 1] = fmaf(x, a.y + b.y, acc[c + 1]);
+              acc[c + 2] = fmaf(x, a.z + b.z, acc[c + 2]);
+              acc[c + 3] = fmaf(x, a.w + b.w, acc[c + 3]);
+            }
+          }
+        }
+      }
+      __syncthreads();  // sCov is rewritten by the next chunk
+    }
+    // variance blocks: thread t < 2S: q = 1 (source) / 2 (target), row t'
+    if (t < 2 * S) {
+      const int q = t / S, tv = t - q * S;
+      const float(*sN)[CV_MAXC] = q == 0 ? sDS : sDT;
+      for (int u = 0; u < n; ++u) {
+        const float x = sVar[u][tv];
+#pragma unroll
+        for (int c = 0; c < CV_MAXC; c += 4) {
+          if (c < HL) {
+            const float4 d4 = *reinterpret_cast<const float4*>(&sN[u][c]);
+            accv[c] = fmaf(x, d4.x, accv[c]);
+            accv[c + 1] = fmaf(x, d4.y, accv[c + 1]);
+            accv[c + 2] = fmaf(x, d4.z, accv[c + 2]);
+            accv[c + 3] = fmaf(x, d4.w, accv[c + 3]);
+          }
         }
       }
     }
   }
-  // this workgroup's slab: partial[blockIdx.x][d][hlp], padding columns zero
-  float* pb = partial + (int64_t)blockIdx.x * D * hlp;
-  for (int k = t; k < D * hlp; k += CV_T) {
-    const int c = k % hlp;
-    if (c >= HL) pb[k] = 0.f;
-  }
+  // this workgroup's slab partial[blockIdx.x][d][hlp]: covariance rows summed
+  // over the groups in group order, then the variance rows
+  __syncthreads();
+  if (cov_t) {
 #pragma unroll
-  for (int j = 0; j < NA; ++j) {
-    const int o = t + CV_T * j;
-    if (o < NO) {
-      const int q = o / (S * HL), r = o - q * S * HL, tt = r / HL, c = r - tt * HL;
-      pb[(q * S + tt) * hlp + c] = acc[j];
+    for (int c = 0; c < CV_MAXC; ++c) sRed[(grp * S + tt) * CV_MAXC + c] = acc[c];
+  }
+  __syncthreads();
+  float* pb = partial + (int64_t)blockIdx.x * D * hlp;
+  for (int k = t; k < S * hlp; k += CV_T) {
+    const int r = k / hlp, c = k - r * hlp;
+    float v = 0.f;
+    if (c < HL) {
+      for (int q = 0; q < NG; ++q) v += sRed[(q * S + r) * CV_MAXC + c];
     }
+    pb[k] = v;
+  }
+  if (t < 2 * S) {
+    const int q = t / S, tv = t - q * S;
+    float* row = pb + (int64_t)((1 + q) * S + tv) * hlp;
+#pragma unroll
+    for (int c = 0; c < CV_MAXC; ++c)
+      if (c < hlp) row[c] = c < HL ? accv[c] : 0.f;
+  }
+  for (int k = CV_MAXC; k < hlp; ++k) {  // columns past CV_MAXC (hlp > 16)
+    if (t < 2 * S) pb[(int64_t)((1 + t / S) * S + t % S) * hlp + k] = 0.f;
   }
 }
 
@@ -1437,8 +1489,10 @@ extern "C" int sv2n_edge_logits_bwd_cv(const float* edge_attr, int64_t num_graph
   }
   const int D = 3 * seq_length, width = D * hl_pad;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(num_graphs, CV_BWD_GRID));
-  const size_t lds = sizeof(float) * ((size_t)n * (n - 1) * num_layers * heads +
-                                      (size_t)CV_PCH * (seq_length + 1));
+  const int hlp4 = (num_layers * heads + 3) & ~3;
+  const size_t lds = sizeof(float) * ((size_t)n * (n - 1) * hlp4 +
+                                      (size_t)CV_PCH * (seq_length + 1) +
+                                      (size_t)(CV_T / seq_length) * seq_length * CV_MAXC);
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)k_edge_bwd_cv,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
