@@ -802,7 +802,7 @@ __global__ void k_block_eid(const int64_t* __restrict__ ei, int64_t E, int64_t N
 // (spotv2net_amd.layout.mark_cov_var: the builders that write it).
 // ---------------------------------------------------------------------------
 constexpr int CV_T = 256, CV_MAXN = 32, CV_MAXS = 64, CV_MAXC = 16, CV_PCH = 64;
-constexpr int CV_BWD_GRID = 256;
+constexpr int CV_BWD_GRID = 1024;
 
 // node u's variance series: the source columns of pair (0, 1) for u = 0, the
 // target columns of pair (0, u) (upper row u - 1) otherwise
@@ -928,147 +928,103 @@ __global__ __launch_bounds__(CV_T) void k_edge_fwd_cv(const float* __restrict__ 
   }
 }
 
-// Backward: one workgroup per graph (grid-stride), 256 threads.  The node
-// variances and the graph's d-logits are staged together; the per-node sums
-// of outgoing / incoming d-logits give the two variance blocks; the
-// covariance block runs over chunks of upper rows (the next chunk's loads in
-// registers while this one is computed), NG = 256 / S thread groups taking
-// every NG-th pair, each thread one t' and all columns in registers.  Group
-// partials are added in group order at the end.
-// dynamic LDS: sDae [E0][HL], sCov [CV_PCH][S + 1], sRed [NG][S][CV_MAXC]
+// Backward: units of (graph, chunk of CV_PCH upper pairs), grid-stride.  A
+// unit stages its pairs' covariance columns, the graph's variance series and
+// the pairs' two d-logit rows; NG = 256 / S thread groups take every NG-th
+// pair, each thread one t' and every column in registers:
+//   cov row t':  x·(d_up + d_low)
+//   src row t':  var_u·d_up + var_v·d_low      (u -> v is the upper edge)
+//   tgt row t':  var_v·d_up + var_u·d_low
+// accumulated over the workgroup's units; at the end the groups are added in
+// group order and the workgroup leaves one [D][hlp] slab (k_reduce_partials).
 __global__ __launch_bounds__(CV_T) void k_edge_bwd_cv(const float* __restrict__ ea, int64_t B,
                                                       int n, int S,
                                                       const uint16_t* __restrict__ canon,
                                                       LayerCPtrs dae, int L, int H, int hlp,
                                                       float* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float sCov[CV_PCH * (CV_MAXS + 1)];
   __shared__ float sVar[CV_MAXN][CV_MAXS + 1];
-  __shared__ __attribute__((aligned(16))) float sDS[CV_MAXN][CV_MAXC];
-  __shared__ __attribute__((aligned(16))) float sDT[CV_MAXN][CV_MAXC];
+  __shared__ __attribute__((aligned(16))) float sDu[CV_PCH][CV_MAXC];
+  __shared__ __attribute__((aligned(16))) float sDl[CV_PCH][CV_MAXC];
+  __shared__ int sPr[CV_PCH];
   const int t = threadIdx.x, D = 3 * S, HL = L * H, E0 = n * (n - 1), P = E0 / 2;
-  const int NG = CV_T / S;                  // thread groups of the covariance block
-  const int grp = t / S, tt = t - grp * S;  // this thread's group and t'
-  const bool cov_t = grp < NG;
-  float* sDae = smem;                                 // [E0][HL] (HL padded to 4)
-  const int HLP = (HL + 3) & ~3;
-  float* sCov = sDae + E0 * HLP;                      // [CV_PCH][S + 1]
-  float* sRed = sCov + CV_PCH * (S + 1);              // [NG][S][CV_MAXC]
-  float acc[CV_MAXC], accv[CV_MAXC];                  // covariance / variance rows
-#pragma unroll
-  for (int c = 0; c < CV_MAXC; ++c) acc[c] = accv[c] = 0.f;
+  const int NG = CV_T / S;
+  const int grp = t / S, tt = t - grp * S;
+  const bool act = grp < NG;
   const int nch = (P + CV_PCH - 1) / CV_PCH;
-  for (int64_t g = blockIdx.x; g < B; g += gridDim.x) {
+  const int64_t U = B * nch;
+  float ac[CV_MAXC], as_[CV_MAXC], at_[CV_MAXC];
+#pragma unroll
+  for (int c = 0; c < CV_MAXC; ++c) ac[c] = as_[c] = at_[c] = 0.f;
+  for (int64_t un = blockIdx.x; un < U; un += gridDim.x) {
+    const int64_t g = un / nch;
+    const int p0 = (int)(un - g * nch) * CV_PCH, np = min(CV_PCH, P - p0);
     const float* gea = ea + g * E0 * D;
-    __syncthreads();  // the previous graph's LDS reads
+    __syncthreads();  // the previous unit's LDS reads
+    cv_stage(np * S, t, [&](int k) { return gea[(int64_t)(p0 + k / S) * D + k % S]; },
+             [&](int k, float v) { sCov[(k / S) * (S + 1) + k % S] = v; });
     cv_stage(n * S, t, [&](int k) { return cv_var_row(gea, k / S, S, D)[k % S]; },
              [&](int k, float v) { sVar[k / S][k % S] = v; });
-    cv_stage(E0 * HLP, t,
+    cv_stage(2 * CV_PCH * CV_MAXC, t,
              [&](int k) {
-               const int c = k % HLP;
-               return c < HL ? cv_col(dae, c, H)[(g * E0 + k / HLP) * H] : 0.f;
+               const int lo = k >= CV_PCH * CV_MAXC, r = k - lo * CV_PCH * CV_MAXC;
+               const int pl = r / CV_MAXC, c = r - pl * CV_MAXC;
+               return (pl < np && c < HL)
+                          ? cv_col(dae, c, H)[(g * E0 + (lo ? P : 0) + p0 + pl) * H]
+                          : 0.f;
              },
-             [&](int k, float v) { sDae[k] = v; });
-    // the first chunk's covariance columns in registers
-    constexpr int CR = (CV_PCH * (CV_MAXS + 1) + CV_T - 1) / CV_T;
-    float cr[CR];
-    auto load_chunk = [&](int p0) {
-      const int np = min(CV_PCH, P - p0);
-#pragma unroll
-      for (int u = 0; u < CR; ++u) {
-        const int k = t + u * CV_T;
-        cr[u] = k < np * S ? gea[(int64_t)(p0 + k / S) * D + k % S] : 0.f;
-      }
-    };
-    load_chunk(0);
+             [&](int k, float v) {
+               const int lo = k >= CV_PCH * CV_MAXC, r = k - lo * CV_PCH * CV_MAXC;
+               (lo ? &sDl[0][0] : &sDu[0][0])[r] = v;
+             });
+    if (t < np) sPr[t] = canon[p0 + t];
     __syncthreads();
-    // per node: d-logits of its outgoing (source) and incoming (target) edges
-    for (int k = t; k < n * HL; k += CV_T) {
-      const int u = k / HL, c = k - u * HL;
-      float ds = 0.f, dt = 0.f;
-      for (int w = 0; w < n; ++w) {
-        if (w == u) continue;
-        const int lo = min(u, w), hi = max(u, w);
-        const int p = lo * n - lo * (lo + 1) / 2 + (hi - lo - 1);  // upper pair (lo, hi)
-        ds += sDae[(u < w ? p : P + p) * HLP + c];
-        dt += sDae[(u < w ? P + p : p) * HLP + c];
-      }
-      sDS[u][c] = ds;
-      sDT[u][c] = dt;
-    }
-    for (int ch = 0; ch < nch; ++ch) {
-      const int p0 = ch * CV_PCH, np = min(CV_PCH, P - p0);
-#pragma unroll
-      for (int u = 0; u < CR; ++u) {
-        const int k = t + u * CV_T;
-        if (k < np * S) sCov[(k / S) * (S + 1) + k % S] = cr[u];
-      }
-      __syncthreads();
-      if (ch + 1 < nch) load_chunk(p0 + CV_PCH);  // in flight during this chunk
-      if (cov_t) {
-        for (int pp = grp; pp < np; pp += NG) {
-          const float x = sCov[pp * (S + 1) + tt];
-          const float* du = sDae + (p0 + pp) * HLP;
-          const float* dl = sDae + (P + p0 + pp) * HLP;
-#pragma unroll
-          for (int c = 0; c < CV_MAXC; c += 4) {
-            if (c < HL) {
-              const float4 a = *reinterpret_cast<const float4*>(du + c);
-              const float4 b = *reinterpret_cast<const float4*>(dl + c);
-              acc[c] = fmaf(x, a.x + b.x, acc[c]);
-              acc[c + 1] = fmaf(x, a.y + b.y, acc[c + 1]);
-              acc[c + 2] = fmaf(x, a.z + b.z, acc[c + 2]);
-              acc[c + 3] = fmaf(x, a.w + b.w, acc[c + 3]);
-            }
-          }
-        }
-      }
-      __syncthreads();  // sCov is rewritten by the next chunk
-    }
-    // variance blocks: thread t < 2S: q = 1 (source) / 2 (target), row t'
-    if (t < 2 * S) {
-      const int q = t / S, tv = t - q * S;
-      const float(*sN)[CV_MAXC] = q == 0 ? sDS : sDT;
-      for (int u = 0; u < n; ++u) {
-        const float x = sVar[u][tv];
+    if (act) {
+      for (int pp = grp; pp < np; pp += NG) {
+        const float x = sCov[pp * (S + 1) + tt];
+        const int pr = sPr[pp];
+        const float vu = sVar[pr & 0xff][tt], vv = sVar[pr >> 8][tt];
 #pragma unroll
         for (int c = 0; c < CV_MAXC; c += 4) {
           if (c < HL) {
-            const float4 d4 = *reinterpret_cast<const float4*>(&sN[u][c]);
-            accv[c] = fmaf(x, d4.x, accv[c]);
-            accv[c + 1] = fmaf(x, d4.y, accv[c + 1]);
-            accv[c + 2] = fmaf(x, d4.z, accv[c + 2]);
-            accv[c + 3] = fmaf(x, d4.w, accv[c + 3]);
+            const float4 du = *reinterpret_cast<const float4*>(&sDu[pp][c]);
+            const float4 dl = *reinterpret_cast<const float4*>(&sDl[pp][c]);
+            ac[c] = fmaf(x, du.x + dl.x, ac[c]);
+            ac[c + 1] = fmaf(x, du.y + dl.y, ac[c + 1]);
+            ac[c + 2] = fmaf(x, du.z + dl.z, ac[c + 2]);
+            ac[c + 3] = fmaf(x, du.w + dl.w, ac[c + 3]);
+            as_[c] = fmaf(vu, du.x, fmaf(vv, dl.x, as_[c]));
+            as_[c + 1] = fmaf(vu, du.y, fmaf(vv, dl.y, as_[c + 1]));
+            as_[c + 2] = fmaf(vu, du.z, fmaf(vv, dl.z, as_[c + 2]));
+            as_[c + 3] = fmaf(vu, du.w, fmaf(vv, dl.w, as_[c + 3]));
+            at_[c] = fmaf(vv, du.x, fmaf(vu, dl.x, at_[c]));
+            at_[c + 1] = fmaf(vv, du.y, fmaf(vu, dl.y, at_[c + 1]));
+            at_[c + 2] = fmaf(vv, du.z, fmaf(vu, dl.z, at_[c + 2]));
+            at_[c + 3] = fmaf(vv, du.w, fmaf(vu, dl.w, at_[c + 3]));
           }
         }
       }
     }
   }
-  // this workgroup's slab partial[blockIdx.x][d][hlp]: covariance rows summed
-  // over the groups in group order, then the variance rows
-  __syncthreads();
-  if (cov_t) {
-#pragma unroll
-    for (int c = 0; c < CV_MAXC; ++c) sRed[(grp * S + tt) * CV_MAXC + c] = acc[c];
-  }
-  __syncthreads();
+  // the slab: for each block q (cov, src, tgt) the groups' rows in group order
   float* pb = partial + (int64_t)blockIdx.x * D * hlp;
-  for (int k = t; k < S * hlp; k += CV_T) {
-    const int r = k / hlp, c = k - r * hlp;
-    float v = 0.f;
-    if (c < HL) {
-      for (int q = 0; q < NG; ++q) v += sRed[(q * S + r) * CV_MAXC + c];
-    }
-    pb[k] = v;
-  }
-  if (t < 2 * S) {
-    const int q = t / S, tv = t - q * S;
-    float* row = pb + (int64_t)((1 + q) * S + tv) * hlp;
+  float* sRed = sCov;  // NG·S·CV_MAXC <= 256·CV_MAXC floats... per block q
 #pragma unroll
-    for (int c = 0; c < CV_MAXC; ++c)
-      if (c < hlp) row[c] = c < HL ? accv[c] : 0.f;
-  }
-  for (int k = CV_MAXC; k < hlp; ++k) {  // columns past CV_MAXC (hlp > 16)
-    if (t < 2 * S) pb[(int64_t)((1 + t / S) * S + t % S) * hlp + k] = 0.f;
+  for (int q = 0; q < 3; ++q) {
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < CV_MAXC; ++c)
+        sRed[(grp * S + tt) * CV_MAXC + c] = q == 0 ? ac[c] : (q == 1 ? as_[c] : at_[c]);
+    }
+    __syncthreads();
+    for (int k = t; k < S * hlp; k += CV_T) {
+      const int r = k / hlp, c = k - r * hlp;
+      float v = 0.f;
+      if (c < HL && c < CV_MAXC)
+        for (int gq = 0; gq < NG; ++gq) v += sRed[(gq * S + r) * CV_MAXC + c];
+      pb[(int64_t)(q * S + r) * hlp + c] = v;
+    }
   }
 }
 
@@ -1488,15 +1444,9 @@ extern "C" int sv2n_edge_logits_bwd_cv(const float* edge_attr, int64_t num_graph
     lp.p[l] = dae_layers[l];
   }
   const int D = 3 * seq_length, width = D * hl_pad;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(num_graphs, CV_BWD_GRID));
-  const int hlp4 = (num_layers * heads + 3) & ~3;
-  const size_t lds = sizeof(float) * ((size_t)n * (n - 1) * hlp4 +
-                                      (size_t)CV_PCH * (seq_length + 1) +
-                                      (size_t)(CV_T / seq_length) * seq_length * CV_MAXC);
-  if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)k_edge_bwd_cv,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-  hipLaunchKernelGGL(k_edge_bwd_cv, dim3(grid), dim3(CV_T), lds, stream, edge_attr, num_graphs,
+  const int64_t units = num_graphs * (((int64_t)n * (n - 1) / 2 + CV_PCH - 1) / CV_PCH);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, CV_BWD_GRID));
+  hipLaunchKernelGGL(k_edge_bwd_cv, dim3(grid), dim3(CV_T), 0, stream, edge_attr, num_graphs,
                      n, seq_length, canon, lp, num_layers, heads, hl_pad, workspace);
   hipLaunchKernelGGL(k_reduce_partials, dim3((unsigned)((width + 15) / 16)), dim3(256), 0, stream,
                      workspace, grid, width, dwfold);

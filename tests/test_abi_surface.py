@@ -48,7 +48,7 @@ def test_argument_errors_without_gpu():
     assert lib.sv2n_dropout_uniform(None, 16, 1, None, 0, None) == -1
     # covariance-layout edge passes: NULL / unsupported shapes
     assert lib.sv2n_edge_logits_fwd_cv(None, 1, 30, 42, None, None, 16, None, 2, 4, None) == -1
-    assert lib.sv2n_edge_logits_bwd_cv_workspace(42, 16) == 256 * 126 * 16
+    assert lib.sv2n_edge_logits_bwd_cv_workspace(42, 16) == 1024 * 126 * 16
 
 
 def _ref_layer_dims(F, D, H, hidden, concat_heads):
