@@ -844,86 +844,127 @@ __device__ __forceinline__ void cv_stage(int total, int t, LOAD load, STORE stor
   }
 }
 
-// Forward: one workgroup per (graph, chunk of CV_PCH upper pairs), four
-// threads per pair.  A thread's covariance loads (t' = cq, cq + 4, ...) are
-// issued first and land while W̃ and the node variances are staged; the four
-// partial dot products of a pair are summed across its lanes (xor 1, 2).
+// rows x cols (cols <= 64) row by row: wave w takes rows w, w + 4, ..., lane =
+// column (coalesced rows, no index division), 8 rows in flight per wave
+template <typename LOAD, typename STORE>
+__device__ __forceinline__ void cv_stage_rows(int rows, int cols, LOAD load, STORE store) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool lv = lane < cols;
+  for (int r0 = w; r0 < rows; r0 += 4 * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = r0 + 4 * u;
+      v[u] = (lv && r < rows) ? load(r, lane) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = r0 + 4 * u;
+      if (lv && r < rows) store(r, lane, v[u]);
+    }
+  }
+}
+
+// Forward: one workgroup per (graph, CV_FSUB·CV_PCH upper pairs), four
+// threads per pair and CV_FSUB pairs per thread group.  A thread's covariance
+// loads (t' = cq, cq + 4, ...) are issued first and land while W̃ and the node
+// variances are staged and the node terms formed; the four partial dot
+// products of a pair are summed across its lanes (xor 1, 2).  NC: logit
+// columns rounded up to 4.
+constexpr int CV_FSUB = 4;
+template <int NC>
 __global__ __launch_bounds__(CV_T) void k_edge_fwd_cv(const float* __restrict__ ea, int n, int S,
                                                       const uint16_t* __restrict__ canon,
                                                       const float* __restrict__ wf, int hlp,
                                                       LayerPtrs ae, int L, int H) {
-  __shared__ __attribute__((aligned(16))) float sW[3 * CV_MAXS][CV_MAXC];
+  __shared__ __attribute__((aligned(16))) float sW[3 * CV_MAXS][NC];
   __shared__ float sVar[CV_MAXN][CV_MAXS + 1];
-  __shared__ float sVs[CV_MAXN][CV_MAXC], sVt[CV_MAXN][CV_MAXC];
+  __shared__ float sVs[CV_MAXN][NC], sVt[CV_MAXN][NC];
   const int t = threadIdx.x, D = 3 * S, HL = L * H, E0 = n * (n - 1), P = E0 / 2;
-  const int nch = (P + CV_PCH - 1) / CV_PCH;
+  constexpr int CH = CV_FSUB * CV_PCH;
+  const int nch = (P + CH - 1) / CH;
   const int64_t g = blockIdx.x / nch;
-  const int p0 = (int)(blockIdx.x - g * nch) * CV_PCH;
-  const int pl = t >> 2, cq = t & 3, p = p0 + pl;
-  const bool pv = p < P;
+  const int p0 = (int)(blockIdx.x - g * nch) * CH;
+  const int pl = t >> 2, cq = t & 3;
   const float* gea = ea + g * E0 * D;
-  float x[CV_MAXS / 4];
+  float x[CV_FSUB][CV_MAXS / 4];
 #pragma unroll
-  for (int k = 0; k < CV_MAXS / 4; ++k) {
-    const int tt = cq + 4 * k;
-    x[k] = (pv && tt < S) ? gea[(int64_t)p * D + tt] : 0.f;
+  for (int sb = 0; sb < CV_FSUB; ++sb) {
+    const int p = p0 + sb * CV_PCH + pl;
+#pragma unroll
+    for (int k = 0; k < CV_MAXS / 4; ++k) {
+      const int tt = cq + 4 * k;
+      x[sb][k] = (p < P && tt < S) ? gea[(int64_t)p * D + tt] : 0.f;
+    }
   }
-  cv_stage(D * CV_MAXC, t,
+  cv_stage(D * NC, t,
            [&](int k) {
-             const int d = k / CV_MAXC, c = k - d * CV_MAXC;
+             const int d = k / NC, c = k - d * NC;
              return c < HL ? wf[d * hlp + c] : 0.f;
            },
-           [&](int k, float v) { sW[k / CV_MAXC][k % CV_MAXC] = v; });
-  cv_stage(n * S, t, [&](int k) { return cv_var_row(gea, k / S, S, D)[k % S]; },
-           [&](int k, float v) { sVar[k / S][k % S] = v; });
+           [&](int k, float v) { (&sW[0][0])[k] = v; });
+  cv_stage_rows(n, S, [&](int r, int c) { return cv_var_row(gea, r, S, D)[c]; },
+                [&](int r, int c, float v) { sVar[r][c] = v; });
   __syncthreads();
-  for (int k = t; k < n * HL; k += CV_T) {
-    const int u = k / HL, c = k - u * HL;
+  // node terms: four lanes per (node, column), each a quarter of the lags
+  for (int k = t; k < 4 * n * NC; k += CV_T) {
+    const int q = k & 3, uc = k >> 2, u = uc / NC, c = uc - u * NC;
     float vs = 0.f, vt = 0.f;
-    for (int tt = 0; tt < S; ++tt) {
+    for (int tt = q; tt < S; tt += 4) {
       vs = fmaf(sVar[u][tt], sW[S + tt][c], vs);
       vt = fmaf(sVar[u][tt], sW[2 * S + tt][c], vt);
     }
-    sVs[u][c] = vs;
-    sVt[u][c] = vt;
-  }
-  float acc[CV_MAXC];
-#pragma unroll
-  for (int c = 0; c < CV_MAXC; ++c) acc[c] = 0.f;
-#pragma unroll
-  for (int k = 0; k < CV_MAXS / 4; ++k) {
-    const int tt = cq + 4 * k;
-    if (tt < S) {
-#pragma unroll
-      for (int c = 0; c < CV_MAXC; c += 4) {
-        const float4 w = *reinterpret_cast<const float4*>(&sW[tt][c]);
-        acc[c] = fmaf(x[k], w.x, acc[c]);
-        acc[c + 1] = fmaf(x[k], w.y, acc[c + 1]);
-        acc[c + 2] = fmaf(x[k], w.z, acc[c + 2]);
-        acc[c + 3] = fmaf(x[k], w.w, acc[c + 3]);
-      }
+    vs += __shfl_xor(vs, 1, 64);
+    vt += __shfl_xor(vt, 1, 64);
+    vs += __shfl_xor(vs, 2, 64);
+    vt += __shfl_xor(vt, 2, 64);
+    if (q == 0) {
+      sVs[u][c] = vs;
+      sVt[u][c] = vt;
     }
   }
-#pragma unroll
-  for (int c = 0; c < CV_MAXC; ++c) {
-    acc[c] += __shfl_xor(acc[c], 1, 64);
-    acc[c] += __shfl_xor(acc[c], 2, 64);
-  }
   __syncthreads();  // sVs / sVt
-  if (!pv) return;
-  const int pr = canon[p];  // (target << 8) | source of upper edge p
-  const int u = pr & 0xff, v = pr >> 8;
-  const int64_t eu = g * E0 + p, el = g * E0 + P + p;
 #pragma unroll
-  for (int i = 0; i < CV_MAXC / 4; ++i) {
-    const int c = cq + 4 * i;
-    float a = acc[0];
+  for (int sb = 0; sb < CV_FSUB; ++sb) {
+    const int p = p0 + sb * CV_PCH + pl;
+    float acc[NC];
 #pragma unroll
-    for (int j = 1; j < CV_MAXC; ++j) a = (j == c) ? acc[j] : a;
-    if (c < HL) {
-      float* col = cv_col(ae, c, H);
-      col[eu * H] = a + sVs[u][c] + sVt[v][c];
-      col[el * H] = a + sVs[v][c] + sVt[u][c];
+    for (int c = 0; c < NC; ++c) acc[c] = 0.f;
+#pragma unroll
+    for (int k = 0; k < CV_MAXS / 4; ++k) {
+      const int tt = cq + 4 * k;
+      if (tt < S) {
+#pragma unroll
+        for (int c = 0; c < NC; c += 4) {
+          const float4 w = *reinterpret_cast<const float4*>(&sW[tt][c]);
+          acc[c] = fmaf(x[sb][k], w.x, acc[c]);
+          acc[c + 1] = fmaf(x[sb][k], w.y, acc[c + 1]);
+          acc[c + 2] = fmaf(x[sb][k], w.z, acc[c + 2]);
+          acc[c + 3] = fmaf(x[sb][k], w.w, acc[c + 3]);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      acc[c] += __shfl_xor(acc[c], 1, 64);
+      acc[c] += __shfl_xor(acc[c], 2, 64);
+    }
+    if (p < P) {
+      const int pr = canon[p];  // (target << 8) | source of upper edge p
+      const int u = pr & 0xff, v = pr >> 8;
+      const int64_t eu = g * E0 + p, el = g * E0 + P + p;
+#pragma unroll
+      for (int i = 0; i < NC / 4; ++i) {
+        const int c = cq + 4 * i;
+        float a = acc[4 * i];
+#pragma unroll
+        for (int j = 1; j < 4; ++j) a = (j == cq) ? acc[4 * i + j] : a;
+        if (c < HL) {
+          float* col = cv_col(ae, c, H);
+          col[eu * H] = a + sVs[u][c] + sVt[v][c];
+          col[el * H] = a + sVs[v][c] + sVt[u][c];
+        }
+      }
     }
   }
 }
@@ -937,6 +978,7 @@ __global__ __launch_bounds__(CV_T) void k_edge_fwd_cv(const float* __restrict__ 
 //   tgt row t':  var_v·d_up + var_u·d_low
 // accumulated over the workgroup's units; at the end the groups are added in
 // group order and the workgroup leaves one [D][hlp] slab (k_reduce_partials).
+template <int NC>
 __global__ __launch_bounds__(CV_T) void k_edge_bwd_cv(const float* __restrict__ ea, int64_t B,
                                                       int n, int S,
                                                       const uint16_t* __restrict__ canon,
@@ -944,37 +986,38 @@ __global__ __launch_bounds__(CV_T) void k_edge_bwd_cv(const float* __restrict__ 
                                                       float* __restrict__ partial) {
   __shared__ float sCov[CV_PCH * (CV_MAXS + 1)];
   __shared__ float sVar[CV_MAXN][CV_MAXS + 1];
-  __shared__ __attribute__((aligned(16))) float sDu[CV_PCH][CV_MAXC];
-  __shared__ __attribute__((aligned(16))) float sDl[CV_PCH][CV_MAXC];
+  __shared__ __attribute__((aligned(16))) float sDu[CV_PCH][NC];
+  __shared__ __attribute__((aligned(16))) float sDl[CV_PCH][NC];
   __shared__ int sPr[CV_PCH];
+  static_assert(CV_T * NC <= CV_PCH * (CV_MAXS + 1), "group reduction area");
   const int t = threadIdx.x, D = 3 * S, HL = L * H, E0 = n * (n - 1), P = E0 / 2;
   const int NG = CV_T / S;
   const int grp = t / S, tt = t - grp * S;
   const bool act = grp < NG;
   const int nch = (P + CV_PCH - 1) / CV_PCH;
   const int64_t U = B * nch;
-  float ac[CV_MAXC], as_[CV_MAXC], at_[CV_MAXC];
+  float ac[NC], as_[NC], at_[NC];
 #pragma unroll
-  for (int c = 0; c < CV_MAXC; ++c) ac[c] = as_[c] = at_[c] = 0.f;
+  for (int c = 0; c < NC; ++c) ac[c] = as_[c] = at_[c] = 0.f;
   for (int64_t un = blockIdx.x; un < U; un += gridDim.x) {
     const int64_t g = un / nch;
     const int p0 = (int)(un - g * nch) * CV_PCH, np = min(CV_PCH, P - p0);
     const float* gea = ea + g * E0 * D;
     __syncthreads();  // the previous unit's LDS reads
-    cv_stage(np * S, t, [&](int k) { return gea[(int64_t)(p0 + k / S) * D + k % S]; },
-             [&](int k, float v) { sCov[(k / S) * (S + 1) + k % S] = v; });
-    cv_stage(n * S, t, [&](int k) { return cv_var_row(gea, k / S, S, D)[k % S]; },
-             [&](int k, float v) { sVar[k / S][k % S] = v; });
-    cv_stage(2 * CV_PCH * CV_MAXC, t,
+    cv_stage_rows(np, S, [&](int r, int c) { return gea[(int64_t)(p0 + r) * D + c]; },
+                  [&](int r, int c, float v) { sCov[r * (S + 1) + c] = v; });
+    cv_stage_rows(n, S, [&](int r, int c) { return cv_var_row(gea, r, S, D)[c]; },
+                  [&](int r, int c, float v) { sVar[r][c] = v; });
+    cv_stage(2 * CV_PCH * NC, t,
              [&](int k) {
-               const int lo = k >= CV_PCH * CV_MAXC, r = k - lo * CV_PCH * CV_MAXC;
-               const int pl = r / CV_MAXC, c = r - pl * CV_MAXC;
+               const int lo = k >= CV_PCH * NC, r = k - lo * CV_PCH * NC;
+               const int pl = r / NC, c = r - pl * NC;
                return (pl < np && c < HL)
                           ? cv_col(dae, c, H)[(g * E0 + (lo ? P : 0) + p0 + pl) * H]
                           : 0.f;
              },
              [&](int k, float v) {
-               const int lo = k >= CV_PCH * CV_MAXC, r = k - lo * CV_PCH * CV_MAXC;
+               const int lo = k >= CV_PCH * NC, r = k - lo * CV_PCH * NC;
                (lo ? &sDl[0][0] : &sDu[0][0])[r] = v;
              });
     if (t < np) sPr[t] = canon[p0 + t];
@@ -985,44 +1028,42 @@ __global__ __launch_bounds__(CV_T) void k_edge_bwd_cv(const float* __restrict__ 
         const int pr = sPr[pp];
         const float vu = sVar[pr & 0xff][tt], vv = sVar[pr >> 8][tt];
 #pragma unroll
-        for (int c = 0; c < CV_MAXC; c += 4) {
-          if (c < HL) {
-            const float4 du = *reinterpret_cast<const float4*>(&sDu[pp][c]);
-            const float4 dl = *reinterpret_cast<const float4*>(&sDl[pp][c]);
-            ac[c] = fmaf(x, du.x + dl.x, ac[c]);
-            ac[c + 1] = fmaf(x, du.y + dl.y, ac[c + 1]);
-            ac[c + 2] = fmaf(x, du.z + dl.z, ac[c + 2]);
-            ac[c + 3] = fmaf(x, du.w + dl.w, ac[c + 3]);
-            as_[c] = fmaf(vu, du.x, fmaf(vv, dl.x, as_[c]));
-            as_[c + 1] = fmaf(vu, du.y, fmaf(vv, dl.y, as_[c + 1]));
-            as_[c + 2] = fmaf(vu, du.z, fmaf(vv, dl.z, as_[c + 2]));
-            as_[c + 3] = fmaf(vu, du.w, fmaf(vv, dl.w, as_[c + 3]));
-            at_[c] = fmaf(vv, du.x, fmaf(vu, dl.x, at_[c]));
-            at_[c + 1] = fmaf(vv, du.y, fmaf(vu, dl.y, at_[c + 1]));
-            at_[c + 2] = fmaf(vv, du.z, fmaf(vu, dl.z, at_[c + 2]));
-            at_[c + 3] = fmaf(vv, du.w, fmaf(vu, dl.w, at_[c + 3]));
-          }
+        for (int c = 0; c < NC; c += 4) {
+          const float4 du = *reinterpret_cast<const float4*>(&sDu[pp][c]);
+          const float4 dl = *reinterpret_cast<const float4*>(&sDl[pp][c]);
+          ac[c] = fmaf(x, du.x + dl.x, ac[c]);
+          ac[c + 1] = fmaf(x, du.y + dl.y, ac[c + 1]);
+          ac[c + 2] = fmaf(x, du.z + dl.z, ac[c + 2]);
+          ac[c + 3] = fmaf(x, du.w + dl.w, ac[c + 3]);
+          as_[c] = fmaf(vu, du.x, fmaf(vv, dl.x, as_[c]));
+          as_[c + 1] = fmaf(vu, du.y, fmaf(vv, dl.y, as_[c + 1]));
+          as_[c + 2] = fmaf(vu, du.z, fmaf(vv, dl.z, as_[c + 2]));
+          as_[c + 3] = fmaf(vu, du.w, fmaf(vv, dl.w, as_[c + 3]));
+          at_[c] = fmaf(vv, du.x, fmaf(vu, dl.x, at_[c]));
+          at_[c + 1] = fmaf(vv, du.y, fmaf(vu, dl.y, at_[c + 1]));
+          at_[c + 2] = fmaf(vv, du.z, fmaf(vu, dl.z, at_[c + 2]));
+          at_[c + 3] = fmaf(vv, du.w, fmaf(vu, dl.w, at_[c + 3]));
         }
       }
     }
   }
   // the slab: for each block q (cov, src, tgt) the groups' rows in group order
   float* pb = partial + (int64_t)blockIdx.x * D * hlp;
-  float* sRed = sCov;  // NG·S·CV_MAXC <= 256·CV_MAXC floats... per block q
+  float* sRed = sCov;
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
     __syncthreads();
     if (act) {
 #pragma unroll
-      for (int c = 0; c < CV_MAXC; ++c)
-        sRed[(grp * S + tt) * CV_MAXC + c] = q == 0 ? ac[c] : (q == 1 ? as_[c] : at_[c]);
+      for (int c = 0; c < NC; ++c)
+        sRed[(grp * S + tt) * NC + c] = q == 0 ? ac[c] : (q == 1 ? as_[c] : at_[c]);
     }
     __syncthreads();
     for (int k = t; k < S * hlp; k += CV_T) {
       const int r = k / hlp, c = k - r * hlp;
       float v = 0.f;
-      if (c < HL && c < CV_MAXC)
-        for (int gq = 0; gq < NG; ++gq) v += sRed[(gq * S + r) * CV_MAXC + c];
+      if (c < HL)
+        for (int gq = 0; gq < NG; ++gq) v += sRed[(gq * S + r) * NC + c];
       pb[(int64_t)(q * S + r) * hlp + c] = v;
     }
   }
@@ -1417,10 +1458,19 @@ extern "C" int sv2n_edge_logits_fwd_cv(const float* edge_attr, int64_t num_graph
     if (!ae_layers[l]) return SV2N_ERR_ARG;
     lp.p[l] = ae_layers[l];
   }
-  const int64_t P = (int64_t)n * (n - 1) / 2, nch = (P + CV_PCH - 1) / CV_PCH;
+  const int64_t P = (int64_t)n * (n - 1) / 2, nch = (P + CV_FSUB * CV_PCH - 1) / (CV_FSUB * CV_PCH);
   if (num_graphs * nch > 0x7fffffff) return SV2N_ERR_SHAPE;
-  hipLaunchKernelGGL(k_edge_fwd_cv, dim3((unsigned)(num_graphs * nch)), dim3(CV_T), 0, stream,
-                     edge_attr, n, seq_length, canon, wfold, hl_pad, lp, num_layers, heads);
+  const dim3 grid((unsigned)(num_graphs * nch));
+  switch ((num_layers * heads + 3) / 4) {
+    case 1: hipLaunchKernelGGL(k_edge_fwd_cv<4>, grid, dim3(CV_T), 0, stream, edge_attr, n,
+                               seq_length, canon, wfold, hl_pad, lp, num_layers, heads); break;
+    case 2: hipLaunchKernelGGL(k_edge_fwd_cv<8>, grid, dim3(CV_T), 0, stream, edge_attr, n,
+                               seq_length, canon, wfold, hl_pad, lp, num_layers, heads); break;
+    case 3: hipLaunchKernelGGL(k_edge_fwd_cv<12>, grid, dim3(CV_T), 0, stream, edge_attr, n,
+                               seq_length, canon, wfold, hl_pad, lp, num_layers, heads); break;
+    default: hipLaunchKernelGGL(k_edge_fwd_cv<16>, grid, dim3(CV_T), 0, stream, edge_attr, n,
+                                seq_length, canon, wfold, hl_pad, lp, num_layers, heads); break;
+  }
   return (int)hipGetLastError();
 }
 
@@ -1446,8 +1496,16 @@ extern "C" int sv2n_edge_logits_bwd_cv(const float* edge_attr, int64_t num_graph
   const int D = 3 * seq_length, width = D * hl_pad;
   const int64_t units = num_graphs * (((int64_t)n * (n - 1) / 2 + CV_PCH - 1) / CV_PCH);
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, CV_BWD_GRID));
-  hipLaunchKernelGGL(k_edge_bwd_cv, dim3(grid), dim3(CV_T), 0, stream, edge_attr, num_graphs,
-                     n, seq_length, canon, lp, num_layers, heads, hl_pad, workspace);
+#define SV2N_CVB(NC)                                                                           \
+  hipLaunchKernelGGL(k_edge_bwd_cv<NC>, dim3(grid), dim3(CV_T), 0, stream, edge_attr, num_graphs, \
+                     n, seq_length, canon, lp, num_layers, heads, hl_pad, workspace)
+  switch ((num_layers * heads + 3) / 4) {
+    case 1: SV2N_CVB(4); break;
+    case 2: SV2N_CVB(8); break;
+    case 3: SV2N_CVB(12); break;
+    default: SV2N_CVB(16); break;
+  }
+#undef SV2N_CVB
   hipLaunchKernelGGL(k_reduce_partials, dim3((unsigned)((width + 15) / 16)), dim3(256), 0, stream,
                      workspace, grid, width, dwfold);
   return (int)hipGetLastError();
