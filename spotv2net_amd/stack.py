@@ -233,10 +233,10 @@ EDGE_TAIL = os.environ.get("SV2N_EDGE_TAIL", "off")
 # "on": edge_attr marked as the reference's covariance layout (layout.mark_cov_var)
 # goes through the covariance-layout edge passes; "off": the generic passes
 # over every edge row (A/B switch for tests and measurements)
-COV_VAR_EDGES = os.environ.get("SV2N_COV_VAR_EDGES", "off")
+COV_VAR_EDGES = os.environ.get("SV2N_COV_VAR_EDGES", "on")
 # the backward's covariance-layout pass (sv2n_edge_logits_bwd_cv); "off": the
-# generic edge-gradient pass over every row (faster today: see DESIGN.md §4)
-COV_VAR_BWD = os.environ.get("SV2N_COV_VAR_BWD", "off")
+# generic edge-gradient pass over every row (A/B switch)
+COV_VAR_BWD = os.environ.get("SV2N_COV_VAR_BWD", "on")
 
 
 def _edge_tail_ok(layout: GraphLayout, convs, ea, hp: int) -> bool:
