@@ -17,6 +17,7 @@ CPU baseline (oracle restatement of PyG GATConv, rank 0 at N = 1 only).
 from __future__ import annotations
 
 import argparse
+import copy
 import json
 import os
 import platform
@@ -173,6 +174,32 @@ def kernel_table(model, data, reps=50):
                                  ptrs, L, HEADS, B, N_NODES, ws.data_ptr(), ws_n,
                                  dwf.data_ptr(), hp, sh)
 
+    # the covariance-layout edge passes, launched as the step launches them
+    # (stack.stack_forward -> sv2n::edge_logits_cv, stack_backward ->
+    # sv2n::edge_logits_bwd_cv: the main pass and its partial-slab reduce)
+    S_cv = D // 3
+    ae_cv = [torch.empty(E, HEADS, device=dev) for _ in range(L)]
+    ptrs_cv = ops._lib.ptr_array([a.data_ptr() for a in ae_cv])
+    ws_cv_n = lib.sv2n_edge_logits_bwd_cv_workspace(S_cv, hp)
+    ws_cv = torch.empty(ws_cv_n, device=dev)
+    dwf_cv = torch.empty(D, hp, device=dev)
+
+    def edge_fwd_cv():
+        lib.sv2n_edge_logits_fwd_cv(data.edge_attr.data_ptr(), B, N_NODES, S_cv,
+                                    layout.canon.data_ptr(), wfp.data_ptr(), hp, ptrs_cv, L,
+                                    HEADS, sh)
+
+    def edge_bwd_cv():
+        lib.sv2n_edge_logits_bwd_cv(data.edge_attr.data_ptr(), B, N_NODES, S_cv,
+                                    layout.canon.data_ptr(), ptrs_cv, L, HEADS, ws_cv.data_ptr(),
+                                    ws_cv_n, dwf_cv.data_ptr(), hp, sh)
+
+    # what the covariance-layout passes must move (cv_edge_bytes): the upper
+    # rows' covariance columns, one variance series per node, and the logits
+    # (written forward, read backward)
+    cv_read = cv_edge_bytes_per_graph(N_NODES, S_cv) * B
+    cv_logits = 4.0 * E * L * HEADS
+
     out0 = torch.empty_like(xs0)
     # the layer-0 projection as the step runs it: the f32-accurate split GEMM
     # (sv2n_gemm_f32x3) on the weight's pre-split bf16 planes
@@ -208,6 +235,10 @@ def kernel_table(model, data, reps=50):
                             None),
         "edge_logits_bwd": (edge_bwd, "hbm", 2.0 * E * D * L * HEADS, 4.0 * (E * D + E * L * HEADS),
                             None),
+        "edge_logits_fwd_cv": (edge_fwd_cv, "hbm", 2.0 * E * D * L * HEADS / 6,
+                               cv_read + cv_logits, None),
+        "edge_logits_bwd_cv": (edge_bwd_cv, "hbm", 2.0 * E * D * L * HEADS / 6,
+                               cv_read + cv_logits, None),
         "gat_attn_fwd_l0": (attn_fwd, "hbm", 2.0 * B * N_NODES * N_NODES * HEADS * conv0.out_channels,
                             4.0 * (xs0.numel() + ae[0].numel() + y0.numel() + ps0.numel()), None),
         # dZ, xs and psave read; dxs, d ae and the bias partials written
@@ -216,8 +247,19 @@ def kernel_table(model, data, reps=50):
                                    dbp.numel()),
                             None),
     }
-    return time_rows(rows, stream, reps, order=["edge_logits_fwd", "gemm_l0_fwd", "gat_attn_fwd_l0",
-                                                "gat_attn_bwd_l0", "gemm_l0_dwT", "edge_logits_bwd"])
+    return time_rows(rows, stream, reps, order=["edge_logits_fwd_cv", "edge_logits_fwd",
+                                                "gemm_l0_fwd", "gat_attn_fwd_l0",
+                                                "gat_attn_bwd_l0", "gemm_l0_dwT", "edge_logits_bwd",
+                                                "edge_logits_bwd_cv"])
+
+
+def cv_edge_bytes_per_graph(n: int, S: int) -> float:
+    """edge_attr bytes a covariance-layout edge pass must read per graph
+    (sv2n_edge.hip k_edge_fwd_cv / k_edge_bwd_cv): the S covariance columns
+    of the n(n-1)/2 upper rows and one S-long variance series per node
+    (utils/dataset.py:228-243: the swapped row repeats the covariance, the
+    variances are node series)."""
+    return 4.0 * (n * (n - 1) // 2 * S + n * S)
 
 
 def time_rows(rows, stream, reps, order):
@@ -559,8 +601,11 @@ def cpu_baseline(model, cfg, batch: int) -> dict:
     torch.set_num_threads(cores)
     state = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     t0 = time.perf_counter()
-    train = _cpu_rate(cfg, state, batch, True)
-    fwd = _cpu_rate(cfg, state, batch, False)
+    # bounded sample (~10-30 s of CPU work): SURVEY 8(d)'s 3 + 20 steps at
+    # small batches, 1 + 5 at the benched config's 512 graphs per step
+    wu, st = (1, 5) if batch >= 256 else (3, 20)
+    train = _cpu_rate(cfg, state, batch, True, warmup=wu, steps=st)
+    fwd = _cpu_rate(cfg, state, batch, False, warmup=wu, steps=st)
     c1 = CONFIGS["c1"]
     c1_train = _cpu_rate(c1, None, c1["batch"], True)
     c1_fwd = _cpu_rate(c1, None, c1["batch"], False)
@@ -570,15 +615,20 @@ def cpu_baseline(model, cfg, batch: int) -> dict:
             "c1_fwd_value": round(c1_fwd, 2), "host_cpu_count": os.cpu_count(),
             "sample": f"oracle PyG-2.3.0-semantics GATModel (unfolded lin_edge, scatter softmax), "
                       f"{cfg['desc'].split(':')[0]} model at B={batch} and C1 at B=32, train "
-                      f"(fwd+MSE+bwd+Adam) and forward, 3 warm-up + 20 timed steps each, "
-                      f"{cores} threads (usable cores of {os.cpu_count()} on the host), "
+                      f"(fwd+MSE+bwd+Adam) and forward, {wu} warm-up + {st} timed steps each "
+                      f"(C1: 3 + 20), {cores} threads = the CPUs this process may run on "
+                      f"(affinity / cgroup quota; {os.cpu_count()} on the host), "
                       f"{el:.1f}s, torch {torch.__version__} CPU, {_cpu_name()}"}
 
 
-def step_roofline(cfg, train_gps: float, fwd_gps: float, dtype: str) -> dict:
+def step_roofline(cfg, train_gps: float, fwd_gps: float, dtype: str,
+                  cov_var: bool = False) -> dict:
     """SURVEY §8(d) whole-step rule: graphs/s ÷ min(HBM-bound, compute-bound)
     graphs/s, from the algorithmic bytes and folded flops per graph (fwd);
-    a train step counts 3x the forward flops."""
+    a train step counts 3x the forward flops.  ``cov_var``: the step's edge
+    passes read edge_attr in the reference's covariance layout; the edge
+    bytes they actually read per graph (cv_edge_bytes_per_graph) and the HBM
+    bound under them are stated beside the rule's full-row figure."""
     n, S, H = cfg["n"], cfg["S"], cfg["heads"]
     F0, D, E0 = n * S, 3 * S, n * (n - 1)
     hidden = cfg["hidden"]
@@ -594,10 +644,20 @@ def step_roofline(cfg, train_gps: float, fwd_gps: float, dtype: str) -> dict:
     hbm_gps = HBM_PEAK_GBS * 1e9 / nbytes
     fwd_bound = min(hbm_gps, peak_tf * 1e12 / flops)
     train_bound = min(hbm_gps, peak_tf * 1e12 / (3 * flops))
-    return {"bytes_per_graph": nbytes, "fwd_flops_per_graph": flops,
-            "compute_peak_TFLOPs": peak_tf, "hbm_bound_gps": round(hbm_gps, 1),
-            "fwd_bound_gps": round(fwd_bound, 1), "train_bound_gps": round(train_bound, 1),
-            "fwd_frac": round(fwd_gps / fwd_bound, 4), "train_frac": round(train_gps / train_bound, 4)}
+    res = {"bytes_per_graph": nbytes, "fwd_flops_per_graph": flops,
+           "compute_peak_TFLOPs": peak_tf, "hbm_bound_gps": round(hbm_gps, 1),
+           "fwd_bound_gps": round(fwd_bound, 1), "train_bound_gps": round(train_bound, 1),
+           "fwd_frac": round(fwd_gps / fwd_bound, 4), "train_frac": round(train_gps / train_bound, 4)}
+    if cov_var:
+        ea_cv = cv_edge_bytes_per_graph(n, S)
+        cv_bytes = 4.0 * (n * F0 + n * out_ch) + ea_cv
+        res.update(edge_bytes_per_graph_rule=4.0 * E0 * D, edge_bytes_per_graph_read=ea_cv,
+                   bytes_per_graph_cv=cv_bytes,
+                   hbm_bound_gps_cv=round(HBM_PEAK_GBS * 1e9 / cv_bytes, 1),
+                   edge_bytes_note="the step's edge passes read the covariance columns of the "
+                                   "upper rows and one variance series per node (covariance "
+                                   "layout); bytes_per_graph keeps SURVEY 8(d)'s full-row count")
+    return res
 
 
 def _ref_model(dev, cfg, args, world):
@@ -704,10 +764,15 @@ def main(argv=None):
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="graphs per GPU (config default)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (no hipGraph)")
-    ap.add_argument("--cpu-batch", type=int, default=128,
-                    help="graphs per CPU-baseline step (per-graph CPU cost is batch independent)")
+    ap.add_argument("--cpu-batch", type=int, default=None,
+                    help="graphs per CPU-baseline step (default: the benched batch, at most "
+                         "445,440 edges = 512 C2 graphs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-table", action="store_true")
+    ap.add_argument("--no-rotating", action="store_true",
+                    help="skip value_rotating (the step over rotating distinct batches)")
+    ap.add_argument("--rotate", type=int, default=3,
+                    help="distinct device-resident batches value_rotating cycles through")
     ap.add_argument("--no-ref-loop", action="store_true",
                     help="skip the eager reference-loop (new batch per step) measurement")
     ap.add_argument("--precision", default=None, choices=("f32", "bf16"),
@@ -758,9 +823,13 @@ def main(argv=None):
     value = world * args.batch * args.steps / el
     loss = float(step.loss.item())
 
+    # the timed step's parameters, checked before anything else trains a copy
+    replicas_ok = replicas_identical(step.flat_params, dev) if world > 1 else None
+
     # the batch's edge_attr is in the reference's covariance layout (written
     # by window_batch, layout.mark_cov_var), so the step's edge passes read
-    # ≈ 1/6 of it; the same step over every edge row, for comparison
+    # ≈ 1/6 of it; the same step over every edge row, for comparison (on a
+    # copy of the model: TrainStep re-flattens the parameters it trains)
     from spotv2net_amd import stack
     cov_var = bool(stack.LAST_PATH.get("cov_var"))
     value_generic = None
@@ -768,7 +837,7 @@ def main(argv=None):
         old = stack.COV_VAR_EDGES
         stack.COV_VAR_EDGES = "off"
         try:
-            gstep = TrainStep(model, data, lr=1e-3, use_graph=not args.no_graph)
+            gstep = TrainStep(copy.deepcopy(model), data, lr=1e-3, use_graph=not args.no_graph)
             for _ in range(args.warmup):
                 gstep()
             gel = max_over_ranks(time_replays(gstep, args.steps), dev)
@@ -777,7 +846,33 @@ def main(argv=None):
         finally:
             stack.COV_VAR_EDGES = old
 
-    replicas_ok = replicas_identical(step.flat_params, dev) if world > 1 else None
+    # a new batch every step, as the reference's loop (5_train_SpotV2Net.py:142-143):
+    # ROTATE distinct device-resident batches (more bytes than the 256 MB
+    # Infinity Cache holds, so no step finds its inputs left there by the
+    # previous one), one captured graph per batch over the same parameters
+    rot = None
+    if not args.no_rotating and not args.no_graph:
+        rot_batches = [data] + [synthetic_batch(args.batch, cfg["S"], n=cfg["n"],
+                                                seed=7000 + 100 * rank + i, device=dev)
+                                for i in range(args.rotate - 1)]
+        rot_bytes = sum(b.x.numel() * 4 + b.edge_attr.numel() * 4 for b in rot_batches)
+        rstep = TrainStep(copy.deepcopy(model), rot_batches[0], lr=1e-3)
+        for b in rot_batches[1:]:
+            rstep.add_shape(b)
+        k = len(rot_batches)
+        it = [0]
+
+        def rstep_call():
+            rstep(it[0] % k)
+            it[0] += 1
+
+        for _ in range(max(args.warmup, k)):
+            rstep_call()
+        rel = max_over_ranks(time_replays(rstep_call, args.steps), dev)
+        rot = {"value": world * args.batch * args.steps / rel, "batches": k,
+               "bytes_per_batch": rot_bytes / k, "bytes_total": rot_bytes,
+               "cov_var": bool(stack.LAST_PATH.get("cov_var"))}
+        del rstep, rot_batches
 
     ref = {}
     if not args.no_ref_loop:
@@ -819,9 +914,10 @@ def main(argv=None):
             roof["traffic"] = load_traffic("c5:" + kname)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            # bounded sample (~10-30 s): at most as many edges as 128 C2 graphs
-            cpu_batch = max(1, min(args.cpu_batch, args.batch,
-                                   111360 // (cfg["n"] * (cfg["n"] - 1))))
+            # the benched batch (C2: 512 graphs); at most as many
+            # edges as 512 C2 graphs for the other configs
+            cpu_batch = max(1, min(args.cpu_batch or args.batch, args.batch,
+                                   445440 // (cfg["n"] * (cfg["n"] - 1))))
             cpu = cpu_baseline(model, cfg, cpu_batch)
         result = {
             "metric": METRIC,
@@ -844,6 +940,10 @@ def main(argv=None):
                               "(utils/dataset.py:228-243), read as such by the edge passes"
                               if cov_var else "generic rows"),
             "value_generic_edges": (round(value_generic, 1) if value_generic else None),
+            "value_rotating": (round(rot["value"], 1) if rot else None),
+            "rotating": ({k: v for k, v in rot.items() if k != "value"} if rot else None),
+            "step_edge_passes": ("edge_logits_fwd_cv / edge_logits_bwd_cv" if cov_var
+                                 else "edge_logits_fwd / edge_logits_bwd"),
             "fwd_graphs_per_s": round(fwd_value, 1),
             **{k: round(v, 1) for k, v in ref.items()},
             "ref_loop_is": "5_train_SpotV2Net.py:142-160 unchanged (new batch per step, "
@@ -854,7 +954,7 @@ def main(argv=None):
                            "the H2D copy inside the step",
             "replicas_bit_identical": replicas_ok,
             "backend": args.backend if world > 1 else None,
-            "step_roofline": step_roofline(cfg, value, fwd_value, args.precision),
+            "step_roofline": step_roofline(cfg, value, fwd_value, args.precision, cov_var),
             "final_loss": loss,
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -884,7 +984,7 @@ def main_c3(args, dev, cfg):
         roof["traffic"] = load_traffic(f"c3_{args.precision}:" + kname)
     if not args.no_cpu_baseline:
         model = build_model(dev, cfg)
-        cpu = cpu_baseline(model, cfg, min(args.cpu_batch, 16))
+        cpu = cpu_baseline(model, cfg, min(args.cpu_batch or 16, 16))
     result = {
         "metric": METRIC,
         "value": round(value, 1),

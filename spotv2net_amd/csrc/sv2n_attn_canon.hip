@@ -1052,7 +1052,7 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
   auto launch = [&](auto kern) {
     if (lds > 65536)
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
+                                (int)lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(canon::THREADS), lds, st, dy, y, xs, ldx, psave,
                        keep, keep_scale, post_u, post_p,
                        post_u ? (float)(1.0 / (1.0 - (double)post_p)) : 1.f, rowmask, dxs, dae,
@@ -1136,7 +1136,7 @@ static void launch_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx
                                         HEAD ? (CONCAT ? H * C : C) : 0);
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)canon::k_fwd<ACT, CONCAT, KEEP, HEAD>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int S = HEAD ? 1 : canon_fwd_splits(B, H, C, CONCAT);
   hipLaunchKernelGGL((canon::k_fwd<ACT, CONCAT, KEEP, HEAD>), dim3(canon_grid(B, S)),
                      dim3(canon::THREADS), lds, st, xs, ldx, ae, ae_edge_order, rowmask, bias, keep,

@@ -693,7 +693,7 @@ template <typename K>
 static void raise_lds_tiled(K kernel, size_t bytes) {
   if (bytes > 65536)
     (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+                              (int)bytes);
 }
 
 static int check_tiled(int64_t B, int n, int H, int C, int ldx, int act) {

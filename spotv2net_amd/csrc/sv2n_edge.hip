@@ -227,7 +227,10 @@ __device__ __forceinline__ void gather_dae(float (&gd)[(EDGE_CHUNK * HLP + EDGE_
   }
 }
 
-template <int HLP, int RF, bool PLANES>
+// NT > 1 (wide shapes: (DP/4)·(HLP/4) thread tiles > 256, e.g. the HPO grid's
+// seq_length 120 with 3 layers x 7 heads): every thread owns tiles t, t + 256,
+// ... and walks every edge of the chunk (ES = 1).
+template <int HLP, int RF, bool PLANES, int NT>
 __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
     const float* __restrict__ ea, int64_t E, int D, int DP, const int64_t* __restrict__ ei,
     const uint16_t* __restrict__ canon, int E0, LayerCPtrs dae, int L, int H, int64_t B, int n,
@@ -247,15 +250,15 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
   __syncthreads();
   const int KG = HLP / 4;
   const int T = (DP / 4) * KG;  // thread tiles
-  const int ES = EDGE_THREADS / T;
-  const int tile = t % T, es = t / T;
-  const bool active = es < ES;
-  const int dg = tile / KG, kg = tile - dg * KG;
+  const int ES = NT == 1 ? EDGE_THREADS / T : 1;
+  const int tile = NT == 1 ? t % T : t, es = NT == 1 ? t / T : 0;
   const int HL = L * H;
 
-  float acc[16];
+  float acc[NT][16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[j][k] = 0.f;
 
   const int64_t nchunks = (E + EDGE_CHUNK - 1) / EDGE_CHUNK;
   ChunkRegs<RF> R;
@@ -287,25 +290,35 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_bwd(
       R.load(ea, e1, ne1, D, t);
       gather_dae<HLP, PLANES>(gd, s_ptr, ei, E, canon, E0, n, B, HL, H, e1, ne1, t);
     }
-    if (active) {
-      for (int le = es; le < ne; le += ES) {
-        const float4 a = *reinterpret_cast<const float4*>(s_ea + le * DP + 4 * dg);
-        const float4 b = *reinterpret_cast<const float4*>(s_dae + le * HLP + 4 * kg);
-        const float av[4] = {a.x, a.y, a.z, a.w};
-        const float bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
+    for (int j = 0; j < NT; ++j) {
+      const int tj = tile + j * EDGE_THREADS;
+      if (es < ES && tj < T) {
+        const int dg = tj / KG, kg = tj - dg * KG;
+        for (int le = es; le < ne; le += ES) {
+          const float4 a = *reinterpret_cast<const float4*>(s_ea + le * DP + 4 * dg);
+          const float4 b = *reinterpret_cast<const float4*>(s_dae + le * HLP + 4 * kg);
+          const float av[4] = {a.x, a.y, a.z, a.w};
+          const float bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-          for (int y = 0; y < 4; ++y) acc[4 * x + y] = fmaf(av[x], bv[y], acc[4 * x + y]);
+          for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+              acc[j][4 * x + y] = fmaf(av[x], bv[y], acc[j][4 * x + y]);
+        }
       }
     }
   }
   // block reduction over the ES edge groups (reuse the chunk buffer)
   __syncthreads();
-  float* s_red = smem;  // [ES][T][16] <= 256*16 floats
-  if (active) {
+  float* s_red = smem;  // [ES][T][16]: <= max(256, T)*16 floats
 #pragma unroll
-    for (int k = 0; k < 16; ++k) s_red[(es * T + tile) * 16 + k] = acc[k];
+  for (int j = 0; j < NT; ++j) {
+    const int tj = tile + j * EDGE_THREADS;
+    if (es < ES && tj < T) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s_red[(es * T + tj) * 16 + k] = acc[j][k];
+    }
   }
   __syncthreads();
   const int O = D * HLP;
@@ -1169,11 +1182,14 @@ static int edge_bwd_small(const float* edge_attr, int64_t num_edges, int edge_di
   return (int)hipGetLastError();
 }
 
+// the dynamic LDS a launch asks for (not 160 KiB: the kernels also hold a
+// little static LDS, and a limit whose sum with it exceeds the CU's 160 KiB is
+// refused, leaving the 64 KiB default in place)
 template <typename K>
 static void raise_lds_limit(K kernel, size_t bytes) {
   if (bytes > 65536)
     (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+                              (int)bytes);
 }
 
 static int edge_fwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim,
@@ -1225,7 +1241,7 @@ static int edge_fwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
   const int rfi = rf <= 2 ? 2 : rf <= 8 ? 8 : rf <= 16 ? 16 : 24;  // instantiated RF
   const size_t lds = sizeof(float) * ((size_t)edge_dim * hl_pad + (size_t)rfi * EDGE_THREADS * 4 +
                                       (size_t)EDGE_CHUNK * hl_pad);
-  if (lds > 160 * 1024) return SV2N_ERR_SHAPE;
+  if (lds > 159 * 1024) return SV2N_ERR_SHAPE;  // room for the static LDS
 #define SV2N_LAUNCH_EF2(HLP, RF, PL)                                                              \
   {                                                                                               \
     raise_lds_limit(k_edge_fwd<HLP, RF, PL>, lds);                                                \
@@ -1279,7 +1295,9 @@ static int edge_bwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
     return SV2N_ERR_SHAPE;
   if ((uintptr_t)edge_attr & 15) return SV2N_ERR_ALIGN;
   const int DP = (edge_dim + 3) & ~3;
-  if ((DP / 4) * (hl_pad / 4) > EDGE_THREADS) return SV2N_ERR_SHAPE;
+  const int tiles = (DP / 4) * (hl_pad / 4);  // 4x4 thread tiles of the [D][hl_pad] gradient
+  if (tiles > 3 * EDGE_THREADS) return SV2N_ERR_SHAPE;
+  const int nt = (tiles + EDGE_THREADS - 1) / EDGE_THREADS;
   LayerCPtrs lp{};
   for (int l = 0; l < num_layers; ++l) {
     if (!dae_layers[l]) return SV2N_ERR_ARG;
@@ -1317,15 +1335,23 @@ static int edge_bwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
   const int rfi = rf <= 2 ? 2 : rf <= 8 ? 8 : rf <= 16 ? 16 : 24;  // instantiated RF
   const size_t ea_floats = std::max((size_t)EDGE_CHUNK * DP, (size_t)rfi * EDGE_THREADS * 4);
   size_t lds = sizeof(float) * (ea_floats + (size_t)EDGE_CHUNK * hl_pad);
-  lds = std::max(lds, sizeof(float) * (size_t)EDGE_THREADS * 16);
-  if (lds > 160 * 1024) return SV2N_ERR_SHAPE;
+  lds = std::max(lds, sizeof(float) * (size_t)std::max(EDGE_THREADS, tiles) * 16);
+  if (lds > 159 * 1024) return SV2N_ERR_SHAPE;  // room for the static LDS
   if (num_edges == 0) return (int)hipMemsetAsync(dwfold, 0, sizeof(float) * O, stream);
+#define SV2N_LAUNCH_EB3(HLP, RF, PL, NT)                                                          \
+  {                                                                                               \
+    raise_lds_limit(k_edge_bwd<HLP, RF, PL, NT>, lds);                                            \
+    hipLaunchKernelGGL((k_edge_bwd<HLP, RF, PL, NT>), dim3(grid), dim3(EDGE_THREADS), lds,        \
+                       stream, edge_attr, num_edges, edge_dim, DP, edge_index, canon, E0, lp,     \
+                       num_layers, heads, num_graphs, n, workspace);                              \
+  }
 #define SV2N_LAUNCH_EB2(HLP, RF, PL)                                                              \
   {                                                                                               \
-    raise_lds_limit(k_edge_bwd<HLP, RF, PL>, lds);                                                \
-    hipLaunchKernelGGL((k_edge_bwd<HLP, RF, PL>), dim3(grid), dim3(EDGE_THREADS), lds, stream,    \
-                       edge_attr, num_edges, edge_dim, DP, edge_index, canon, E0, lp, num_layers, \
-                       heads, num_graphs, n, workspace);                                          \
+    if (nt == 1) SV2N_LAUNCH_EB3(HLP, RF, PL, 1)                                                  \
+    else if constexpr (HLP >= 16 && RF >= 16) { /* tiles > 256 need DP > 4096 / HLP */           \
+      if (nt == 2) SV2N_LAUNCH_EB3(HLP, RF, PL, 2)                                                \
+      else SV2N_LAUNCH_EB3(HLP, RF, PL, 3)                                                        \
+    } else return SV2N_ERR_SHAPE;                                                                 \
   }
 #define SV2N_LAUNCH_EB(HLP, RF)                                  \
   {                                                              \
@@ -1350,6 +1376,7 @@ static int edge_bwd_impl(const float* edge_attr, int64_t num_edges, int edge_dim
 #undef SV2N_LAUNCH_EB_RF
 #undef SV2N_LAUNCH_EB
 #undef SV2N_LAUNCH_EB2
+#undef SV2N_LAUNCH_EB3
   hipLaunchKernelGGL(k_reduce_partials, dim3((O + 15) / 16), dim3(256), 0, stream, workspace,
                      grid, O, dwfold);
   return (int)hipGetLastError();

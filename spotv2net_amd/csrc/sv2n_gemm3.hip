@@ -49,7 +49,7 @@ static int launch_gemm3_p(hipStream_t st, const float* A, int64_t lda, const uns
   static_assert(lds <= 160 * 1024, "LDS budget");
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)k_gemm3<NW, MT, NT, BK, 1, 3, PIPE>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const dim3 grid((unsigned)((M + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN));
   hipLaunchKernelGGL((k_gemm3<NW, MT, NT, BK, 1, 3, PIPE>), grid, dim3(Cfg::THREADS), lds, st, A,
                      lda, Bp, Kp, N * Kp, C, ldc, M, N, K);
@@ -98,7 +98,7 @@ static int launch_gemm_bf16(hipStream_t st, const float* A, int64_t lda, const u
   static_assert(lds <= 160 * 1024, "LDS budget");
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)k_gemm3<NW, MT, NT, BK, 1, 1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const dim3 grid((unsigned)((M + Cfg::BM - 1) / Cfg::BM), (unsigned)((N + Cfg::BN - 1) / Cfg::BN));
   hipLaunchKernelGGL((k_gemm3<NW, MT, NT, BK, 1, 1>), grid, dim3(Cfg::THREADS), lds, st, A, lda,
                      Bp, Kp, N * Kp, C, ldc, M, N, K);

@@ -70,6 +70,16 @@ def _tsig(t: Optional[torch.Tensor]):
     return (t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype)
 
 
+def _switches():
+    """The process-wide path switches a capture bakes in (stack's A/B
+    switches) and whether the forward draws its dropout from the device
+    generator (stack.device_dropout, keyed on a step count): flipping one
+    must capture again, not replay the old variant."""
+    from . import stack
+    return (stack.COV_VAR_EDGES, stack.COV_VAR_BWD, stack.HEAD_FUSE, stack.BF16_OPERANDS,
+            stack.EDGE_FUSED, stack.EDGE_TAIL, stack._drop_rng_key())
+
+
 def _layout_sig(lay: GraphLayout):
     def shp(t):
         return None if t is None else (tuple(t.shape), t.dtype)
@@ -274,7 +284,7 @@ def forward(model, data, x, edge_index, edge_attr, layout: GraphLayout) -> Optio
     key = (model.training, train_graph, precision, torch.is_autocast_enabled("cuda"),
            model._act_code, model.dropout, tuple(c.dropout for c in model.gat_layers),
            _tsig(x), _tsig(edge_attr), cov_var_seq_length(edge_attr), _layout_sig(layout), needs,
-           tuple(p.data_ptr() for p in ps))
+           tuple(p.data_ptr() for p in ps), _switches())
     entry = cache.entries.get(key)
     if entry is None:
         k = cache.seen.get(key, 0) + 1

@@ -87,6 +87,13 @@ def _direct_mode() -> bool:
     return getattr(_mode, "direct", False)
 
 
+def _int64_seed(seed: int) -> int:
+    """A 64-bit seed as the signed int64 with the same bit pattern (the
+    dispatcher refuses ints >= 2**63 for an ``int`` schema argument)."""
+    s = int(seed) & 0xFFFFFFFFFFFFFFFF
+    return s - (1 << 64) if s >= (1 << 63) else s
+
+
 @contextlib.contextmanager
 def device_dropout(seed: int, step: torch.Tensor):
     """Within this context the post-layer dropout of the n <= 32 attention
@@ -94,13 +101,24 @@ def device_dropout(seed: int, step: torch.Tensor):
     by (``seed``, the device step count ``step``, layer) instead of torch's
     generator, so a captured step holds no torch random op (whose replays
     each launch two generator-state fills).  ``train.TrainStep`` uses it with
-    its Adam step counter; outside it every draw is torch.rand."""
+    its Adam step counter; outside it every draw is torch.rand.
+
+    ``seed`` may be any 64-bit unsigned value (``torch.initial_seed()``): it
+    is folded into the int64 range of the op's schema here and reinterpreted
+    as uint64 on the C side."""
     prev = getattr(_mode, "drop_rng", None)
-    _mode.drop_rng = (int(seed), step)
+    _mode.drop_rng = (_int64_seed(seed), step)
     try:
         yield
     finally:
         _mode.drop_rng = prev
+
+
+def _drop_rng_key():
+    """(seed, step-tensor pointer) of the active device_dropout context, or
+    None (a capture's draws depend on both)."""
+    rng = getattr(_mode, "drop_rng", None)
+    return None if rng is None else (rng[0], rng[1].data_ptr())
 
 
 def _post_uniforms(rows: int, cols: int, layer: int, dev) -> torch.Tensor:
@@ -673,6 +691,17 @@ def gat_train_head_mse(x: torch.Tensor, edge_attr: Optional[torch.Tensor], convs
                                           head=(linear, target, ghw, ghb, loss_sum),
                                           x_bf16=x_bf16)
         stack_backward(saved, meta, tuple(convs), layout, meta.head_dz, False, grad_of)
+        if layout.pending is not None:
+            # the kernels added the loss to loss_sum and the gradients to
+            # p.grad themselves: carry the deferred edge check's NaN poison
+            # into those too (x·1 is exact; one multi-tensor launch), as the
+            # unfused path's NaN outputs would
+            f = torch.where(layout.pending[0] != 0, float("nan"), 1.0).to(torch.float32)
+            bufs = [q.grad for q in params + [linear.weight, linear.bias]
+                    if q is not None and q.grad is not None]
+            if loss_sum is not None:
+                bufs.append(loss_sum)
+            torch._foreach_mul_(bufs, f)
     return layout.poison(loss).reshape(())
 
 

@@ -28,6 +28,27 @@ def test_uniforms_match_restatement(dev, rows, cols, seed, step, salt):
     assert np.array_equal(u.cpu().numpy(), want)
 
 
+def test_seed_at_or_above_2_63(dev):
+    """torch.seed() draws any 64-bit value; TrainStep's default dropout seed
+    is torch.initial_seed(), so a seed >= 2**63 must run (folded into the
+    op's int64 argument, reinterpreted as uint64: the restatement's draws)."""
+    from spotv2net_amd import GATModel, synthetic_batch
+    from spotv2net_amd.stack import _int64_seed
+    from spotv2net_amd.train import TrainStep
+    big = 2 ** 63 + 5
+    st = torch.full((1,), 2.0, device=dev)
+    u = torch.ops.sv2n.dropout_uniform(30, 40, st, _int64_seed(big), 1)
+    assert np.array_equal(u.cpu().numpy(), dropout_uniform_ref(1200, big, 2, 1).reshape(30, 40))
+    torch.manual_seed(big)
+    assert torch.initial_seed() == big
+    m = GATModel(120, 12, 4, 1, [16, 8], dropout=0.2, concat_heads=True).to(dev)
+    data = synthetic_batch(8, 4, seed=3, device=dev)
+    step = TrainStep(m, data, lr=1e-3, use_graph=True)
+    assert step.device_rng and step.dropout_seed == big
+    losses = [float(step()) for _ in range(2)]
+    assert all(np.isfinite(losses)), losses
+
+
 def test_mask_statistics(dev):
     st = torch.zeros(1, device=dev)
     u = torch.ops.sv2n.dropout_uniform(4096, 1000, st, 77, 0)

@@ -27,3 +27,14 @@ def test_uniform_range_and_layout():
     # step and salt give different streams
     assert not np.array_equal(u, dropout_uniform_ref(10001, 1234, 8, 1))
     assert not np.array_equal(u, dropout_uniform_ref(10001, 1234, 7, 0))
+
+
+def test_dropout_seed_folds_into_int64():
+    """TrainStep's default dropout seed is torch.initial_seed(), any 64-bit
+    unsigned value; stack.device_dropout hands the op (an int64 schema
+    argument) the same bit pattern as a signed value."""
+    from spotv2net_amd.stack import _int64_seed
+    for s in (0, 5154, 2 ** 63 - 1, 2 ** 63, 2 ** 63 + 5, 2 ** 64 - 1):
+        v = _int64_seed(s)
+        assert -2 ** 63 <= v < 2 ** 63
+        assert v & 0xFFFFFFFFFFFFFFFF == s

@@ -30,6 +30,12 @@ KERNELS = {
     "gat_attn_fwd_l0": "sv2n::canon::k_fwd<1, true, false, false>",
     "gat_attn_bwd_l0": "sv2n::canon::k_bwd<0, true, false, 3>",
     "gat_attn_fwd_l1_head": "sv2n::canon::k_fwd<1, false, false, true>",
+    # the covariance-layout passes the C2 step runs (bench kernel_table
+    # edge_logits_fwd_cv / _bwd_cv); the backward's slab reduce shares its
+    # kernel name with the generic pass's and is listed on its own
+    "edge_logits_fwd_cv": "sv2n::k_edge_fwd_cv<8>",
+    "edge_logits_bwd_cv": "sv2n::k_edge_bwd_cv<8>",
+    "edge_reduce_partials": "sv2n::k_reduce_partials",
 }
 
 
