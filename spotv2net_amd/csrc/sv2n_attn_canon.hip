@@ -114,7 +114,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
   int64_t g;
   int split;
   if (!graph_split(B, S, g, split)) return;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int slot = 4 * split + wave, NS = 4 * S;
   const int l32 = lane & 31, half = lane >> 5;
   const int HC = H * C, OC = CONCAT ? HC : C;
@@ -521,7 +521,7 @@ __host__ __device__ inline int canon_bwd_tail_off(bool edge, int HS) {
 __device__ __forceinline__ void edge_grad_tail(const EdgeTail& et, int64_t g, int n, int H,
                                                const float* sDL, const float* sSh,
                                                const uint16_t* sDec, float* smem) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int E0 = n * (n - 1), P = E0 / 2, D = et.D;
   float* sE = smem;  // [E0][ET_COLS]
   // this layer's d-logits (dl + the self-loop share of row ti), PyG's per-edge
@@ -636,7 +636,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   int64_t g;
   int split;
   if (!graph_split(B, S, g, split)) return;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int l32 = lane & 31, half = lane >> 5;
   const int HC = H * C, OC = CONCAT ? HC : C;
   const int E0 = n * (n - 1);

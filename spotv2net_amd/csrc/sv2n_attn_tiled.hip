@@ -312,7 +312,7 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
   int64_t g;
   int h;
   block_gh(H, g, h);
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int gq = lane >> 4, q = lane & 15;
   const int64_t row0 = g * n;
   const int HC = H * C;
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
   int64_t g;
   int h;
   block_gh(H, g, h);
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int gq = lane >> 4, q = lane & 15;
   const int64_t row0 = g * n;
   const int HC = H * C;

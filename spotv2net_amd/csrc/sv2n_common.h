@@ -288,14 +288,36 @@ __device__ __forceinline__ bool decode_edge(int64_t e, const int64_t* __restrict
 // accesses need no branch and the compiler can count vmcnt across them.
 // Build descriptors only from wave-uniform values (kernel args, blockIdx);
 // `bytes` = 0 makes every access through the descriptor a no-op.
+// The wave's index in its workgroup as a wave-uniform (SGPR) value.  threadIdx.x
+// >> 6 is uniform in fact, but the compiler cannot prove it, and a buffer
+// descriptor or soffset derived from it would then be made uniform lane by
+// lane around every buffer instruction (a v_readfirstlane waterfall loop per
+// load; tools/isa_waterfall.py finds them).
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int OOB = 0x7ffffff0;  // byte offset past any buffer (< 2^31)
 
+// Every descriptor in this library is wave-uniform by construction (bases and
+// sizes from block, graph and wave indices).  Values the compiler computed on
+// the vector ALU (e.g. a runtime division of blockIdx.x) would otherwise give
+// a waterfall loop around every buffer instruction that uses the descriptor:
+// the base and size go through v_readfirstlane here.  Never build a descriptor
+// from a per-lane value.
+// (inline asm: the compiler folds __builtin_amdgcn_readfirstlane of a value it
+// knows to be uniform, even one it keeps in a VGPR)
+__device__ __forceinline__ uint32_t to_sgpr(uint32_t v) {
+  uint32_t r;
+  asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(r) : "v"(v));
+  return r;
+}
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
-                                           0x00020000);
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  const uint64_t lo = to_sgpr((uint32_t)b), hi = to_sgpr((uint32_t)(b >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((hi << 32) | lo), (short)0,
+                                           (int)to_sgpr(bytes), 0x00020000);
 }
 // (the b32/b128 builtins move raw bits: unsigned int / uint x4)
 __device__ __forceinline__ uint32_t bld_u32(rsrc_t r, int off) {

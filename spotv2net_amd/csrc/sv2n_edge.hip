@@ -477,7 +477,7 @@ __global__ __launch_bounds__(256) void k_edge_bwd_small(
     const uint16_t* __restrict__ canon, int E0, ColCPtrs col, int L, int H, int64_t B, int n,
     float* __restrict__ partial) {
   constexpr int KQ = HLP / 4;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int HL = L * H;
   float acc[DS][KQ];
 #pragma unroll
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(256) void k_edge_bwd_mfma(const float* __restrict__
   constexpr int NT = HLP >= 16 ? HLP / 16 : 1;
   typedef float f4 __attribute__((ext_vector_type(4)));
   __shared__ float s_red[4][16 * NT * 16];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, lk = lane >> 4;
   f4 acc[NT];
 #pragma unroll
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(256, 4) void k_edge_fwd_mx(const float* __restrict_
                                                         int D, const float* __restrict__ wf,
                                                         int hlp, LayerPtrs ae, int L, int H) {
   __shared__ __attribute__((aligned(16))) float s_img[MX_WAVES][(MX_TE + 1) * MX_PF];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int li = lane & 15, g = lane >> 4;
   const int HL = L * H;
   float* img = s_img[wave];
@@ -708,7 +708,7 @@ __global__ __launch_bounds__(256, 4) void k_edge_bwd_mx(const float* __restrict_
                                                                   float* __restrict__ partial) {
   constexpr int NM = NS / 2, NP = NM / 2;  // M tiles of 16 d; float2 pieces per row
   __shared__ __attribute__((aligned(16))) float s_red[MX_WAVES * 8 * NS * 16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int li = lane & 15, g = lane >> 4;
   const int HL = L * H;
   const float* inp = li < HL ? mx_col_ptr<const float>(dae, li, L, H) : nullptr;
@@ -1079,6 +1079,345 @@ __global__ __launch_bounds__(CV_T) void k_edge_bwd_cv(const float* __restrict__ 
         for (int gq = 0; gq < NG; ++gq) v += sRed[(gq * S + r) * NC + c];
       pb[(int64_t)(q * S + r) * hlp + c] = v;
     }
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Round 5 (even S): both covariance-layout passes with ONE workgroup of 8
+// waves per graph and the inner products on v_mfma_f32_16x16x4_f32 (exact f32
+// products, f32 sums).  The graph's P upper rows go in tiles of 16 pairs, tile
+// k on wave k % 8.  What the round-4 passes spent their time on (PMC,
+// profiles/r05_cv_pmc.txt): the covariance columns loaded 4 lanes x 16 B per
+// row (16 rows per load instruction), the variance series re-read by every
+// 64-pair unit, and per-unit staging phases between barriers.
+//
+// forward: every wave issues the covariance loads of ALL its tiles up front
+//   (flat float2 pieces of the tile's 16 x S block: 512 contiguous bytes over
+//   ~3 rows per instruction; a graph's ~73 KB in flight), after the small
+//   loads the workgroup needs first (variance series, the fold's node rows,
+//   the pair table), so waiting for those never waits for the stream.  The
+//   node terms Vs = var·W̃[S..2S), Vt = var·W̃[2S..3S) are formed while the
+//   stream lands (four lanes per (node, column)).  Per tile the wave writes
+//   its rows into a private LDS image (row stride 8·NJ + 4 floats: the 16 rows
+//   of a half-wave's b64 reads start on distinct 4-bank groups) and runs
+//   A[p][c] = Σ_t cov[p][t]·W̃[t][c] (MFMA step (s, c') pairs lane group g with
+//   t = 8s + 2g + c'), then writes A + Vs[u] + Vt[v] and A + Vs[v] + Vt[u].
+// backward: per tile the A operands come straight from HBM (M tile m holds
+//   t = 32(m/2) + 2i + (m&1): lane (i, g) loads the pieces of two M tiles as
+//   one float2, 4 rows x 128 contiguous bytes per instruction), B = d_up +
+//   d_low of the tile's pairs, the next tile's loads in flight; the d-logits
+//   also go into an LDS table of the graph, from which the per-node sums of
+//   the outgoing / incoming edges' d-logits are added in a fixed order, then
+//   dW̃[S + t] = Σ_u var_t(u)·Σ_out(u), dW̃[2S + t] = Σ_u var_t(u)·Σ_in(u).
+//   One [D][hl_pad] partial per workgroup (fixed summation order throughout),
+//   k_reduce_partials finishes.
+// ---------------------------------------------------------------------------
+constexpr int CV2_WAVES = 8, CV2_T = 64 * CV2_WAVES, CV2_TW = 4;  // tiles of 16 pairs per wave
+constexpr int CV2_BWD_GRID = 512;
+static_assert(CV2_WAVES * CV2_TW * 16 >= CV_MAXN * (CV_MAXN - 1) / 2, "tiles cover every pair");
+static_assert(CV2_BWD_GRID <= CV_BWD_GRID, "workspace of sv2n_edge_logits_bwd_cv_workspace");
+
+// (u, v), u < v, of upper pair p: (v << 8) | u in the pair table
+__device__ __forceinline__ int cv2_pair_index(int a, int b, int n) {  // a < b
+  return a * (2 * n - a - 1) / 2 + (b - a - 1);
+}
+
+template <int NJ, int NC, int ABL = 0>  // ABL: timing ablations of tools/cv_tune.hip only
+__global__ __launch_bounds__(CV2_T) void k_edge_fwd_cv2(const float* __restrict__ ea, int n, int S,
+                                                        const uint16_t* __restrict__ canon,
+                                                        const float* __restrict__ wf, int hlp,
+                                                        LayerPtrs ae, int L, int H) {
+  constexpr int RS = 8 * NJ + 4;       // image row stride (floats)
+  constexpr int IMG = 16 * RS + 128;   // + where the pieces past the tile land
+  __shared__ __attribute__((aligned(16))) float s_img[CV2_WAVES][IMG];
+  __shared__ float sVar[CV_MAXN][CV_MAXS + 1];
+  __shared__ float sWn[2 * CV_MAXS][NC];  // the fold's source / target rows
+  __shared__ float sV[2][CV_MAXN][NC];    // node terms (source, target)
+  __shared__ int sPr[CV_MAXN * (CV_MAXN - 1) / 2];
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
+  const int li = lane & 15, gq = lane >> 4;
+  const int D = 3 * S, HL = L * H, E0 = n * (n - 1), P = E0 / 2, TP = (P + 15) / 16;
+  const int S2 = S >> 1;
+  const int64_t g = blockIdx.x;
+  const rsrc_t rg = make_rsrc(ea + g * E0 * D, (uint32_t)(E0 * D) * 4u);
+
+  // 1) the loads the workgroup needs first: variance series (node u: the
+  //    source columns of upper row 0 for u = 0, the target columns of upper
+  //    row u - 1 otherwise), the fold's node rows, the pair table
+  u32x2 vv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int k = t + CV2_T * i, u = k / S2, c2 = k - u * S2;
+    const int off = u == 0 ? S + 2 * c2 : (u - 1) * D + 2 * S + 2 * c2;
+    vv[i] = __builtin_amdgcn_raw_buffer_load_b64(rg, k < n * S2 ? 4 * off : OOB, 0, 0);
+  }
+  float wn[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = t + CV2_T * i, d = k / NC, c = k - d * NC;
+    wn[i] = (k < 2 * S * NC && c < HL) ? wf[(S + d) * hlp + c] : 0.f;
+  }
+  const int pr = t < P ? (int)canon[t] : 0;
+  float wb[NJ][2];  // B operands: W̃[t][li], t = 8s + 2g + c
+#pragma unroll
+  for (int s = 0; s < NJ; ++s)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int tt = 8 * s + 2 * gq + c;
+      wb[s][c] = (tt < S && li < HL) ? wf[tt * hlp + li] : 0.f;
+    }
+  // 2) the covariance stream: flat float2 pieces f = 128j + 2·lane of each
+  //    of the wave's tiles (16 rows x S floats)
+  int loff[NJ];
+  u32x2 v[CV2_TW][NJ];
+  {
+    int goff[NJ];
+    const int nf = 16 * S;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int f = 128 * j + 2 * lane, r = f / S, c = f - r * S;
+      goff[j] = f < nf ? 4 * (r * D + c) : OOB;
+      loff[j] = f < nf ? r * RS + c : 16 * RS + 2 * lane;
+    }
+#pragma unroll
+    for (int k = 0; k < CV2_TW; ++k) {
+      const int tile = wave + CV2_WAVES * k;
+      const bool ok = tile < TP;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        v[k][j] = __builtin_amdgcn_raw_buffer_load_b64(rg, ok ? goff[j] : OOB,
+                                                        ok ? tile * 16 * D * 4 : 0, 0);
+    }
+  }
+  float* img = s_img[wave];
+  for (int k = lane; k < 16 * (8 * NJ - S); k += 64) {  // lags S .. 8·NJ of the image: 0
+    const int r = k / (8 * NJ - S);
+    img[r * RS + S + (k - r * (8 * NJ - S))] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int k = t + CV2_T * i, u = k / S2, c2 = k - u * S2;
+    if (k < n * S2) {
+      sVar[u][2 * c2] = __uint_as_float(vv[i][0]);
+      sVar[u][2 * c2 + 1] = __uint_as_float(vv[i][1]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = t + CV2_T * i;
+    if (k < 2 * S * NC) (&sWn[0][0])[k] = wn[i];
+  }
+  if (t < P) sPr[t] = pr;
+  __syncthreads();
+  // 3) node terms, four lanes per (node, column), lags q, q + 4, ...
+  for (int k0 = 0; k0 < ((ABL & 4) ? 0 : 4 * n * NC); k0 += CV2_T) {
+    const int k = k0 + t;
+    const int q = k & 3, uc = k >> 2, u = min(uc / NC, n - 1), c = uc - (uc / NC) * NC;
+    float vs = 0.f, vt = 0.f;
+    for (int tt = q; tt < S; tt += 4) {
+      vs = fmaf(sVar[u][tt], sWn[tt][c], vs);
+      vt = fmaf(sVar[u][tt], sWn[S + tt][c], vt);
+    }
+    vs += __shfl_xor(vs, 1, 64);
+    vt += __shfl_xor(vt, 1, 64);
+    vs += __shfl_xor(vs, 2, 64);
+    vt += __shfl_xor(vt, 2, 64);
+    if (q == 0 && uc < n * NC) {
+      sV[0][u][c] = vs;
+      sV[1][u][c] = vt;
+    }
+  }
+  __syncthreads();
+  // 4) per tile: LDS image, MFMA, node terms, both directions out
+  float* outp = li < HL ? mx_col_ptr<float>(ae, li, L, H) : nullptr;
+  const int64_t gE0 = g * E0;
+#pragma unroll
+  for (int k = 0; k < CV2_TW; ++k) {
+    const int tile = wave + CV2_WAVES * k;
+    if (tile >= TP) break;  // wave-uniform
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) *reinterpret_cast<u32x2*>(img + loff[j]) = v[k][j];
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NJ; ++s) {
+      if (ABL & 2) break;
+      const float2 a = *reinterpret_cast<const float2*>(img + li * RS + 8 * s + 2 * gq);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wb[s][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wb[s][1], acc, 0, 0, 0);
+    }
+    if (ABL & 1) {
+      if (acc[0] == 12345.f) outp[0] = acc[1];
+    } else if (outp) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = tile * 16 + 4 * gq + r;
+        if (p < P) {
+          const int pp = sPr[p], u = pp & 0xff, w = pp >> 8;
+          outp[(gE0 + p) * H] = acc[r] + sV[0][u][li] + sV[1][w][li];
+          outp[(gE0 + P + p) * H] = acc[r] + sV[0][w][li] + sV[1][u][li];
+        }
+      }
+    }
+  }
+}
+
+template <int NP, int NC>
+__global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void k_edge_bwd_cv2(const float* __restrict__ ea, int64_t B,
+                                                        int n, int S,
+                                                        const uint16_t* __restrict__ canon,
+                                                        LayerCPtrs dae, int L, int H, int hlp,
+                                                        float* __restrict__ partial) {
+  constexpr int NM = 2 * NP;  // M tiles of 16 lags
+  constexpr int PMAX = CV_MAXN * (CV_MAXN - 1) / 2;
+  constexpr int SD = 2 * PMAX * NC, SR = CV2_WAVES * 32 * NP * 16;
+  __shared__ float sVar[CV_MAXN][CV_MAXS + 1];
+  // the graph's d-logits [2][PMAX][NC] ([0] up u -> v, [1] low v -> u); at
+  // the end the waves' accumulators [wave][32·NP lags][16 columns]
+  __shared__ float sBuf[SD > SR ? SD : SR];
+  __shared__ float sDn[2][CV_MAXN][NC];     // per node: Σ over outgoing [0] / incoming [1] edges
+  __shared__ float sVarRes[2 * CV_MAXS][NC];
+  auto sD = [&](int side, int p) __attribute__((always_inline)) { return sBuf + (side * PMAX + p) * NC; };
+  float* sRed = sBuf;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
+  const int li = lane & 15, gq = lane >> 4;
+  const int D = 3 * S, HL = L * H, E0 = n * (n - 1), P = E0 / 2, TP = (P + 15) / 16;
+  const int S2 = S >> 1;
+  const float* inp = li < HL ? mx_col_ptr<const float>(dae, li, L, H) : nullptr;
+  f32x4 acc[NM];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the variance-term outputs this thread owns: o = t + 512·i over [2][S][NC]
+  constexpr int KV = (2 * CV_MAXS * NC + CV2_T - 1) / CV2_T;
+  float av[KV];
+#pragma unroll
+  for (int i = 0; i < KV; ++i) av[i] = 0.f;
+  // lane (li, g): row 4g + q of a tile, lags 32·mm + 2li (+1)
+  const int vo = ((4 * gq) * D + 2 * li) * 4;
+
+  for (int64_t g = blockIdx.x; g < B; g += gridDim.x) {
+    const rsrc_t rg = make_rsrc(ea + g * E0 * D, (uint32_t)(E0 * D) * 4u);
+    const float* ib = inp ? inp + g * E0 * H : nullptr;  // this graph's d-logits, this column
+    u32x2 vv[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = t + CV2_T * i, u = k / S2, c2 = k - u * S2;
+      const int off = u == 0 ? S + 2 * c2 : (u - 1) * D + 2 * S + 2 * c2;
+      vv[i] = __builtin_amdgcn_raw_buffer_load_b64(rg, k < n * S2 ? 4 * off : OOB, 0, 0);
+    }
+    u32x2 pc[4][NP];
+    float du[4], dl[4];
+    auto load = [&](int tile) __attribute__((always_inline)) {
+      const bool ok = tile < TP;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int mm = 0; mm < NP; ++mm)
+          pc[q][mm] = __builtin_amdgcn_raw_buffer_load_b64(
+              rg, (ok && 32 * mm + 2 * li < S) ? vo : OOB, ok ? ((tile * 16 + q) * D + 32 * mm) * 4 : 0,
+              0);
+        const int p = tile * 16 + 4 * gq + q;
+        const bool pv = ok && inp && p < P;
+        du[q] = pv ? ib[p * H] : 0.f;
+        dl[q] = pv ? ib[(P + p) * H] : 0.f;
+      }
+    };
+    __syncthreads();  // the previous graph's sD / sVar / sDn reads
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = t + CV2_T * i, u = k / S2, c2 = k - u * S2;
+      if (k < n * S2) {
+        sVar[u][2 * c2] = __uint_as_float(vv[i][0]);
+        sVar[u][2 * c2 + 1] = __uint_as_float(vv[i][1]);
+      }
+    }
+    load(wave);
+#pragma unroll 1
+    for (int k = 0; k < CV2_TW; ++k) {
+      const int tile = wave + CV2_WAVES * k;
+      if (tile >= TP) break;  // wave-uniform
+      float b[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        b[q] = du[q] + dl[q];
+        const int p = tile * 16 + 4 * gq + q;
+        if (li < NC && p < P) {
+          sD(0, p)[li] = du[q];
+          sD(1, p)[li] = dl[q];
+        }
+      }
+      u32x2 a[4][NP];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int mm = 0; mm < NP; ++mm) a[q][mm] = pc[q][mm];
+      load(tile + CV2_WAVES);  // the next tile in flight (nothing past TP)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int mm = 0; mm < NP; ++mm) {
+          acc[2 * mm] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[q][mm][0]), b[q],
+                                                             acc[2 * mm], 0, 0, 0);
+          acc[2 * mm + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[q][mm][1]),
+                                                                 b[q], acc[2 * mm + 1], 0, 0, 0);
+        }
+    }
+    __syncthreads();  // sD, sVar complete
+    // per-node sums in a fixed order: outgoing [0] and incoming [1] edges
+    for (int k = t; k < 2 * n * NC; k += CV2_T) {
+      const int side = k / (n * NC), uc = k - side * n * NC, u = uc / NC, c = uc - u * NC;
+      float sm = 0.f;
+      for (int w = 0; w < n; ++w) {
+        if (w == u) continue;
+        // u -> w is the up edge of pair (u, w) if u < w, else the low edge of (w, u)
+        const int pw = u < w ? cv2_pair_index(u, w, n) : cv2_pair_index(w, u, n);
+        // side 0 (outgoing): up if u < w; side 1 (incoming): low if u < w
+        sm += sD((side == 0) == (u < w) ? 0 : 1, pw)[c];
+      }
+      sDn[side][u][c] = sm;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < KV; ++i) {
+      const int o = t + CV2_T * i;
+      if (o < 2 * S * NC) {
+        const int side = o / (S * NC), r = o - side * S * NC, tt = r / NC, c = r - tt * NC;
+        float sm = av[i];
+        for (int u = 0; u < n; ++u) sm = fmaf(sVar[u][tt], sDn[side][u][c], sm);
+        av[i] = sm;
+      }
+    }
+  }
+  // the workgroup's partial: covariance rows from the waves' accumulators
+  // (added in wave order), variance rows from the threads' sums
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < NM; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tt = 32 * (m >> 1) + 2 * (4 * gq + r) + (m & 1);
+      sRed[(wave * 32 * NP + tt) * 16 + li] = acc[m][r];
+    }
+#pragma unroll
+  for (int i = 0; i < KV; ++i) {
+    const int o = t + CV2_T * i;
+    if (o < 2 * S * NC) (&sVarRes[0][0])[o] = av[i];
+  }
+  __syncthreads();
+  float* pb = partial + (int64_t)blockIdx.x * D * hlp;
+  for (int o = t; o < D * hlp; o += CV2_T) {
+    const int d = o / hlp, c = o - d * hlp;
+    float v = 0.f;
+    if (c < HL) {
+      if (d < S) {
+        v = sRed[d * 16 + c];
+#pragma unroll
+        for (int w = 1; w < CV2_WAVES; ++w) v += sRed[(w * 32 * NP + d) * 16 + c];
+      } else {
+        v = sVarRes[d - S][c];
+      }
+    }
+    pb[o] = v;
   }
 }
 
@@ -1463,7 +1802,16 @@ extern "C" int sv2n_block_rowmask_checked(const int64_t* edge_index, int64_t num
   return (int)hipGetLastError();
 }
 
-// ---- covariance-layout edge features (k_edge_fwd_cv / k_edge_bwd_cv) ----
+// ---- covariance-layout edge features (k_edge_fwd_cv2 / k_edge_bwd_cv2; odd
+// seq_length: k_edge_fwd_cv / k_edge_bwd_cv) ----
+// SV2N_CV_ROUND4=1: the round-4 kernels for every seq_length (A/B switch)
+static bool cv_round4() {
+  static const bool v = [] {
+    const char* e = std::getenv("SV2N_CV_ROUND4");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 static int cv_check(const float* ea, int64_t B, int n, int S, const uint16_t* canon, int L,
                     int H, int hlp) {
   if (!ea || !canon || B < 0 || L < 1 || L > SV2N_MAX_LAYERS || H < 1) return SV2N_ERR_ARG;
@@ -1484,6 +1832,31 @@ extern "C" int sv2n_edge_logits_fwd_cv(const float* edge_attr, int64_t num_graph
   for (int l = 0; l < num_layers; ++l) {
     if (!ae_layers[l]) return SV2N_ERR_ARG;
     lp.p[l] = ae_layers[l];
+  }
+  if ((seq_length & 1) == 0 && !cv_round4()) {
+    // round 5: one workgroup per graph, MFMA (even seq_length)
+    if (num_graphs > 0x7fffffff) return SV2N_ERR_SHAPE;
+    const int nj = seq_length <= 16 ? 2 : seq_length <= 32 ? 4 : seq_length <= 48 ? 6 : 8;
+    const int nc = (num_layers * heads + 3) / 4;
+#define SV2N_CVF2(NJ, NC)                                                                        \
+  hipLaunchKernelGGL((k_edge_fwd_cv2<NJ, NC>), dim3((unsigned)num_graphs), dim3(CV2_T), 0, stream, \
+                     edge_attr, n, seq_length, canon, wfold, hl_pad, lp, num_layers, heads)
+#define SV2N_CVF2_NC(NJ)                                         \
+  switch (nc) {                                                  \
+    case 1: SV2N_CVF2(NJ, 4); break;                             \
+    case 2: SV2N_CVF2(NJ, 8); break;                             \
+    case 3: SV2N_CVF2(NJ, 12); break;                            \
+    default: SV2N_CVF2(NJ, 16); break;                           \
+  }
+    switch (nj) {
+      case 2: SV2N_CVF2_NC(2) break;
+      case 4: SV2N_CVF2_NC(4) break;
+      case 6: SV2N_CVF2_NC(6) break;
+      default: SV2N_CVF2_NC(8) break;
+    }
+#undef SV2N_CVF2_NC
+#undef SV2N_CVF2
+    return (int)hipGetLastError();
   }
   const int64_t P = (int64_t)n * (n - 1) / 2, nch = (P + CV_FSUB * CV_PCH - 1) / (CV_FSUB * CV_PCH);
   if (num_graphs * nch > 0x7fffffff) return SV2N_ERR_SHAPE;
@@ -1521,6 +1894,28 @@ extern "C" int sv2n_edge_logits_bwd_cv(const float* edge_attr, int64_t num_graph
     lp.p[l] = dae_layers[l];
   }
   const int D = 3 * seq_length, width = D * hl_pad;
+  if ((seq_length & 1) == 0 && !cv_round4()) {
+    // round 5: one workgroup per graph (grid-stride past CV2_BWD_GRID), MFMA
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(num_graphs, CV2_BWD_GRID));
+    const int nc = (num_layers * heads + 3) / 4;
+#define SV2N_CVB2(NP, NC)                                                                          \
+  hipLaunchKernelGGL((k_edge_bwd_cv2<NP, NC>), dim3(grid), dim3(CV2_T), 0, stream, edge_attr,      \
+                     num_graphs, n, seq_length, canon, lp, num_layers, heads, hl_pad, workspace)
+#define SV2N_CVB2_NC(NP)                                         \
+  switch (nc) {                                                  \
+    case 1: SV2N_CVB2(NP, 4); break;                             \
+    case 2: SV2N_CVB2(NP, 8); break;                             \
+    case 3: SV2N_CVB2(NP, 12); break;                            \
+    default: SV2N_CVB2(NP, 16); break;                           \
+  }
+    if (seq_length <= 32) SV2N_CVB2_NC(1)
+    else SV2N_CVB2_NC(2)
+#undef SV2N_CVB2_NC
+#undef SV2N_CVB2
+    hipLaunchKernelGGL(k_reduce_partials, dim3((unsigned)((width + 15) / 16)), dim3(256), 0, stream,
+                       workspace, grid, width, dwfold);
+    return (int)hipGetLastError();
+  }
   const int64_t units = num_graphs * (((int64_t)n * (n - 1) / 2 + CV_PCH - 1) / CV_PCH);
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, CV_BWD_GRID));
 #define SV2N_CVB(NC)                                                                           \

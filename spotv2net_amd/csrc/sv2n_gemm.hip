@@ -90,7 +90,7 @@ __device__ __forceinline__ void wgrad_att_block(int blk, const float* __restrict
                                                 float* __restrict__ g_as, float* __restrict__ g_ad,
                                                 float* __restrict__ s_fold, int nslab = 1) {
   // s_fold: [2][nh][F] (dynamic LDS)
-  const int HC = H * C, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int HC = H * C, t = threadIdx.x, lane = t & 63, wv = wave_id();
   const int o0 = blk * ATT_RB, o1 = min(HC, o0 + ATT_RB);
   const int h0 = o0 / C, nh = (o1 - 1) / C - h0 + 1;
   const rsrc_t rt = make_rsrc(T, (uint32_t)F * (uint32_t)ldt * 4u * (uint32_t)nslab);
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) void k_wgrad_epi_t(
     float* __restrict__ g_bias) {
   __shared__ float s_red[16][17];
   const int HC = H * C;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wv = wave_id();
   const int bx = blockIdx.x;  // att blocks first, then the row blocks, then bias
   if (bx < natt) {
     extern __shared__ float s_dyn[];

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3(const float* __restrict__ A, 
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
   unsigned short* sA = lds;                    // [NP][BM][ROW]
   unsigned short* sB = lds + NP * BM * ROW;    // [NP][BN][ROW]
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, lg = lane >> 4;
   const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
 
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3_t(const float* __restrict__ A
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
   unsigned short* sA = lds;                    // [NP][BM][ROW]
   unsigned short* sB = lds + NP * BM * ROW;    // [NP][BN][ROW]
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, lg = lane >> 4;
   const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
   const int64_t kbeg = (int64_t)blockIdx.z * kslice, kend = min(K, kbeg + kslice);
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3b(const float* __restrict__ A,
   constexpr int TH = Cfg::THREADS, BM = Cfg::BM, BN = Cfg::BN, ROW = Cfg::ROW, BV = Cfg::BV;
   constexpr int STAGE = Cfg::STAGE, BC = BK / 8, KS = BK / 32;
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, lg = lane >> 4;
   // XCD-grouped block order: id = q*8*nn + n*8 + r  ->  row block q*8 + r, column block n
   const int id = blockIdx.x;
@@ -637,7 +637,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3c(const float* __restrict__ A,
 #ifdef SV2N_GEMM_CLOCK
   const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, lg = lane >> 4;
   const int id = blockIdx.x;
   const int q = id / (8 * nn), rem = id - q * 8 * nn;
@@ -816,7 +816,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
   static_assert(BV + 1 < NT, "interleave needs enough column tiles");
   static_assert(AP >= 2 && AP <= 3, "A register sets");
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, lg = lane >> 4;
   const int id = blockIdx.x;
   const int q = id / (8 * nn), rem = id - q * 8 * nn;

@@ -29,7 +29,7 @@ static __global__ __attribute__((unused)) __launch_bounds__(256, 2) void k_gemm_
                                                          int64_t ldc, int64_t M, int64_t N,
                                                          int64_t K, int nm, int nn) {
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, lg = lane >> 4;
   const int wm = wave >> 1, wn = wave & 1;
   // XCD-grouped order: id = q*8*nn + nb*8 + r -> row block q*8 + r, column block nb

@@ -87,7 +87,7 @@ __global__ __launch_bounds__(512) void k_gemm_bw(const void* __restrict__ Av, in
   constexpr int PA = Cfg::PA, PB = Cfg::PB, RA = Cfg::RA, RB = Cfg::RB;
   constexpr int EA = AF ? 4 : 2, EB = BF ? 4 : 2;  // bytes per element in HBM
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, lg = lane >> 4;
   const int wm = wave / Cfg::WN, wn = wave - wm * Cfg::WN;
   // XCD-grouped order: id = q*8*nn + nb*8 + r -> row tile q*8 + r, column tile nb

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_f32(
     bx = tile - by * gridDim.x;
     if (bz >= nz) return;
   }
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int64_t m0 = (int64_t)bx * Cfg::BM, n0 = (int64_t)by * Cfg::BN;
   const int64_t kb = (int64_t)bz * kslice;
   const int64_t ke = min(K, kb + kslice);

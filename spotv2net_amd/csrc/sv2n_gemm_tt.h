@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void k_gemm_tt(const float* __restrict__ A, in
   constexpr int MT = Cfg::MT, NT = Cfg::NT, STAGE = Cfg::STAGE;
   constexpr int PA = Cfg::PLANE_A, PB = Cfg::PLANE_B;
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int wm = wave & 1, wn = wave >> 1;
   const int li = lane & 15, lg = lane >> 4;
   const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(512) void k_gemm_tt3w(const float* __restrict__ A, 
   const int by = tile / gridDim.x, bx = tile - by * gridDim.x;
   if (bz >= nz) return;
 
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, lg = lane >> 4;
   const int64_t m0 = (int64_t)bx * BM, n0 = (int64_t)by * BN;
   const int64_t kbeg = (int64_t)bz * kslice, kend = min(K, kbeg + kslice);
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(512) void k_gemm_tt3y(const float* __restrict__ A, 
   const int by = tile / gridDim.x, bx = tile - by * gridDim.x;
   if (bz >= nz) return;
 
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, lg = lane >> 4;
   const int64_t m0 = (int64_t)bx * Cfg::BM, n0 = (int64_t)by * BN;
   const int64_t kbeg = (int64_t)bz * kslice, kend = min(K, kbeg + kslice);

@@ -481,7 +481,7 @@ __global__ __launch_bounds__(256) void k_head_mse_train_w(
   constexpr int RB = KC >= 8 ? 4 : (KC >= 4 ? 8 : 16);  // rows in flight per wave
   extern __shared__ __attribute__((aligned(16))) float s_w4[];  // [4][stride] wave partials
   __shared__ int s_flag;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int CP = C + 1, stride = OUT * CP + 1;  // [o][c], [o][C] bias, [OUT·CP] loss
   float w[OUT][KC], bo[OUT], gw[OUT][KC], gbs[OUT];
 #pragma unroll

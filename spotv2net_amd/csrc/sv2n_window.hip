@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void k_window_rows(
   if ((S & 1) == 0 && RW <= 2 * 64 && (((uintptr_t)up) & 7) == 0 && (((uintptr_t)lo) & 7) == 0) {
     // one wave per edge row, two adjacent columns per lane (8-B stores; S even:
     // both columns have the same kind), (kind, t) decoded once
-    const int lane = t & 63, wv = t >> 6;
+    const int lane = t & 63, wv = wave_id();
     const int q = 2 * lane, kind = q / S, tq = q - kind * S;
     const bool qv = q < RW;
     for (int r = wv; r < m; r += 4) {
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void k_window_rows(
   if (RW <= 4 * 64) {
     // one wave per edge row, a lane's columns fixed: (kind, t) decoded once
     // (the flat element loop divided twice per element)
-    const int lane = t & 63, wv = t >> 6;
+    const int lane = t & 63, wv = wave_id();
     int kind[4], tq[4];
 #pragma unroll
     for (int qi = 0; qi < 4; ++qi) {

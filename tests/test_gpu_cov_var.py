@@ -21,7 +21,11 @@ def _wfold(D, hp, dev, seed=0):
 
 
 @pytest.mark.parametrize("B,S,n,L,H", [(64, 42, 30, 2, 4), (5, 2, 30, 1, 6), (3, 7, 9, 3, 5),
-                                       (2, 40, 32, 2, 8)])
+                                       (2, 40, 32, 2, 8),
+                                       # past the backward's 512-graph grid; widest lags,
+                                       # two-node graphs, odd n, 14 columns
+                                       (600, 42, 30, 2, 4), (3, 64, 30, 3, 5), (6, 8, 2, 1, 3),
+                                       (4, 30, 17, 1, 2), (2, 58, 24, 2, 7)])
 def test_cov_var_logits_match_generic(dev, B, S, n, L, H):
     from spotv2net_amd import synthetic_batch
     from spotv2net_amd.layout import canonical_table, cov_var_seq_length

@@ -1,0 +1,26 @@
+"""Reports kernels whose buffer loads / stores sit in waterfall loops (a
+resource descriptor or soffset the compiler cannot prove wave-uniform is
+made uniform lane by lane: v_readfirstlane + s_and_saveexec around the
+memory instruction, one loop per instruction).  Usage:
+    python tools/isa_waterfall.py spotv2net_amd/csrc/*.hip"""
+import re
+import subprocess
+import sys
+
+for src in sys.argv[1:]:
+    asm = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
+                          "-Iinclude", "--cuda-device-only", "-S", src, "-o", "/dev/stdout"],
+                         capture_output=True, text=True).stdout
+    for m in re.finditer(r"^(_Z\S+):\s*;?.*\n", asm, re.M):
+        end = asm.find(".Lfunc_end", m.end())
+        body = asm[m.end():end]
+        wf = 0
+        for h in re.finditer(r"; =>This Inner Loop Header", body):
+            seg = body[h.start():body.find("s_cbranch_execnz", h.start()) + 1].split("\n")[1:]
+            # the waterfall shape: readfirstlanes first, then a compare, the
+            # exec mask, one buffer instruction, the exec flip, the back edge
+            wf += bool(len(seg) < 24 and seg and "v_readfirstlane" in seg[0]
+                   and any("s_and_saveexec" in x for x in seg)
+                   and any("buffer_" in x for x in seg))
+        if wf:
+            print(f"{src.split('/')[-1]}: {m.group(1)[:100]} waterfall buffer ops: {wf}")
