@@ -306,12 +306,15 @@ constexpr int OOB = 0x7ffffff0;  // byte offset past any buffer (< 2^31)
 // a waterfall loop around every buffer instruction that uses the descriptor:
 // the base and size go through v_readfirstlane here.  Never build a descriptor
 // from a per-lane value.
-// (inline asm: the compiler folds __builtin_amdgcn_readfirstlane of a value it
-// knows to be uniform, even one it keeps in a VGPR)
+// The compiler folds __builtin_amdgcn_readfirstlane of a value it knows to be
+// uniform, even one it keeps in a VGPR: an empty asm makes the value opaque
+// first.  (The readfirstlane itself stays the builtin, so the hazard
+// recognizer sees it and keeps the wait states between a VALU write of an
+// SGPR and a memory instruction reading that SGPR; a readfirstlane written as
+// inline asm does not get them.)
 __device__ __forceinline__ uint32_t to_sgpr(uint32_t v) {
-  uint32_t r;
-  asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(r) : "v"(v));
-  return r;
+  asm volatile("" : "+v"(v));
+  return __builtin_amdgcn_readfirstlane(v);
 }
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   const uint64_t b = reinterpret_cast<uint64_t>(base);

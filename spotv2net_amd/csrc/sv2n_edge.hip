@@ -1262,28 +1262,35 @@ __global__ __launch_bounds__(CV2_T) void k_edge_fwd_cv2(const float* __restrict_
   }
 }
 
+// SPLIT (at most 8 logit columns): the B operand's 16 columns carry d_up of
+// column c in lane column c and d_low in lane column 8 + c, so one MFMA per
+// M tile serves both directions and each lane loads one d-logit per pair
+// (the halves are added at the end); otherwise B = d_up + d_low.
 template <int NP, int NC>
-__global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void k_edge_bwd_cv2(const float* __restrict__ ea, int64_t B,
-                                                        int n, int S,
-                                                        const uint16_t* __restrict__ canon,
-                                                        LayerCPtrs dae, int L, int H, int hlp,
-                                                        float* __restrict__ partial) {
+__global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void k_edge_bwd_cv2(
+    const float* __restrict__ ea, int64_t B, int n, int S, const uint16_t* __restrict__ canon,
+    LayerCPtrs dae, int L, int H, int hlp, float* __restrict__ partial) {
+  constexpr bool SPLIT = NC <= 8;
   constexpr int NM = 2 * NP;  // M tiles of 16 lags
   constexpr int PMAX = CV_MAXN * (CV_MAXN - 1) / 2;
-  constexpr int SD = 2 * PMAX * NC, SR = CV2_WAVES * 32 * NP * 16;
+  constexpr int SR = CV2_WAVES * 32 * NP * 16, SN = CV2_WAVES * 2 * CV_MAXN * NC;
   __shared__ float sVar[CV_MAXN][CV_MAXS + 1];
-  // the graph's d-logits [2][PMAX][NC] ([0] up u -> v, [1] low v -> u); at
-  // the end the waves' accumulators [wave][32·NP lags][16 columns]
-  __shared__ float sBuf[SD > SR ? SD : SR];
+  // per graph: each wave's node sums [wave][out, in][node][column] (a wave
+  // adds only into its own slice, in program order: deterministic); at the
+  // end: the waves' lag accumulators [wave][32·NP lags][16 columns]
+  __shared__ float sBuf[SR > SN ? SR : SN];
   __shared__ float sDn[2][CV_MAXN][NC];     // per node: Σ over outgoing [0] / incoming [1] edges
   __shared__ float sVarRes[2 * CV_MAXS][NC];
-  auto sD = [&](int side, int p) __attribute__((always_inline)) { return sBuf + (side * PMAX + p) * NC; };
+  __shared__ int sPr[PMAX];
   float* sRed = sBuf;
   const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, gq = lane >> 4;
   const int D = 3 * S, HL = L * H, E0 = n * (n - 1), P = E0 / 2, TP = (P + 15) / 16;
   const int S2 = S >> 1;
-  const float* inp = li < HL ? mx_col_ptr<const float>(dae, li, L, H) : nullptr;
+  // SPLIT: lane column li reads column li & 7 of the up (li < 8) or low rows
+  const int col = SPLIT ? (li & 7) : li, low = SPLIT ? (li >> 3) : 0;
+  const float* inp = col < HL ? mx_col_ptr<const float>(dae, col, L, H) : nullptr;
+  if (t < P) sPr[t] = canon[t];  // read after the first graph's barrier
   f32x4 acc[NM];
 #pragma unroll
   for (int m = 0; m < NM; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1294,6 +1301,8 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
   for (int i = 0; i < KV; ++i) av[i] = 0.f;
   // lane (li, g): row 4g + q of a tile, lags 32·mm + 2li (+1)
   const int vo = ((4 * gq) * D + 2 * li) * 4;
+  constexpr int ND = SPLIT ? 1 : 2;  // d-logit loads per pair and lane
+  float* sNw = sBuf + wave * 2 * CV_MAXN * NC;
 
   for (int64_t g = blockIdx.x; g < B; g += gridDim.x) {
     const rsrc_t rg = make_rsrc(ea + g * E0 * D, (uint32_t)(E0 * D) * 4u);
@@ -1306,7 +1315,7 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
       vv[i] = __builtin_amdgcn_raw_buffer_load_b64(rg, k < n * S2 ? 4 * off : OOB, 0, 0);
     }
     u32x2 pc[4][NP];
-    float du[4], dl[4];
+    float dd[4][ND];
     auto load = [&](int tile) __attribute__((always_inline)) {
       const bool ok = tile < TP;
 #pragma unroll
@@ -1314,15 +1323,15 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
 #pragma unroll
         for (int mm = 0; mm < NP; ++mm)
           pc[q][mm] = __builtin_amdgcn_raw_buffer_load_b64(
-              rg, (ok && 32 * mm + 2 * li < S) ? vo : OOB, ok ? ((tile * 16 + q) * D + 32 * mm) * 4 : 0,
-              0);
+              rg, (ok && 32 * mm + 2 * li < S) ? vo : OOB,
+              ok ? ((tile * 16 + q) * D + 32 * mm) * 4 : 0, 0);
         const int p = tile * 16 + 4 * gq + q;
-        const bool pv = ok && inp && p < P;
-        du[q] = pv ? ib[p * H] : 0.f;
-        dl[q] = pv ? ib[(P + p) * H] : 0.f;
+        const bool pv = ok && ib && p < P;
+#pragma unroll
+        for (int s = 0; s < ND; ++s) dd[q][s] = pv ? ib[((low | s) ? P + p : p) * H] : 0.f;
       }
     };
-    __syncthreads();  // the previous graph's sD / sVar / sDn reads
+    __syncthreads();  // the previous graph's sVar / sBuf / sDn reads (first graph: sPr)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int k = t + CV2_T * i, u = k / S2, c2 = k - u * S2;
@@ -1331,49 +1340,52 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
         sVar[u][2 * c2 + 1] = __uint_as_float(vv[i][1]);
       }
     }
+    for (int k = lane; k < 2 * CV_MAXN * NC; k += 64) sNw[k] = 0.f;
     load(wave);
 #pragma unroll 1
     for (int k = 0; k < CV2_TW; ++k) {
       const int tile = wave + CV2_WAVES * k;
       if (tile >= TP) break;  // wave-uniform
-      float b[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        b[q] = du[q] + dl[q];
-        const int p = tile * 16 + 4 * gq + q;
-        if (li < NC && p < P) {
-          sD(0, p)[li] = du[q];
-          sD(1, p)[li] = dl[q];
-        }
-      }
+      float x[4][ND];
       u32x2 a[4][NP];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int s = 0; s < ND; ++s) x[q][s] = dd[q][s];
 #pragma unroll
         for (int mm = 0; mm < NP; ++mm) a[q][mm] = pc[q][mm];
+      }
       load(tile + CV2_WAVES);  // the next tile in flight (nothing past TP)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q) {
+        const float b = SPLIT ? x[q][0] : x[q][0] + x[q][ND - 1];
 #pragma unroll
         for (int mm = 0; mm < NP; ++mm) {
-          acc[2 * mm] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[q][mm][0]), b[q],
+          acc[2 * mm] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[q][mm][0]), b,
                                                              acc[2 * mm], 0, 0, 0);
-          acc[2 * mm + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[q][mm][1]),
-                                                                 b[q], acc[2 * mm + 1], 0, 0, 0);
+          acc[2 * mm + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[q][mm][1]), b,
+                                                                 acc[2 * mm + 1], 0, 0, 0);
         }
+        // node sums: edge u -> v (up) counts as outgoing of u and incoming of
+        // v, v -> u (low) the other way round
+        const int p = tile * 16 + 4 * gq + q;
+        if (p < P && col < NC) {
+          const int pr = sPr[p], u = pr & 0xff, v = pr >> 8;
+#pragma unroll
+          for (int s = 0; s < ND; ++s) {
+            const bool lw = low | s;
+            atomicAdd(&sNw[(0 * CV_MAXN + (lw ? v : u)) * NC + col], x[q][s]);
+            atomicAdd(&sNw[(1 * CV_MAXN + (lw ? u : v)) * NC + col], x[q][s]);
+          }
+        }
+      }
     }
-    __syncthreads();  // sD, sVar complete
-    // per-node sums in a fixed order: outgoing [0] and incoming [1] edges
+    __syncthreads();
     for (int k = t; k < 2 * n * NC; k += CV2_T) {
       const int side = k / (n * NC), uc = k - side * n * NC, u = uc / NC, c = uc - u * NC;
-      float sm = 0.f;
-      for (int w = 0; w < n; ++w) {
-        if (w == u) continue;
-        // u -> w is the up edge of pair (u, w) if u < w, else the low edge of (w, u)
-        const int pw = u < w ? cv2_pair_index(u, w, n) : cv2_pair_index(w, u, n);
-        // side 0 (outgoing): up if u < w; side 1 (incoming): low if u < w
-        sm += sD((side == 0) == (u < w) ? 0 : 1, pw)[c];
-      }
+      float sm = sBuf[(side * CV_MAXN + u) * NC + c];
+#pragma unroll
+      for (int w = 1; w < CV2_WAVES; ++w) sm += sBuf[((w * 2 + side) * CV_MAXN + u) * NC + c];
       sDn[side][u][c] = sm;
     }
     __syncthreads();
@@ -1413,6 +1425,12 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
         v = sRed[d * 16 + c];
 #pragma unroll
         for (int w = 1; w < CV2_WAVES; ++w) v += sRed[(w * 32 * NP + d) * 16 + c];
+        if constexpr (SPLIT) {  // + the low half (lane columns 8 + c)
+          float vl = sRed[d * 16 + 8 + c];
+#pragma unroll
+          for (int w = 1; w < CV2_WAVES; ++w) vl += sRed[(w * 32 * NP + d) * 16 + 8 + c];
+          v += vl;
+        }
       } else {
         v = sVarRes[d - S][c];
       }

@@ -1,7 +1,11 @@
-"""Reports kernels whose buffer loads / stores sit in waterfall loops (a
+"""(1) Reports kernels whose buffer loads / stores sit in waterfall loops (a
 resource descriptor or soffset the compiler cannot prove wave-uniform is
 made uniform lane by lane: v_readfirstlane + s_and_saveexec around the
-memory instruction, one loop per instruction).  Usage:
+memory instruction, one loop per instruction).  (2) Reports a v_readfirstlane
+writing an SGPR that a buffer / global instruction reads within 5 wait states
+(the VALU-writes-SGPR -> VMEM-reads-it hazard; an inline-asm readfirstlane does
+not get the compiler's wait states, and round 5 faulted a GPU on exactly
+that: a stale buffer descriptor).  Usage:
     python tools/isa_waterfall.py spotv2net_amd/csrc/*.hip"""
 import re
 import subprocess
@@ -24,3 +28,20 @@ for src in sys.argv[1:]:
                    and any("buffer_" in x for x in seg))
         if wf:
             print(f"{src.split('/')[-1]}: {m.group(1)[:100]} waterfall buffer ops: {wf}")
+        lines = body.split("\n")
+        for k, ln in enumerate(lines):
+            r = re.search(r"v_readfirstlane_b32 s(\d+), v", ln)
+            if not r:
+                continue
+            reg, ws = int(r.group(1)), 0
+            for l2 in lines[k + 1:k + 30]:
+                tt = l2.strip()
+                if not tt or tt[0] in ";.":
+                    continue
+                nop = re.match(r"s_nop (\d+)", tt)
+                ws += int(nop.group(1)) + 1 if nop else 1
+                if ws > 5:
+                    break
+                if re.search(r"(buffer_|global_)", tt) and any(
+                        int(a) <= reg <= int(b) for a, b in re.findall(r"s\[(\d+):(\d+)\]", tt)):
+                    print(f"{src.split('/')[-1]}: {m.group(1)[:100]} HAZARD: {ln.strip()} -> {tt}")
