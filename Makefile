@@ -9,6 +9,14 @@ LIB ?= spotv2net_amd/libsv2n.so
 ifeq ($(STAMPS),1)
 HIPFLAGS += -DSV2N_STAMPS   # diagnostic phase stamps (tools/stamps.py)
 endif
+# diagnostic bound checks (SV2N_CHK, sv2n_check_hits): make CHECK=1 builds
+# build_check/ -> spotv2net_amd/libsv2n_check.so; tests load it with
+# SV2N_LIB=spotv2net_amd/libsv2n_check.so (tools/r5_check.sh)
+ifeq ($(CHECK),1)
+HIPFLAGS += -DSV2N_CHECK
+BUILD = build_check
+LIB = spotv2net_amd/libsv2n_check.so
+endif
 SRC := $(wildcard spotv2net_amd/csrc/*.hip)
 OBJ := $(patsubst spotv2net_amd/csrc/%.hip,$(BUILD)/%.o,$(SRC))
 

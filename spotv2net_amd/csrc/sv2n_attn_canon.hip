@@ -114,6 +114,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
   int64_t g;
   int split;
   if (!graph_split(B, S, g, split)) return;
+  SV2N_CHK(301, g, B);  // every other access of the graph goes through its buffer descriptors
   const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int slot = 4 * split + wave, NS = 4 * S;
   const int l32 = lane & 31, half = lane >> 5;
@@ -402,6 +403,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       float sacc = 0.f;
       for (int row = 0; row < n; ++row)
         sacc = fmaf(sD[row], sY[row * OC1 + oc] * mfac(row, oc), sacc);
+      SV2N_CHK(302, (int64_t)g * (OC + 2) + oc, B * (OC + 2));
       pg[oc] = sacc;
     }
     if (t == THREADS - 1) {
@@ -410,6 +412,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
         sd += sD[row];
         sl += sL[row];
       }
+      SV2N_CHK(303, (int64_t)g * (OC + 2) + OC + 1, B * (OC + 2));
       pg[OC] = sd;
       pg[OC + 1] = sl;
     }
@@ -636,6 +639,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   int64_t g;
   int split;
   if (!graph_split(B, S, g, split)) return;
+  SV2N_CHK(301, g, B);  // every other access of the graph goes through its buffer descriptors
   const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int l32 = lane & 31, half = lane >> 5;
   const int HC = H * C, OC = CONCAT ? HC : C;
@@ -1184,3 +1188,5 @@ void attn_canon_fwd(int64_t B, hipStream_t st, const float* xs, int ldx, const f
 }
 
 }  // namespace sv2n
+
+SV2N_CHK_EXPORT(canon)

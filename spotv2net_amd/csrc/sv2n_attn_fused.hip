@@ -281,9 +281,11 @@ __global__ __launch_bounds__(WT, (EIDM || KEEP) ? 2 : 4) void k_fattn_fwd(
   const int CQ = (HC + H + 3) >> 2;  // 16-B chunks of [xs | a_src] per row
   const float slope2 = slope * L2E;
   const bool hv = hh < H;
+  const int64_t Nrows = (int64_t)gridDim.x / NT * n;  // bound checks (SV2N_CHK) only
 
   if (t < MH * dpad<D>()) {
     const int h = t / dpad<D>(), d = t - h * dpad<D>();
+    if (h < H && d < D) SV2N_CHK(201, d * hl_pad + col0 + h, D * hl_pad);
     sWT[t] = (h < H && d < D) ? wf[d * hl_pad + col0 + h] : 0.f;
   }
   if (eidm && t < 2 * FT) sPres[t >> 5][t & 31] = 0u;
@@ -315,6 +317,7 @@ __global__ __launch_bounds__(WT, (EIDM || KEEP) ? 2 : 4) void k_fattn_fwd(
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     const int i = i0 + 16 * rt + li;
+    if (hv && i < n) SV2N_CHK(202, (row0 + i) * ldx + HC + H + hh, Nrows * ldx);
     ad[rt] = (hv && i < n) ? xs[(row0 + i) * ldx + HC + H + hh] : 0.f;
     mrow[rt] = -INFINITY;
     lrow[rt] = 0.f;  // this lane's share of the row sum
@@ -341,6 +344,7 @@ __global__ __launch_bounds__(WT, (EIDM || KEEP) ? 2 : 4) void k_fattn_fwd(
       int cid = -1;
       int64_t gid = -1;
       if constexpr (eidm) {
+        if (i < n && j < n && i != j) SV2N_CHK(203, (row0 + i) * n + j, Nrows * n);
         gid = (i < n && j < n && i != j) ? eid[(row0 + i) * n + j] : -1;
       } else {
         cid = canon_id(i, j, n);
@@ -386,6 +390,7 @@ __global__ __launch_bounds__(WT, (EIDM || KEEP) ? 2 : 4) void k_fattn_fwd(
         for (int h = 0; h < MH; ++h) dst[h * FHS] = lg[k][h];
         if constexpr (eidm) {
           const int i = i0 + il, j = j0 + jl;
+          if (i < n && j < n && i != j) SV2N_CHK(204, (row0 + i) * n + j, Nrows * n);
           const bool pres = i < n && j < n && i != j && eid[(row0 + i) * n + j] >= 0;
           if (pres) atomicOr(&sPres[par][il], 1u << jl);
         }
@@ -461,6 +466,7 @@ __global__ __launch_bounds__(WT, (EIDM || KEEP) ? 2 : 4) void k_fattn_fwd(
           pk[k] = p;
           if constexpr (KEEP) {
             const int j = j0 + 4 * lk + (k & 3) + 16 * (k >> 2);
+            if (i < n && j < n) SV2N_CHK(205, ((g * H + hh) * (int64_t)n + i) * n + j, Nrows * H * n);
             pk[k] = (i < n && j < n && keep[((g * H + hh) * (int64_t)n + i) * n + j]) ?
                         p * keep_scale : 0.f;
           }
@@ -498,6 +504,7 @@ __global__ __launch_bounds__(WT, (EIDM || KEEP) ? 2 : 4) void k_fattn_fwd(
       const float l = lk_sum(lrow[rt]);
       const float es = lk_sum(esum[rt]);
       const float cn = eidm ? lk_sum(cnt[rt]) : (float)(n - 1);
+      if (i < n) SV2N_CHK(206, (row0 + i) * ldx + HC + hh, Nrows * ldx);
       const float as_self = i < n ? xs[(row0 + i) * ldx + HC + hh] : 0.f;
       const float loopv = cn > 0.f ? es / cn : 0.f;
       const float vs = as_self + ad[rt] + loopv;
@@ -509,6 +516,8 @@ __global__ __launch_bounds__(WT, (EIDM || KEEP) ? 2 : 4) void k_fattn_fwd(
       const float lt = l * al + ps;
       const float inv = 1.f / (lt + 1e-16f);
       float pks = ps;
+      if constexpr (KEEP)
+        if (i < n) SV2N_CHK(207, ((g * H + hh) * (int64_t)n + i) * n + i, Nrows * H * n);
       if constexpr (KEEP) pks = (i < n && keep[((g * H + hh) * (int64_t)n + i) * n + i]) ?
                                     ps * keep_scale : 0.f;
       if (lk == 0) {
@@ -538,6 +547,8 @@ __global__ __launch_bounds__(WT, (EIDM || KEEP) ? 2 : 4) void k_fattn_fwd(
         if (i < n && c < C) {
           const int q = hh * FT + il;
           const int64_t row = row0 + i;
+          SV2N_CHK(208, row * ldx + hh * C + c, Nrows * ldx);
+          SV2N_CHK(209, row * HC + hh * C + c, Nrows * HC);
           const float xv1 = xs[row * ldx + hh * C + c];
           const float out = fmaf(av[r], sAl[q], sPs[q] * xv1) * sInv[q];
           if (agg) agg[row * HC + hh * C + c] = out;
@@ -559,6 +570,7 @@ __global__ __launch_bounds__(WT, (EIDM || KEEP) ? 2 : 4) void k_fattn_fwd(
       if (i < n) {
         float s = 0.f;
         for (int h = 0; h < H; ++h) s += sOut[il * HC + h * C + c];
+        SV2N_CHK(210, (row0 + i) * C + c, Nrows * C);
         y[(row0 + i) * C + c] = act_fwd_rt(act, s * invH + (bias ? bias[c] : 0.f));
       }
     }
@@ -598,6 +610,8 @@ __global__ __launch_bounds__(PT) void k_fattn_bprep(
     const int i = i0 + rh + 2 * q;
     const bool ok = colv && i < n;
     const int64_t row = row0 + (ok ? i : 0);
+    if (ok) SV2N_CHK(211, row * ldx + hc, (int64_t)gridDim.x / NT * n * ldx);
+    if (ok) SV2N_CHK(212, row * HC + hc, (int64_t)gridDim.x / NT * n * HC);
     vdy[q] = ok ? dy[row * OC + oc] : 0.f;
     vy[q] = ok ? y[row * OC + oc] : 0.f;
     vag[q] = ok ? agg[row * HC + hc] : 0.f;
@@ -610,6 +624,7 @@ __global__ __launch_bounds__(PT) void k_fattn_bprep(
     const bool ok = colv && i < n;
     const float dz = act_bwd_rt(act, vdy[q], vy[q]);
     const float d = dz * oscale;
+    if (ok) SV2N_CHK(213, (row0 + i) * HC + hc, (int64_t)gridDim.x / NT * n * HC);
     if (ok) dout[(row0 + i) * HC + hc] = d;
     sRt[il * 128 + hc] = ok ? d * vag[q] : 0.f;
     sDp[il * 128 + hc] = ok ? d * vx[q] : 0.f;
@@ -739,6 +754,7 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
     sjl = along_i ? (t >> 4) : (t & 31);
     const int i = i0 + sil, j = j0 + sjl;
     if constexpr (EIDM) {
+      if (i < n && j < n && i != j) SV2N_CHK(214, (row0 + i) * n + j, Ntot * n);
       const int64_t gid = (i < n && j < n && i != j) ? eid[(row0 + i) * n + j] : -1;
       presn = gid >= 0;
       const float* p = ea + (presn ? gid : 0) * D;
@@ -872,6 +888,7 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
           float dP = r == 0 ? pa.x : (r == 1 ? pa.y : (r == 2 ? pa.z : pa.w));
           float pk = p;
           if constexpr (KEEP) {
+            if (valid) SV2N_CHK(215, ((g * H + hh) * (int64_t)n + i) * n + j, Ntot * H * n);
             const bool kp = valid && keep[((g * H + hh) * (int64_t)n + i) * n + j] != 0;
             pk = kp ? p * keep_scale : 0.f;
             dP = kp ? dP * keep_scale : 0.f;
@@ -893,6 +910,8 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
         }
         // d a_dst partial of this source tile: the row sum over the 16 lanes li
         const float s = row16_sum(rowacc);
+        if (li == 0 && i < n)
+          SV2N_CHK(216, ((int64_t)js * Ntot + row0 + i) * H + hh, (int64_t)NS * Ntot * H);
         if (li == 0 && i < n) adst_row[__mul24(i, H)] = s;
       }
     };
@@ -919,6 +938,8 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
       const int j = j0 + 16 * jt + li;
       if (lk == 0 && j < n) {
         const int64_t row = row0 + j;
+        SV2N_CHK(217, row * ldx + HC + hh, Ntot * ldx);
+        SV2N_CHK(218, row * 4 * H + H + hh, Ntot * 4 * H);
         dxs[row * ldx + HC + hh] = s + rs[row * 4 * H + H + hh];
       }
     }
@@ -931,6 +952,8 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
         const int j = j0 + 16 * jt + 4 * lk + r, c = li;
         if (j < n && c < C) {
           const int64_t row = row0 + j;
+          SV2N_CHK(219, row * ldx + hh * C + c, Ntot * ldx);
+          SV2N_CHK(220, row * HC + hh * C + c, Ntot * HC);
           dxs[row * ldx + hh * C + c] =
               fmaf(rs[row * 4 * H + 2 * H + hh], dout[row * HC + hh * C + c], dv[r]);
         }
@@ -941,6 +964,7 @@ __global__ __launch_bounds__(WT, 4) void k_fattn_bwd2(
     const int padc = ldx - HC - 2 * H;
     for (int idx = t; idx < BS * padc; idx += WT) {
       const int jl = idx / padc, j = j0 + jl;
+      if (j < n) SV2N_CHK(221, (row0 + j) * ldx + HC + 2 * H + (idx - jl * padc), Ntot * ldx);
       if (j < n) dxs[(row0 + j) * ldx + HC + 2 * H + (idx - jl * padc)] = 0.f;
     }
   }
@@ -975,6 +999,8 @@ __global__ __launch_bounds__(PT) void k_fattn_bfinish(
       const int64_t i = idx / H;
       const int h = (int)(idx - i * H);
       float s = 0.f;
+      SV2N_CHK(222, ((NS - 1) * N + i) * H + h, (int64_t)NS * N * H);
+      SV2N_CHK(223, i * ldx + HC + H + h, N * ldx);
       for (int q = 0; q < NS; ++q) s += adst_part[(q * N + i) * H + h];
       dxs[i * ldx + HC + H + h] = s + rs[i * 4 * H + H + h];
     }
@@ -998,6 +1024,8 @@ __global__ __launch_bounds__(PT) void k_fattn_bfinish(
 
 }  // namespace fused
 }  // namespace sv2n
+
+SV2N_CHK_EXPORT(fused)
 
 // ============================ C-ABI ========================================
 using namespace sv2n::fused;

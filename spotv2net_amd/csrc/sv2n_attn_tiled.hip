@@ -122,8 +122,9 @@ __device__ __forceinline__ int canon_logit_id(int upb, int i, int j, int n) {
 // past n (the padding rows of a graph's last target block, which for the
 // last graph lie past the end of the map) reads element 0 instead.
 __device__ __forceinline__ int eid_logit_id(const int32_t* __restrict__ eid, int64_t erow, int i,
-                                            int j, int n) {
+                                            int j, int n, int64_t ext = 0) {
   const bool ok = i < n && j < n && j != i;
+  if (ok) SV2N_CHK(101, erow + j, ext);  // ext: N·n, the map's entries
   const int e = eid[ok ? erow + j : 0];
   return ok ? e : -1;
 }
@@ -138,11 +139,12 @@ struct RowIn {
 // plane (edge-id map: erow = (g*n + i)*n).
 __device__ __forceinline__ void load_row(RowIn& R, rsrc_t rae, rsrc_t rxs, const LaneConst& K,
                                          const int32_t* __restrict__ eid, int64_t erow, int i,
-                                         int n, int U, int q, int adoff, int ldx) {
+                                         int n, int U, int q, int adoff, int ldx,
+                                         int64_t ext = 0) {
   int id[16];
   if (eid) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) id[k] = eid_logit_id(eid, erow, i, src_of(q, k), n);
+    for (int k = 0; k < 16; ++k) id[k] = eid_logit_id(eid, erow, i, src_of(q, k), n, ext);
   } else {
     const int upb = U + tri_off(n, i) - i - 1;
 #pragma unroll
@@ -172,7 +174,7 @@ struct RowSoft {
 __device__ __forceinline__ void row_softmax(RowSoft& S, float (&e)[16], const LaneConst& K,
                                             float ad, int i, int n, int q, bool general,
                                             const uint32_t* __restrict__ rowmask, int64_t grow,
-                                            bool has_ae, float slope) {
+                                            bool has_ae, float slope, int64_t nrows = 0) {
   const int kd = ((i >> 2) & 15) == q ? 4 * (i >> 6) + (i & 3) : -1;
   S.kd = kd;
   float esum = 0.f;
@@ -184,6 +186,7 @@ __device__ __forceinline__ void row_softmax(RowSoft& S, float (&e)[16], const La
     for (int k = 0; k < 16; ++k) {
       const int j = src_of(q, k);
       const bool in = i < n && j < n && j != i;
+      if (rowmask && in) SV2N_CHK(102, grow * W + (j >> 5), nrows * W);
       // rows past n (last graph: past the end of the mask) read word 0
       const uint32_t w = rowmask ? rowmask[in ? grow * W + (j >> 5) : 0] : ~0u;
       pres |= ((in && ((w >> (j & 31)) & 1u)) ? 1u : 0u) << k;
@@ -233,12 +236,13 @@ __device__ __forceinline__ void row_softmax(RowSoft& S, float (&e)[16], const La
 
 // keep[((g*H+h)*n + i)*n + j] of the lane's 16 sources (dropout on attention)
 __device__ __forceinline__ uint32_t keep_bits(const uint8_t* __restrict__ keep, int64_t base,
-                                              int i, int n, int q) {
+                                              int i, int n, int q, int64_t ext = 0) {
   uint32_t kb = 0u;
   if (i < n) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int j = src_of(q, k);
+      if (j < n) SV2N_CHK(103, base + (int64_t)i * n + j, ext);
       if (j < n && keep[base + (int64_t)i * n + j]) kb |= 1u << k;
     }
   }
@@ -321,14 +325,16 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
   const rsrc_t rae = plane_rsrc(ae_planes, E, eid, g, h, n);
   const rsrc_t rxs = make_rsrc(xs + row0 * ldx, (uint32_t)(4 * n * ldx));
   const int U = (n * (n - 1)) / 2;
+  const int64_t Nrows = (int64_t)gridDim.x / H * n;  // bound checks (SV2N_CHK) only
 
   LaneConst K;
   init_lane_const(K, rxs, n, q, ldx, HC + h);
   RowIn R;
   load_row(R, rae, rxs, K, eid, (row0 + wave * 4 + gq) * n, wave * 4 + gq, n, U, q, HC + H + h,
-           ldx);
+           ldx, Nrows * n);
   for (int idx = t; idx < NP * CW; idx += TT) {
     const int j = idx / CW, c = idx - j * CW;
+    if (j < n && c < C) SV2N_CHK(104, (row0 + j) * ldx + h * C + c, Nrows * ldx);
     sXT[c * XT + j] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
   }
   const int64_t kbase = (g * H + h) * (int64_t)n * n;
@@ -343,11 +349,12 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
       unpack(e, R);
       const float ad = R.ad;
       if (i0 + TB < n)
-        load_row(R, rae, rxs, K, eid, (row0 + i + TB) * n, i + TB, n, U, q, HC + H + h, ldx);
+        load_row(R, rae, rxs, K, eid, (row0 + i + TB) * n, i + TB, n, U, q, HC + H + h, ldx,
+                 Nrows * n);
       RowSoft S;
-      row_softmax(S, e, K, ad, i, n, q, general, rowmask, row0 + i, has_ae, slope);
+      row_softmax(S, e, K, ad, i, n, q, general, rowmask, row0 + i, has_ae, slope, Nrows);
       if (keep) {
-        const uint32_t kb = keep_bits(keep, kbase, i, n, q);
+        const uint32_t kb = keep_bits(keep, kbase, i, n, q, Nrows * H * n);
 #pragma unroll
         for (int k = 0; k < 16; ++k) S.p[k] = ((kb >> k) & 1u) ? S.p[k] * keep_scale : 0.f;
       }
@@ -384,6 +391,7 @@ __global__ __launch_bounds__(TT) void k_attn_tiled_fwd(
       const int rr = idx / CW, c = idx - rr * CW;
       const int ii = i0 + rr;
       if (ii < n && c < C) {
+        SV2N_CHK(105, (row0 + ii) * HC + h * C + c, Nrows * HC);
         const float* pr = sR + c * SRS + rr;
         const float v = (pr[0] + pr[CW * SRS]) + (pr[2 * CW * SRS] + pr[3 * CW * SRS]);
         if (CONCAT) {
@@ -410,6 +418,7 @@ __global__ __launch_bounds__(256) void k_head_mean(const float* __restrict__ ws,
   const int64_t row = idx / C;
   const int c = (int)(idx - row * C);
   const float* w = ws + row * H * C + c;
+  SV2N_CHK(106, row * H * C + c + (H - 1) * C, N * H * C);
   float s = 0.f;
   for (int h = 0; h < H; ++h) s += w[h * C];
   y[idx] = act_fwd<ACT>(s * (1.f / (float)H) + (bias ? bias[c] : 0.f));
@@ -461,6 +470,7 @@ __global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
   const rsrc_t rxs = make_rsrc(xs + row0 * ldx, (uint32_t)(4 * n * ldx));
   const rsrc_t rdy = make_rsrc(dy + row0 * OC, (uint32_t)(4 * n * OC));
   const rsrc_t ry = make_rsrc(y + row0 * OC, (uint32_t)(4 * n * OC));
+  const int64_t Nrows = (int64_t)gridDim.x / H * n;  // bound checks (SV2N_CHK) only
 
   // dOut rows of a block: TB*CW values, CT per thread
   float pdy[CT], py[CT];
@@ -478,10 +488,11 @@ __global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
   init_lane_const(K, rxs, n, q, ldx, HC + h);
   RowIn R;
   load_row(R, rae, rxs, K, eid, (row0 + wave * 4 + gq) * n, wave * 4 + gq, n, U, q, HC + H + h,
-           ldx);
+           ldx, Nrows * n);
   load_dout(0);
   for (int idx = t; idx < NP * CW; idx += TT) {
     const int j = idx / CW, c = idx - j * CW;
+    if (j < n && c < C) SV2N_CHK(107, (row0 + j) * ldx + h * C + c, Nrows * ldx);
     sX[j * XR + c] = (j < n && c < C) ? xs[(row0 + j) * ldx + h * C + c] : 0.f;
   }
   const int64_t kbase = (g * H + h) * (int64_t)n * n;
@@ -539,11 +550,12 @@ __global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
       unpack(e, R);
       const float ad = R.ad;
       if (i0 + TB < n) {
-        load_row(R, rae, rxs, K, eid, (row0 + i + TB) * n, i + TB, n, U, q, HC + H + h, ldx);
+        load_row(R, rae, rxs, K, eid, (row0 + i + TB) * n, i + TB, n, U, q, HC + H + h, ldx,
+                 Nrows * n);
         load_dout(i0 + TB);
       }
       RowSoft S;
-      row_softmax(S, e, K, ad, i, n, q, general, rowmask, row0 + i, has_ae, slope);
+      row_softmax(S, e, K, ad, i, n, q, general, rowmask, row0 + i, has_ae, slope, Nrows);
       float d[16];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -557,7 +569,7 @@ __global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
       }
       float pd[16];
       if (keep) {
-        const uint32_t kb = keep_bits(keep, kbase, i, n, q);
+        const uint32_t kb = keep_bits(keep, kbase, i, n, q, Nrows * H * n);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
           const bool kp = (kb >> k) & 1u;
@@ -584,6 +596,7 @@ __global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
       }
       rsum = row16_sum(rsum);
       dloop = row16_sum(dloop);  // one lane holds it, the others add 0
+      if (rv && q == 0) SV2N_CHK(108, (row0 + i) * ldx + HC + H + h, Nrows * ldx);
       if (rv && q == 0) dxs[(row0 + i) * ldx + HC + H + h] = rsum;  // d a_dst
       const float dshare = (has_ae && S.cnt > 0.f) ? dloop / S.cnt : 0.f;
       // d(edge logit) of every present edge of the row: with an edge-id map
@@ -593,7 +606,7 @@ __global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
           // eid holds -1 for absent edges (rowmask agrees)
-          const int id = eid_logit_id(eid, (row0 + i) * n, i, src_of(q, k), n);
+          const int id = eid_logit_id(eid, (row0 + i) * n, i, src_of(q, k), n, Nrows * n);
           bst(rdae, id >= 0 ? 4 * id : OOB, d[k] + dshare);
         }
       } else if (dae_planes) {
@@ -641,8 +654,10 @@ __global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
     }
   }
   __syncthreads();
-  for (int j = t; j < n; j += TT)
+  for (int j = t; j < n; j += TT) {
+    SV2N_CHK(109, (row0 + j) * ldx + HC + h, Nrows * ldx);
     dxs[(row0 + j) * ldx + HC + h] = (sDa[j] + sDa[NP + j]) + (sDa[2 * NP + j] + sDa[3 * NP + j]);
+  }
   // ---- write dxs_h, padding columns, bias partial ----
 #pragma unroll
   for (int a = 0; a < MAXJT; ++a) {
@@ -655,6 +670,7 @@ __global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int j = 16 * jt + 4 * lk + rr;
+            if (j < n) SV2N_CHK(110, (row0 + j) * ldx + h * C + c, Nrows * ldx);
             if (j < n) dxs[(row0 + j) * ldx + h * C + c] = dacc[a][b][rr];
           }
         }
@@ -665,13 +681,17 @@ __global__ __launch_bounds__(TT, 2) void k_attn_tiled_bwd(
     const int padc = ldx - HC - 2 * H;
     for (int idx = t; idx < n * padc; idx += TT) {
       const int j = idx / padc;
+      SV2N_CHK(111, (row0 + j) * ldx + HC + 2 * H + (idx - j * padc), Nrows * ldx);
       dxs[(row0 + j) * ldx + HC + 2 * H + (idx - j * padc)] = 0.f;
     }
   }
+  if (t < C && (CONCAT || h == 0)) SV2N_CHK(112, g * OC + oc0 + t, Nrows / n * OC);
   if (t < C && (CONCAT || h == 0)) dbias[g * OC + oc0 + t] = dbias_acc;
 }
 
 }  // namespace sv2n
+
+SV2N_CHK_EXPORT(tiled)
 
 // ============================ C-ABI ========================================
 using namespace sv2n;

@@ -288,6 +288,37 @@ __device__ __forceinline__ bool decode_edge(int64_t e, const int64_t* __restrict
 // accesses need no branch and the compiler can count vmcnt across them.
 // Build descriptors only from wave-uniform values (kernel args, blockIdx);
 // `bytes` = 0 makes every access through the descriptor a no-op.
+// Diagnostic bound checks (make CHECK=1; tests/conftest.py checks the count
+// after every test when the library exports sv2n_check_hits).  SV2N_CHK
+// compares a plain-pointer global index with its allocation's extent and
+// COUNTS a violation (one device word per translation unit, plus the first
+// failing site id) instead of dereferencing it; buffer loads and stores need
+// no check (the descriptor bounds them).  Release builds compile it away.
+#ifdef SV2N_CHECK
+static __device__ unsigned int sv2n_chk_hits[2];
+__device__ __noinline__ void sv2n_chk_fail(unsigned site) {
+  if (__hip_atomic_fetch_add(&sv2n_chk_hits[0], 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    __hip_atomic_store(&sv2n_chk_hits[1], site, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#define SV2N_CHK(site, idx, extent)                                              \
+  do {                                                                           \
+    if ((uint64_t)(int64_t)(idx) >= (uint64_t)(int64_t)(extent)) sv2n_chk_fail(site); \
+  } while (0)
+#define SV2N_CHK_EXPORT(tu)                                                      \
+  extern "C" unsigned sv2n_check_hits_##tu(unsigned* first) {                    \
+    unsigned h[2] = {0u, 0u};                                                    \
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(sv2n::sv2n_chk_hits), sizeof(h));        \
+    const unsigned z[2] = {0u, 0u};                                              \
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(sv2n::sv2n_chk_hits), z, sizeof(z));        \
+    if (first && h[0]) *first = h[1];                                            \
+    return h[0];                                                                 \
+  }
+#else
+#define SV2N_CHK(site, idx, extent) ((void)0)
+#define SV2N_CHK_EXPORT(tu)
+#endif
+
 // The wave's index in its workgroup as a wave-uniform (SGPR) value.  threadIdx.x
 // >> 6 is uniform in fact, but the compiler cannot prove it, and a buffer
 // descriptor or soffset derived from it would then be made uniform lane by

@@ -169,6 +169,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_fwd(
       for (int idx = t; idx < L * nh; idx += EDGE_THREADS) {
         const int l = idx / nh, r = idx - l * nh;
         const int le = r / H, h = r - le * H;
+        SV2N_CHK(402, e0 * H + r, E * H);
         s_ptr[l][e0 * H + r] = s_out[le * HLP + l * H + h];
       }
     } else {
@@ -178,6 +179,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_fwd(
         int i, j;
         if (!decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) continue;
         const int l = k / H, h = k - l * H;
+        SV2N_CHK(401, ((g * n + i) * n + j) * H + h, B * n * n * H);
         s_ptr[l][((g * n + i) * n + j) * H + h] = s_out[le * HLP + k];
       }
     }
@@ -212,6 +214,7 @@ __device__ __forceinline__ void gather_dae(float (&gd)[(EDGE_CHUNK * HLP + EDGE_
       const int le = idx / HLP, k = idx - le * HLP;
       if (le < ne && k < HL) {
         const int l = k / H, h = k - l * H;
+        SV2N_CHK(404, (e0 + le) * H + h, E * H);
         v = s_ptr[l][(e0 + le) * H + h];
       }
     } else {
@@ -220,6 +223,7 @@ __device__ __forceinline__ void gather_dae(float (&gd)[(EDGE_CHUNK * HLP + EDGE_
       int i, j;
       if (le < ne && k < HL && decode_edge(e0 + le, ei, E, canon, E0, n, B, g, i, j)) {
         const int l = k / H, h = k - l * H;
+        SV2N_CHK(403, ((g * n + i) * n + j) * H + h, B * n * n * H);
         v = s_ptr[l][((g * n + i) * n + j) * H + h];
       }
     }
@@ -694,7 +698,10 @@ __global__ __launch_bounds__(256, 4) void k_edge_fwd_mx(const float* __restrict_
       const int64_t e0 = tile * MX_TE + 4 * g;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (e0 + r < E) outp[(e0 + r) * H] = acc[r];
+        if (e0 + r < E) {
+          SV2N_CHK(405, (e0 + r) * H + (li - (li / H) * H), E * H);
+          outp[(e0 + r) * H] = acc[r];
+        }
     }
   }
 }
@@ -736,6 +743,7 @@ __global__ __launch_bounds__(256, 4) void k_edge_bwd_mx(const float* __restrict_
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int64_t e = t * MX_TE + 4 * g + q;
+      if (inp && e < E) SV2N_CHK(406, e * H, E * H);
       bb[q] = (inp && e < E) ? inp[e * H] : 0.f;
     }
   };
@@ -1254,6 +1262,8 @@ __global__ __launch_bounds__(CV2_T) void k_edge_fwd_cv2(const float* __restrict_
         const int p = tile * 16 + 4 * gq + r;
         if (p < P) {
           const int pp = sPr[p], u = pp & 0xff, w = pp >> 8;
+          SV2N_CHK(407, (gE0 + P + p) * H, (int64_t)gridDim.x * E0 * H);
+          SV2N_CHK(408, u * 32 + w, n * 32);
           outp[(gE0 + p) * H] = acc[r] + sV[0][u][li] + sV[1][w][li];
           outp[(gE0 + P + p) * H] = acc[r] + sV[0][w][li] + sV[1][u][li];
         }
@@ -1265,7 +1275,10 @@ __global__ __launch_bounds__(CV2_T) void k_edge_fwd_cv2(const float* __restrict_
 // SPLIT (at most 8 logit columns): the B operand's 16 columns carry d_up of
 // column c in lane column c and d_low in lane column 8 + c, so one MFMA per
 // M tile serves both directions and each lane loads one d-logit per pair
-// (the halves are added at the end); otherwise B = d_up + d_low.
+// (the halves are added at the end); otherwise B = d_up + d_low.  The
+// d-logits also go into an LDS table of the graph; after the tiles the
+// per-node sums over the outgoing / incoming edges are read from it in a
+// fixed order through a [node][partner] index table built once.
 template <int NP, int NC>
 __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void k_edge_bwd_cv2(
     const float* __restrict__ ea, int64_t B, int n, int S, const uint16_t* __restrict__ canon,
@@ -1273,15 +1286,18 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
   constexpr bool SPLIT = NC <= 8;
   constexpr int NM = 2 * NP;  // M tiles of 16 lags
   constexpr int PMAX = CV_MAXN * (CV_MAXN - 1) / 2;
-  constexpr int SR = CV2_WAVES * 32 * NP * 16, SN = CV2_WAVES * 2 * CV_MAXN * NC;
+  // the graph's d-logits [2 · PMAX + 1][NC] ([0, PMAX) up u -> v, [PMAX,
+  // 2·PMAX) low v -> u, the last row zero); at the end the waves' lag
+  // accumulators [wave][32·NP lags][16 columns]
+  constexpr int SD = (2 * PMAX + 1) * NC, SR = CV2_WAVES * 32 * NP * 16;
+  constexpr int ZROW = 2 * PMAX;
   __shared__ float sVar[CV_MAXN][CV_MAXS + 1];
-  // per graph: each wave's node sums [wave][out, in][node][column] (a wave
-  // adds only into its own slice, in program order: deterministic); at the
-  // end: the waves' lag accumulators [wave][32·NP lags][16 columns]
-  __shared__ float sBuf[SR > SN ? SR : SN];
+  __shared__ float sBuf[SD > SR ? SD : SR];
   __shared__ float sDn[2][CV_MAXN][NC];     // per node: Σ over outgoing [0] / incoming [1] edges
   __shared__ float sVarRes[2 * CV_MAXS][NC];
-  __shared__ int sPr[PMAX];
+  // sOut[u][w]: row of sD holding the d-logit of edge u -> w (ZROW for w = u);
+  // the edge w -> u is the other half of the same pair: row ± PMAX
+  __shared__ short sOut[CV_MAXN][CV_MAXN];
   float* sRed = sBuf;
   const int t = threadIdx.x, lane = t & 63, wave = wave_id();
   const int li = lane & 15, gq = lane >> 4;
@@ -1290,7 +1306,12 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
   // SPLIT: lane column li reads column li & 7 of the up (li < 8) or low rows
   const int col = SPLIT ? (li & 7) : li, low = SPLIT ? (li >> 3) : 0;
   const float* inp = col < HL ? mx_col_ptr<const float>(dae, col, L, H) : nullptr;
-  if (t < P) sPr[t] = canon[t];  // read after the first graph's barrier
+  for (int k = t; k < n * n; k += CV2_T) {
+    const int u = k / n, w = k - u * n;
+    sOut[u][w] = (short)(u == w ? ZROW : u < w ? cv2_pair_index(u, w, n)
+                                               : PMAX + cv2_pair_index(w, u, n));
+  }
+  if (t < NC) sBuf[ZROW * NC + t] = 0.f;
   f32x4 acc[NM];
 #pragma unroll
   for (int m = 0; m < NM; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1302,7 +1323,6 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
   // lane (li, g): row 4g + q of a tile, lags 32·mm + 2li (+1)
   const int vo = ((4 * gq) * D + 2 * li) * 4;
   constexpr int ND = SPLIT ? 1 : 2;  // d-logit loads per pair and lane
-  float* sNw = sBuf + wave * 2 * CV_MAXN * NC;
 
   for (int64_t g = blockIdx.x; g < B; g += gridDim.x) {
     const rsrc_t rg = make_rsrc(ea + g * E0 * D, (uint32_t)(E0 * D) * 4u);
@@ -1327,11 +1347,12 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
               ok ? ((tile * 16 + q) * D + 32 * mm) * 4 : 0, 0);
         const int p = tile * 16 + 4 * gq + q;
         const bool pv = ok && ib && p < P;
+        if (pv) SV2N_CHK(409, (g * E0 + P + p) * H, B * E0 * H);
 #pragma unroll
         for (int s = 0; s < ND; ++s) dd[q][s] = pv ? ib[((low | s) ? P + p : p) * H] : 0.f;
       }
     };
-    __syncthreads();  // the previous graph's sVar / sBuf / sDn reads (first graph: sPr)
+    __syncthreads();  // the previous graph's sVar / sBuf / sDn reads (first: sOut)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int k = t + CV2_T * i, u = k / S2, c2 = k - u * S2;
@@ -1340,7 +1361,6 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
         sVar[u][2 * c2 + 1] = __uint_as_float(vv[i][1]);
       }
     }
-    for (int k = lane; k < 2 * CV_MAXN * NC; k += 64) sNw[k] = 0.f;
     load(wave);
 #pragma unroll 1
     for (int k = 0; k < CV2_TW; ++k) {
@@ -1358,6 +1378,11 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
       load(tile + CV2_WAVES);  // the next tile in flight (nothing past TP)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        const int p = tile * 16 + 4 * gq + q;
+        if (p < P && col < NC) {
+#pragma unroll
+          for (int s = 0; s < ND; ++s) sBuf[(((low | s) ? PMAX : 0) + p) * NC + col] = x[q][s];
+        }
         const float b = SPLIT ? x[q][0] : x[q][0] + x[q][ND - 1];
 #pragma unroll
         for (int mm = 0; mm < NP; ++mm) {
@@ -1366,26 +1391,21 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
           acc[2 * mm + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[q][mm][1]), b,
                                                                  acc[2 * mm + 1], 0, 0, 0);
         }
-        // node sums: edge u -> v (up) counts as outgoing of u and incoming of
-        // v, v -> u (low) the other way round
-        const int p = tile * 16 + 4 * gq + q;
-        if (p < P && col < NC) {
-          const int pr = sPr[p], u = pr & 0xff, v = pr >> 8;
-#pragma unroll
-          for (int s = 0; s < ND; ++s) {
-            const bool lw = low | s;
-            atomicAdd(&sNw[(0 * CV_MAXN + (lw ? v : u)) * NC + col], x[q][s]);
-            atomicAdd(&sNw[(1 * CV_MAXN + (lw ? u : v)) * NC + col], x[q][s]);
-          }
-        }
       }
     }
-    __syncthreads();
+    __syncthreads();  // the d-logit table and sVar complete
+    // per-node sums in a fixed order (partners w = 0 .. n-1; the self row is
+    // the zero row): outgoing [0] reads row sOut[u][w], incoming [1] the
+    // pair's other half
     for (int k = t; k < 2 * n * NC; k += CV2_T) {
       const int side = k / (n * NC), uc = k - side * n * NC, u = uc / NC, c = uc - u * NC;
-      float sm = sBuf[(side * CV_MAXN + u) * NC + c];
-#pragma unroll
-      for (int w = 1; w < CV2_WAVES; ++w) sm += sBuf[((w * 2 + side) * CV_MAXN + u) * NC + c];
+      float sm = 0.f;
+#pragma unroll 8
+      for (int w = 0; w < n; ++w) {
+        int r = sOut[u][w];
+        if (side) r = r == ZROW ? ZROW : (r >= PMAX ? r - PMAX : r + PMAX);
+        sm += sBuf[r * NC + c];
+      }
       sDn[side][u][c] = sm;
     }
     __syncthreads();
@@ -1440,6 +1460,8 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
 }
 
 }  // namespace sv2n
+
+SV2N_CHK_EXPORT(edge)
 
 // ============================ C-ABI ========================================
 using namespace sv2n;
