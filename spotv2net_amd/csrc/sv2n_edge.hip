@@ -1139,6 +1139,7 @@ __global__ __launch_bounds__(CV2_T) void k_edge_fwd_cv2(const float* __restrict_
   constexpr int RS = 8 * NJ + 4;       // image row stride (floats)
   constexpr int IMG = 16 * RS + 128;   // + where the pieces past the tile land
   __shared__ __attribute__((aligned(16))) float s_img[CV2_WAVES][IMG];
+  __shared__ float s_out[CV2_WAVES][2 * 16 * 17];  // a tile's logits [dir][pair][column]
   __shared__ float sVar[CV_MAXN][CV_MAXS + 1];
   __shared__ float sWn[2 * CV_MAXS][NC];  // the fold's source / target rows
   __shared__ float sV[2][CV_MAXN][NC];    // node terms (source, target)
@@ -1199,6 +1200,7 @@ __global__ __launch_bounds__(CV2_T) void k_edge_fwd_cv2(const float* __restrict_
     }
   }
   float* img = s_img[wave];
+  float* sO = s_out[wave];
   for (int k = lane; k < 16 * (8 * NJ - S); k += 64) {  // lags S .. 8·NJ of the image: 0
     const int r = k / (8 * NJ - S);
     img[r * RS + S + (k - r * (8 * NJ - S))] = 0.f;
@@ -1256,16 +1258,41 @@ __global__ __launch_bounds__(CV2_T) void k_edge_fwd_cv2(const float* __restrict_
     }
     if (ABL & 1) {
       if (acc[0] == 12345.f) outp[0] = acc[1];
-    } else if (outp) {
+    } else if (ABL & 8) {  // (timing reference: lane-scattered 4·H-byte stores)
+      if (outp) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = tile * 16 + 4 * gq + r;
+          if (p < P) {
+            const int pp = sPr[p], u = pp & 0xff, w = pp >> 8;
+            outp[(gE0 + p) * H] = acc[r] + sV[0][u][li] + sV[1][w][li];
+            outp[(gE0 + P + p) * H] = acc[r] + sV[0][w][li] + sV[1][u][li];
+          }
+        }
+      }
+    } else {
+      // both directions' logits of the tile through the wave's LDS scratch
+      // [dir][pair][column], then per (direction, layer) the 16 pairs' H
+      // heads are one contiguous run of 16·H floats: consecutive lanes store
+      // consecutive floats (the MFMA layout would give 16-B pieces per lane)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int p = tile * 16 + 4 * gq + r;
-        if (p < P) {
-          const int pp = sPr[p], u = pp & 0xff, w = pp >> 8;
-          SV2N_CHK(407, (gE0 + P + p) * H, (int64_t)gridDim.x * E0 * H);
-          SV2N_CHK(408, u * 32 + w, n * 32);
-          outp[(gE0 + p) * H] = acc[r] + sV[0][u][li] + sV[1][w][li];
-          outp[(gE0 + P + p) * H] = acc[r] + sV[0][w][li] + sV[1][u][li];
+        const int pp = sPr[min(p, P - 1)], u = pp & 0xff, w = pp >> 8;
+        SV2N_CHK(408, u * 32 + w, n * 32);
+        sO[(0 * 16 + 4 * gq + r) * 17 + li] = acc[r] + sV[0][u][li] + sV[1][w][li];
+        sO[(1 * 16 + 4 * gq + r) * 17 + li] = acc[r] + sV[0][w][li] + sV[1][u][li];
+      }
+      const int np = min(16, P - tile * 16);
+      for (int l = 0; l < L; ++l) {
+#pragma unroll
+        for (int dir = 0; dir < 2; ++dir) {
+          float* dst = ae.p[l] + (gE0 + (dir ? P : 0) + tile * 16) * H;
+          for (int k = lane; k < np * H; k += 64) {
+            const int pr = k / H, h = k - pr * H;
+            SV2N_CHK(407, gE0 + (dir ? P : 0) + tile * 16 + pr, (int64_t)gridDim.x * E0);
+            dst[k] = sO[(dir * 16 + pr) * 17 + l * H + h];
+          }
         }
       }
     }

@@ -174,6 +174,7 @@ int main() {
   run("fwd-mx", FWD(2), cvb);
   run("fwd-nt", FWD(4), cvb);
   run("fwd-all", FWD(7), cvb);
+  run("fwd-scat", FWD(8), cvb);
   CK(hipDeviceSynchronize());
   return 0;
 }
