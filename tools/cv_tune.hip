@@ -152,7 +152,7 @@ int main() {
       (double)B * P * S * 4);
   run("covln", [&] { hipLaunchKernelGGL(k_cov<2>, dim3(B), dim3(512), 0, 0, ea, out); },
       (double)B * P * S * 4);
-  // the library's forward and its ablations (C2: L 2, H 4; wfold [126][16])
+  // the library's forward (C2: L 2, H 4; wfold [126][16])
   uint16_t* canon;
   float *wf, *ae0, *ae1;
   CK(hipMalloc(&canon, P * 2));
@@ -168,13 +168,7 @@ int main() {
   lp.p[0] = ae0;
   lp.p[1] = ae1;
   const double cvb = (double)B * (P * S + NN * S) * 4 + (double)B * E0 * 8 * 4;
-#define FWD(ABL) [&] { hipLaunchKernelGGL((k_edge_fwd_cv2<6, 8, ABL>), dim3(B), dim3(512), 0, 0, ea, NN, S, canon, wf, 16, lp, 2, 4); }
-  run("fwd", FWD(0), cvb);
-  run("fwd-st", FWD(1), cvb);
-  run("fwd-mx", FWD(2), cvb);
-  run("fwd-nt", FWD(4), cvb);
-  run("fwd-all", FWD(7), cvb);
-  run("fwd-scat", FWD(8), cvb);
+  run("fwd", [&] { hipLaunchKernelGGL((k_edge_fwd_cv2<6, 8>), dim3(B), dim3(512), 0, 0, ea, NN, S, canon, wf, 16, lp, 2, 4); }, cvb);
   CK(hipDeviceSynchronize());
   return 0;
 }

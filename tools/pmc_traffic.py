@@ -33,8 +33,8 @@ KERNELS = {
     # the covariance-layout passes the C2 step runs (bench kernel_table
     # edge_logits_fwd_cv / _bwd_cv); the backward's slab reduce shares its
     # kernel name with the generic pass's and is listed on its own
-    "edge_logits_fwd_cv": "sv2n::k_edge_fwd_cv<8>",
-    "edge_logits_bwd_cv": "sv2n::k_edge_bwd_cv<8>",
+    "edge_logits_fwd_cv": "sv2n::k_edge_fwd_cv2<6, 8>",
+    "edge_logits_bwd_cv": "sv2n::k_edge_bwd_cv2<2, 8>",
     "edge_reduce_partials": "sv2n::k_reduce_partials",
 }
 

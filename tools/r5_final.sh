@@ -10,6 +10,7 @@ mkdir -p $O
 cd $R
 timeout -k 10 400 python bench.py > $O/bench_n1.json 2> $O/bench_n1.err || { tail -20 $O/bench_n1.err; exit 1; }
 cat $O/bench_n1.json
+timeout -k 10 60 tools/probe_bin/cv_tune > $O/cv_tune.txt 2>&1 || exit 6
 cd /tmp && export TMPDIR=/tmp
 C2="python3 $R/bench.py --no-cpu-baseline --no-kernel-table --no-ref-loop --no-rotating --steps 20 --warmup 5"
 timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $O/c2t -o p --output-format csv -- $C2 > $O/c2t.log 2>&1 || exit 2
