@@ -800,7 +800,9 @@ __device__ __forceinline__ void static_for(F&& f) {
 // so after the barrier a wave only waits for its first B fragments.
 // Scheduling-group barriers hold the compiler to that interleave.
 // ---------------------------------------------------------------------------
-template <int NW, int MT, int NT, int AP, bool MASK = false>
+// BD: B fragments read BD column tiles ahead of their MFMAs (BD + 1 register
+// sets; 1 = the next tile's reads under the current tile's MFMAs).
+template <int NW, int MT, int NT, int AP, bool MASK = false, int BD = 1>
 __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A, int64_t lda,
                                                     const unsigned short* __restrict__ Bp,
                                                     int64_t ldb, int64_t bplane,
@@ -936,18 +938,22 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
     for (int a = 0; a < MT; ++a)
 #pragma unroll
       for (int p = 0; p < 3; ++p) af[a][p] = __builtin_bit_cast(bf16x8, afc[a][p]);
-    bf16x8 bq[2][3];
+    static_assert(BD >= 1 && BD < NT, "B read distance");
+    bf16x8 bq[BD + 1][3];
+    static_for<BD>([&](auto bc) __attribute__((always_inline)) {
+      constexpr int b = decltype(bc)::value;
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
-      bq[0][p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + li) * ROW + 8 * lg);
-    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+      for (int p = 0; p < 3; ++p)
+        bq[b][p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + 16 * b + li) * ROW + 8 * lg);
+    });
+    __builtin_amdgcn_sched_group_barrier(0x100, 3 * BD, 0);
     static_for<NT>([&](auto bc) __attribute__((always_inline)) {
       constexpr int b = decltype(bc)::value;
-      if constexpr (b + 1 < NT) {
+      if constexpr (b + BD < NT) {
 #pragma unroll
         for (int p = 0; p < 3; ++p)
-          bq[(b + 1) & 1][p] = *reinterpret_cast<const bf16x8*>(
-              sB + (p * BN + 16 * (b + 1) + li) * ROW + 8 * lg);
+          bq[(b + BD) % (BD + 1)][p] = *reinterpret_cast<const bf16x8*>(
+              sB + (p * BN + 16 * (b + BD) + li) * ROW + 8 * lg);
         __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
       }
       if constexpr (b < BV) {
@@ -966,7 +972,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
         __builtin_amdgcn_sched_group_barrier(0x002, 11 * PPT, 0);
       }
 #pragma unroll
-      for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<3>(af[a], bq[b & 1], acc[a][b]);
+      for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<3>(af[a], bq[b % (BD + 1)], acc[a][b]);
       __builtin_amdgcn_sched_group_barrier(0x008, 6 * MT, 0);
     });
 #pragma unroll

@@ -261,9 +261,40 @@ def _eligible(model, x, edge_attr) -> bool:
     return head_fits(lin.in_features, lin.out_features)
 
 
+# Bumped whenever any module registers a parameter or a submodule (attribute
+# assignment of an nn.Parameter / nn.Module goes through these hooks), so a
+# model's cached parameter list is rebuilt after a replacement.  Walking the
+# modules costs ~15-30 µs of nn.Module attribute lookups per call, host time
+# the GPU waits through at the start of a synchronised step.
+_PARAM_GEN = [0]
+
+
+def _bump_param_gen(*_):
+    _PARAM_GEN[0] += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_bump_param_gen)
+torch.nn.modules.module.register_module_module_registration_hook(_bump_param_gen)
+
+
 def _params(model) -> list:
-    return [p for c in model.gat_layers for p in layer_params(c)] + \
+    c = model.__dict__.get("_sv2n_params")
+    if c is not None and c[0] == _PARAM_GEN[0]:
+        return c[1]
+    ps = [p for c in model.gat_layers for p in layer_params(c)] + \
         [model.linear.weight] + ([model.linear.bias] if model.linear.bias is not None else [])
+    model.__dict__["_sv2n_params"] = (_PARAM_GEN[0], ps)
+    return ps
+
+
+def _convs(model) -> tuple:
+    """model.gat_layers as a tuple, cached like the parameter list."""
+    c = model.__dict__.get("_sv2n_convs")
+    if c is not None and c[0] == _PARAM_GEN[0]:
+        return c[1]
+    convs = tuple(model.gat_layers)
+    model.__dict__["_sv2n_convs"] = (_PARAM_GEN[0], convs)
+    return convs
 
 
 def forward(model, data, x, edge_index, edge_attr, layout: GraphLayout) -> Optional[torch.Tensor]:
@@ -282,9 +313,9 @@ def forward(model, data, x, edge_index, edge_attr, layout: GraphLayout) -> Optio
     train_graph = torch.is_grad_enabled() and any(needs)
     precision = resolve_precision(model.precision)
     key = (model.training, train_graph, precision, torch.is_autocast_enabled("cuda"),
-           model._act_code, model.dropout, tuple(c.dropout for c in model.gat_layers),
+           model._act_code, model.dropout, tuple(c.dropout for c in _convs(model)),
            _tsig(x), _tsig(edge_attr), cov_var_seq_length(edge_attr), _layout_sig(layout), needs,
-           tuple(p.data_ptr() for p in ps), _switches())
+           tuple([p.data_ptr() for p in ps]), _switches())
     entry = cache.entries.get(key)
     if entry is None:
         k = cache.seen.get(key, 0) + 1

@@ -90,14 +90,15 @@ void run3(const Shape& sh, hipStream_t st, const float* A, const unsigned short*
   fflush(stdout);
 }
 
-template <int NW, int MT, int NT, int BK, int AP, bool CV = false, int ABL = 0, int PD = 1, bool DV = false>
+template <int NW, int MT, int NT, int BK, int AP, bool CV = false, int ABL = 0, int PD = 1, bool DV = false,
+          int BD = 1>
 void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short* Bp, int64_t Kp,
            float* C, const std::vector<double>& ref, const std::vector<double>& absr) {
   using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
   const size_t lds = Cfg::LDS;
   if (lds > 160 * 1024) return;
   static_assert(DV, "k_gemm3d only (the product's projection kernel)");
-  auto kern = k_gemm3d<NW, MT, NT, AP, false>;
+  auto kern = k_gemm3d<NW, MT, NT, AP, false, BD>;
   if (lds > 65536)
     CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   const int nm = (int)((sh.M + Cfg::BM - 1) / Cfg::BM), nn = (int)((sh.N + Cfg::BN - 1) / Cfg::BN);
@@ -143,7 +144,7 @@ void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short
 #endif
   if (ABL) printf("  [ablation %d]", ABL);
   if (PD != 1) printf("  [PD %d]", PD);
-  if (DV) printf("  [3d]");
+  if (DV) printf("  [3d BD%d]", BD);
   printf("  gemm3%s NW%d MT%d NT%-2d BK%d AP%d %8.1f us %7.1f TF(f32-eq)  max|err| %.2e  max err/S|ab| %.2e\n",
          CV ? "c" : "b", NW, MT, NT, BK, AP, us, 2.0 * sh.M * sh.N * sh.K / us / 1e6, maxabs, maxrel);
   fflush(stdout);
@@ -205,17 +206,14 @@ int main() {
              2.0 * M * N * K / us / 1e6, maxabs, maxrel);
     }
     run3b<8, 1, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    // round 5: B fragments read 2-3 column tiles ahead of their MFMAs
+    run3b<8, 1, 13, 32, 2, true, 0, 1, true, 2>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 13, 32, 2, true, 0, 1, true, 3>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<8, 1, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 2, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 9, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    // round 4: three A register sets; four waves of two row tiles (one wave per SIMD)
-    run3b<8, 1, 13, 32, 3, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 1, 7, 32, 2, true, 0, 1, true, 2>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<4, 2, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<4, 2, 13, 32, 3, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    // round 4: more, smaller workgroups (240 -> 480-960 per launch at C2 sizes)
-    run3b<4, 1, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 4, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 5, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<4, 2, 13, 32, 2, true, 0, 1, true, 2>(sh, st, A, Bp, Kp, C, ref, absr);
+    run3b<8, 2, 7, 32, 2, true, 0, 1, true, 2>(sh, st, A, Bp, Kp, C, ref, absr);
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(S)); CK(hipFree(Bp));
   }
   return 0;

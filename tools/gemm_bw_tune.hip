@@ -81,12 +81,12 @@ double check(const float* C, const std::vector<double>& ref, int64_t M, int64_t 
   return worst / fmax(scale, 1e-30);
 }
 
-template <int BM, int BN, bool KO, bool AF, bool BF>
+template <int BM, int BN, bool KO, bool AF, bool BF, int WM = 2, int WN = 4>
 void run_bw(const char* tag, hipStream_t st, const void* A, int64_t lda, const void* B, int64_t ldb,
             float* C, int64_t M, int64_t N, int64_t K, int splitk, const std::vector<double>& ref,
             double flops) {
-  using Cfg = GemmBWCfg<BM, BN, KO, AF, BF>;
-  auto kern = k_gemm_bw<BM, BN, KO, AF, BF>;
+  using Cfg = GemmBWCfg<BM, BN, KO, AF, BF, WM, WN>;
+  auto kern = k_gemm_bw<BM, BN, KO, AF, BF, WM, WN>;
   CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                          (int)Cfg::LDS));
   const int nm = (int)((M + BM - 1) / BM), nn = (int)((N + BN - 1) / BN);
@@ -102,7 +102,7 @@ void run_bw(const char* tag, hipStream_t st, const void* A, int64_t lda, const v
   const double us = timeit(st, f);
   double err = -1;
   if (nz == 1) err = check(C, ref, M, N, N);
-  printf("  %-28s BM%d BN%d split%d %8.1f us %7.1f TF  err %.2e\n", tag, BM, BN, nz, us,
+  printf("  %-28s BM%d BN%d W%dx%d split%d %8.1f us %7.1f TF  err %.2e\n", tag, BM, BN, WM, WN, nz, us,
          flops / us / 1e6, err);
   fflush(stdout);
 }
@@ -188,18 +188,17 @@ int main() {
       printf("  %-28s %8.1f us %7.1f TF  (2 slabs, no check)\n", "round-3 k_gemm_tt<128,128,1>", us,
              fl / us / 1e6);
     }
-    run_bw<128, 256, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 1, ref, fl);
-    run_bw<128, 256, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 2, ref, fl);
-    run_bw<128, 256, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 3, ref, fl);
-    run_bw<128, 128, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 1, ref, fl);
-    run_bw<128, 128, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 2, ref, fl);
-    run_bw<128, 192, true, true, true>("bw A fp32, B fp32", st, A, ldA, B, ldB, C, M, N, K, 2, ref, fl);
-    run_bw<128, 256, true, false, true>("bw A bf16, B fp32", st, Ab, ldAb, B, ldB, C, M, N, K, 2, ref, fl);
-    run_bw<128, 256, true, true, false>("bw A fp32, B bf16", st, A, ldA, Bb, ldBb, C, M, N, K, 2, ref, fl);
-    run_bw<128, 256, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 1, ref, fl);
-    run_bw<128, 256, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
     run_bw<128, 128, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 1, ref, fl);
     run_bw<128, 128, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
+    // round 5: 4-wave workgroups (wave tile 64 x 64: half the LDS reads per MFMA)
+    run_bw<128, 128, true, false, false, 2, 2>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 1, ref, fl);
+    run_bw<128, 128, true, false, false, 2, 2>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
+    run_bw<128, 128, true, false, false, 2, 2>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 3, ref, fl);
+    run_bw<128, 256, true, false, false, 2, 4>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
+    run_bw<256, 128, true, false, false, 4, 2>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
+    run_bw<128, 256, true, false, false, 2, 2>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
+    run_bw<64, 128, true, false, false, 1, 2>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 1, ref, fl);
+    run_bw<64, 128, true, false, false, 1, 2>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(Ab)); CK(hipFree(Bb));
   }
   return 0;
