@@ -206,14 +206,20 @@ int main() {
              2.0 * M * N * K / us / 1e6, maxabs, maxrel);
     }
     run3b<8, 1, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    // round 5: B fragments read 2-3 column tiles ahead of their MFMAs
-    run3b<8, 1, 13, 32, 2, true, 0, 1, true, 2>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 13, 32, 2, true, 0, 1, true, 3>(sh, st, A, Bp, Kp, C, ref, absr);
     run3b<8, 1, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 7, 32, 2, true, 0, 1, true, 2>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<4, 2, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<4, 2, 13, 32, 2, true, 0, 1, true, 2>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 2, 7, 32, 2, true, 0, 1, true, 2>(sh, st, A, Bp, Kp, C, ref, absr);
+    if (sh.K <= 400) {
+      // round 5: the LDS-staged kernel (no interleave constraint) with 2-4 waves
+      // per workgroup, so that several short-K workgroups share a CU
+      run3<4, 1, 13, 32, 2, 0>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3<4, 1, 13, 32, 2, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3<4, 1, 7, 32, 2, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3<4, 2, 7, 32, 2, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3<2, 2, 13, 32, 2, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3<4, 1, 13, 64, 1, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3<4, 1, 7, 64, 2, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3<8, 1, 7, 32, 2, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3<4, 2, 13, 32, 1, 1>(sh, st, A, Bp, Kp, C, ref, absr);
+    }
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(S)); CK(hipFree(Bp));
   }
   return 0;
