@@ -458,21 +458,43 @@ class Fit:
         data, idx = self._batch[b], self._idx[b]
         return data, (lambda: self.ds.fill(data, idx))
 
-    def _eval_step(self, b: int) -> ForwardStep:
-        if b not in self._eval:
-            data, prep = self._static(b)
+    def _eval_pass(self) -> ForwardStep:
+        """The test pass (5_train_SpotV2Net.py:166-180: sequential batches of
+        ``bs``, each batch's MSE added up) as ONE captured forward over every
+        test window: the graphs are independent and eval mode draws no
+        dropout, so each window's output is the one its batch would give, and
+        each batch's loss is its own row slice's mean (one fused head + MSE
+        launch per batch, added to the epoch's test sum in batch order)."""
+        if "all" not in self._eval:
+            n_test, bs = self.n_test, self.bs
+            # buffers of its own (a training shape of the same size refills its
+            # index buffer every step)
+            idx = torch.arange(self.n_train, self.n_train + n_test, device=self.dev)
+            data = self.ds.empty_batch(
+                n_test, bf16_x=getattr(self.model, "precision", None) == "bf16")
+            self.ds.fill(data, idx)
+            prep = (lambda: self.ds.fill(data, idx))
+            rows = data.x.shape[0] // n_test  # nodes per window
+            tot = self._tot_test
+
+            def fn(m, d):
+                from .stack import head_mse_loss
+                h = m._hidden(d)
+                y = d.y_x.view(n_test * rows, -1)
+                for k in range(0, n_test, bs):
+                    b = min(bs, n_test - k)
+                    head_mse_loss(h[k * rows:(k + b) * rows], m.linear,
+                                  y[k * rows:(k + b) * rows].reshape(-1), tot)
+                return tot
+
             was = self.model.training
             self.model.eval()
-            # the loss joins _tot_test inside the head launch; the warm-up and
-            # capture calls' additions are undone here
             saved = self._tot_test.clone()
-            tot = self._tot_test
-            self._eval[b] = ForwardStep(self.model, data, use_graph=self.use_graph,
-                                        fn=lambda m, d: m.mse_loss(d, loss_sum=tot).reshape(()),
-                                        prepare=prep)
-            self._tot_test.copy_(saved)
+            self._eval["all"] = ForwardStep(self.model, data, use_graph=self.use_graph, fn=fn,
+                                            prepare=prep)
+            self._tot_test.copy_(saved)  # undo the warm-up and capture calls
             self.model.train(was)
-        return self._eval[b]
+        return self._eval["all"]
 
     def run_epoch(self, checkpoint_path: Optional[str] = None, tolerance: float = 1e-9) -> dict:
         """One epoch: training pass, test pass, history entry (and checkpoint)."""
@@ -488,16 +510,11 @@ class Fit:
                 self.step_hook(self.epoch, nb)
             self.step(self._train_shape[b])   # adds its loss to _tot_train
             nb += 1
-        nt = 0
+        nt = -(-self.n_test // self.bs)   # test batches
         self._tot_test.zero_()   # an empty test split reports 0, not the last epoch's sum
         self.model.eval()
-        test_idx = torch.arange(self.n_train, self.n_train + self.n_test, device=dev)
-        for k in range(0, self.n_test, self.bs):
-            b = min(self.bs, self.n_test - k)
-            fs = self._eval_step(b)   # its capture restores _tot_test after warming up
-            self._idx[b].copy_(test_idx[k:k + b])
-            fs()                               # adds its loss to _tot_test
-            nt += 1
+        if self.n_test > 0:
+            self._eval_pass()()   # adds every test batch's loss to _tot_test
         self.model.train()
         train_loss = float(self._tot_train) / max(nb, 1)   # one host sync per epoch
         test_loss = float(self._tot_test) / max(nt, 1)

@@ -170,3 +170,28 @@ def test_c3_full_size_bf16_curve_matches_oracle(curves_full):
     for (tr, te), (rtr, rte) in zip(curves_full["bf16"], curves_full["oracle"]):
         assert _rel(tr, rtr) < 3e-2, (tr, rtr)
         assert _rel(te, rte) < 3e-2, (te, rte)
+
+
+@pytest.mark.parametrize("bs", [16, 12])
+def test_test_pass_equals_per_batch_losses(dev, bs):
+    """Fit's test pass — one forward over every test window, each batch's MSE
+    from its own row slice — gives the reference's per-batch loop
+    (5_train_SpotV2Net.py:166-180: model(data) + MSELoss on each sequential
+    test batch, averaged over the batches), ragged last batch included."""
+    from spotv2net_amd import GATModel
+    from spotv2net_amd.train import Fit
+    _, ds = _data(dev)
+    torch.manual_seed(11)
+    m = GATModel(30 * S, 3 * S, 4, 1, [32, 16], concat_heads=True).to(dev)
+    f = Fit(m, ds, bs, generator=torch.Generator().manual_seed(3))
+    assert f.n_test % bs != 0  # a ragged last batch is part of the check
+    rec = f.run_epoch()
+    m.eval()
+    losses = []
+    with torch.no_grad():
+        for k in range(f.n_train, len(ds), bs):
+            idx = torch.arange(k, min(k + bs, len(ds)), device=dev)
+            b = ds.batch(idx)
+            losses.append(torch.nn.functional.mse_loss(m(b), b.y_x).item())
+    want = sum(losses) / len(losses)
+    assert abs(rec["test_loss"] - want) <= 1e-6 * abs(want), (rec["test_loss"], want)
