@@ -11,6 +11,7 @@ import re
 import subprocess
 import sys
 
+nk = nwf = nhz = 0
 for src in sys.argv[1:]:
     asm = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
                           "-Iinclude", "--cuda-device-only", "-S", src, "-o", "/dev/stdout"],
@@ -19,6 +20,7 @@ for src in sys.argv[1:]:
         end = asm.find(".Lfunc_end", m.end())
         body = asm[m.end():end]
         wf = 0
+        nk += 1
         for h in re.finditer(r"; =>This Inner Loop Header", body):
             seg = body[h.start():body.find("s_cbranch_execnz", h.start()) + 1].split("\n")[1:]
             # the waterfall shape: readfirstlanes first, then a compare, the
@@ -27,6 +29,7 @@ for src in sys.argv[1:]:
                    and any("s_and_saveexec" in x for x in seg)
                    and any("buffer_" in x for x in seg))
         if wf:
+            nwf += 1
             print(f"{src.split('/')[-1]}: {m.group(1)[:100]} waterfall buffer ops: {wf}")
         lines = body.split("\n")
         for k, ln in enumerate(lines):
@@ -44,4 +47,7 @@ for src in sys.argv[1:]:
                     break
                 if re.search(r"(buffer_|global_)", tt) and any(
                         int(a) <= reg <= int(b) for a, b in re.findall(r"s\[(\d+):(\d+)\]", tt)):
+                    nhz += 1
                     print(f"{src.split('/')[-1]}: {m.group(1)[:100]} HAZARD: {ln.strip()} -> {tt}")
+print(f"{nk} kernels in {len(sys.argv) - 1} sources: {nwf} with waterfall buffer ops, "
+      f"{nhz} readfirstlane -> VMEM hazards")
