@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 18
+#define SV2N_ABI_VERSION 19
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -315,7 +315,8 @@ typedef struct sv2n_prep_layer {
   const float* att_src;   /* [H*C] */
   const float* att_dst;   /* [H*C] */
   int heads, channels, in_features, ldx;
-  float* waug;            /* [ldx][F] */
+  float* waug;            /* [ldx][F], or NULL: not written (ABI 19; the planes
+                             are the GEMMs' only operand, e.g. in bf16 mode) */
   uint16_t* planes;       /* [nplanes][ldx][kp] */
   uint16_t* planes_t;     /* [nplanes][F][kpt] or NULL */
   const float* W_edge;    /* lin_edge.weight [H*C][edge_dim] or NULL */

@@ -51,7 +51,7 @@ __device__ __forceinline__ float fold_tree16(const float* v, int stride) {
   return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
-// rows [cb, ce) of head h copied (waug; planes when given: kp columns, zero
+// rows [cb, ce) of head h copied (waug when given; planes when given: kp columns, zero
 // past F); with fold, the att_src / att_dst folds over ALL C rows written to
 // waug rows HC+h and HC+H+h (and their planes).  cols: F (node) or D (edge).
 struct PrepBlock {
@@ -59,14 +59,14 @@ struct PrepBlock {
   float* waug; uint16_t* planes; int64_t kp, plane; int np;
 };
 
-// one row piece (4 columns) of waug and its bf16 planes; 16-B / 8-B stores when
+// one row piece (4 columns) of waug (when given) and its bf16 planes; 16-B / 8-B stores when
 // the piece lies inside the row
 __device__ __forceinline__ void prep_put_piece(const PrepBlock& P, int64_t row, int col,
                                                const float (&w)[4]) {
   const int F = P.F;
-  if ((F & 3) == 0 && col + 3 < F) {
+  if (P.waug && (F & 3) == 0 && col + 3 < F) {
     *reinterpret_cast<f32x4*>(P.waug + row * F + col) = f32x4{w[0], w[1], w[2], w[3]};
-  } else {
+  } else if (P.waug) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (col + j < F) P.waug[row * F + col + j] = w[j];
@@ -159,14 +159,14 @@ __device__ __forceinline__ void prep_node_block(const PrepBlock& P, int h, int c
     const int q = t >> 6, cl = t & 63, c = col0 + cl;
     const float v = fold_tree16(&s_red[q][0][cl], 64);
     const int64_t row = HC + q * P.H + h;
-    if (c < F) P.waug[row * F + c] = v;
+    if (P.waug && c < F) P.waug[row * F + c] = v;
     if (P.planes && c < P.kp) put3(P.planes, P.plane, row * P.kp + c, v, P.np);
   }
   if (h == 0) {  // zero padding rows
     for (int k = t; k < (P.ldx - HC - 2 * P.H) * 64; k += 256) {
       const int64_t row = HC + 2 * P.H + k / 64;
       const int c = col0 + (k & 63);
-      if (c < F) P.waug[row * F + c] = 0.f;
+      if (P.waug && c < F) P.waug[row * F + c] = 0.f;
       if (P.planes && c < P.kp) put3(P.planes, P.plane, row * P.kp + c, 0.f, P.np);
     }
   }
@@ -567,7 +567,7 @@ extern "C" int sv2n_gat_prep_fwd_all(const sv2n_prep_layer* layers, int num_laye
   int nb = 0;
   for (int l = 0; l < num_layers; ++l) {
     const sv2n_prep_layer& P = layers[l];
-    if (!P.W || !P.att_src || !P.att_dst || !P.waug || !P.planes) return SV2N_ERR_ARG;
+    if (!P.W || !P.att_src || !P.att_dst || !P.planes) return SV2N_ERR_ARG;
     if (P.heads < 1 || P.channels < 1 || P.in_features < 1) return SV2N_ERR_ARG;
     if (P.heads > SV2N_MAX_HEADS || P.ldx < P.heads * P.channels + 2 * P.heads)
       return SV2N_ERR_SHAPE;

@@ -185,6 +185,12 @@ def _prep_shapes(W, heads, channels, need_t, kpad, np=3):
     return out
 
 
+def _waug_placeholder(w: torch.Tensor, shape) -> torch.Tensor:
+    """Waug's shape without its data (bf16-mode gat_prep): consumers read only
+    the shape; ops.project / weight_planes refuse it (ops._has_data)."""
+    return w.new_zeros(1).expand(shape)
+
+
 def _kpad(K: int) -> int:
     return (K + 63) // 64 * 64  # sv2n_split3_kpad
 
@@ -202,12 +208,14 @@ def _gat_prep(W, att_src, att_dst, W_edge, att_edge, heads, channels, hl_pad, ne
     waugs, planes, planes_t = [], [], []
     np = 1 if bf16 else 3
     for l, (s_w, s_p, s_t) in enumerate(_prep_shapes(W, heads, channels, need_t, _kpad, np)):
-        waug = torch.empty(s_w, device=dev)
+        # bf16 mode: every GEMM takes the planes, so Waug itself is not
+        # written (ABI 19) and stands as a stride-0 placeholder of its shape
+        waug = _waug_placeholder(W[l], s_w) if bf16 else torch.empty(s_w, device=dev)
         pl = torch.empty(s_p, device=dev, dtype=torch.int16)
         plt = torch.empty(s_t, device=dev, dtype=torch.int16)
         arr[l] = _lib.PrepLayer(
             W[l].data_ptr(), att_src[l].data_ptr(), att_dst[l].data_ptr(), heads[l], channels[l],
-            W[l].shape[1], s_w[0], waug.data_ptr(), pl.data_ptr(), _p(plt),
+            W[l].shape[1], s_w[0], None if bf16 else waug.data_ptr(), pl.data_ptr(), _p(plt),
             W_edge[l].data_ptr() if use_edge else None,
             att_edge[l].data_ptr() if use_edge else None, D, hl_pad, l * heads[0],
             _p(wf) if use_edge else None, np)
@@ -225,7 +233,7 @@ def _gat_prep_fake(W, att_src, att_dst, W_edge, att_edge, heads, channels, hl_pa
     D = W_edge[0].shape[1] if use_edge else 0
     w0 = W[0]
     shp = _prep_shapes(W, heads, channels, need_t, _kpad, 1 if bf16 else 3)
-    return ([w0.new_empty(a) for a, _, _ in shp],
+    return ([_waug_placeholder(w0, a) if bf16 else w0.new_empty(a) for a, _, _ in shp],
             [w0.new_empty(b, dtype=torch.int16) for _, b, _ in shp],
             [w0.new_empty(c, dtype=torch.int16) for _, _, c in shp],
             w0.new_empty((D, hl_pad) if use_edge else (0,)))

@@ -80,12 +80,19 @@ def weight_planes(w: torch.Tensor, transpose: bool) -> torch.Tensor:
     """The three bf16 planes [3][rows][Kp] of a weight used as the B operand of
     sv2n_gemm_f32x3: B(n, k) = w[n][k] (transpose False) or w[k][n] (True)."""
     lib = _lib.load()
+    _has_data(w)
     rows, K = (w.shape[1], w.shape[0]) if transpose else (w.shape[0], w.shape[1])
     Kp = lib.sv2n_split3_kpad(K)
     out = torch.empty(3, rows, Kp, device=w.device, dtype=torch.int16)
     _lib.check(lib.sv2n_split3(w.data_ptr(), rows, K, w.stride(0), int(transpose), out.data_ptr(),
                                _stream(w.device)), "sv2n_split3")
     return out
+
+
+def _has_data(w: torch.Tensor) -> None:
+    if w.dim() == 2 and w.numel() > 1 and w.stride() == (0, 0):
+        raise RuntimeError("sv2n: Waug placeholder of bf16-mode gat_prep has no data; "
+                           "pass the layer's planes")
 
 
 def _split_ok(a: torch.Tensor) -> bool:
@@ -97,6 +104,7 @@ def project(a: torch.Tensor, w: torch.Tensor, transpose_w: bool) -> torch.Tensor
     [M][K] k-contiguous.  bf16-split MFMA when a is aligned, else exact f32."""
     M, K = a.shape
     N = w.shape[1] if transpose_w else w.shape[0]
+    _has_data(w)
     if _split_ok(a):
         lib = _lib.load()
         planes = weight_planes(w, transpose_w)

@@ -140,3 +140,75 @@ def test_prep_fwd_all_matches_per_layer(dev):
         assert torch.equal(pl, pl_r)
         assert torch.equal(plt, plt_r)
     assert torch.equal(wf_all, wf_ref)
+
+
+def test_prep_fwd_all_without_waug(dev):
+    """ABI 19: sv2n_gat_prep_fwd_all with waug NULL (bf16 mode) writes the same
+    planes (and planes_t, wfold) as with waug, and nothing in place of waug."""
+    import ctypes
+    from spotv2net_amd import _lib
+    lib = _lib.load()
+    st = _lib.stream_handle(dev)
+    g = torch.Generator().manual_seed(4)
+    shapes = [(6, 500, 1260), (6, 30, 3012)]  # C3-sized layer 0, a second layer
+    D, H, hp = 126, 6, 12
+    runs = []
+    for with_waug in (True, False):
+        arr = (_lib.PrepLayer * len(shapes))()
+        wf = torch.zeros(D, hp, device=dev)
+        keep = []
+        for l, (Hh, C, F) in enumerate(shapes):
+            g.manual_seed(10 + l)
+            HC = Hh * C
+            ldx = (HC + 2 * Hh + 3) // 4 * 4
+            W = torch.randn(HC, F, generator=g).to(dev)
+            a_s, a_d, a_e = (torch.randn(HC, generator=g).to(dev) for _ in range(3))
+            We = torch.randn(HC, D, generator=g).to(dev)
+            kp, kpt = lib.sv2n_split3_kpad(F), lib.sv2n_split3_kpad(ldx)
+            waug = torch.full((ldx, F), 7.0, device=dev)
+            pl = torch.empty(1, ldx, kp, device=dev, dtype=torch.int16)
+            plt = torch.empty(1, F, kpt, device=dev, dtype=torch.int16)
+            arr[l] = _lib.PrepLayer(W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), Hh, C, F, ldx,
+                                    waug.data_ptr() if with_waug else None, pl.data_ptr(),
+                                    plt.data_ptr(), We.data_ptr(), a_e.data_ptr(), D, hp, l * H,
+                                    wf.data_ptr(), 1)
+            keep.append((W, a_s, a_d, a_e, We, waug, pl, plt))
+        _lib.check(lib.sv2n_gat_prep_fwd_all(ctypes.addressof(arr), len(shapes), st),
+                   "prep_fwd_all")
+        torch.cuda.synchronize()
+        runs.append((keep, wf))
+    (with_k, wf_a), (without_k, wf_b) = runs
+    assert torch.equal(wf_a, wf_b)
+    for a, b in zip(with_k, without_k):
+        assert torch.equal(a[6], b[6]) and torch.equal(a[7], b[7])
+        assert not torch.equal(a[5], b[5])  # written with, untouched without
+        assert bool((b[5] == 7.0).all())
+
+
+def test_bf16_prep_waug_placeholder(dev):
+    """bf16-mode gat_prep returns Waug as a stride-0 placeholder of its shape;
+    the projections that take the planes run, the ones that would read Waug
+    refuse it loudly."""
+    from spotv2net_amd import GATModel, library  # noqa: F401
+    ops = torch.ops.sv2n
+    torch.manual_seed(0)
+    m = GATModel(60, 6, 2, 1, [8, 4], concat_heads=True).to(dev)
+    c0, c1 = m.gat_layers
+    args = ([c0.lin_src.weight, c1.lin_src.weight], [c0.att_src, c1.att_src],
+            [c0.att_dst, c1.att_dst], [c0.lin_edge.weight, c1.lin_edge.weight],
+            [c0.att_edge, c1.att_edge], [2, 2], [8, 4], 4, [False, True], True)
+    w32, p32, _, wf32 = ops.gat_prep(*args, bf16=False)
+    w16, p16, pt16, wf16 = ops.gat_prep(*args, bf16=True)
+    assert torch.equal(wf32, wf16)
+    for a, b, pl in zip(w32, w16, p16):
+        assert b.shape == a.shape and b.stride() == (0, 0)
+        # plane 0 of bf16 mode is bf16_rn(Waug) (zero past F)
+        ref = a.to(torch.bfloat16).view(torch.int16)
+        assert torch.equal(pl[0, :, :a.shape[1]], ref)
+    x = torch.randn(96, 60, device=dev)
+    xs = ops.project(x, p16[0], w16[0], False, True)
+    assert xs.shape == (96, w32[0].shape[0])
+    with pytest.raises(RuntimeError, match="placeholder"):
+        ops.project(x, None, w16[0], False, True)
+    with pytest.raises(RuntimeError, match="placeholder"):
+        ops.project(x, None, w16[0], False, False)
