@@ -508,6 +508,22 @@ int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_features, const
                         float* loss_sum, float* dx, float* g_weight, float* g_bias,
                         float* workspace, int64_t workspace_floats, hipStream_t stream);
 
+/* sv2n_head_mse_train in two launches (ABI 19; the wave-per-rows form only:
+ * out_features <= 4 and out_features * ceil(in_features / 64) <= 32, else
+ * SV2N_ERR_SHAPE).  _rows writes dx and the per-block partials into the
+ * workspace; _reduce (same workspace, num_rows and widths, any stream ordered
+ * after _rows) sums them into loss, loss_sum, g_weight, g_bias.  The caller
+ * runs _reduce after the layer backwards, which need only dx, instead of the
+ * one-launch form's ticket chain ahead of them.  Bitwise equal to the
+ * one-launch sv2n_head_mse_train. */
+int sv2n_head_mse_train_rows(const float* x, int64_t num_rows, int in_features,
+                             const float* weight, const float* bias, int out_features,
+                             const float* target, float* dx, float* workspace,
+                             int64_t workspace_floats, hipStream_t stream);
+int sv2n_head_mse_train_reduce(const float* workspace, int64_t num_rows, int in_features,
+                               int out_features, float* loss, float* loss_sum, float* g_weight,
+                               float* g_bias, hipStream_t stream);
+
 /* Fused attention for dense-block graphs of 32 < n <= 256 nodes (any n <= 256
  * works; n <= 32 is faster on sv2n_gat_attn_fwd/bwd).  Same semantics and
  * arguments as sv2n_gat_attn_fwd/bwd except:

@@ -134,6 +134,8 @@ _SIGNATURES = {
     "sv2n_head_mse_train_workspace": (_i64, [_i64, _i32, _i32]),
     "sv2n_head_mse_train": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _i64,
                                    _p]),
+    "sv2n_head_mse_train_rows": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _i64, _p]),
+    "sv2n_head_mse_train_reduce": (_i32, [_p, _i64, _i32, _i32, _p, _p, _p, _p, _p]),
     "sv2n_head_mse_fwd": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "sv2n_head_mse_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "sv2n_head_fwd": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p]),

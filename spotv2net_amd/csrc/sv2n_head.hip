@@ -471,7 +471,9 @@ __global__ __launch_bounds__(256) void k_head_mse_train(
 // groups in order).  The block-at-a-time kernel above read every partial in
 // one workgroup: C3 (240 partials of 502 floats) spent most of its 33 us there.
 // ---------------------------------------------------------------------------
-template <int OUT, int KC>
+// DEFER (sv2n_head_mse_train_rows): each block only publishes its partial
+// (plain stores); k_head_mse_reduce_w sums them later, in the same order.
+template <int OUT, int KC, bool DEFER = false>
 __global__ __launch_bounds__(256) void k_head_mse_train_w(
     const float* __restrict__ x, int64_t N, int C, const float* __restrict__ W,
     const float* __restrict__ b, const float* __restrict__ target, float* __restrict__ dx,
@@ -557,6 +559,12 @@ __global__ __launch_bounds__(256) void k_head_mse_train_w(
   __syncthreads();
   float* part = ws + HEAD_WS_HDR;
   const unsigned nb = gridDim.x;
+  if constexpr (DEFER) {
+    for (int oc = t; oc < stride; oc += 256)
+      part[(int64_t)blockIdx.x * stride + oc] =
+          (s_w4[oc] + s_w4[stride + oc]) + (s_w4[2 * stride + oc] + s_w4[3 * stride + oc]);
+    return;
+  }
   for (int oc = t; oc < stride; oc += 256)
     st_sc1(part + (int64_t)blockIdx.x * stride + oc,
            (s_w4[oc] + s_w4[stride + oc]) + (s_w4[2 * stride + oc] + s_w4[3 * stride + oc]));
@@ -593,6 +601,53 @@ __global__ __launch_bounds__(256) void k_head_mse_train_w(
       } else if (gb) {
         gb[o] += s;
       }
+    }
+  }
+}
+
+// The deferred reduction of k_head_mse_train_w<..., true>'s nb block partials
+// (a launch of its own, after the layer backwards that need only dx).  Block of 512 = 8 groups x 64 columns: thread (g, l) sums
+// partials g, g + 8, ... of column oc in block order, as group_last_sc1's
+// finisher does, and group 0 adds the 8 group sums as top_last_sc1's finisher
+// does: the same floating-point order, so the same bits as the one-launch form.
+__global__ __launch_bounds__(512) void k_head_mse_reduce_w(
+    const float* __restrict__ ws, unsigned nb, int OUT, int C, float* __restrict__ gW,
+    float* __restrict__ gb, float* __restrict__ loss, float* __restrict__ loss_sum,
+    float inv_count) {
+  __shared__ float s_g[8][64];
+  const int t = threadIdx.x, g = t >> 6, l = t & 63;
+  const int CP = C + 1, stride = OUT * CP + 1;
+  const int oc = blockIdx.x * 64 + l;
+  const float* part = ws + HEAD_WS_HDR;
+  const unsigned members = (unsigned)g < nb ? (nb - (unsigned)g + 7u) / 8u : 0u;
+  float s = 0.f;
+  if (oc < stride) {
+    for (unsigned m0 = 0; m0 < members; m0 += 32) {
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
+        v[u] = m0 + u < members ? part[(int64_t)(g + 8u * (m0 + u)) * stride + oc] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 32; ++u) s += v[u];
+    }
+  }
+  s_g[g][l] = s;
+  __syncthreads();
+  if (g != 0 || oc >= stride) return;
+  const int groups = nb < 8u ? (int)nb : 8;
+  float v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = u < groups ? s_g[u][l] : 0.f;
+  const float r = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+  if (oc == OUT * CP) {
+    loss[0] = r * inv_count;
+    if (loss_sum) loss_sum[0] += r * inv_count;
+  } else {
+    const int o = oc / CP, c = oc - o * CP;
+    if (c < C) {
+      if (gW) gW[o * C + c] += r;
+    } else if (gb) {
+      gb[o] += r;
     }
   }
 }
@@ -737,6 +792,61 @@ extern "C" int64_t sv2n_head_mse_train_workspace(int64_t num_rows, int in_featur
   return HEAD_WS_HDR + head_bwd_blocks(num_rows, in_features, out_features) * stride;
 }
 
+template <bool DEFER>
+static int head_w_launch(const float* x, int64_t num_rows, int C, const float* weight,
+                         const float* bias, int out_ch, const float* target, float* loss,
+                         float* loss_sum, float* dx, float* g_weight, float* g_bias,
+                         float* workspace, hipStream_t stream) {
+  const float inv_count = 1.f / (float)(num_rows * out_ch);
+  const float scale = 2.f / (float)(num_rows * (int64_t)out_ch);
+  const int RW = head_w_rows(num_rows), kc = head_w_kc(C);
+  const unsigned grid = (unsigned)head_w_blocks(num_rows);
+  const size_t lds = sizeof(float) * 4 * ((size_t)out_ch * (C + 1) + 1);
+#define SV2N_HW(O, K)                                                                           \
+  if (out_ch == O && kc == K) {                                                                 \
+    hipLaunchKernelGGL((k_head_mse_train_w<O, K, DEFER>), dim3(grid), dim3(256), lds, stream,  \
+                       x, num_rows, C, weight, bias, target, dx, workspace, g_weight, g_bias,   \
+                       loss, loss_sum, inv_count, scale, RW);                                   \
+    return (int)hipGetLastError();                                                              \
+  }
+  SV2N_HW(1, 1) SV2N_HW(1, 2) SV2N_HW(1, 4) SV2N_HW(1, 8) SV2N_HW(1, 16)
+  SV2N_HW(2, 1) SV2N_HW(2, 2) SV2N_HW(2, 4) SV2N_HW(2, 8) SV2N_HW(2, 16)
+  SV2N_HW(3, 1) SV2N_HW(3, 2) SV2N_HW(3, 4) SV2N_HW(3, 8)
+  SV2N_HW(4, 1) SV2N_HW(4, 2) SV2N_HW(4, 4) SV2N_HW(4, 8)
+#undef SV2N_HW
+  return SV2N_ERR_SHAPE;
+}
+
+extern "C" int sv2n_head_mse_train_rows(const float* x, int64_t num_rows, int in_features,
+                                        const float* weight, const float* bias, int out_features,
+                                        const float* target, float* dx, float* workspace,
+                                        int64_t workspace_floats, hipStream_t stream) {
+  const int out_ch = out_features;
+  if (!x || !weight || !target || !dx || !workspace) return SV2N_ERR_ARG;
+  if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
+  if (!head_w_ok(in_features, out_ch)) return SV2N_ERR_SHAPE;
+  if (workspace_floats < sv2n_head_mse_train_workspace(num_rows, in_features, out_ch))
+    return SV2N_ERR_WORKSPACE;
+  if ((uintptr_t)workspace & 15) return SV2N_ERR_ALIGN;
+  return head_w_launch<true>(x, num_rows, in_features, weight, bias, out_ch, target, nullptr,
+                             nullptr, dx, nullptr, nullptr, workspace, stream);
+}
+
+extern "C" int sv2n_head_mse_train_reduce(const float* workspace, int64_t num_rows,
+                                          int in_features, int out_features, float* loss,
+                                          float* loss_sum, float* g_weight, float* g_bias,
+                                          hipStream_t stream) {
+  const int out_ch = out_features;
+  if (!workspace || !loss) return SV2N_ERR_ARG;
+  if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
+  if (!head_w_ok(in_features, out_ch)) return SV2N_ERR_SHAPE;
+  const int stride = out_ch * (in_features + 1) + 1;
+  hipLaunchKernelGGL(k_head_mse_reduce_w, dim3((unsigned)((stride + 63) / 64)), dim3(512), 0,
+                     stream, workspace, (unsigned)head_w_blocks(num_rows), out_ch, in_features,
+                     g_weight, g_bias, loss, loss_sum, 1.f / (float)(num_rows * out_ch));
+  return (int)hipGetLastError();
+}
+
 extern "C" int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_features,
                                    const float* weight, const float* bias, int out_features,
                                    const float* target, float* loss, float* loss_sum, float* dx,
@@ -750,23 +860,9 @@ extern "C" int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_feat
   if ((uintptr_t)workspace & 15) return SV2N_ERR_ALIGN;
   const float inv_count = 1.f / (float)(num_rows * out_ch);
   const float scale = 2.f / (float)(num_rows * (int64_t)out_ch);
-  if (head_w_ok(in_features, out_ch)) {
-    const int C = in_features, RW = head_w_rows(num_rows), kc = head_w_kc(C);
-    const unsigned grid = (unsigned)head_w_blocks(num_rows);
-    const size_t lds = sizeof(float) * 4 * ((size_t)out_ch * (C + 1) + 1);
-#define SV2N_HW(O, K)                                                                           \
-  if (out_ch == O && kc == K) {                                                                 \
-    hipLaunchKernelGGL((k_head_mse_train_w<O, K>), dim3(grid), dim3(256), lds, stream, x,      \
-                       num_rows, C, weight, bias, target, dx, workspace, g_weight, g_bias, loss, \
-                       loss_sum, inv_count, scale, RW);                                         \
-    return (int)hipGetLastError();                                                              \
-  }
-    SV2N_HW(1, 1) SV2N_HW(1, 2) SV2N_HW(1, 4) SV2N_HW(1, 8) SV2N_HW(1, 16)
-    SV2N_HW(2, 1) SV2N_HW(2, 2) SV2N_HW(2, 4) SV2N_HW(2, 8) SV2N_HW(2, 16)
-    SV2N_HW(3, 1) SV2N_HW(3, 2) SV2N_HW(3, 4) SV2N_HW(3, 8)
-    SV2N_HW(4, 1) SV2N_HW(4, 2) SV2N_HW(4, 4) SV2N_HW(4, 8)
-#undef SV2N_HW
-  }
+  if (head_w_ok(in_features, out_ch))
+    return head_w_launch<false>(x, num_rows, in_features, weight, bias, out_ch, target, loss,
+                                loss_sum, dx, g_weight, g_bias, workspace, stream);
   const int R = head_rows_per_block(in_features, out_ch, num_rows);
   const unsigned grid = (unsigned)((num_rows + R - 1) / R);
   const size_t lds = head_lds_bytes(in_features, out_ch, num_rows);

@@ -107,6 +107,11 @@ _SCHEMAS = {
     "head_mse_train": "(Tensor x, Tensor weight, Tensor? bias, Tensor target, "
                       "Tensor(a!)? g_weight, Tensor(b!)? g_bias, Tensor(c!)? loss_sum=None) "
                       "-> (Tensor, Tensor)",
+    "head_mse_train_rows": "(Tensor x, Tensor weight, Tensor? bias, Tensor target, "
+                           "Tensor(a!) ws) -> Tensor",
+    "head_mse_train_reduce": "(Tensor ws, int num_rows, int in_features, int out_features, "
+                             "Tensor(a!) loss, Tensor(b!)? g_weight, Tensor(c!)? g_bias, "
+                             "Tensor(d!)? loss_sum=None) -> ()",
     "head_mse_bwd": "(Tensor x, Tensor weight, Tensor diff, Tensor grad_loss, "
                     "Tensor(a!)? g_weight, Tensor(b!)? g_bias) -> Tensor",
     "dropout_uniform": "(int rows, int cols, Tensor step, int seed, int salt) -> Tensor",
@@ -1060,6 +1065,65 @@ def _head_mse_train(x, weight, bias, target, g_weight, g_bias, loss_sum=None):
 @_fake("head_mse_train")
 def _head_mse_train_fake(x, weight, bias, target, g_weight, g_bias, loss_sum=None):
     return x.new_empty(()), torch.empty_like(x)
+
+
+def head_split_fits(in_features: int, out_features: int) -> bool:
+    """Whether sv2n_head_mse_train_rows / _reduce take this head (the
+    wave-per-rows kernel: in <= 1024, out <= 4, out * ceil(in / 64) <= 32)."""
+    kc = (in_features + 63) // 64
+    kc = 1 if kc <= 1 else 2 if kc <= 2 else 4 if kc <= 4 else 8 if kc <= 8 else 16
+    return 0 < out_features <= 4 and 0 < in_features <= 1024 and out_features * kc <= 32
+
+
+def head_split_workspace(num_rows: int, in_features: int, out_features: int,
+                         device) -> torch.Tensor:
+    """The persistent workspace of the two-launch head (its own key: the
+    reduce may still run on a side stream while other head ops run)."""
+    n = _lib.load().sv2n_head_mse_train_workspace(num_rows, in_features, out_features)
+    return _lib.persistent_zeros("head_split", n, device)
+
+
+@_impl("head_mse_train_rows")
+def _head_mse_train_rows(x, weight, bias, target, ws):
+    """First launch of the two-launch head + MSE training step
+    (sv2n_head_mse_train_rows): dx, and the block partials in ``ws``."""
+    lib = _lib.load()
+    _f32(x, weight, bias, target, ws)
+    _dense(x, weight, bias, ws)
+    N, C = x.shape
+    O = weight.shape[0]
+    target = target.reshape(-1).contiguous()
+    _need(target.numel() == N * O, f"target has {target.numel()} elements, expected {N * O}")
+    dx = torch.empty_like(x)
+    _lib.check(lib.sv2n_head_mse_train_rows(x.data_ptr(), N, C, weight.data_ptr(), _p(bias), O,
+                                            target.data_ptr(), dx.data_ptr(), ws.data_ptr(),
+                                            ws.numel(), _st(x)), "sv2n_head_mse_train_rows")
+    return dx
+
+
+@_fake("head_mse_train_rows")
+def _head_mse_train_rows_fake(x, weight, bias, target, ws):
+    return torch.empty_like(x)
+
+
+@_impl("head_mse_train_reduce")
+def _head_mse_train_reduce(ws, num_rows, in_features, out_features, loss, g_weight, g_bias,
+                           loss_sum=None):
+    """Second launch (sv2n_head_mse_train_reduce), on the current stream:
+    loss, loss_sum and the head's parameter gradients from ``ws``."""
+    lib = _lib.load()
+    _f32(ws, loss, g_weight, g_bias, loss_sum)
+    _dense(ws, loss, g_weight, g_bias, loss_sum)
+    _lib.check(lib.sv2n_head_mse_train_reduce(ws.data_ptr(), num_rows, in_features,
+                                              out_features, loss.data_ptr(), _p(loss_sum),
+                                              _p(g_weight), _p(g_bias), _st(ws)),
+               "sv2n_head_mse_train_reduce")
+
+
+@_fake("head_mse_train_reduce")
+def _head_mse_train_reduce_fake(ws, num_rows, in_features, out_features, loss, g_weight, g_bias,
+                                loss_sum=None):
+    return None
 
 
 # --------------------------------------------------------------------------

@@ -830,6 +830,40 @@ def head_mse_train(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tenso
                                          target, gw, gb, loss_sum)
 
 
+def head_mse_train_split(x: torch.Tensor, linear: torch.nn.Linear, target: torch.Tensor,
+                         loss_sum: Optional[torch.Tensor] = None):
+    """``head_mse_train`` in two launches: dx and the per-block partials now,
+    their reduction into the loss, ``loss_sum`` and the head's parameter
+    gradients when the caller runs ``finish()`` (``train.TrainStep``: after
+    the layer backwards, which need only dx).  The one-launch kernel's
+    two-level ticket chain sits between dx and the backward; the separate
+    reduce launch does not (C3 loop 433-437 K -> 439-443 K windows/s; running
+    it on a side stream beside the backward instead cost the hipGraph's
+    fork/join more than it saved: 421-423 K).  Returns ``(loss, dx, finish)``,
+    bitwise ``head_mse_train``'s results once ``finish`` ran; ``None`` when
+    the head does not fit the wave-per-rows kernel."""
+    _require_params((linear.weight, linear.bias))
+    _require_device(x, target)
+    if not (head_fits(linear.in_features, linear.out_features) and
+            library.head_split_fits(linear.in_features, linear.out_features)):
+        return None
+    gw = _grad_buf(linear.weight)
+    gb = _grad_buf(linear.bias) if linear.bias is not None else None
+    xa = _aligned(x.detach())
+    N, C = xa.shape
+    O = linear.out_features
+    ws = library.head_split_workspace(N, C, O, xa.device)
+    dx = torch.ops.sv2n.head_mse_train_rows(
+        xa, linear.weight.detach(), None if linear.bias is None else linear.bias.detach(),
+        target, ws)
+    loss = torch.empty((), device=xa.device)
+
+    def finish() -> None:
+        torch.ops.sv2n.head_mse_train_reduce(ws, N, C, O, loss, gw, gb, loss_sum)
+
+    return loss, dx, finish
+
+
 def linear_head(x: torch.Tensor, linear: torch.nn.Linear) -> torch.Tensor:
     """``linear(x)`` for GATModel's output layer on the sv2n head kernels
     (in_features <= 1024, out_features <= 16; otherwise the nn.Linear itself)."""

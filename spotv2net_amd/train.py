@@ -209,7 +209,7 @@ class TrainStep:
             return self._fwd_bwd_inner(sh)
 
     def _fwd_bwd_inner(self, sh: _Shape) -> None:
-        from .stack import direct_grad_accumulation, head_mse_train
+        from .stack import direct_grad_accumulation, head_mse_train, head_mse_train_split
         if sh.prepare is not None:
             sh.prepare()
         if not getattr(self.opt, "zeroes_grads", False):
@@ -225,9 +225,17 @@ class TrainStep:
                 if loss is not None:
                     sh.loss = loss.detach()
                     return
-                # ... or head + loss forward AND backward in one launch (the
-                # upstream gradient of the loss is 1), then the stack's backward
+                # ... or head + loss forward AND backward (the upstream
+                # gradient of the loss is 1), then the stack's backward: dx
+                # first, the loss and head-gradient reduction after the backward
                 h = self.model._hidden(sh.data)
+                res = head_mse_train_split(h, self.model.linear, sh.data.y_x, self.loss_sum)
+                if res is not None:
+                    loss, dh, finish = res
+                    torch.autograd.backward(h, dh)
+                    finish()
+                    sh.loss = loss.detach()
+                    return
                 res = head_mse_train(h, self.model.linear, sh.data.y_x, self.loss_sum)
                 if res is not None:
                     loss, dh = res

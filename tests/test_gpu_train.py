@@ -133,6 +133,38 @@ def test_head_mse_train_matches_fwd_bwd(dev, out_ch, rows, C):
     assert torch.equal(loss1, loss3) and torch.equal(dx1, dx3)
 
 
+@pytest.mark.parametrize("out_ch,rows,C", [(1, 15360, 50), (3, 180, 50), (1, 3840, 500),
+                                           (4, 1001, 500), (2, 777, 130), (1, 7, 500)])
+def test_head_mse_train_split_is_bitwise_one_launch(dev, out_ch, rows, C):
+    """sv2n_head_mse_train_rows + _reduce (ABI 19; the reduce after other
+    work, as TrainStep runs it) give the one-launch sv2n_head_mse_train's loss,
+    dx, accumulated head grads and loss_sum bit for bit."""
+    from spotv2net_amd import library
+    from spotv2net_amd.stack import head_mse_train_split
+    ops = torch.ops.sv2n
+    assert library.head_split_fits(C, out_ch)
+    torch.manual_seed(4)
+    x = torch.randn(rows, C, device=dev)
+    lin = torch.nn.Linear(C, out_ch).to(dev)
+    y = torch.randn(rows * out_ch, device=dev)
+    with torch.no_grad():
+        lin.weight.grad = torch.full_like(lin.weight, 0.5)
+        lin.bias.grad = torch.full_like(lin.bias, 0.25)
+    gw1, gb1 = lin.weight.grad.clone(), lin.bias.grad.clone()
+    ls1 = torch.full((), 1.5, device=dev)
+    ls2 = ls1.clone()
+    loss1, dx1 = ops.head_mse_train(x, lin.weight.detach(), lin.bias.detach(), y, gw1, gb1, ls1)
+    loss2, dx2, finish = head_mse_train_split(x, lin, y, ls2)
+    _ = x * 2.0  # unrelated work between the two launches
+    finish()
+    torch.cuda.synchronize()
+    assert torch.equal(loss1, loss2) and torch.equal(dx1, dx2)
+    assert torch.equal(gw1, lin.weight.grad) and torch.equal(gb1, lin.bias.grad)
+    assert torch.equal(ls1, ls2)
+    # the ops themselves: shape refusal outside the wave-per-rows kernel
+    assert not library.head_split_fits(2000, 1) and not library.head_split_fits(50, 5)
+
+
 def test_trainstep_fused_head_matches_reference_steps(dev):
     """TrainStep's captured step (fused head+loss launch, then the GAT stack's
     backward) == k eager steps of nn.MSELoss + backward + torch.optim.Adam
