@@ -674,6 +674,23 @@ int sv2n_window_gather_bf16x(const float* vol, const float* volvol, const float*
                              int64_t num_windows, int seq_length, int future_steps,
                              const uint16_t* canon, float* x, uint16_t* x_bf16, int64_t ld_xb,
                              float* edge_attr, float* y, hipStream_t stream);
+/* The window gather for a consumer that reads edge_attr only through the
+ * covariance-layout edge passes (sv2n_edge_logits_fwd_cv / _bwd_cv; ABI 19):
+ * x, y (and bf16(x) when x_bf16 is not NULL, as sv2n_window_gather_bf16x)
+ * in full, but of edge_attr only the covariance columns [0, S) of the upper
+ * rows, the source-variance columns [S, 2S) of upper row 0 and the
+ * target-variance columns [2S, 3S) of the upper rows of the pairs (0, w),
+ * and the covariance columns of the first (16 - P % 16) % 16 lower rows
+ * (the even-S passes' last tile of 16 upper rows runs into them with zero
+ * d-logits): what those passes read (≈ 1/6 of the edge bytes).  The rest of edge_attr
+ * is left as it was; any other reader of it is the caller's error.  Windows
+ * outside the series give NaN rows as in sv2n_window_gather_diag.  Row-kernel
+ * shapes only (see sv2n_window_gather_bf16x); else SV2N_ERR_SHAPE. */
+int sv2n_window_gather_cv(const float* vol, const float* volvol, const float* diag, int n,
+                          int64_t num_matrices, const int64_t* starts, int64_t start_offset,
+                          int64_t num_windows, int seq_length, int future_steps,
+                          const uint16_t* canon, float* x, uint16_t* x_bf16, int64_t ld_xb,
+                          float* edge_attr, float* y, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -145,6 +145,8 @@ _SIGNATURES = {
                                        _p, _p, _p]),
     "sv2n_window_gather_bf16x": (_i32, [_p, _p, _p, _i32, _i64, _p, _i64, _i64, _i32, _i32, _p,
                                         _p, _p, _i64, _p, _p, _p]),
+    "sv2n_window_gather_cv": (_i32, [_p, _p, _p, _i32, _i64, _p, _i64, _i64, _i32, _i32, _p,
+                                     _p, _p, _i64, _p, _p, _p]),
     "sv2n_head_bwd_workspace": (_i64, [_i64, _i32, _i32]),
     "sv2n_head_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _p, _p, _i64, _p]),
 }

@@ -79,11 +79,17 @@ __global__ __launch_bounds__(256) void k_window_gather(
 //   copies (canonical order: both runs are contiguous, 3S floats per row)
 //   y[(b*n+u)*F .. +F)
 // 3 * S * (n+1) floats of LDS.  diag (optional): diag[t][v] = volvol[t][v][v].
+// cv_only (sv2n_window_gather_cv): of the edge rows only what the
+// covariance-layout edge passes read (sv2n_edge.hip cv_var_row): the
+// covariance columns of the upper rows, and in workgroup u = 0 the target
+// variance columns of the pairs (0, w) and the source variance columns of
+// pair (0, 1), plus the covariance columns of the lower rows the passes' last
+// 16-row tile reaches — ≈ 1/6 of the edge bytes; the rest is not written.
 __global__ __launch_bounds__(256) void k_window_rows(
     const float* __restrict__ vol, const float* __restrict__ volvol, int n, int64_t T,
     const int64_t* __restrict__ starts, int64_t soff, int S, int F,
     const float* __restrict__ diag, float* __restrict__ x, float* __restrict__ ea,
-    float* __restrict__ y, unsigned short* __restrict__ xb, int64_t ldxb) {
+    float* __restrict__ y, unsigned short* __restrict__ xb, int64_t ldxb, int cv_only) {
   extern __shared__ float lds[];
   const int NP = n + 1;
   float* sv = lds;             // [S][NP] vol[t][u][v]
@@ -170,6 +176,24 @@ __global__ __launch_bounds__(256) void k_window_rows(
   const int RW = 3 * S;
   float* up = ea + (b * E0 + e0) * (int64_t)RW;
   float* lo = ea + (b * E0 + P + e0) * (int64_t)RW;
+  if (cv_only) {
+    // the passes' last tile of 16 upper rows runs into the first lower rows
+    // (their d-logits are zero there): those rows' covariance columns too, so
+    // the products stay finite and bitwise those of the full gather
+    const int pad = (16 - P % 16) % 16;
+    const int lane = t & 63, wv = wave_id();
+    for (int r = wv; r < m; r += 4) {
+      const int w = u + 1 + r;
+      const int qe = u == 0 ? RW : S;  // u > 0: the covariance columns only
+      for (int q = lane; q < qe; q += 64) {
+        const int kind = q / S, tt = q - kind * S;
+        if (kind == 1 && r != 0) continue;  // source variance: pair (0, 1) only
+        up[r * RW + q] = kind == 0 ? sw[tt * NP + w] : (kind == 1 ? sw[tt * NP + u] : sd[tt * NP + w]);
+        if (kind == 0 && e0 + r < pad) lo[r * RW + q] = sw[tt * NP + w];
+      }
+    }
+    return;
+  }
   if ((S & 1) == 0 && RW <= 2 * 64 && (((uintptr_t)up) & 7) == 0 && (((uintptr_t)lo) & 7) == 0) {
     // one wave per edge row, two adjacent columns per lane (8-B stores; S even:
     // both columns have the same kind), (kind, t) decoded once
@@ -255,7 +279,29 @@ extern "C" int sv2n_window_gather_bf16x(const float* vol, const float* volvol,
     return SV2N_ERR_SHAPE;
   hipLaunchKernelGGL(k_window_rows, dim3((unsigned)(num_windows * n)), dim3(256), lds, stream,
                      vol, volvol, n, num_matrices, starts, start_offset, seq_length, future_steps,
-                     diag, x, edge_attr, y, reinterpret_cast<unsigned short*>(x_bf16), ld_xb);
+                     diag, x, edge_attr, y, reinterpret_cast<unsigned short*>(x_bf16), ld_xb, 0);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sv2n_window_gather_cv(const float* vol, const float* volvol, const float* diag,
+                                     int n, int64_t num_matrices, const int64_t* starts,
+                                     int64_t start_offset, int64_t num_windows, int seq_length,
+                                     int future_steps, const uint16_t* canon, float* x,
+                                     uint16_t* x_bf16, int64_t ld_xb, float* edge_attr, float* y,
+                                     hipStream_t stream) {
+  if (!vol || !volvol || !starts || !canon || !x || !edge_attr || !y) return SV2N_ERR_ARG;
+  if (n < 2 || n > SV2N_MAX_N_TILED || num_windows < 1 || seq_length < 1 || future_steps < 1 ||
+      num_matrices < 1)
+    return SV2N_ERR_SHAPE;
+  const size_t lds = sizeof(float) * 3 * (size_t)seq_length * (n + 1);
+  if (lds > 64 * 1024 || future_steps > 256) return SV2N_ERR_SHAPE;
+  if (x_bf16 && (((int64_t)n * seq_length) % 4 || ld_xb < (int64_t)n * seq_length ||
+                 (ld_xb & 3) || ((uintptr_t)x & 15) || ((uintptr_t)x_bf16 & 7)))
+    return SV2N_ERR_SHAPE;
+  hipLaunchKernelGGL(k_window_rows, dim3((unsigned)(num_windows * n)), dim3(256), lds, stream,
+                     vol, volvol, n, num_matrices, starts, start_offset, seq_length, future_steps,
+                     diag, x, edge_attr, y, reinterpret_cast<unsigned short*>(x_bf16),
+                     x_bf16 ? ld_xb : (int64_t)0, 1);
   return (int)hipGetLastError();
 }
 
@@ -276,7 +322,7 @@ extern "C" int sv2n_window_gather_diag(const float* vol, const float* volvol,
   if (lds <= 64 * 1024 && future_steps <= 256) {
     hipLaunchKernelGGL(k_window_rows, dim3((unsigned)(num_windows * n)), dim3(256), lds, stream,
                        vol, volvol, n, num_matrices, starts, start_offset, seq_length, future_steps,
-                       diag, x, edge_attr, y, (unsigned short*)nullptr, (int64_t)0);
+                       diag, x, edge_attr, y, (unsigned short*)nullptr, (int64_t)0, 0);
     return (int)hipGetLastError();
   }
   const int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);

@@ -22,7 +22,8 @@ from typing import Optional, Sequence
 
 import torch
 
-from .layout import canonical_edge_index, canonical_pairs, is_canonical_graph, mark_cov_var
+from .layout import (canonical_edge_index, canonical_pairs, is_canonical_graph, mark_cov_var,
+                     mark_cov_var_only)
 
 _FIELDS = ("x", "edge_index", "edge_attr", "y_x")
 
@@ -248,13 +249,19 @@ class WindowDataset:
         self.diag = torch.diagonal(volvol, dim1=1, dim2=2).contiguous() \
             if volvol.dtype == torch.float32 else None
 
-    def empty_batch(self, batch_size: int, bf16_x: bool = False) -> Batch:
+    def empty_batch(self, batch_size: int, bf16_x: bool = False,
+                    cov_var_only: bool = False) -> Batch:
         """Static device buffers of one batch of ``batch_size`` windows (the
         layout of ``batch``), for ``fill``: a hipGraph-captured train step
         reads the same tensors every replay.  ``bf16_x``: ``fill`` also
         writes bf16(x) (round to nearest even) beside x, which the bf16
         execution mode's layer-0 GEMMs read instead of rounding x themselves
-        (``bf16_twin``)."""
+        (``bf16_twin``).  ``cov_var_only``: ``fill`` writes of edge_attr only
+        the columns the covariance-layout edge passes read
+        (sv2n_window_gather_cv, ≈ 1/6 of its bytes) — for a consumer that
+        reads it through those passes alone (``train.Fit`` when
+        ``stack.cov_var_edges_only`` says so); any other edge path refuses the
+        batch (``layout.check_full_edge_attr``)."""
         B, n, S = batch_size, self.n, self.S
         E0 = n * (n - 1)
         dev = self.vol.device
@@ -271,6 +278,10 @@ class WindowDataset:
                 b._x_bf16 = torch.zeros(B * n, (n * S + 63) // 64 * 64, device=dev,
                                         dtype=torch.bfloat16)
                 b._x_bf16_of = (b.x.data_ptr(), b.x._version)
+        if cov_var_only and dev.type == "cuda" and self.vol.dtype == torch.float32 and \
+                self.volvol.dtype == torch.float32 and 3 * S * (n + 1) * 4 <= 64 * 1024 and \
+                self.future_steps <= 256:
+            b._cov_var_only = True
         return b
 
     def fill(self, out: Batch, idx: torch.Tensor) -> None:
@@ -292,11 +303,15 @@ class WindowDataset:
             from . import library  # noqa: F401
             from .layout import canonical_table
             xb = bf16_twin(out)
+            cv_only = bool(getattr(out, "_cov_var_only", False))
             torch.ops.sv2n.window_gather(self.vol.contiguous(), self.volvol.contiguous(),
                                          idx if idx.dtype == torch.long else idx.long(), S, Fs,
                                          canonical_table(n, self.vol.device), out.x,
-                                         out.edge_attr, out.y_x, self.cut, self.diag, xb)
+                                         out.edge_attr, out.y_x, self.cut, self.diag, xb,
+                                         cv_only)
             mark_cov_var(out.edge_attr, S)
+            if cv_only:
+                mark_cov_var_only(out.edge_attr)
             return
         st = self.starts.index_select(0, idx)
         tidx = st.view(B, 1) + self._arS.view(1, S)                               # [B, S]

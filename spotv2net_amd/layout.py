@@ -97,6 +97,25 @@ def canonical_pairs(n: int) -> tuple[list[int], list[int]]:
 _canon_cache: dict = {}
 
 
+def mark_cov_var_only(edge_attr: torch.Tensor) -> torch.Tensor:
+    """Record that ``edge_attr`` holds only the columns the covariance-layout
+    edge passes read (sv2n_window_gather_cv: the covariance columns of the
+    upper rows and one variance series per node); the rest is unwritten.  The
+    flag is permanent (not tied to the tensor's version): the fused stack
+    refuses such a tensor on any other edge path, and so does GATModel's
+    edge BatchNorm (``check_full_edge_attr``)."""
+    edge_attr._sv2n_cov_var_only = True
+    return edge_attr
+
+
+def check_full_edge_attr(edge_attr: Optional[torch.Tensor], what: str) -> None:
+    """Raise when ``edge_attr`` is a ``mark_cov_var_only`` buffer."""
+    if edge_attr is not None and getattr(edge_attr, "_sv2n_cov_var_only", False):
+        raise RuntimeError(
+            f"sv2n: {what} reads all of edge_attr, but this batch holds only the columns "
+            "of the covariance-layout edge passes (WindowDataset.empty_batch(cov_var_only=True))")
+
+
 def mark_cov_var(edge_attr: Optional[torch.Tensor], seq_length: int):
     """Record that ``edge_attr`` holds edge features in the reference's
     covariance layout (utils/dataset.py:228-243, :279-282: row s -> t is

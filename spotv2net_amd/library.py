@@ -121,7 +121,7 @@ _SCHEMAS = {
     "window_gather": "(Tensor vol, Tensor volvol, Tensor starts, int seq_length, "
                      "int future_steps, Tensor canon, Tensor(a!) x, Tensor(b!) edge_attr, "
                      "Tensor(c!) y, int start_offset=0, Tensor? diag=None, "
-                     "Tensor(d!)? x_bf16=None) -> ()",
+                     "Tensor(d!)? x_bf16=None, bool cov_var_only=False) -> ()",
     "project_a16": "(Tensor a_bf16, int k, Tensor planes, Tensor w) -> Tensor",
 }
 for _name, _schema in _SCHEMAS.items():
@@ -1172,7 +1172,10 @@ def _adam_step_fake(param, grad, exp_avg, exp_avg_sq, step, ticket, lr, beta1, b
 
 @_impl("window_gather")
 def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y,
-                   start_offset=0, diag=None, x_bf16=None):
+                   start_offset=0, diag=None, x_bf16=None, cov_var_only=False):
+    """``cov_var_only``: of edge_attr only what the covariance-layout edge
+    passes read (sv2n_window_gather_cv); the caller vouches that nothing
+    else reads it (data.WindowDataset.empty_batch(cov_var_only=True))."""
     lib = _lib.load()
     _f32(vol, volvol, x, edge_attr, y)
     _need(vol.is_contiguous() and volvol.is_contiguous(), "series must be contiguous")
@@ -1191,6 +1194,15 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
     if x_bf16 is not None:  # bf16(x) beside x (sv2n_window_gather_bf16x)
         _need(x_bf16.dtype == torch.bfloat16 and x_bf16.dim() == 2 and
               x_bf16.shape[0] == x.shape[0] and x_bf16.stride(1) == 1, "x_bf16 layout")
+    if cov_var_only:
+        _lib.check(lib.sv2n_window_gather_cv(
+            vol.data_ptr(), volvol.data_ptr(), _p(diag), vol.shape[1], vol.shape[0],
+            starts.data_ptr(), start_offset, starts.numel(), seq_length, future_steps,
+            canon.data_ptr(), x.data_ptr(), _p(x_bf16),
+            0 if x_bf16 is None else x_bf16.stride(0), edge_attr.data_ptr(), y.data_ptr(),
+            _st(vol)), "sv2n_window_gather_cv")
+        return
+    if x_bf16 is not None:
         _lib.check(lib.sv2n_window_gather_bf16x(
             vol.data_ptr(), volvol.data_ptr(), _p(diag), vol.shape[1], vol.shape[0],
             starts.data_ptr(), start_offset, starts.numel(), seq_length, future_steps,
@@ -1207,7 +1219,7 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
 
 @_fake("window_gather")
 def _window_gather_fake(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y,
-                        start_offset=0, diag=None, x_bf16=None):
+                        start_offset=0, diag=None, x_bf16=None, cov_var_only=False):
     return None
 
 

@@ -29,7 +29,7 @@ from torch import nn
 from . import graphed, ops
 from .conv import GATConv
 from .data import bf16_twin
-from .layout import GraphLayout, analyze_edge_index, declare_canonical
+from .layout import GraphLayout, analyze_edge_index, check_full_edge_attr, declare_canonical
 from .stack import gat_stack, gat_train_head_mse, head_mse_loss, linear_head
 
 
@@ -128,6 +128,7 @@ class GATModel(nn.Module):
         if self.standardize:
             x = self.bnorm_node(x)
             if edge_attr is not None:
+                check_full_edge_attr(edge_attr, "GATModel's edge BatchNorm (standardize)")
                 edge_attr = self.bnorm_edge(edge_attr)
         if layout is None:
             layout = _layout_of(data, x, edge_index)

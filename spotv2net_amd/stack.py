@@ -37,7 +37,7 @@ from typing import Optional, Sequence
 import torch
 
 from . import _lib, library  # noqa: F401  (library registers torch.ops.sv2n)
-from .layout import GraphLayout, cov_var_seq_length
+from .layout import GraphLayout, check_full_edge_attr, cov_var_seq_length
 from .library import edge_order, fused_supported
 from .ops import ACT_CODES, _aligned, _require_device, relu_mask_fusable, resolve_precision
 
@@ -216,6 +216,24 @@ def _side_stream(dev):
     return _SIDE[key]
 
 
+def cov_var_edges_only(convs, n: int, seq_length: int) -> bool:
+    """Whether the fused stack reads the edge features of canonical complete
+    batches (n nodes, edge_attr in the covariance layout of windows of
+    ``seq_length``) only through the covariance-layout edge passes, forward
+    and backward — the condition for ``WindowDataset.empty_batch(
+    cov_var_only=True)`` (``train.Fit``).  Mirrors ``stack_forward``'s ``cv``
+    test, which refuses such a batch on any other path."""
+    if COV_VAR_EDGES != "on" or COV_VAR_BWD != "on" or not convs:
+        return False
+    if any(c.lin_edge is None for c in convs):
+        return False
+    H = convs[0].heads
+    if any(c.heads != H for c in convs):
+        return False
+    # even seq_length: the k_edge_*_cv2 passes, whose reads sv2n_window_gather_cv covers
+    return 2 <= n <= 32 and seq_length <= 64 and seq_length % 2 == 0 and len(convs) * H <= 16
+
+
 def _use_fused(layout: GraphLayout, convs, D: int, num_edges: int) -> bool:
     """Edge-fused attention (sv2n_attn_fused.hip) instead of edge pass + planes.
 
@@ -356,6 +374,8 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
               layout.kind == "canonical" and 2 <= n <= 32 and s_cv <= 64 and L * H <= 16 and
               ea.size(1) == 3 * s_cv and ea.size(0) == B * n * (n - 1))
     LAST_PATH["cov_var"] = cv
+    if use_edge and not (cv and (COV_VAR_BWD == "on" or not training)):
+        check_full_edge_attr(edge_attr, "this model's edge path (not the covariance-layout passes)")
 
     def edge_fwd():
         if cv:

@@ -433,6 +433,11 @@ class Fit:
         self.epoch = 0
         self._idx = {}     # batch size -> static index buffer
         self._batch = {}   # batch size -> static Batch
+        # the edge features are read only by the covariance-layout edge passes:
+        # the gather writes just their columns (sv2n_window_gather_cv)
+        from .stack import cov_var_edges_only
+        self._cv_only = bool(not getattr(model, "standardize", False) and
+                             cov_var_edges_only(list(model.gat_layers), dataset.n, dataset.S))
         sizes = [self.bs] if self.n_train >= self.bs else []
         if self.n_train % self.bs:
             sizes.append(self.n_train % self.bs)
@@ -461,7 +466,8 @@ class Fit:
             self._idx[b] = torch.zeros(b, dtype=torch.long, device=self.dev)
             # the bf16 mode's layer-0 GEMMs read bf16(x) from the gather
             self._batch[b] = self.ds.empty_batch(
-                b, bf16_x=getattr(self.model, "precision", None) == "bf16")
+                b, bf16_x=getattr(self.model, "precision", None) == "bf16",
+                cov_var_only=self._cv_only)
             self.ds.fill(self._batch[b], self._idx[b])
         data, idx = self._batch[b], self._idx[b]
         return data, (lambda: self.ds.fill(data, idx))
@@ -479,7 +485,8 @@ class Fit:
             # index buffer every step)
             idx = torch.arange(self.n_train, self.n_train + n_test, device=self.dev)
             data = self.ds.empty_batch(
-                n_test, bf16_x=getattr(self.model, "precision", None) == "bf16")
+                n_test, bf16_x=getattr(self.model, "precision", None) == "bf16",
+                cov_var_only=self._cv_only)
             self.ds.fill(data, idx)
             prep = (lambda: self.ds.fill(data, idx))
             rows = data.x.shape[0] // n_test  # nodes per window

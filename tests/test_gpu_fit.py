@@ -195,3 +195,30 @@ def test_test_pass_equals_per_batch_losses(dev, bs):
             losses.append(torch.nn.functional.mse_loss(m(b), b.y_x).item())
     want = sum(losses) / len(losses)
     assert abs(rec["test_loss"] - want) <= 1e-6 * abs(want), (rec["test_loss"], want)
+
+
+def test_fit_cov_var_only_gather_is_bitwise_full_gather(dev, monkeypatch):
+    """Fit gathers only the covariance-layout columns of edge_attr when the
+    model reads them through those passes alone (sv2n_window_gather_cv); the
+    loss history and the trained parameters are those of the full gather."""
+    import copy
+
+    from spotv2net_amd import GATModel, stack
+    from spotv2net_amd.train import Fit
+    _, ds = _data(dev)
+    torch.manual_seed(11)
+    m0 = GATModel(30 * S, 3 * S, 4, 1, [32, 16], concat_heads=True, dropout=0.1).to(dev)
+    runs = []
+    for cv in (True, False):
+        if not cv:
+            monkeypatch.setattr(stack, "cov_var_edges_only", lambda *a: False)
+        m = copy.deepcopy(m0)
+        torch.manual_seed(5)
+        f = Fit(m, ds, 24, generator=torch.Generator().manual_seed(3))
+        assert f._cv_only == cv
+        hist = [f.run_epoch() for _ in range(2)]
+        runs.append((hist, [p.detach().clone() for p in m.parameters()]))
+    (h0, p0), (h1, p1) = runs
+    assert h0 == h1
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b)
