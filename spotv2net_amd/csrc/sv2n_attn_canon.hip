@@ -22,6 +22,8 @@
 //    scalar offset register), ahead of the MFMAs that use them.
 #include "sv2n_common.h"
 
+#include <cstdlib>
+
 namespace sv2n {
 namespace canon {
 
@@ -1017,14 +1019,30 @@ struct CanonBwdPlan {
 };
 // single: the fewest splits (the edge-gradient tail needs a whole graph per
 // workgroup, whatever B)
-static CanonBwdPlan canon_bwd_plan(int64_t B, int H, int C, bool single = false) {
+// SV2N_CANON_BWD_S=s: that many head splits where valid (A/B switch)
+static int canon_bwd_forced_s() {
+  static const int v = [] {
+    const char* e = std::getenv("SV2N_CANON_BWD_S");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+// mean (head-mean layers): every split re-reads the graph's dy / y / dropout
+// draws, so the split count stops at 384 workgroups (C3, B 128: 3 splits of
+// two heads, 44.9 µs in the loop against 51.3 for 6 splits of one,
+// profiles/r05_c3_bwd_splits.txt)
+constexpr int64_t CANON_FILL_MEAN = 384;
+static CanonBwdPlan canon_bwd_plan(int64_t B, int H, int C, bool single = false,
+                                   bool mean = false) {
   const int nch = (C + 31) >> 5;
   int S = 1;
+  const int fs = single ? 0 : canon_bwd_forced_s();
+  const int64_t fill = mean ? CANON_FILL_MEAN : CANON_FILL;
   for (int s = 1; s <= H; ++s) {
     const int hs = (H + s - 1) / s;
     if (hs > 4 || (H + hs - 1) / hs != s) continue;  // one head per wave; no empty split
     S = s;
-    if (single || B * s >= CANON_FILL) break;
+    if (fs > 0 ? s >= fs : (single || B * s >= fill)) break;
   }
   const int HS = (H + S - 1) / S;
   const int WPH = max(1, min(4 / HS, nch));
@@ -1048,7 +1066,7 @@ static void launch_canon_bwd(int64_t B, hipStream_t st, const float* dy, const f
                              const uint32_t* rowmask, float* dxs, float* dae,
                              int ae_edge_order, float* dbias, int n, int H, int C, float slope,
                              const EdgeTail& et, unsigned short* dxb, int ldb) {
-  const CanonBwdPlan pl = canon_bwd_plan(B, H, C, et.ea != nullptr);
+  const CanonBwdPlan pl = canon_bwd_plan(B, H, C, et.ea != nullptr, !CONCAT);
   const size_t lds = attn_canon_bwd_lds(pl.HS);
   const unsigned grid = canon_grid(B, pl.S);
   // two chunks in flight per wave when every workgroup is resident at 2 waves
