@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 19
+#define SV2N_ABI_VERSION 20
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -515,14 +515,17 @@ int sv2n_head_mse_train(const float* x, int64_t num_rows, int in_features, const
  * after _rows) sums them into loss, loss_sum, g_weight, g_bias.  The caller
  * runs _reduce after the layer backwards, which need only dx, instead of the
  * one-launch form's ticket chain ahead of them.  Bitwise equal to the
- * one-launch sv2n_head_mse_train. */
+ * one-launch sv2n_head_mse_train.  ABI 20: _reduce takes the workspace size
+ * too and refuses one smaller than sv2n_head_mse_train_workspace (a mismatch
+ * with the _rows launch would otherwise read past the caller's buffer). */
 int sv2n_head_mse_train_rows(const float* x, int64_t num_rows, int in_features,
                              const float* weight, const float* bias, int out_features,
                              const float* target, float* dx, float* workspace,
                              int64_t workspace_floats, hipStream_t stream);
-int sv2n_head_mse_train_reduce(const float* workspace, int64_t num_rows, int in_features,
-                               int out_features, float* loss, float* loss_sum, float* g_weight,
-                               float* g_bias, hipStream_t stream);
+int sv2n_head_mse_train_reduce(const float* workspace, int64_t workspace_floats,
+                               int64_t num_rows, int in_features, int out_features, float* loss,
+                               float* loss_sum, float* g_weight, float* g_bias,
+                               hipStream_t stream);
 
 /* Fused attention for dense-block graphs of 32 < n <= 256 nodes (any n <= 256
  * works; n <= 32 is faster on sv2n_gat_attn_fwd/bwd).  Same semantics and

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SV2N_LIB: an alternative build of the same library (diagnostic builds, e.g.
 # tools/stamps.py); default the in-tree one
 LIB_PATH = os.environ.get("SV2N_LIB") or os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p
@@ -135,7 +135,7 @@ _SIGNATURES = {
     "sv2n_head_mse_train": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _i64,
                                    _p]),
     "sv2n_head_mse_train_rows": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _i64, _p]),
-    "sv2n_head_mse_train_reduce": (_i32, [_p, _i64, _i32, _i32, _p, _p, _p, _p, _p]),
+    "sv2n_head_mse_train_reduce": (_i32, [_p, _i64, _i64, _i32, _i32, _p, _p, _p, _p, _p]),
     "sv2n_head_mse_fwd": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "sv2n_head_mse_bwd": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "sv2n_head_fwd": (_i32, [_p, _i64, _i32, _p, _p, _i32, _p, _p]),

@@ -832,14 +832,16 @@ extern "C" int sv2n_head_mse_train_rows(const float* x, int64_t num_rows, int in
                              nullptr, dx, nullptr, nullptr, workspace, stream);
 }
 
-extern "C" int sv2n_head_mse_train_reduce(const float* workspace, int64_t num_rows,
-                                          int in_features, int out_features, float* loss,
-                                          float* loss_sum, float* g_weight, float* g_bias,
-                                          hipStream_t stream) {
+extern "C" int sv2n_head_mse_train_reduce(const float* workspace, int64_t workspace_floats,
+                                          int64_t num_rows, int in_features, int out_features,
+                                          float* loss, float* loss_sum, float* g_weight,
+                                          float* g_bias, hipStream_t stream) {
   const int out_ch = out_features;
   if (!workspace || !loss) return SV2N_ERR_ARG;
   if (int rc = head_check(num_rows, in_features, out_ch)) return rc;
   if (!head_w_ok(in_features, out_ch)) return SV2N_ERR_SHAPE;
+  if (workspace_floats < sv2n_head_mse_train_workspace(num_rows, in_features, out_ch))
+    return SV2N_ERR_WORKSPACE;
   const int stride = out_ch * (in_features + 1) + 1;
   hipLaunchKernelGGL(k_head_mse_reduce_w, dim3((unsigned)((stride + 63) / 64)), dim3(512), 0,
                      stream, workspace, (unsigned)head_w_blocks(num_rows), out_ch, in_features,

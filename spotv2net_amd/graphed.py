@@ -277,13 +277,23 @@ torch.nn.modules.module.register_module_parameter_registration_hook(_bump_param_
 torch.nn.modules.module.register_module_module_registration_hook(_bump_param_gen)
 
 
+def _optional_slots(model) -> tuple:
+    """(parameter dict, the bias it held) of the head and of every layer.
+    ``module.bias = None`` goes through ``register_parameter(name, None)``,
+    which calls no registration hook, so the cached list also checks these
+    slots by identity (a stale list would replay a graph that still adds the
+    removed bias)."""
+    mods = [model.linear, *model.gat_layers]
+    return tuple((m._parameters, m._parameters.get("bias")) for m in mods)
+
+
 def _params(model) -> list:
     c = model.__dict__.get("_sv2n_params")
-    if c is not None and c[0] == _PARAM_GEN[0]:
+    if c is not None and c[0] == _PARAM_GEN[0] and all(d.get("bias") is b for d, b in c[2]):
         return c[1]
     ps = [p for c in model.gat_layers for p in layer_params(c)] + \
         [model.linear.weight] + ([model.linear.bias] if model.linear.bias is not None else [])
-    model.__dict__["_sv2n_params"] = (_PARAM_GEN[0], ps)
+    model.__dict__["_sv2n_params"] = (_PARAM_GEN[0], ps, _optional_slots(model))
     return ps
 
 

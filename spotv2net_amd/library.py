@@ -1114,7 +1114,11 @@ def _head_mse_train_reduce(ws, num_rows, in_features, out_features, loss, g_weig
     lib = _lib.load()
     _f32(ws, loss, g_weight, g_bias, loss_sum)
     _dense(ws, loss, g_weight, g_bias, loss_sum)
-    _lib.check(lib.sv2n_head_mse_train_reduce(ws.data_ptr(), num_rows, in_features,
+    need = lib.sv2n_head_mse_train_workspace(num_rows, in_features, out_features)
+    if ws.numel() < need:
+        raise ValueError(f"head_mse_train_reduce: workspace has {ws.numel()} floats, "
+                         f"the shape needs {need}")
+    _lib.check(lib.sv2n_head_mse_train_reduce(ws.data_ptr(), ws.numel(), num_rows, in_features,
                                               out_features, loss.data_ptr(), _p(loss_sum),
                                               _p(g_weight), _p(g_bias), _st(ws)),
                "sv2n_head_mse_train_reduce")

@@ -350,7 +350,11 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
     # 1) weight preparation: every layer's folded Waug, its bf16 split planes
     #    (and the transposed ones the backward's dx GEMM needs) and the edge
     #    fold, in one launch (sv2n::gat_prep)
-    need_t = [bool(training and (l > 0 or x.requires_grad)) for l in range(L)]
+    # the transposed planes feed the backward's dX GEMMs: whenever a backward
+    # may run (need_saved: training, or eval mode with a gradient asked for),
+    # not only in training — in bf16 mode Waug is a placeholder the dX GEMM
+    # cannot fall back to
+    need_t = [bool(need_saved and (l > 0 or x.requires_grad)) for l in range(L)]
     waugs, planes, planes_t, wf = ops.gat_prep(
         [c.lin_src.weight for c in convs], [c.att_src for c in convs],
         [c.att_dst for c in convs], [c.lin_edge.weight for c in convs] if use_edge else [],

@@ -22,6 +22,7 @@ concatenated batch for a mean-reduced loss of equal per-rank batch sizes.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional
 
 import torch
@@ -404,6 +405,10 @@ class ForwardStep:
 # ---------------------------------------------------------------------------
 # the reference's training loop (5_train_SpotV2Net.py:86-197) on the device
 # ---------------------------------------------------------------------------
+# device-memory budget of one captured test forward (Fit.eval_chunk): C3's
+# 432 test windows (~2 MB each) stay one forward
+EVAL_BYTES = int(os.environ.get("SV2N_EVAL_BYTES", 1 << 30))
+
 class Fit:
     """5_train_SpotV2Net.py's loop over a device-resident WindowDataset:
     train/test split ``int(split * len)`` (:86-88), DataLoader(shuffle=True)
@@ -472,44 +477,81 @@ class Fit:
         data, idx = self._batch[b], self._idx[b]
         return data, (lambda: self.ds.fill(data, idx))
 
-    def _eval_pass(self) -> ForwardStep:
+    def _window_bytes(self) -> int:
+        """Device bytes one test window costs in the captured test forward:
+        x (and its bf16 twin), edge_attr, and per layer xs, y and the layer
+        output (an upper bound: the gather may write fewer edge columns)."""
+        n, S = self.ds.n, self.ds.S
+        b = 6 * n * n * S + 4 * n * (n - 1) * 3 * S
+        for c in self.model.gat_layers:
+            b += 3 * 4 * n * (c.heads * c.out_channels + 2 * c.heads)
+        return b
+
+    def eval_chunk(self) -> int:
+        """Test windows per captured test forward: every test window in one
+        forward while that fits EVAL_BYTES, else the largest multiple of the
+        batch size that does (at least one batch), so the test pass's memory
+        is bounded by the budget, not by the test split."""
+        nb = -(-self.n_test // self.bs)
+        k = max(1, min(nb, EVAL_BYTES // max(1, self._window_bytes() * self.bs)))
+        return min(self.n_test, k * self.bs)
+
+    def _eval_pass(self):
         """The test pass (5_train_SpotV2Net.py:166-180: sequential batches of
-        ``bs``, each batch's MSE added up) as ONE captured forward over every
-        test window: the graphs are independent and eval mode draws no
-        dropout, so each window's output is the one its batch would give, and
-        each batch's loss is its own row slice's mean (one fused head + MSE
-        launch per batch, added to the epoch's test sum in batch order)."""
+        ``bs``, each batch's MSE added up) as captured forwards over chunks of
+        ``eval_chunk()`` test windows (normally one chunk: all of them): the
+        graphs are independent and eval mode draws no dropout, so each window's
+        output is the one its batch would give, and each batch's loss is its
+        own row slice's mean (one fused head + MSE launch per batch, added to
+        the epoch's test sum in batch order; chunks are multiples of the batch
+        size, so batch boundaries never straddle a chunk).  Returns
+        ({chunk size: (ForwardStep, index buffer)}, chunk, test indices)."""
         if "all" not in self._eval:
             n_test, bs = self.n_test, self.bs
-            # buffers of its own (a training shape of the same size refills its
-            # index buffer every step)
-            idx = torch.arange(self.n_train, self.n_train + n_test, device=self.dev)
-            data = self.ds.empty_batch(
-                n_test, bf16_x=getattr(self.model, "precision", None) == "bf16",
-                cov_var_only=self._cv_only)
-            self.ds.fill(data, idx)
-            prep = (lambda: self.ds.fill(data, idx))
-            rows = data.x.shape[0] // n_test  # nodes per window
-            tot = self._tot_test
+            chunk = self.eval_chunk()
+            all_idx = torch.arange(self.n_train, self.n_train + n_test, device=self.dev)
+            steps = {}
+            for size in dict.fromkeys([chunk] + ([n_test % chunk] if n_test % chunk else [])):
+                # buffers of its own (a training shape of the same size refills
+                # its index buffer every step)
+                idx = all_idx[:size].clone()
+                data = self.ds.empty_batch(
+                    size, bf16_x=getattr(self.model, "precision", None) == "bf16",
+                    cov_var_only=self._cv_only)
+                self.ds.fill(data, idx)
+                rows = data.x.shape[0] // size  # nodes per window
+                tot = self._tot_test
 
-            def fn(m, d):
-                from .stack import head_mse_loss
-                h = m._hidden(d)
-                y = d.y_x.view(n_test * rows, -1)
-                for k in range(0, n_test, bs):
-                    b = min(bs, n_test - k)
-                    head_mse_loss(h[k * rows:(k + b) * rows], m.linear,
-                                  y[k * rows:(k + b) * rows].reshape(-1), tot)
-                return tot
+                def fn(m, d, size=size, rows=rows, tot=tot):
+                    from .stack import head_mse_loss
+                    h = m._hidden(d)
+                    y = d.y_x.view(size * rows, -1)
+                    for k in range(0, size, bs):
+                        b = min(bs, size - k)
+                        head_mse_loss(h[k * rows:(k + b) * rows], m.linear,
+                                      y[k * rows:(k + b) * rows].reshape(-1), tot)
+                    return tot
 
-            was = self.model.training
-            self.model.eval()
-            saved = self._tot_test.clone()
-            self._eval["all"] = ForwardStep(self.model, data, use_graph=self.use_graph, fn=fn,
-                                            prepare=prep)
-            self._tot_test.copy_(saved)  # undo the warm-up and capture calls
-            self.model.train(was)
+                was = self.model.training
+                self.model.eval()
+                saved = self._tot_test.clone()
+                steps[size] = (ForwardStep(self.model, data, use_graph=self.use_graph, fn=fn,
+                                           prepare=(lambda data=data, idx=idx:
+                                                    self.ds.fill(data, idx))), idx)
+                self._tot_test.copy_(saved)  # undo the warm-up and capture calls
+                self.model.train(was)
+            self._eval["all"] = (steps, chunk, all_idx)
         return self._eval["all"]
+
+    def _test_pass(self) -> None:
+        """Adds every test batch's loss to _tot_test, chunk by chunk in order."""
+        steps, chunk, all_idx = self._eval_pass()
+        for k0 in range(0, self.n_test, chunk):
+            size = min(chunk, self.n_test - k0)
+            step, idx = steps[size]
+            if chunk < self.n_test:  # one chunk: its index buffer never changes
+                idx.copy_(all_idx[k0:k0 + size])
+            step()
 
     def run_epoch(self, checkpoint_path: Optional[str] = None, tolerance: float = 1e-9) -> dict:
         """One epoch: training pass, test pass, history entry (and checkpoint)."""
@@ -529,7 +571,7 @@ class Fit:
         self._tot_test.zero_()   # an empty test split reports 0, not the last epoch's sum
         self.model.eval()
         if self.n_test > 0:
-            self._eval_pass()()   # adds every test batch's loss to _tot_test
+            self._test_pass()   # adds every test batch's loss to _tot_test
         self.model.train()
         train_loss = float(self._tot_train) / max(nb, 1)   # one host sync per epoch
         test_loss = float(self._tot_test) / max(nt, 1)

@@ -144,6 +144,34 @@ def test_c3_model_bf16_close_to_fp32_oracle(dev):
         assert_close(p.grad, q.grad, tol=BF16_TOL, what=f"d{name}")
 
 
+@pytest.mark.parametrize("x_grad", [False, True])
+def test_bf16_eval_mode_backward(dev, x_grad):
+    """model.eval() and still a backward (a gradient asked for outside
+    training): the bf16 mode's dX GEMMs need the transposed weight planes,
+    since its f32 Waug is a placeholder.  Two layers, so layer 1's dX runs;
+    with x.requires_grad layer 0's too.  Against the fp32 oracle at BF16_TOL."""
+    from spotv2net_amd import Data, synthetic_batch
+    S = 4
+    mine, ref = twin_model(seed=11, num_node_features=30 * S, num_edge_features=3 * S,
+                           num_heads=4, output_node_channels=1, dim_hidden_layers=[24, 12],
+                           concat_heads=True)
+    mine = mine.to(dev).set_precision("bf16").eval()
+    ref.eval()
+    data = synthetic_batch(6, S, seed=4)
+    x = data.x.clone().to(dev).requires_grad_(x_grad)
+    gd = Data(x=x, edge_index=data.edge_index.to(dev), edge_attr=data.edge_attr.to(dev))
+    out = mine(gd)
+    torch.nn.functional.mse_loss(out, data.y_x.to(dev)).backward()
+    xr = data.x.clone().requires_grad_(x_grad)
+    rout = ref(Data(x=xr, edge_index=data.edge_index, edge_attr=data.edge_attr))
+    torch.nn.functional.mse_loss(rout, data.y_x).backward()
+    assert_close(out, rout, tol=BF16_TOL, what="forward")
+    for (name, p), (_, q) in zip(mine.named_parameters(), ref.named_parameters()):
+        assert_close(p.grad, q.grad, tol=BF16_TOL, what=f"d{name}")
+    if x_grad:
+        assert_close(x.grad, xr.grad, tol=BF16_TOL, what="dx")
+
+
 def test_autocast_selects_bf16_mode(dev):
     """Inside torch.autocast("cuda", dtype=torch.bfloat16) the model runs the
     bf16 mode (as set_precision("bf16")); outside it, fp32."""

@@ -197,6 +197,32 @@ def test_test_pass_equals_per_batch_losses(dev, bs):
     assert abs(rec["test_loss"] - want) <= 1e-6 * abs(want), (rec["test_loss"], want)
 
 
+def test_test_pass_chunked_by_memory_budget(dev, monkeypatch):
+    """With a device-memory budget below the whole test split the test pass
+    runs in chunks of whole batches (Fit.eval_chunk): same per-epoch test
+    loss, bit for bit, as one forward over every test window."""
+    import copy
+
+    from spotv2net_amd import GATModel, train
+    from spotv2net_amd.train import Fit
+    _, ds = _data(dev)
+    torch.manual_seed(11)
+    m0 = GATModel(30 * S, 3 * S, 4, 1, [32, 16], concat_heads=True).to(dev)
+    bs = 12
+    recs = []
+    for budget in (1 << 40, None):
+        m = copy.deepcopy(m0)
+        f = Fit(m, ds, bs, generator=torch.Generator().manual_seed(3))
+        if budget is None:  # two batches per chunk, ragged tail chunk
+            budget = 2 * bs * f._window_bytes()
+        monkeypatch.setattr(train, "EVAL_BYTES", budget)
+        chunk = f.eval_chunk()
+        assert chunk == (f.n_test if budget == 1 << 40 else 2 * bs)
+        recs.append([f.run_epoch() for _ in range(2)])
+    assert f.n_test % (2 * bs) != 0 and f.n_test > 2 * bs
+    assert recs[0] == recs[1]
+
+
 def test_fit_cov_var_only_gather_is_bitwise_full_gather(dev, monkeypatch):
     """Fit gathers only the covariance-layout columns of edge_attr when the
     model reads them through those passes alone (sv2n_window_gather_cv); the

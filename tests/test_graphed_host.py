@@ -42,3 +42,20 @@ def test_param_list_of_deep_copy_is_the_copys():
     m2 = copy.deepcopy(m)
     ids = {id(p) for p in m2.parameters()}
     assert all(id(p) in ids for p in graphed._params(m2))
+
+
+def test_param_list_follows_bias_set_to_none():
+    """``module.bias = None`` calls no registration hook
+    (register_parameter(name, None)): the cached list still drops it."""
+    from spotv2net_amd import graphed
+    m = _model()
+    ps = graphed._params(m)
+    assert any(p is m.linear.bias for p in ps)
+    old_lb, old_cb = m.linear.bias, m.gat_layers[1].bias
+    m.linear.bias = None
+    ps = graphed._params(m)
+    assert not any(p is old_lb for p in ps)
+    m.gat_layers[1].bias = None
+    ps = graphed._params(m)
+    assert not any(p is old_cb for p in ps)
+    assert graphed._params(m) is ps
