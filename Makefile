@@ -1,5 +1,5 @@
-# Builds the MI355X (gfx950) shared library behind include/sv2n.h and the
-# oracle's C helpers.  `python -c "import __graft_entry__ as g; g.build()"`
+# Builds the MI355X (gfx950) shared library behind include/sv2n.h (the
+# oracle is Python and needs no build).  `python -c "import __graft_entry__ as g; g.build()"`
 # runs the same recipe.
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950

@@ -733,10 +733,9 @@ def run_c3_loop(args, dev, cfg) -> dict:
     from spotv2net_amd.train import Fit
     V, W = synthetic_series(10556, cfg["n"], seed=1234, device=dev)
     ds = WindowDataset(V, W, cfg["S"], cut=8357)
-    out = {}
-    precs = [args.precision] + ([] if args.no_compare else
-                                ["f32" if args.precision == "bf16" else "bf16"])
-    for prec in precs:
+    from spotv2net_amd import stack
+
+    def one(prec):
         model = build_model(dev, cfg).set_precision(prec)
         f = Fit(model, ds, args.batch, lr=1e-3, split=0.8,
                 generator=torch.Generator().manual_seed(5154), use_graph=not args.no_graph)
@@ -749,11 +748,32 @@ def run_c3_loop(args, dev, cfg) -> dict:
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         steps = args.epochs * (-(-f.n_train // args.batch))
-        out[prec] = {"graphs_per_s": args.epochs * len(ds) / el,
-                     "train_graphs_per_s_upper": args.epochs * f.n_train / el,
-                     "seconds": el, "train_steps": steps, "epoch_record": rec,
-                     "history": f.history}
-    return {"windows": len(ds), "n_train": f.n_train, "n_test": f.n_test, "runs": out}
+        return f, {"graphs_per_s": args.epochs * len(ds) / el,
+                   "train_graphs_per_s_upper": args.epochs * f.n_train / el,
+                   "seconds": el, "train_steps": steps, "epoch_record": rec,
+                   "history": f.history, "cov_var_only_gather": f._cv_only,
+                   "cov_var_edge_passes": bool(stack.LAST_PATH.get("cov_var"))}
+
+    out = {}
+    precs = [args.precision] + ([] if args.no_compare else
+                                ["f32" if args.precision == "bf16" else "bf16"])
+    for prec in precs:
+        f, out[prec] = one(prec)
+    variants = {}
+    if not args.no_compare:
+        # what the line owes to the edge features' covariance layout: the same
+        # loop (a) gathering every edge_attr column (the passes unchanged), and
+        # (b) through the generic edge passes, which read every edge row
+        old_only, old_cv = stack.cov_var_edges_only, stack.COV_VAR_EDGES
+        try:
+            stack.cov_var_edges_only = lambda *a: False
+            variants["full_gather"] = one(args.precision)[1]
+            stack.COV_VAR_EDGES = "off"
+            variants["generic_edges"] = one(args.precision)[1]
+        finally:
+            stack.cov_var_edges_only, stack.COV_VAR_EDGES = old_only, old_cv
+    return {"windows": len(ds), "n_train": f.n_train, "n_test": f.n_test, "runs": out,
+            "variants": variants}
 
 
 def main(argv=None):
@@ -1005,6 +1025,16 @@ def main_c3(args, dev, cfg):
                    "parallelism": "dp1", "hipgraph": not args.no_graph,
                    "epochs_timed": args.epochs},
         "value_is": "windows processed (train + test) per second over whole epochs",
+        "edge_features": ("reference covariance layout [cov | var_src | var_dst] per lag "
+                          "(utils/dataset.py:228-243): the window gather writes only the "
+                          "columns the covariance-layout edge passes read "
+                          "(sv2n_window_gather_cv)" if main_run["cov_var_only_gather"] else
+                          ("reference covariance layout, full gather"
+                           if main_run["cov_var_edge_passes"] else "generic rows")),
+        "value_full_gather": (round(res["variants"]["full_gather"]["graphs_per_s"], 1)
+                              if "full_gather" in res["variants"] else None),
+        "value_generic_edges": (round(res["variants"]["generic_edges"]["graphs_per_s"], 1)
+                                if "generic_edges" in res["variants"] else None),
         "c3_loop": {k: {kk: (round(vv, 2) if isinstance(vv, float) else vv)
                         for kk, vv in v.items() if kk != "history"}
                     for k, v in res["runs"].items()},
