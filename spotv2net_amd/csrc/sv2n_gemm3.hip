@@ -89,6 +89,17 @@ static int launch_gemm3d(hipStream_t st, const float* A, int64_t lda, const unsi
   return (int)hipGetLastError();
 }
 
+// Round 6: 12-wave workgroups of 192 rows x 144 columns (k_gemm3d<12, 1, 9>:
+// three waves per SIMD instead of two, 122 VGPRs) where they fill the chip in
+// one round and pad N by at most 10 % (MI355X, tools/gemm3_tune.hip,
+// profiles/r06_gemm3_waves.txt: C2 L0 fwd 15360 x 408 x 1260 89.0-90.7 ->
+// 85.8-86.3 us, C2 L1 dX x 400 x 208 23.8 -> 23.1-23.3, C5 L0 fwd 262144 x 144
+// x 1024 549-559 (8 waves) -> 501-505 us)
+static bool twelve_waves(int64_t M, int64_t N) {
+  const int64_t nb = (N + 143) / 144;
+  return ((M + 191) / 192) * nb >= 240 && nb * 144 * 10 <= 11 * N;
+}
+
 // bf16 operands (one plane), fp32 accumulation: the bf16 execution mode
 template <int NW, int MT, int NT, int BK>
 static int launch_gemm_bf16(hipStream_t st, const float* A, int64_t lda, const unsigned short* Bp,
@@ -240,6 +251,8 @@ extern "C" int sv2n_gemm_f32x3(const float* A, int64_t lda, const uint16_t* Bp, 
   // 144-column tiles when they pad N less than 208-column ones (C5: N = 144)
   const bool t144 = (N + 143) / 144 * 144 < (N + 207) / 208 * 208 && mb * ((N + 143) / 144) >= 240;
   if (K % 4 == 0) {
+    if (twelve_waves(M, N))
+      return launch_gemm3d<12, 1, 9, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
     if (t144) return launch_gemm3d<8, 1, 9, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
     if (wide) return launch_gemm3d<8, 1, 13, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
     return launch_gemm3d<8, 1, 7, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
@@ -269,6 +282,8 @@ extern "C" int sv2n_gemm_f32x3_relu(const float* A, int64_t lda, const uint16_t*
   const int64_t mb = (M + 127) / 128;
   const bool wide = mb * ((N + 207) / 208) >= 240;
   const bool t144 = (N + 143) / 144 * 144 < (N + 207) / 208 * 208 && mb * ((N + 143) / 144) >= 240;
+  if (twelve_waves(M, N))
+    return launch_gemm3d<12, 1, 9, 2, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
   if (t144)
     return launch_gemm3d<8, 1, 9, 2, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
   if (wide)

@@ -453,15 +453,23 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3_t(const float* __restrict__ A
 // together onto one XCD (id % 8 picks the XCD): they share A through L2.
 // Requires K % 4 == 0, lda % 4 == 0, 16-B aligned A (checked by the caller).
 // ---------------------------------------------------------------------------
-template <int NW, int MT, int NT, int BK>
+// SWZ (k_gemm3d, BK = 32): B rows unpadded (64 B) with the 16-B chunk c of
+// row r stored at c ^ PI[(r >> 2) & 3], PI = {0, 2, 3, 1} (swz_chunk): the 16
+// lanes of each ds_read_b128 lane group and the 8 of each ds_write_b128 group
+// land in distinct 16-B bank slots, as with the 32-B pad, in 2/3 of the LDS
+// (80 KB for NT = 13 double-buffered: two workgroups fit a CU)
+template <int NW, int MT, int NT, int BK, bool SWZ = false, int NSTG = 2>
 struct Gemm3bCfg {
   static constexpr int THREADS = 64 * NW;
   static constexpr int BM = 16 * MT * NW, BN = 16 * NT;
-  static constexpr int ROW = BK + 16;  // conflict-free ds_read_b128 (see Gemm3Cfg)
+  static constexpr int ROW = SWZ ? BK : BK + 16;  // conflict-free ds_read_b128 (see Gemm3Cfg)
   static constexpr int BV = (3 * BN * (BK / 8) + THREADS - 1) / THREADS;  // uint4 per thread
   static constexpr int STAGE = 3 * BN * ROW;                              // bf16 per stage
-  static constexpr size_t LDS = sizeof(unsigned short) * 2 * STAGE;
+  static constexpr size_t LDS = sizeof(unsigned short) * NSTG * STAGE;
 };
+__device__ __forceinline__ int swz_chunk(int c, int r) {
+  return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3);  // PI = {0, 2, 3, 1}[(r >> 2) & 3]
+}
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 // eight elements (two float4) -> the three plane fragments
@@ -802,7 +810,8 @@ __device__ __forceinline__ void static_for(F&& f) {
 // ---------------------------------------------------------------------------
 // BD: B fragments read BD column tiles ahead of their MFMAs (BD + 1 register
 // sets; 1 = the next tile's reads under the current tile's MFMAs).
-template <int NW, int MT, int NT, int AP, bool MASK = false, int BD = 1>
+template <int NW, int MT, int NT, int AP, bool MASK = false, int BD = 1, bool SWZ = false,
+          bool STG = false>
 __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A, int64_t lda,
                                                     const unsigned short* __restrict__ Bp,
                                                     int64_t ldb, int64_t bplane,
@@ -810,9 +819,20 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
                                                     int64_t N, int64_t K, int nm, int nn,
                                                     const float* __restrict__ Y, int64_t ldy) {
   constexpr int BK = 32;
-  using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
+  static_assert(!STG || SWZ, "three padded stages do not fit the LDS");
+  constexpr int NSTG = STG ? 3 : 2;
+  using Cfg = Gemm3bCfg<NW, MT, NT, BK, SWZ, NSTG>;
   constexpr int TH = Cfg::THREADS, BN = Cfg::BN, ROW = Cfg::ROW, BV = Cfg::BV;
   constexpr int STAGE = Cfg::STAGE, BC = BK / 8;
+  // STG (with SWZ): waves NW/2.. run half a K-step behind the first half —
+  // their barrier sits after column tile MIDB, the first half's at the end of
+  // the step — so the two waves of a SIMD are never in the same phase (one
+  // resumes MFMAs on fragments read before the barrier while the other waits
+  // for its first ones).  B stages in a ring of three: during barrier
+  // interval k every wave writes stage k+1, the first half reads stage k,
+  // the second half stages k-1 and k.
+  constexpr int MIDB = (NT + 1) / 2 - 1;
+  static_assert(!STG || BV <= MIDB, "the second half stages B before its barrier");
   constexpr int NPAIR = 4 * MT;  // split3_pk pairs per step (8 floats per fragment)
   constexpr int PPT = (NPAIR + NT - 1) / NT;  // pairs split per column tile
   static_assert(BV + 1 < NT, "interleave needs enough column tiles");
@@ -870,8 +890,10 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
   auto store_b1 = [&](int sv, unsigned short* sB) __attribute__((always_inline)) {
     int p, r, c;
     b_slot(sv, p, r, c);
-    *reinterpret_cast<u32x4_t*>(sB + (p * BN + r) * ROW + 8 * c) = rb[sv];
+    *reinterpret_cast<u32x4_t*>(sB + (p * BN + r) * ROW + 8 * (SWZ ? swz_chunk(c, r) : c)) = rb[sv];
   };
+  // fragment chunk of lane group lg in rows 16b + li (the swizzle depends on li only)
+  const int bchunk = 8 * (SWZ ? swz_chunk(lg, li) : lg);
   // packed bf16 planes of the current step's A fragments, and the next step's
   u32x4_t afc[MT][3], afn[MT][3];
   auto split_pair = [&](u32x4_t (&dst)[MT][3], const f32x4 (&src)[MT][2], int pr) {
@@ -928,8 +950,8 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
 
   auto step = [&](int s, auto set_c) __attribute__((always_inline)) {
     constexpr int set = decltype(set_c)::value, nset = (set + 1) % AP;
-    const unsigned short* sB = lds + (s & 1) * STAGE;
-    unsigned short* sW = lds + ((s + 1) & 1) * STAGE;
+    const unsigned short* sB = lds + (STG ? s % 3 : s & 1) * STAGE;
+    unsigned short* sW = lds + (STG ? (s + 1) % 3 : (s + 1) & 1) * STAGE;
     // the last steps stage a copy nobody reads (the other stage is free after
     // the barrier) and reload the last K-step: no branch in the block
     const int64_t kb2 = (int64_t)min(s + 2, nk - 1) * BK;
@@ -944,7 +966,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
       constexpr int b = decltype(bc)::value;
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        bq[b][p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + 16 * b + li) * ROW + 8 * lg);
+        bq[b][p] = *reinterpret_cast<const bf16x8*>(sB + (p * BN + 16 * b + li) * ROW + bchunk);
     });
     __builtin_amdgcn_sched_group_barrier(0x100, 3 * BD, 0);
     static_for<NT>([&](auto bc) __attribute__((always_inline)) {
@@ -953,7 +975,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
 #pragma unroll
         for (int p = 0; p < 3; ++p)
           bq[(b + BD) % (BD + 1)][p] = *reinterpret_cast<const bf16x8*>(
-              sB + (p * BN + 16 * (b + BD) + li) * ROW + 8 * lg);
+              sB + (p * BN + 16 * (b + BD) + li) * ROW + bchunk);
         __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
       }
       if constexpr (b < BV) {
@@ -974,13 +996,20 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
 #pragma unroll
       for (int a = 0; a < MT; ++a) acc[a][b] = mfma_planes<3>(af[a], bq[b % (BD + 1)], acc[a][b]);
       __builtin_amdgcn_sched_group_barrier(0x008, 6 * MT, 0);
+      if constexpr (STG && b == MIDB) {
+        if (wave >= NW / 2) __syncthreads();  // the second half's barrier: mid-step
+      }
     });
 #pragma unroll
     for (int a = 0; a < MT; ++a)
 #pragma unroll
       for (int p = 0; p < 3; ++p) afc[a][p] = afn[a][p];
     if (s + AP < nk) load_a(set, (int64_t)(s + AP) * BK);
-    __syncthreads();
+    if constexpr (STG) {
+      if (wave < NW / 2) __syncthreads();
+    } else {
+      __syncthreads();
+    }
   };
   for (int s = 0; s < nk; s += AP) {
     step(s, std::integral_constant<int, 0>{});

@@ -251,14 +251,14 @@ void run3(const Shape& sh, hipStream_t st, const float* A, const unsigned short*
 }
 
 template <int NW, int MT, int NT, int BK, int AP, bool CV = false, int ABL = 0, int PD = 1, bool DV = false,
-          int BD = 1>
+          int BD = 1, bool SWZ = false, bool STG = false>
 void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short* Bp, int64_t Kp,
            float* C, const std::vector<double>& ref, const std::vector<double>& absr) {
-  using Cfg = Gemm3bCfg<NW, MT, NT, BK>;
+  using Cfg = Gemm3bCfg<NW, MT, NT, BK, SWZ, STG ? 3 : 2>;
   const size_t lds = Cfg::LDS;
   if (lds > 160 * 1024) return;
   static_assert(DV, "k_gemm3d only (the product's projection kernel)");
-  auto kern = k_gemm3d<NW, MT, NT, AP, false, BD>;
+  auto kern = k_gemm3d<NW, MT, NT, AP, false, BD, SWZ, STG>;
   if (lds > 65536)
     CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   const int nm = (int)((sh.M + Cfg::BM - 1) / Cfg::BM), nn = (int)((sh.N + Cfg::BN - 1) / Cfg::BN);
@@ -304,7 +304,7 @@ void run3b(const Shape& sh, hipStream_t st, const float* A, const unsigned short
 #endif
   if (ABL) printf("  [ablation %d]", ABL);
   if (PD != 1) printf("  [PD %d]", PD);
-  if (DV) printf("  [3d BD%d]", BD);
+  if (DV) printf("  [3d BD%d%s%s grid %u, LDS %zu]", BD, SWZ ? " SWZ" : "", STG ? " STG" : "", grid, lds);
   printf("  gemm3%s NW%d MT%d NT%-2d BK%d AP%d %8.1f us %7.1f TF(f32-eq)  max|err| %.2e  max err/S|ab| %.2e\n",
          CV ? "c" : "b", NW, MT, NT, BK, AP, us, 2.0 * sh.M * sh.N * sh.K / us / 1e6, maxabs, maxrel);
   fflush(stdout);
@@ -353,7 +353,8 @@ void run3g(const Shape& sh, hipStream_t st, const float* A, const unsigned short
 
 int main() {
   std::vector<Shape> shapes = {{"fwd L0", 15360, 408, 1260}, {"fwd L1", 15360, 208, 400},
-                               {"dX L1", 15360, 400, 208}, {"C5 fwd L0", 262144, 144, 1024}};
+                               {"dX L1", 15360, 400, 208}, {"C5 fwd L0", 262144, 144, 1024},
+                               {"C5 fwd L1", 262144, 144, 128}};
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (auto& sh : shapes) {
@@ -406,11 +407,20 @@ int main() {
       printf("  f32 MFMA NT13     %8.1f us %7.1f TF          max|err| %.2e  max err/Σ|ab| %.2e\n", us,
              2.0 * M * N * K / us / 1e6, maxabs, maxrel);
     }
-    run3b<8, 1, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3b<8, 1, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3g<13>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3g<7>(sh, st, A, Bp, Kp, C, ref, absr);
-    run3g<9>(sh, st, A, Bp, Kp, C, ref, absr);
+    // round 6: XOR-swizzled unpadded B stages (SWZ, 80 KB at NT = 13), 8-wave
+    // and 4-wave workgroups (two 4-wave workgroups per CU, barriers apart)
+    // (round 6, first pass: SWZ alone is neutral, 4-wave pairs 89.8 -> 138 us);
+    // STG: the second half of the waves half a K-step behind, three B stages
+    // (second pass: STG 88.1 -> 98.8 us at C2 L0, slower on every shape);
+    // third pass: 12- and 16-wave workgroups (3 / 4 waves per SIMD)
+    // (third pass: profiles/r06_gemm3_waves.txt — <12, 1, 9> kept where it fills the chip)
+    for (int rep = 0; rep < 2; ++rep) {
+      run3b<8, 1, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3b<8, 1, 9, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3b<12, 1, 9, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3b<16, 1, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3b<8, 1, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+    }
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(S)); CK(hipFree(Bp));
   }
   return 0;
