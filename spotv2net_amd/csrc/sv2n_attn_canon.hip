@@ -39,6 +39,12 @@ __device__ unsigned long long g_stamps[4096 * 4 * 16];
 #define SV2N_STAMP(k, v)
 #endif
 
+// diagnostic timing builds only (results wrong; never in the library):
+// SV2N_ATTN_ABL bit 1 drops the forward's y stores, bit 2 its xs loads, bit 4
+// its psave stores
+#ifndef SV2N_ATTN_ABL
+#define SV2N_ATTN_ABL 0
+#endif
 constexpr int THREADS = 256;
 constexpr int PS = SV2N_PSTR;  // LDS row stride of a probability row (floats)
 constexpr int AEV = 8;         // 16-B slots per thread covering E0·H <= 992·8
@@ -148,13 +154,22 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     }
   };
   // xs rows 16·half + kk of head h's columns of tile tc: the B operand
-  auto load_b = [&](int q, float (&b)[16]) {
+  // branch-free: an item past the wave's last (q >= nq) reads 0 (OOB), so
+  // the compiler's wait counts stay exact (a conditional load made the
+  // softmax's first wait a vmcnt(0) on every xs load)
+  // The item's bias value comes with its operands (loaded at the end of the
+  // item, it was the youngest load there, and its wait a vmcnt(0) on the
+  // later items' operands still in flight).
+  auto load_b = [&](int q, float (&b)[16], float& bb) {
     int h, tc;
     item(q, h, tc);
     const int c = 32 * tc + l32;
-    const int voff = c < C ? ((16 * half) * ldx + h * C + c) * 4 : OOB;
+    const bool ok = c < C && q < nq;
+    const int voff = ok ? ((16 * half) * ldx + h * C + c) * 4 : OOB;
+    bb = bld(rb, ok ? ((CONCAT ? h * C : 0) + c) * 4 : OOB);
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) b[kk] = bld_s(rx, voff, kk * ldx * 4);
+    for (int kk = 0; kk < 16; ++kk)
+      b[kk] = (SV2N_ATTN_ABL & 2) ? (float)(kk + voff) * 1e-3f : bld_s(rx, voff, kk * ldx * 4);
   };
 
   // ---- prologue: every load before any store ----
@@ -162,16 +177,18 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
   const rsrc_t ra = make_rsrc(ae ? ae + (int64_t)g * nae : nullptr, (uint32_t)nae * 4u);
   const int nv = (nae + 3) >> 2;
   const bool ae_vec = (nae & 3) == 0 && ((uintptr_t)ae & 15) == 0;
+  if (ae_vec) {  // (uniform) unconditional loads, past the logits OOB (0)
 #pragma unroll
-  for (int q = 0; q < AEV; ++q) {
-    if (q * THREADS < nv) {  // wave-uniform
+    for (int q = 0; q < AEV; ++q) {
       const int k = t + THREADS * q;
-      if (ae_vec) {
-        av[q] = bld4(ra, k < nv ? k * 16 : OOB);
-      } else {
+      av[q] = bld4(ra, k < nv ? k * 16 : OOB);
+    }
+  } else {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) av[q][c] = bld(ra, 4 * k + c < nae ? (4 * k + c) * 4 : OOB);
-      }
+    for (int q = 0; q < AEV; ++q) {
+      const int k = t + THREADS * q;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) av[q][c] = bld(ra, 4 * k + c < nae ? (4 * k + c) * 4 : OOB);
     }
   }
   float asd[2];
@@ -180,16 +197,18 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     const int idx = t + THREADS * s, k = idx >> 5, j = idx & 31;
     asd[s] = bld(rx, k < 2 * H ? (j * ldx + HC + k) * 4 : OOB);  // rows j >= n read 0
   }
-  // B operands of the wave's first four work items (C2: all of them)
-  float bq[4][16];
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-    if (u < nq) load_b(u, bq[u]);
-  // sources of target row l32 (block layouts: the row mask; else all n)
+  // sources of target row l32 (block layouts: the row mask; else all n) —
+  // loaded BEFORE the xs operands: the softmax waits for it, and a load
+  // issued after the 64 xs loads made that wait a vmcnt(0), i.e. the softmax
+  // started only once the whole graph's xs had landed (round 6)
   const uint32_t allm = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
-  const uint32_t rbits =
-      (rowmask ? bld_u32(make_rsrc(rowmask + (int64_t)g * n, (uint32_t)n * 4u), l32 * 4) : allm) &
-      ~(1u << l32);
+  const uint32_t rmw = bld_u32(make_rsrc(rowmask ? rowmask + (int64_t)g * n : nullptr,
+                                          rowmask ? (uint32_t)n * 4u : 0u), l32 * 4);
+  const uint32_t rbits = (rowmask ? rmw : allm) & ~(1u << l32);
+  // B operands of the wave's first four work items (C2: all of them)
+  float bq[4][16], bbq[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) load_b(u, bq[u], bbq[u]);
 
 #pragma unroll
   for (int q = 0; q < AEV; ++q) {
@@ -293,9 +312,10 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     const int off = ((h * 32 + i) * 32 + 16 * half) * 4;
 #pragma unroll
     for (int k4 = 0; k4 < 4; ++k4)
-      bst4(rp, off + 16 * k4,
-           f32x4{pkeep[s2][4 * k4], pkeep[s2][4 * k4 + 1], pkeep[s2][4 * k4 + 2],
-                 pkeep[s2][4 * k4 + 3]});
+      if (!(SV2N_ATTN_ABL & 4) || pkeep[s2][4 * k4] == 1234.5f)
+        bst4(rp, off + 16 * k4,
+             f32x4{pkeep[s2][4 * k4], pkeep[s2][4 * k4 + 1], pkeep[s2][4 * k4 + 2],
+                   pkeep[s2][4 * k4 + 3]});
   }
   SV2N_STAMP(3, SV2N_T());
   __syncthreads();  // sP complete
@@ -308,7 +328,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
   const float invH = 1.f / (float)H;
   float* sY = sAE + ((nae + 3) & ~3);  // HEAD: the layer output [32][OC + 1]
   float uv[16];  // post-dropout draws of the work item's outputs (loaded at its first sub-item)
-  auto run = [&](int q, const float (&b)[16]) {
+  auto run = [&](int q, const float (&b)[16], float bv) {
     int h, tc;
     item(q, h, tc);
     if (post && (CONCAT || h == 0)) {
@@ -328,7 +348,6 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       const int c = 32 * tc + l32;
       const int oc = (CONCAT ? h * C : 0) + c;
       const bool cv = c < C;
-      const float bv = bld(rb, cv ? oc * 4 : OOB);
       const int voff = cv ? (4 * half * OC + oc) * 4 : OOB;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -338,7 +357,8 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
           const int row = crow(r, half);
           if (cv && row < n) sY[row * (OC + 1) + oc] = a;
         } else {
-          bst_s(ry, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4, a);
+          if (!(SV2N_ATTN_ABL & 1) || a == 1234.5f)
+            bst_s(ry, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4, a);
           if (post)
             bst_s(ro, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4,
                   uv[r] >= post_p ? a * post_scale : 0.f);
@@ -352,8 +372,8 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     for (int u = 0; u < 4; ++u) {
       const int q = q0 + u;
       if (q < nq) {
-        run(q, bq[u]);
-        if (q + 4 < nq) load_b(q + 4, bq[u]);
+        run(q, bq[u], bbq[u]);
+        load_b(q + 4, bq[u], bbq[u]);  // past the last item: OOB (0), no branch
       }
     }
   }
@@ -713,7 +733,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     int c0, cw;
     chunk_range(ch, c0, cw);
     const int c = c0 + l32;
-    const bool cv = l32 < cw;
+    const bool cv = l32 < cw && q < nseq;  // past the wave's last step: OOB (0), no branch
     const int xo = cv ? (half * ldx + h * C + c) * 4 : OOB;
     const int zo = cv ? (half * OC + (CONCAT ? h * C : 0) + c) * 4 : OOB;
 #pragma unroll
@@ -722,7 +742,8 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       rdy_[b][m] = bld_s(rdy, zo, 2 * m * OC * 4);
       if constexpr (ACT != ACT_ID) ry_[b][m] = bld_s(ryy, zo, 2 * m * OC * 4);
     }
-    if (post) {
+    if (post) {  // (a uniform branch: unconditional loads of nothing cost C2's
+                 // layer-1 backward 19.9 -> 21.4 us, more than the exact waits gain)
 #pragma unroll
       for (int m = 0; m < 16; ++m) ru_[b][m] = bld_s(ru, zo, 2 * m * OC * 4);
     }
@@ -735,26 +756,27 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
     const int base = ((h * 32 + l32) * 32 + 4 * half) * 4;
 #pragma unroll
     for (int m = 0; m < 4; ++m) pr[m] = bld4(rps, base + 32 * m);
-    if constexpr (KEEP) {
-      const rsrc_t rk = make_rsrc(keep + (g * H + h) * 1024, 1024u);
+    if constexpr (KEEP) {  // (h >= H: a wave without a head, nothing read)
+      const rsrc_t rk = make_rsrc(h < H ? keep + (g * H + h) * 1024 : nullptr, h < H ? 1024u : 0u);
 #pragma unroll
       for (int m = 0; m < 4; ++m) kb[m] = bld_u32(rk, (l32 * 32 + 4 * half) + 8 * m);
     }
   };
 
-  if (nseq > 0) {
-    load_p(h0 + grp);
-    load_chunk(0, std::integral_constant<int, 0>{});
-    if constexpr (DEPTH > 1)
-      if (nseq > 1) load_chunk(1, std::integral_constant<int, 1>{});
-    if constexpr (DEPTH > 2)
-      if (nseq > 2) load_chunk(2, std::integral_constant<int, 2>{});
-  }
-  // sources of target row l32 (block layouts: the row mask; else all n)
+  // sources of target row l32 (block layouts: the row mask; else all n),
+  // then the first chunks — every load unconditional (past the wave's steps,
+  // or without a row mask, OOB: 0), so the compiler's wait counts stay exact.
+  // Round 6: the row-mask select after conditional chunk loads made the
+  // prologue wait vmcnt(0) on every chunk in flight (C2: all three), and
+  // its later use a second vmcnt(0).
   const uint32_t allm = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
-  const uint32_t rbits =
-      (rowmask ? bld_u32(make_rsrc(rowmask + g * n, (uint32_t)n * 4u), l32 * 4) : allm) &
-      ~(1u << l32);
+  const uint32_t rmw = bld_u32(make_rsrc(rowmask ? rowmask + g * n : nullptr,
+                                          rowmask ? (uint32_t)n * 4u : 0u), l32 * 4);
+  const uint32_t rbits = (rowmask ? rmw : allm) & ~(1u << l32);
+  load_p(h0 + grp);  // a wave without a head (h >= H) reads past psave: 0
+  load_chunk(0, std::integral_constant<int, 0>{});
+  if constexpr (DEPTH > 1) load_chunk(1, std::integral_constant<int, 1>{});
+  if constexpr (DEPTH > 2) load_chunk(2, std::integral_constant<int, 2>{});
   floatx16 G;
 #pragma unroll
   for (int r = 0; r < 16; ++r) G[r] = 0.f;
@@ -835,7 +857,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes, in order
       SV2N_STAMP(3 + 2 * min(q, 3), SV2N_T());
-      if (q + DEPTH < nseq) load_chunk(q + DEPTH, set_tag);  // refill this set
+      load_chunk(q + DEPTH, set_tag);  // refill this set (past the last step: OOB)
       // bias partials: column sums of dz (concat: this head's columns; mean: once)
       if (CONCAT || h == 0) {
         float sb = 0.f;

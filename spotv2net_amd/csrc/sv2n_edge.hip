@@ -1326,7 +1326,10 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
 
   for (int64_t g = blockIdx.x; g < B; g += gridDim.x) {
     const rsrc_t rg = make_rsrc(ea + g * E0 * D, (uint32_t)(E0 * D) * 4u);
-    const float* ib = inp ? inp + g * E0 * H : nullptr;  // this graph's d-logits, this column
+    // this graph's d-logits, this column (a lane column past the logits: an
+    // empty descriptor; unconditional loads, so the compiler's wait counts
+    // stay exact — a conditional plain load here waited vmcnt(0) per tile)
+    const rsrc_t rdl = make_rsrc(inp ? inp + g * E0 * H : nullptr, inp ? (uint32_t)(E0 * H) * 4u : 0u);
     u32x2 vv[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1346,10 +1349,10 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
               rg, (ok && 32 * mm + 2 * li < S) ? vo : OOB,
               ok ? ((tile * 16 + q) * D + 32 * mm) * 4 : 0, 0);
         const int p = tile * 16 + 4 * gq + q;
-        const bool pv = ok && ib && p < P;
-        if (pv) SV2N_CHK(409, (g * E0 + P + p) * H, B * E0 * H);
+        const bool pv = ok && p < P;
 #pragma unroll
-        for (int s = 0; s < ND; ++s) dd[q][s] = pv ? ib[((low | s) ? P + p : p) * H] : 0.f;
+        for (int s = 0; s < ND; ++s)
+          dd[q][s] = bld(rdl, pv ? (((low | s) ? P + p : p) * H) * 4 : OOB);
       }
     };
     __syncthreads();  // the previous graph's sVar / sBuf / sDn reads (first: sOut)

@@ -31,11 +31,11 @@
 
 namespace sv2n {
 
-// WM x WN waves per workgroup (default 2 x 4)
-template <int BM, int BN, bool KO, bool AF, bool BF, int WM_ = 2, int WN_ = 4>
+// WM x WN waves per workgroup (default 2 x 4); BK_ the K step per barrier
+template <int BM, int BN, bool KO, bool AF, bool BF, int WM_ = 2, int WN_ = 4, int BK_ = 64>
 struct GemmBWCfg {
   static constexpr int WM = WM_, WN = WN_, NW = WM * WN, THREADS = 64 * NW;
-  static constexpr int BK = 64;
+  static constexpr int BK = BK_;
   static constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // MFMA tiles per wave
   static constexpr int padko(int w) {  // k-outer rows: row dwords ≡ 8 (mod 16)
     int p = 8;
@@ -75,14 +75,14 @@ struct Piece {
   }
 };
 
-template <int BM, int BN, bool KO, bool AF, bool BF, int WM_ = 2, int WN_ = 4>
+template <int BM, int BN, bool KO, bool AF, bool BF, int WM_ = 2, int WN_ = 4, int BK_ = 64>
 __global__ __launch_bounds__(64 * WM_ * WN_) void k_gemm_bw(const void* __restrict__ Av, int64_t lda,
                                                  const void* __restrict__ Bv, int64_t ldb,
                                                  float* __restrict__ C, int64_t ldc, int64_t M,
                                                  int64_t N, int64_t K, int64_t kslice, int nm,
                                                  int nn, unsigned short* __restrict__ Aex = nullptr,
                                                  int64_t ldex = 0) {
-  using Cfg = GemmBWCfg<BM, BN, KO, AF, BF, WM_, WN_>;
+  using Cfg = GemmBWCfg<BM, BN, KO, AF, BF, WM_, WN_, BK_>;
   constexpr int BK = Cfg::BK, TM = Cfg::TM, TN = Cfg::TN, SA = Cfg::SA, SB = Cfg::SB;
   constexpr int IA = Cfg::IA, STAGE = Cfg::STAGE, TH = Cfg::THREADS;
   constexpr int PA = Cfg::PA, PB = Cfg::PB, RA = Cfg::RA, RB = Cfg::RB;

@@ -192,8 +192,10 @@ def _prep_shapes(W, heads, channels, need_t, kpad, np=3):
 
 def _waug_placeholder(w: torch.Tensor, shape) -> torch.Tensor:
     """Waug's shape without its data (bf16-mode gat_prep): consumers read only
-    the shape; ops.project / weight_planes refuse it (ops._has_data)."""
-    return w.new_zeros(1).expand(shape)
+    the shape; ops.project / weight_planes refuse it (ops._has_data).  One
+    uninitialised element, expanded: no fill launch (new_zeros launched a
+    4.6 µs fill kernel in every captured C3 step)."""
+    return w.new_empty(1).expand(shape)
 
 
 def _kpad(K: int) -> int:

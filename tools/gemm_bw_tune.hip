@@ -81,17 +81,17 @@ double check(const float* C, const std::vector<double>& ref, int64_t M, int64_t 
   return worst / fmax(scale, 1e-30);
 }
 
-template <int BM, int BN, bool KO, bool AF, bool BF, int WM = 2, int WN = 4>
+template <int BM, int BN, bool KO, bool AF, bool BF, int WM = 2, int WN = 4, int BK = 64>
 void run_bw(const char* tag, hipStream_t st, const void* A, int64_t lda, const void* B, int64_t ldb,
             float* C, int64_t M, int64_t N, int64_t K, int splitk, const std::vector<double>& ref,
             double flops) {
-  using Cfg = GemmBWCfg<BM, BN, KO, AF, BF, WM, WN>;
-  auto kern = k_gemm_bw<BM, BN, KO, AF, BF, WM, WN>;
+  using Cfg = GemmBWCfg<BM, BN, KO, AF, BF, WM, WN, BK>;
+  auto kern = k_gemm_bw<BM, BN, KO, AF, BF, WM, WN, BK>;
   CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                          (int)Cfg::LDS));
   const int nm = (int)((M + BM - 1) / BM), nn = (int)((N + BN - 1) / BN);
   int64_t ks = (K + splitk - 1) / splitk;
-  ks = (ks + 63) / 64 * 64;
+  ks = (ks + BK - 1) / BK * BK;
   const int nz = (int)((K + ks - 1) / ks);
   const dim3 grid((unsigned)(((nm + 7) / 8) * 8 * nn), 1, (unsigned)nz);
   CK(hipMemset(C, 0, sizeof(float) * M * N * nz));
@@ -102,8 +102,8 @@ void run_bw(const char* tag, hipStream_t st, const void* A, int64_t lda, const v
   const double us = timeit(st, f);
   double err = -1;
   if (nz == 1) err = check(C, ref, M, N, N);
-  printf("  %-28s BM%d BN%d W%dx%d split%d %8.1f us %7.1f TF  err %.2e\n", tag, BM, BN, WM, WN, nz, us,
-         flops / us / 1e6, err);
+  printf("  %-28s BM%d BN%d W%dx%d BK%d split%d %8.1f us %7.1f TF  err %.2e\n", tag, BM, BN, WM, WN,
+         BK, nz, us, flops / us / 1e6, err);
   fflush(stdout);
 }
 
@@ -190,6 +190,11 @@ int main() {
     }
     run_bw<128, 128, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 1, ref, fl);
     run_bw<128, 128, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
+    // round 6: K steps of 128 per barrier (half the barriers, 147 KB of LDS)
+    run_bw<128, 128, true, false, false, 2, 4, 128>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 1, ref, fl);
+    run_bw<128, 128, true, false, false, 2, 4, 128>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
+    run_bw<128, 128, true, false, false, 2, 2, 128>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
+    run_bw<128, 128, true, false, false>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 1, ref, fl);
     // round 5: 4-wave workgroups (wave tile 64 x 64: half the LDS reads per MFMA)
     run_bw<128, 128, true, false, false, 2, 2>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 1, ref, fl);
     run_bw<128, 128, true, false, false, 2, 2>("bw A bf16, B bf16", st, Ab, ldAb, Bb, ldBb, C, M, N, K, 2, ref, fl);
