@@ -253,9 +253,12 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       float a = 0.f;
       if (ae) {
         const bool ev = iv && ((rbits >> j) & 1u);
-        const int e = !ae_edge_order ? i * n + j
-                      : j < i        ? ((j * (2 * n - 1 - j)) >> 1) - j - 1 + i
-                                     : Ehi + j;
+        // both canonical branches computed, then selected (as a ternary over
+        // the multiply the compiler branched per source under exec masks)
+        const int e_lo = ((j * (2 * n - 1 - j)) >> 1) - j - 1 + i;
+        const int e_hi = Ehi + j;
+        const int e_c = j < i ? e_lo : e_hi;
+        const int e = ae_edge_order ? e_c : i * n + j;
         const float v = sAE[ev ? e * H + h : 0];
         a = ev ? v : 0.f;
       }
@@ -265,6 +268,12 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     esum += __shfl_xor(esum, 32, 64);
     const int cnt = __popc(rbits);
     const float loopv = (ae && cnt > 0) ? esum / (float)cnt : 0.f;
+    // the lane's valid sources kk (incoming edges and the self loop) as bits:
+    // every step below is a select, not a branch (round 6: a conditional
+    // expf made the compiler branch per source under exec masks, with its
+    // masks spilled to VGPR lanes — 566 readlanes, the forward's softmax
+    // phase 17.5K cycles)
+    const uint32_t vbits = iv ? ((rbits | (1u << i)) >> (16 * half)) & 0xffffu : 0u;
     float mx = -INFINITY;
     uint32_t negm = 0u;
 #pragma unroll
@@ -275,14 +284,14 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       negm |= neg ? (1u << kk) : 0u;
       v = neg ? v * slope : v;
       lg[kk] = v;
-      if (iv && (j == i || ((rbits >> j) & 1u))) mx = fmaxf(mx, v);
+      mx = fmaxf(mx, ((vbits >> kk) & 1u) ? v : -INFINITY);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     float den = 0.f;
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
-      const int j = 16 * half + kk;
-      lg[kk] = (iv && (j == i || ((rbits >> j) & 1u))) ? __expf(lg[kk] - mx) : 0.f;
+      const float ex = __expf(lg[kk] - mx);
+      lg[kk] = ((vbits >> kk) & 1u) ? ex : 0.f;
       den += lg[kk];
     }
     den += __shfl_xor(den, 32, 64);
@@ -295,8 +304,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       for (int c = 0; c < 4; ++c) {
         const int kk = 4 * k4 + c;
         const float p = lg[kk] * inv;
-        const int jv = 16 * half + kk;
-        const bool valid = iv && (jv == i || ((rbits >> jv) & 1u));
+        const bool valid = (vbits >> kk) & 1u;
         pkeep[s2][kk] = valid ? (((negm >> kk) & 1u) ? -p : p) : 0.f;
         float d = p;
         if constexpr (KEEP) d = ((kw[k4] >> (8 * c)) & 0xffu) ? d * keep_scale : 0.f;
@@ -354,8 +362,9 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
         const float z = (CONCAT ? acc[r] : acc[r] * invH) + bv;
         const float a = act_fwd<ACT>(z);
         if constexpr (HEAD) {
-          const int row = crow(r, half);
-          if (cv && row < n) sY[row * (OC + 1) + oc] = a;
+          // unconditional (a branch per r otherwise): rows past n land in
+          // sY's unread rows, columns past C in its unread padding column OC
+          sY[crow(r, half) * (OC + 1) + (cv ? oc : OC)] = a;
         } else {
           if (!(SV2N_ATTN_ABL & 1) || a == 1234.5f)
             bst_s(ry, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4, a);
@@ -786,14 +795,19 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
   // ---- softmax / leaky_relu backward of head h (local hl) from Gh: lane (i,
   //      half), rows j = crow(r, half) ----
   auto softmax_bwd = [&](int hl, const floatx16& Gh) {
+    // validity as one per-lane bit mask and selects (round 6: the
+    // short-circuit `iv && (jr == i || bit)` compiled to exec-mask branches
+    // around every accumulator read, as the forward's conditional expf did)
+    const uint32_t vmask = iv ? (rbits | (1u << i)) : 0u;
     float ps[16], dp[16];
     float tl = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int jr = crow(r, half);
       ps[r] = pr[r >> 2][r & 3];
-      const bool valid = iv && (jr == i || ((rbits >> jr) & 1u));
-      float d = valid ? (CONCAT ? Gh[r] : Gh[r] * invH) : 0.f;
+      const bool valid = (vmask >> jr) & 1u;
+      const float gv = CONCAT ? Gh[r] : Gh[r] * invH;
+      float d = valid ? gv : 0.f;
       if constexpr (KEEP) d = ((kb[r >> 2] >> (8 * (r & 3))) & 0xffu) ? d * keep_scale : 0.f;
       dp[r] = d;
       tl += fabsf(ps[r]) * d;
@@ -804,7 +818,7 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int jr = crow(r, half);
-      const bool valid = iv && (jr == i || ((rbits >> jr) & 1u));
+      const bool valid = (vmask >> jr) & 1u;
       const float ds = fabsf(ps[r]) * (dp[r] - tl);
       const float dl = valid ? (signbit(ps[r]) ? ds * slope : ds) : 0.f;
       dad += dl;

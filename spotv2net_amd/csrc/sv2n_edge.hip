@@ -1306,6 +1306,7 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
   // SPLIT: lane column li reads column li & 7 of the up (li < 8) or low rows
   const int col = SPLIT ? (li & 7) : li, low = SPLIT ? (li >> 3) : 0;
   const float* inp = col < HL ? mx_col_ptr<const float>(dae, col, L, H) : nullptr;
+  const float* col0 = mx_col_ptr<const float>(dae, 0, L, H);
   for (int k = t; k < n * n; k += CV2_T) {
     const int u = k / n, w = k - u * n;
     sOut[u][w] = (short)(u == w ? ZROW : u < w ? cv2_pair_index(u, w, n)
@@ -1326,10 +1327,12 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
 
   for (int64_t g = blockIdx.x; g < B; g += gridDim.x) {
     const rsrc_t rg = make_rsrc(ea + g * E0 * D, (uint32_t)(E0 * D) * 4u);
-    // this graph's d-logits, this column (a lane column past the logits: an
-    // empty descriptor; unconditional loads, so the compiler's wait counts
-    // stay exact — a conditional plain load here waited vmcnt(0) per tile)
-    const rsrc_t rdl = make_rsrc(inp ? inp + g * E0 * H : nullptr, inp ? (uint32_t)(E0 * H) * 4u : 0u);
+    // this graph's d-logits, this column.  The column's array differs per
+    // lane (layer col / H), so no buffer descriptor (those are wave-uniform):
+    // a plain load, unconditional (a lane past the logits or the pairs reads
+    // column 0's first d-logit and drops it), so the compiler's wait counts
+    // stay exact — a conditional load here waited vmcnt(0) per tile
+    const float* ib = (inp ? inp : col0) + g * E0 * H;
     u32x2 vv[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1349,10 +1352,13 @@ __global__ __launch_bounds__(CV2_T) __attribute__((amdgpu_waves_per_eu(4))) void
               rg, (ok && 32 * mm + 2 * li < S) ? vo : OOB,
               ok ? ((tile * 16 + q) * D + 32 * mm) * 4 : 0, 0);
         const int p = tile * 16 + 4 * gq + q;
-        const bool pv = ok && p < P;
+        const bool pv = ok && p < P && inp;
+        if (pv) SV2N_CHK(409, (g * E0 + P + p) * H, B * E0 * H);
 #pragma unroll
-        for (int s = 0; s < ND; ++s)
-          dd[q][s] = bld(rdl, pv ? (((low | s) ? P + p : p) * H) * 4 : OOB);
+        for (int s = 0; s < ND; ++s) {
+          const float v = ib[pv ? ((low | s) ? P + p : p) * H : 0];
+          dd[q][s] = pv ? v : 0.f;
+        }
       }
     };
     __syncthreads();  // the previous graph's sVar / sBuf / sDn reads (first: sOut)
