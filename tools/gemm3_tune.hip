@@ -2,6 +2,7 @@
 // against an fp64 reference and the exact-f32 MFMA GEMM (sv2n_gemm_kernel.h), on the
 // C2 forward projection shapes.  Build:
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -Iinclude tools/gemm3_tune.hip -o build/gemm3_tune
+#include <cstring>
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
@@ -351,13 +352,14 @@ void run3g(const Shape& sh, hipStream_t st, const float* A, const unsigned short
   fflush(stdout);
 }
 
-int main() {
+int main(int argc, char** argv) {
   std::vector<Shape> shapes = {{"fwd L0", 15360, 408, 1260}, {"fwd L1", 15360, 208, 400},
                                {"dX L1", 15360, 400, 208}, {"C5 fwd L0", 262144, 144, 1024},
                                {"C5 fwd L1", 262144, 144, 128}};
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (auto& sh : shapes) {
+    if (argc > 1 && !strstr(argv[1], sh.name)) continue;  // e.g. "fwd L0|dX L1"
     const int64_t M = sh.M, N = sh.N, K = sh.K;
     const int64_t Kp = (K + 63) / 64 * 64;
     float *A, *B, *C;
@@ -414,12 +416,16 @@ int main() {
     // (second pass: STG 88.1 -> 98.8 us at C2 L0, slower on every shape);
     // third pass: 12- and 16-wave workgroups (3 / 4 waves per SIMD)
     // (third pass: profiles/r06_gemm3_waves.txt — <12, 1, 9> kept where it fills the chip)
+    // fourth pass: two row tiles per wave (MT = 2: half the B fragment reads
+    // per MFMA)
     for (int rep = 0; rep < 2; ++rep) {
-      run3b<8, 1, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-      run3b<8, 1, 9, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
       run3b<12, 1, 9, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
-      run3b<16, 1, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
       run3b<8, 1, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3b<8, 2, 7, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3b<12, 2, 5, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3b<8, 2, 5, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3b<4, 2, 13, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
+      run3b<8, 2, 4, 32, 2, true, 0, 1, true>(sh, st, A, Bp, Kp, C, ref, absr);
     }
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(S)); CK(hipFree(Bp));
   }

@@ -25,7 +25,7 @@ from collections import defaultdict
 # 5 added defaulted template parameters: k_gemm3d's B read distance, k_gemm_bw's
 # wave grid, which now appear in the names)
 KERNELS = {
-    "gemm_l0_fwd": "sv2n::k_gemm3d<8, 1, 13, 2, false, 1>",
+    "gemm_l0_fwd": "sv2n::k_gemm3d<12, 1, 9, 2, false, 1, false, false>",  # round 6: 12 waves
     "gemm_l0_dwT": "sv2n::k_gemm_tt3y<13, 2, false>",
     "edge_logits_fwd": "sv2n::k_edge_fwd_mx<16>",
     "edge_logits_bwd": "sv2n::k_edge_bwd_mx<16, 1>",
@@ -41,22 +41,22 @@ KERNELS = {
 }
 
 
-# C5 (tools/pmc_c5_traffic.sh): keys prefixed "c5:" in the same JSON
+# C5 (tools/measure.sh pmc): keys prefixed "c5:" in the same JSON
 KERNELS_C5 = {
     "gat_attn_fused_fwd_l0": "sv2n::fused::k_fattn_fwd<12, false, false>",
     "gat_attn_fused_bwd_l0": "sv2n::fused::k_fattn_bwd2<12, false, false>",
-    "gemm_l0_fwd": "sv2n::k_gemm3d<8, 1, 9, 2, false, 1>",
+    "gemm_l0_fwd": "sv2n::k_gemm3d<12, 1, 9, 2, false, 1, false, false>",
 }
 
-# C3 bf16 loop (tools/r4_pmc.sh): keys "c3_bf16:..."; a list sums its kernels
+# C3 bf16 loop (tools/measure.sh pmc): keys "c3_bf16:..."; a list sums its kernels
 # (the weight-gradient node is the GEMM and its epilogue launch)
 KERNELS_C3 = {
     "gemm_fwd": "sv2n::k_gemm_bw<256, 192, false, false, false, 2, 4>",  # a16: bf16 x twin
     "wgrad_node": ["sv2n::k_gemm_bw<128, 128, true, false, false, 2, 4>", "sv2n::k_wgrad_epi_t"],
     "gat_attn_fwd": "sv2n::canon::k_fwd<1, false, false, false>",
-    "gat_attn_bwd": "sv2n::canon::k_bwd<1, false, false, 1>",
+    "gat_attn_bwd": "sv2n::canon::k_bwd<1, false, false, 2>",
     "window_gather": "sv2n::k_window_rows",
-    "head_mse_train": "sv2n::k_head_mse_train_w<1, 8>",
+    "head_mse_train": "sv2n::k_head_mse_train_w<1, 8, true>",
 }
 
 
