@@ -51,8 +51,8 @@ KERNELS_C5 = {
 # C3 bf16 loop (tools/measure.sh pmc): keys "c3_bf16:..."; a list sums its kernels
 # (the weight-gradient node is the GEMM and its epilogue launch)
 KERNELS_C3 = {
-    "gemm_fwd": "sv2n::k_gemm_bw<256, 192, false, false, false, 2, 4>",  # a16: bf16 x twin
-    "wgrad_node": ["sv2n::k_gemm_bw<128, 128, true, false, false, 2, 4>", "sv2n::k_wgrad_epi_t"],
+    "gemm_fwd": "sv2n::k_gemm_bw<256, 192, false, false, false, 2, 4, 64>",  # a16: bf16 x twin
+    "wgrad_node": ["sv2n::k_gemm_bw<128, 128, true, false, false, 2, 4, 64>", "sv2n::k_wgrad_epi_t"],
     "gat_attn_fwd": "sv2n::canon::k_fwd<1, false, false, false>",
     "gat_attn_bwd": "sv2n::canon::k_bwd<1, false, false, 2>",
     "window_gather": "sv2n::k_window_rows",
