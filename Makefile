@@ -5,13 +5,15 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Wall -Wno-unused-result
 BUILD ?= build
+# EXTRA: extra compiler flags for diagnostic A/B builds (into their own BUILD / LIB)
+HIPFLAGS += $(EXTRA)
 LIB ?= spotv2net_amd/libsv2n.so
 ifeq ($(STAMPS),1)
 HIPFLAGS += -DSV2N_STAMPS   # diagnostic phase stamps (tools/stamps.py)
 endif
 # diagnostic bound checks (SV2N_CHK, sv2n_check_hits): make CHECK=1 builds
 # build_check/ -> spotv2net_amd/libsv2n_check.so; tests load it with
-# SV2N_LIB=spotv2net_amd/libsv2n_check.so (tools/r5_check.sh)
+# SV2N_LIB=spotv2net_amd/libsv2n_check.so (tools/measure.sh check)
 ifeq ($(CHECK),1)
 HIPFLAGS += -DSV2N_CHECK
 BUILD = build_check
