@@ -205,6 +205,16 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
   const uint32_t rmw = bld_u32(make_rsrc(rowmask ? rowmask + (int64_t)g * n : nullptr,
                                           rowmask ? (uint32_t)n * 4u : 0u), l32 * 4);
   const uint32_t rbits = (rowmask ? rmw : allm) & ~(1u << l32);
+  // HEAD: the output head's weights (OC <= 512: two per thread), staged into
+  // LDS at the head phase (their loads in the prologue, ahead of the xs
+  // operands: the head loops then read LDS instead of waiting on L2 per
+  // column)
+  float hw[2] = {0.f, 0.f};
+  if constexpr (HEAD) {
+    const rsrc_t rw = make_rsrc(hf.w, (uint32_t)OC * 4u);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) hw[k] = bld(rw, t + THREADS * k < OC ? (t + THREADS * k) * 4 : OOB);
+  }
   // B operands of the wave's first four work items (C2: all of them)
   float bq[4][16], bbq[4];
 #pragma unroll
@@ -390,7 +400,10 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     const int OC1 = OC + 1;
     float* sD = sY + 32 * OC1;  // dout per row
     float* sL = sD + 32;        // diff² per row
-    const rsrc_t rw = make_rsrc(hf.w, (uint32_t)OC * 4u);
+    float* sHw = sL + 32;       // the head weights [OC]
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (t + THREADS * k < OC) sHw[t + THREADS * k] = hw[k];
     // post-dropout factor of (row, oc): the forward's mask and scale
     auto mfac = [&](int row, int oc) {
       return post ? (bld(ru, (row * OC + oc) * 4) >= post_p ? post_scale : 0.f) : 1.f;
@@ -401,7 +414,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       float sacc = 0.f;
       if (row < n)
         for (int oc = sub; oc < OC; oc += 8)
-          sacc = fmaf(sY[row * OC1 + oc] * mfac(row, oc), bld(rw, oc * 4), sacc);
+          sacc = fmaf(sY[row * OC1 + oc] * mfac(row, oc), sHw[oc], sacc);
       sacc += __shfl_xor(sacc, 1, 64);
       sacc += __shfl_xor(sacc, 2, 64);
       sacc += __shfl_xor(sacc, 4, 64);
@@ -423,7 +436,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     for (int k = t; k < n * OC; k += THREADS) {
       const int row = k / OC, oc = k - row * OC;
       const float a = sY[row * OC1 + oc];
-      bst(rz, k * 4, act_bwd<ACT>(sD[row] * bld(rw, oc * 4) * mfac(row, oc), a));
+      bst(rz, k * 4, act_bwd<ACT>(sD[row] * sHw[oc] * mfac(row, oc), a));
     }
     // the graph's partials, rows summed in order (k_head_fuse_finish sums
     // them in graph order: round 4, summing them in this launch with two-level
@@ -1169,12 +1182,12 @@ void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, 
 #undef SV2N_CB
 }
 
-// HEAD: + the layer output [32][OC + 1] and two [32] row vectors
+// HEAD: + the layer output [32][OC + 1], two [32] row vectors and the head weights [OC]
 size_t attn_canon_fwd_lds(int n, int H, bool has_ae, bool edge_order, int head_oc) {
   const int nae = has_ae ? (edge_order ? n * (n - 1) : n * n) * H : 0;
   return sizeof(float) * ((size_t)H * 32 * canon::PS + 2 * (size_t)H * 32 +
                           (size_t)((nae + 3) & ~3) +
-                          (head_oc > 0 ? (size_t)32 * (head_oc + 1) + 64 : 0));
+                          (head_oc > 0 ? (size_t)32 * (head_oc + 1) + 64 + head_oc : 0));
 }
 
 // the output head fuses into the layer's forward when one workgroup runs each
