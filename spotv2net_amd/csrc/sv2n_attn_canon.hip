@@ -438,27 +438,39 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       const float a = sY[row * OC1 + oc];
       bst(rz, k * 4, act_bwd<ACT>(sD[row] * sHw[oc] * mfac(row, oc), a));
     }
-    // the graph's partials, rows summed in order (k_head_fuse_finish sums
-    // them in graph order: round 4, summing them in this launch with two-level
-    // tickets made the C2 layer-1 forward 31.4 us against 24.9 + 4.9 for the
-    // forward and the separate finish launch)
+    // the graph's partials (k_head_fuse_finish sums them in graph order:
+    // round 4, summing them in this launch with two-level tickets made the C2
+    // layer-1 forward 31.4 us against 24.9 + 4.9 for the forward and the
+    // separate finish launch).  Column oc by G consecutive lanes, lane sub
+    // summing rows sub, sub + G, ... in order, the G sums added in a fixed
+    // xor tree (round 6: one lane per column walked all n rows, a serial LDS
+    // chain of ~4 K cycles at the end of every workgroup)
     float* pg = hf.part + (int64_t)g * (OC + 2);
-    for (int oc = t; oc < OC; oc += THREADS) {
+    const int G = OC <= THREADS / 8 ? 8 : (OC <= THREADS / 4 ? 4 : (OC <= THREADS / 2 ? 2 : 1));
+    for (int oc0 = 0; oc0 < OC; oc0 += THREADS / G) {  // (uniform)
+      const int oc = oc0 + t / G, sub = t & (G - 1);
       float sacc = 0.f;
-      for (int row = 0; row < n; ++row)
-        sacc = fmaf(sD[row], sY[row * OC1 + oc] * mfac(row, oc), sacc);
-      SV2N_CHK(302, (int64_t)g * (OC + 2) + oc, B * (OC + 2));
-      pg[oc] = sacc;
-    }
-    if (t == THREADS - 1) {
-      float sd = 0.f, sl = 0.f;
-      for (int row = 0; row < n; ++row) {
-        sd += sD[row];
-        sl += sL[row];
+      if (oc < OC)
+        for (int row = sub; row < n; row += G)
+          sacc = fmaf(sD[row], sY[row * OC1 + oc] * mfac(row, oc), sacc);
+      for (int m = 1; m < G; m <<= 1) sacc += __shfl_xor(sacc, m, 64);
+      if (sub == 0 && oc < OC) {
+        SV2N_CHK(302, (int64_t)g * (OC + 2) + oc, B * (OC + 2));
+        pg[oc] = sacc;
       }
-      SV2N_CHK(303, (int64_t)g * (OC + 2) + OC + 1, B * (OC + 2));
-      pg[OC] = sd;
-      pg[OC + 1] = sl;
+    }
+    if (wave == THREADS / 64 - 1) {  // Σ dout, Σ diff² over the rows: the last wave, a xor tree
+      float sd = lane < n ? sD[lane] : 0.f, sl = lane < n ? sL[lane] : 0.f;
+#pragma unroll
+      for (int m = 1; m < 32; m <<= 1) {
+        sd += __shfl_xor(sd, m, 64);
+        sl += __shfl_xor(sl, m, 64);
+      }
+      if (lane == 0) {
+        SV2N_CHK(303, (int64_t)g * (OC + 2) + OC + 1, B * (OC + 2));
+        pg[OC] = sd;
+        pg[OC + 1] = sl;
+      }
     }
   }
   SV2N_STAMP(5, SV2N_T());
