@@ -431,6 +431,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       }
     }
     __syncthreads();
+    SV2N_STAMP(7, SV2N_T());
     // dZ in y's place (coalesced rows)
     const rsrc_t rz = make_rsrc(y + (int64_t)g * n * OC, (uint32_t)(n * OC) * 4u);
     for (int k = t; k < n * OC; k += THREADS) {
@@ -438,6 +439,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
       const float a = sY[row * OC1 + oc];
       bst(rz, k * 4, act_bwd<ACT>(sD[row] * sHw[oc] * mfac(row, oc), a));
     }
+    SV2N_STAMP(8, SV2N_T());
     // the graph's partials (k_head_fuse_finish sums them in graph order:
     // round 4, summing them in this launch with two-level tickets made the C2
     // layer-1 forward 31.4 us against 24.9 + 4.9 for the forward and the

@@ -1,7 +1,7 @@
 """Phase timeline of the canonical attention kernels (diagnostic build).
 
 Build:  make STAMPS=1 LIB=spotv2net_amd/libsv2n_stamps.so BUILD=build/stamps
-Run:    SV2N_LIB=spotv2net_amd/libsv2n_stamps.so python tools/stamps.py [B | c3]
+Run:    SV2N_LIB=spotv2net_amd/libsv2n_stamps.so python tools/stamps.py [B | c3 | l1]
 
 Launches the C2 layer-0 attention forward and backward once each (after a
 warm-up) through the C-ABI and prints, per phase, the median and max over
@@ -133,8 +133,44 @@ def main(B=512):
             (10, 11, "barrier"), (11, 12, "d ae + tail")], 0, 13)
 
 
+def main_l1(B=512):
+    """The C2 model's last layer with the output head + MSE fused in
+    (k_fwd<HEAD>): phases up to the aggregation, then the head's output /
+    residual, the dZ stores and the per-graph partials."""
+    dev = torch.device("cuda", 0)
+    cfg = bench.CONFIGS["c2"]
+    model = bench.build_model(dev, cfg)
+    lib = ops._lib.load()
+    lib.sv2n_diag_stamps.restype = ctypes.c_int
+    lib.sv2n_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    n, H = bench.N_NODES, bench.HEADS
+    conv1 = model.gat_layers[1]
+    C, ldx = conv1.out_channels, (H * conv1.out_channels + 2 * H + 3) // 4 * 4
+    torch.manual_seed(0)
+    N = B * n
+    xs = torch.randn(N, ldx, device=dev) * 0.1
+    ae = torch.randn(B * n * (n - 1), H, device=dev)
+    tgt = torch.randn(N, device=dev)
+    gw = torch.zeros_like(model.linear.weight)
+    gb = torch.zeros_like(model.linear.bias)
+
+    def fwd():
+        torch.ops.sv2n.gat_attn_fwd_head_mse(
+            xs, ae, None, conv1.bias, None, 1.0, None, 0.0, model.linear.weight.view(-1),
+            model.linear.bias, tgt, gw, gb, B, n, H, C, bool(conv1.concat), 1, 0.2, True)
+
+    for _ in range(5):
+        fwd()
+    fwd()
+    report("fwd L1 + head + MSE", read(lib, B),
+           [(1, 2, "prologue loads -> AE staged"), (2, 3, "softmax"), (3, 4, "barrier"),
+            (4, 7, "aggregation + head output"), (7, 8, "dZ stores"), (8, 5, "partials")], 0, 6)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "c3":
+    if len(sys.argv) > 1 and sys.argv[1] == "l1":
+        main_l1()
+    elif len(sys.argv) > 1 and sys.argv[1] == "c3":
         main_c3()
     else:
         main(int(sys.argv[1]) if len(sys.argv) > 1 else 512)
