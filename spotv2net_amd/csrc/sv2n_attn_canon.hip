@@ -257,21 +257,36 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     for (int k4 = 0; k4 < 4; ++k4) as4[k4] = asr[k4];
     float lg[16];
     float esum = 0.f;
+    // the 16 edge logits of the lane's sources: every LDS address first, then
+    // the 16 reads back to back and one wait.  Uniform choices (logits present,
+    // edge order) are masks, not conditions: as conditions inside the loop
+    // the compiler branched on them per source and waited lgkmcnt(0) after
+    // each read — a serial chain of 16 LDS round trips (round 6).
+    float av16[16];
+    {
+      const int j0 = 16 * half;
+      const int eom = ae_edge_order ? -1 : 0;           // edge order vs dense [n][n]
+      const uint32_t aem = ae ? 0xffffffffu : 0u;       // no logits: every source reads 0
+      const uint32_t evb = iv ? (rbits & aem) : 0u;     // sources with a logit to read
+      int elo = ((j0 * (2 * n - 1 - j0)) >> 1) - j0 - 1 + i;  // e(i, j) for j < i, j = j0
+      int idx[16];
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const int j = j0 + kk;
+        const int e_c = j < i ? elo : Ehi + j;
+        const int e = (e_c & eom) | ((i * n + j) & ~eom);
+        // masked by an AND (as a select the compiler branched around the multiply)
+        idx[kk] = (__mul24(e, H) + h) & -(int)((evb >> j) & 1u);
+        elo += n - 2 - j;  // T(j + 1) - T(j) - 1
+      }
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) av16[kk] = sAE[idx[kk]];
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) av16[kk] = ((evb >> (j0 + kk)) & 1u) ? av16[kk] : 0.f;
+    }
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
-      const int j = 16 * half + kk;
-      float a = 0.f;
-      if (ae) {
-        const bool ev = iv && ((rbits >> j) & 1u);
-        // both canonical branches computed, then selected (as a ternary over
-        // the multiply the compiler branched per source under exec masks)
-        const int e_lo = ((j * (2 * n - 1 - j)) >> 1) - j - 1 + i;
-        const int e_hi = Ehi + j;
-        const int e_c = j < i ? e_lo : e_hi;
-        const int e = ae_edge_order ? e_c : i * n + j;
-        const float v = sAE[ev ? e * H + h : 0];
-        a = ev ? v : 0.f;
-      }
+      const float a = av16[kk];
       esum += a;
       lg[kk] = as4[kk >> 2][kk & 3] + ad + a;
     }

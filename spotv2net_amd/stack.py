@@ -203,7 +203,31 @@ def _overlap_edge(training: bool) -> bool:
     """Run the edge-logit pass on a side stream beside the layer-0 projection
     GEMM: inference only (MI355X, C2 B = 512: forward 2.18-2.19 M -> 2.24-2.26
     M graphs/s; in the training step 0.5485 vs 0.5473 ms, within noise)."""
+    if FWD_OVERLAP != "auto":
+        return FWD_OVERLAP == "on"
     return not training
+
+
+# "on": the backward runs the work off its critical path on a side stream —
+# the weight gradients of layers l > 0 beside layer l's dX GEMM and layer
+# l-1's attention backward, and the edge-logit gradient pass (+ its fold)
+# beside layer 0's weight gradient — joined before the node returns (inside a
+# captured step the fork/join becomes graph edges); "off": one stream;
+# "auto" (default): the bf16 mode only.  MI355X, round 6
+# (`profiles/r06_bwd_overlap_ab.txt`): C3 (bf16, B = 128) 465 -> 474 K
+# windows/s; C2 (f32, B = 512) 1,133-1,140 -> 1,112-1,121 K graphs/s — each
+# cross-stream dependency of the replayed graph leaves the GPU idle 5-10 us,
+# and the concurrent GEMMs slow each other (L1 dX 26 -> 44 us beside L1 dW).
+BWD_OVERLAP = os.environ.get("SV2N_BWD_OVERLAP", "auto")
+# "auto": the forward's edge pass beside the layer-0 projection in inference
+# only (_overlap_edge); "on" / "off": always / never (A/B switch)
+FWD_OVERLAP = os.environ.get("SV2N_FWD_OVERLAP", "auto")
+
+
+def _overlap_bwd(dev, bf16: bool) -> bool:
+    if dev.type != "cuda" or BWD_OVERLAP == "off":
+        return False
+    return BWD_OVERLAP == "on" or bf16
 
 
 _SIDE = {}
@@ -542,6 +566,58 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
     edge_tail = bool(need_edge and not fused and not layout.tiled and eo and not meta.cv and
                      _edge_tail_ok(layout, convs, ea, hp))
     LAST_PATH["edge_tail"] = edge_tail
+
+    def edge_grads():
+        # every layer's edge-logit weight gradient, then the edge folds
+        nonlocal dwf
+        if not (use_edge and ea is not None):
+            return
+        # grads exist (zeros) even without edges, as in PyG
+        need_e = [(grad_of(c.lin_edge.weight), grad_of(c.att_edge)) for c in convs]
+        if ea.size(0) > 0 and any(a is not None or b is not None for a, b in need_e):
+            ei = layout.edge_index if layout.kind == "block" else None
+            if meta.cv and COV_VAR_BWD == "on":
+                dwf = ops.edge_logits_bwd_cv(ea, layout.canon, daes, H, B, n, hp)
+            elif not fused and not edge_tail:
+                dwf = ops.edge_logits_bwd(ea, ei, layout.canon, daes, H, B, n, hp,
+                                          layout.tiled)
+            if all(a is not None and b is not None for a, b in need_e):
+                # every layer's edge-fold backward in one launch
+                ops.prep_bwd_edge_all(dwf, [l * H for l in range(L)],
+                                      [c.lin_edge.weight for c in convs],
+                                      [c.att_edge for c in convs], [c.heads for c in convs],
+                                      [c.out_channels for c in convs],
+                                      [a for a, _ in need_e], [b for _, b in need_e])
+            else:
+                for l, c in enumerate(convs):
+                    gWe, gae = need_e[l]
+                    ops.prep_bwd_edge(dwf, l * H, c.lin_edge.weight, c.att_edge, c.heads,
+                                      c.out_channels, gWe, gae)
+
+    # work off the critical path (BWD_OVERLAP) goes to a side stream: it waits
+    # for everything the main stream queued so far, the tensors it reads stay
+    # referenced until the join at the end (so the caching allocator cannot
+    # hand their memory to a main-stream allocation while the side stream
+    # still reads them), and the gradient buffers it writes are only read
+    # after the join
+    side = _side_stream(dev) if _overlap_bwd(dev, meta.bf16) else None
+    main = torch.cuda.current_stream(dev) if side is not None else None
+    held = []
+    edge_forked = False
+
+    def on_side(fn, *reads):
+        side.wait_stream(main)
+        held.extend(t for t in reads if t is not None)
+        with torch.cuda.stream(side):
+            fn()
+
+    def fork_edge():
+        # after layer 0's attention backward every d-logit plane exists
+        nonlocal edge_forked
+        if side is not None and not edge_forked:
+            edge_forked = True
+            on_side(edge_grads, ea, dwf, *daes)
+
     for l in range(L - 1, -1, -1):
         c = convs[l]
         Hc, C = c.heads, c.out_channels
@@ -569,6 +645,7 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
                 B, n, Hc, C, c.concat, act_l, float(c.negative_slope), eo, post_u,
                 meta.post_p[l] or 0.0)
             daes[l] = _opt(dae)
+            fork_edge()
             ops.gat_wgrad_bf16b(xb0, dxb, c.lin_src.weight, c.att_src, c.att_dst, dbp, Hc, C,
                                 grad_of(c.lin_src.weight), grad_of(c.att_src),
                                 grad_of(c.att_dst), grad_of(c.bias))
@@ -585,6 +662,8 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
                 B, n, Hc, C, c.concat, act_l, float(c.negative_slope), eo, post_u,
                 meta.post_p[l] or 0.0)
         daes[l] = _opt(dae)
+        if l == 0:
+            fork_edge()
         gW = grad_of(c.lin_src.weight)
         gas = grad_of(c.att_src)
         gad = grad_of(c.att_dst)
@@ -592,8 +671,15 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
         if any(g is not None for g in (gW, gas, gad, gb)):
             # split-K dWaugᵀ GEMM + one fused epilogue (fold, transpose,
             # att and bias grads), accumulated into the gradient buffers
-            ops.gat_wgrad(xs_in[l], dxs, c.lin_src.weight, c.att_src, c.att_dst, dbp, Hc, C,
-                          meta.bf16, gW, gas, gad, gb)
+            def wgrad(l=l, c=c, dxs=dxs, dbp=dbp, gW=gW, gas=gas, gad=gad, gb=gb):
+                ops.gat_wgrad(xs_in[l], dxs, c.lin_src.weight, c.att_src, c.att_dst, dbp, Hc,
+                              C, meta.bf16, gW, gas, gad, gb)
+            if side is not None and l > 0:
+                # off the critical path: layer l's dX GEMM and layer l-1's
+                # attention backward run beside it
+                on_side(wgrad, xs_in[l], dxs, dbp)
+            else:
+                wgrad()
         act_l = act
         if l > 0 or need_x0:
             # dxs · Waug; ahead of a ReLU layer on the n <= 32 path the GEMM
@@ -605,28 +691,11 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
                 relu_y, act_l = ys[l - 1], 0
             dy = ops.project(dxs, _opt(planes_t[l]), waugs[l], True, meta.bf16, relu_y)
 
-    if use_edge and ea is not None:
-        # grads exist (zeros) even without edges, as in PyG
-        need_e = [(grad_of(c.lin_edge.weight), grad_of(c.att_edge)) for c in convs]
-        if ea.size(0) > 0 and any(a is not None or b is not None for a, b in need_e):
-            ei = layout.edge_index if layout.kind == "block" else None
-            if meta.cv and COV_VAR_BWD == "on":
-                dwf = ops.edge_logits_bwd_cv(ea, layout.canon, daes, H, B, n, hp)
-            elif not fused and not edge_tail:
-                dwf = ops.edge_logits_bwd(ea, ei, layout.canon, daes, H, B, n, hp,
-                                          layout.tiled)
-            if all(a is not None and b is not None for a, b in need_e):
-                # every layer's edge-fold backward in one launch
-                ops.prep_bwd_edge_all(dwf, [l * H for l in range(L)],
-                                      [c.lin_edge.weight for c in convs],
-                                      [c.att_edge for c in convs], [c.heads for c in convs],
-                                      [c.out_channels for c in convs],
-                                      [a for a, _ in need_e], [b for _, b in need_e])
-            else:
-                for l, c in enumerate(convs):
-                    gWe, gae = need_e[l]
-                    ops.prep_bwd_edge(dwf, l * H, c.lin_edge.weight, c.att_edge, c.heads,
-                                      c.out_channels, gWe, gae)
+    if not edge_forked:
+        edge_grads()
+    if side is not None:
+        main.wait_stream(side)  # the join: gradients complete on the main stream
+        held.clear()
     return dy if need_x0 else None
 
 
