@@ -252,10 +252,10 @@ extern "C" int sv2n_gemm_f32x3(const float* A, int64_t lda, const uint16_t* Bp, 
   const bool t144 = (N + 143) / 144 * 144 < (N + 207) / 208 * 208 && mb * ((N + 143) / 144) >= 240;
   if (K % 4 == 0) {
     if (twelve_waves(M, N))
-      return launch_gemm3d<12, 1, 9, SV2N_GEMM_AP>(stream, A, lda, B, Kp, N, C, ldc, M, K);
-    if (t144) return launch_gemm3d<8, 1, 9, SV2N_GEMM_AP>(stream, A, lda, B, Kp, N, C, ldc, M, K);
-    if (wide) return launch_gemm3d<8, 1, 13, SV2N_GEMM_AP>(stream, A, lda, B, Kp, N, C, ldc, M, K);
-    return launch_gemm3d<8, 1, 7, SV2N_GEMM_AP>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+      return launch_gemm3d<12, 1, 9, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+    if (t144) return launch_gemm3d<8, 1, 9, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+    if (wide) return launch_gemm3d<8, 1, 13, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
+    return launch_gemm3d<8, 1, 7, 2>(stream, A, lda, B, Kp, N, C, ldc, M, K);
   }
   if (t144)
     return longk ? launch_gemm3<8, 1, 9, 64>(stream, A, lda, B, Kp, N, C, ldc, M, K)
@@ -283,10 +283,10 @@ extern "C" int sv2n_gemm_f32x3_relu(const float* A, int64_t lda, const uint16_t*
   const bool wide = mb * ((N + 207) / 208) >= 240;
   const bool t144 = (N + 143) / 144 * 144 < (N + 207) / 208 * 208 && mb * ((N + 143) / 144) >= 240;
   if (twelve_waves(M, N))
-    return launch_gemm3d<12, 1, 9, SV2N_GEMM_AP, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
+    return launch_gemm3d<12, 1, 9, 2, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
   if (t144)
-    return launch_gemm3d<8, 1, 9, SV2N_GEMM_AP, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
+    return launch_gemm3d<8, 1, 9, 2, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
   if (wide)
-    return launch_gemm3d<8, 1, 13, SV2N_GEMM_AP, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
-  return launch_gemm3d<8, 1, 7, SV2N_GEMM_AP, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
+    return launch_gemm3d<8, 1, 13, 2, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
+  return launch_gemm3d<8, 1, 7, 2, true>(stream, A, lda, B, Kp, N, C, ldc, M, K, Y, ldy);
 }

@@ -27,24 +27,6 @@
 #include <utility>
 #include "sv2n_common.h"
 
-// 1: k_gemm3d keeps the next step's A split inside the MFMA block (see the
-// pin in its step); 0: as the compiler places it (A/B builds)
-#ifndef SV2N_GEMM_PIN
-#define SV2N_GEMM_PIN 1
-#endif
-// k_gemm3d: A register sets in flight (the loads for step s+AP issue at the
-// end of step s) and whether the next step's split sits under the first (0)
-// or the last (1) column tiles of the step
-#ifndef SV2N_GEMM_AP
-#define SV2N_GEMM_AP 2
-#endif
-#ifndef SV2N_GEMM_SPLIT_LATE
-#define SV2N_GEMM_SPLIT_LATE 0
-#endif
-#ifndef SV2N_GEMM_ALOAD_UNCOND
-#define SV2N_GEMM_ALOAD_UNCOND 1
-#endif
-
 namespace sv2n {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
@@ -944,25 +926,6 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
       }
   }
   const int nk = (int)((K + BK - 1) / BK);
-#if SV2N_GEMM_ALOAD_UNCOND
-  // the loads left in flight at the loop entry in the order of the steady
-  // state at the top of step s — A(s+1 .. s+AP-2), B(s+1), A(s+AP-1) — so the
-  // wait-count pass sees the same queue on the entry and the back edge (a
-  // different order made it wait vmcnt(0) at the loop head, i.e. for the A
-  // loads issued just before)
-  load_a(0, 0);
-#pragma unroll
-  for (int sv = 0; sv < BV; ++sv) load_b1(sv, 0);
-#pragma unroll
-  for (int sv = 0; sv < BV; ++sv) store_b1(sv, lds);
-#pragma unroll
-  for (int pr = 0; pr < NPAIR; ++pr) split_pair(afc, ra[0], pr);
-#pragma unroll
-  for (int s = 1; s + 1 < AP; ++s) load_a(s, (int64_t)s * BK);
-#pragma unroll
-  for (int sv = 0; sv < BV; ++sv) load_b1(sv, (int64_t)min(1, nk - 1) * BK);
-  load_a(AP - 1, (int64_t)(AP - 1) * BK);
-#else
 #pragma unroll
   for (int s = 0; s < AP; ++s)
     if (s < nk) load_a(s, (int64_t)s * BK);
@@ -975,7 +938,6 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
     for (int sv = 0; sv < BV; ++sv) load_b1(sv, BK);
 #pragma unroll
   for (int pr = 0; pr < NPAIR; ++pr) split_pair(afc, ra[0], pr);
-#endif
   __syncthreads();
   if constexpr (MASK) {  // the mask lives in registers from here (no sinking into the epilogue)
 #pragma unroll
@@ -1024,10 +986,9 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
         for (int sv = 0; sv < BV; ++sv) load_b1(sv, kb2);
         __builtin_amdgcn_sched_group_barrier(0x020, BV, 0);
       }
-      constexpr int bs = SV2N_GEMM_SPLIT_LATE ? b - (NT - (NPAIR + PPT - 1) / PPT) : b;
-      if constexpr (bs >= 0 && bs * PPT < NPAIR) {
+      if constexpr (b * PPT < NPAIR) {
         static_for<PPT>([&](auto pc) __attribute__((always_inline)) {
-          constexpr int pr = bs * PPT + decltype(pc)::value;
+          constexpr int pr = b * PPT + decltype(pc)::value;
           if constexpr (pr < NPAIR) split_pair(afn, ra[nset], pr);
         });
         __builtin_amdgcn_sched_group_barrier(0x002, 11 * PPT, 0);
@@ -1039,28 +1000,11 @@ __global__ __launch_bounds__(64 * NW) void k_gemm3d(const float* __restrict__ A,
         if (wave >= NW / 2) __syncthreads();  // the second half's barrier: mid-step
       }
     });
-#if SV2N_GEMM_PIN
-    // pin the next step's split planes here, inside the MFMA block: without
-    // this use the compiler sank the split (only consumed next step) past
-    // the MFMAs and the barrier, into one VALU-only block per step in which
-    // all waves of a SIMD stood idle on the matrix pipe at once
-#pragma unroll
-    for (int a = 0; a < MT; ++a)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(afn[a][p]));
-#endif
 #pragma unroll
     for (int a = 0; a < MT; ++a)
 #pragma unroll
       for (int p = 0; p < 3; ++p) afc[a][p] = afn[a][p];
-#if SV2N_GEMM_ALOAD_UNCOND
-    // unconditional: past K every offset is OOB (0, no traffic).  Under a
-    // branch the wait-count pass merged the paths pessimistically and the
-    // next step's B staging waited vmcnt(0) — for these A loads too
-    load_a(set, (int64_t)(s + AP) * BK);
-#else
     if (s + AP < nk) load_a(set, (int64_t)(s + AP) * BK);
-#endif
     if constexpr (STG) {
       if (wave < NW / 2) __syncthreads();
     } else {
