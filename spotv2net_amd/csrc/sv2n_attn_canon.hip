@@ -13,16 +13,20 @@
 //      e(i, j) = T(j) + i - j - 1              (j < i: the upper pair (j, i))
 //              = P + T(i) + j - i - 1          (j > i: the swapped pair),
 //    T(x) = x(2n - x - 1)/2, P = n(n - 1)/2;
-//  * lane (i, half) of a wave owns target row i and sources 16·half .. +15:
-//    its 16 probabilities are the A operand of the 16 steps of
-//    v_mfma_f32_32x32x2f32 (step kk pairs source kk with source 16 + kk), read
-//    back from LDS with four ds_read_b128 by whichever wave aggregates the head;
+//  * lane (i, half) of a wave owns target row i and sources 16·half .. +15 in
+//    the softmax; it writes their three bf16 planes (round 6; f32-accurate
+//    bf16x3, as the projection GEMMs) to LDS, from where whichever wave
+//    aggregates the head reads the A operand of v_mfma_f32_32x32x16_bf16
+//    (two K steps of 16 sources, six products each; the backward still
+//    aggregates on exact-f32 v_mfma_f32_32x32x2f32);
 //  * the xs / dy / y operands are read straight from HBM in the MFMA operand
 //    layouts (dword buffer loads, 128 B per half-wave, the row stride in a
 //    scalar offset register), ahead of the MFMAs that use them.
 #include "sv2n_common.h"
 
 #include <cstdlib>
+
+#include "sv2n_gemm3_kernel.h"  // split3_pk, bf16x8, u32x4_t
 
 namespace sv2n {
 namespace canon {
@@ -50,6 +54,44 @@ constexpr int PS = SV2N_PSTR;  // LDS row stride of a probability row (floats)
 constexpr int AEV = 8;         // 16-B slots per thread covering E0·H <= 992·8
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// Forward aggregation P·xs: 1 = f32-accurate bf16x3 on v_mfma_f32_32x32x16_bf16
+// (P and xs split into three bf16 planes, the six products with plane orders
+// p + q <= 2, as the projection GEMMs: 12 MFMAs of 32 cycles per 32 x 32
+// tile); 0 = exact f32 on v_mfma_f32_32x32x2f32 (16 MFMAs of 64 cycles)
+#ifndef SV2N_AGG_X3
+#define SV2N_AGG_X3 1
+#endif
+constexpr int PBR = 40;  // bf16 row stride of a probability plane row (80 B: distinct b128 bank slots)
+// floats of the probability area sP of the forward: f32 rows, or three bf16 planes
+__host__ __device__ constexpr int sp_floats(int H) {
+  return SV2N_AGG_X3 ? 3 * H * 32 * PBR / 2 : H * 32 * PS;
+}
+// the six bf16x3 products of one 32 x 32 x 16 step (small terms first)
+__device__ __forceinline__ floatx16 mfma32_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3],
+                                              floatx16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+// eight floats -> their three bf16 planes (split3_pk pairs, low half first)
+__device__ __forceinline__ void split8_x3(const float* v, bf16x8 (&h)[3]) {
+  u32x4_t w0, w1, w2;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    unsigned a, b, c;
+    split3_pk(v[2 * q], v[2 * q + 1], a, b, c);
+    w0[q] = a;
+    w1[q] = b;
+    w2[q] = c;
+  }
+  h[0] = __builtin_bit_cast(bf16x8, w0);
+  h[1] = __builtin_bit_cast(bf16x8, w1);
+  h[2] = __builtin_bit_cast(bf16x8, w2);
+}
 
 // row of accumulator register r in lane half hf (32x32 MFMA C/D layout)
 __device__ __forceinline__ int crow(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
@@ -80,7 +122,8 @@ __device__ __forceinline__ void bst_s(rsrc_t r, int voff, int soff, float v) {
 // computes the whole softmax (cheap) and aggregates its share of the work
 // items.  Block b -> graph 8·(b / 8S) + b % 8, split (b / 8) % S: the splits of
 // a graph run on one XCD (they share its logits and xs rows through L2).
-// LDS: sP[H][32][PS] (dropped-out probabilities, the MFMA A operand) |
+// LDS: sP (dropped-out probabilities, the MFMA A operand: three bf16 planes
+//      [3][H][32][PBR], or f32 [H][32][PS] without SV2N_AGG_X3) |
 //      sAS[H][32] a_src | sAD[H][32] a_dst | sAE[E0·H]
 // Work items of wave slot u = 4s + w (after the softmax): concat — (head h,
 // 32-column tile tc) pairs u, u + 4S, ...; mean — tiles tc = u, u + 4S, ...,
@@ -112,8 +155,10 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     float post_p, float post_scale, float* __restrict__ post_out, int n, int H, int C, float slope,
     int S, int64_t B, HeadFuse hf) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sP = smem;
-  float* sAS = sP + H * 32 * PS;
+  float* sP = smem;  // SV2N_AGG_X3: three bf16 planes [3][H][32][PBR]
+  unsigned short* sPb = reinterpret_cast<unsigned short*>(smem);
+  const int PL = H * 32 * PBR;  // bf16 plane stride
+  float* sAS = sP + sp_floats(H);
   float* sAD = sAS + H * 32;
   float* sAE = sAD + H * 32;
 
@@ -165,11 +210,21 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     item(q, h, tc);
     const int c = 32 * tc + l32;
     const bool ok = c < C && q < nq;
-    const int voff = ok ? ((16 * half) * ldx + h * C + c) * 4 : OOB;
     bb = bld(rb, ok ? ((CONCAT ? h * C : 0) + c) * 4 : OOB);
+#if SV2N_AGG_X3
+    // element e: source 16·(e / 8) + 8·half + e % 8 (K step e / 8 of the
+    // 32x32x16 B operand)
+    const int voff = ok ? ((8 * half) * ldx + h * C + c) * 4 : OOB;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+      b[kk] = (SV2N_ATTN_ABL & 2) ? (float)(kk + voff) * 1e-3f
+                                  : bld_s(rx, voff, (16 * (kk >> 3) + (kk & 7)) * ldx * 4);
+#else
+    const int voff = ok ? ((16 * half) * ldx + h * C + c) * 4 : OOB;
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk)
       b[kk] = (SV2N_ATTN_ABL & 2) ? (float)(kk + voff) * 1e-3f : bld_s(rx, voff, kk * ldx * 4);
+#endif
   };
 
   // ---- prologue: every load before any store ----
@@ -321,10 +376,9 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
     }
     den += __shfl_xor(den, 32, 64);
     const float inv = 1.f / (den + 1e-16f);
-    float* prow = sP + (h * 32 + i) * PS + 16 * half;
+    float pdv[16];
 #pragma unroll
     for (int k4 = 0; k4 < 4; ++k4) {
-      f32x4 pd;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int kk = 4 * k4 + c;
@@ -333,10 +387,28 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
         pkeep[s2][kk] = valid ? (((negm >> kk) & 1u) ? -p : p) : 0.f;
         float d = p;
         if constexpr (KEEP) d = ((kw[k4] >> (8 * c)) & 0xffu) ? d * keep_scale : 0.f;
-        pd[c] = d;
+        pdv[kk] = d;
       }
-      *reinterpret_cast<f32x4*>(prow + 4 * k4) = pd;
     }
+#if SV2N_AGG_X3
+    {  // row i, sources 16·half .. +15 of each plane: two 16-B pieces per plane
+      unsigned short* prow = sPb + (h * 32 + i) * PBR + 16 * half;
+#pragma unroll
+      for (int k8 = 0; k8 < 2; ++k8) {
+        bf16x8 pl[3];
+        split8_x3(pdv + 8 * k8, pl);
+#pragma unroll
+        for (int pp = 0; pp < 3; ++pp)
+          *reinterpret_cast<bf16x8*>(prow + pp * PL + 8 * k8) = pl[pp];
+      }
+    }
+#else
+    float* prow = sP + (h * 32 + i) * PS + 16 * half;
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4)
+      *reinterpret_cast<f32x4*>(prow + 4 * k4) =
+          f32x4{pdv[4 * k4], pdv[4 * k4 + 1], pdv[4 * k4 + 2], pdv[4 * k4 + 3]};
+#endif
   }
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
@@ -370,6 +442,20 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 #pragma unroll
       for (int r = 0; r < 16; ++r) uv[r] = bld_s(ru, voff, ((r & 3) + 8 * (r >> 2)) * OC * 4);
     }
+#if SV2N_AGG_X3
+    {  // K steps s = 0, 1 (sources 16s .. 16s + 15): lane (i, half) holds 8·half .. +7
+      const unsigned short* pa = sPb + (h * 32 + l32) * PBR + 8 * half;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 a3[3], b3[3];
+#pragma unroll
+        for (int pp = 0; pp < 3; ++pp)
+          a3[pp] = *reinterpret_cast<const bf16x8*>(pa + pp * PL + 16 * ks);
+        split8_x3(b + 8 * ks, b3);
+        acc = mfma32_x3(a3, b3, acc);
+      }
+    }
+#else
     const f32x4* pa = reinterpret_cast<const f32x4*>(sP + (h * 32 + l32) * PS + 16 * half);
     f32x4 a4[4];
 #pragma unroll
@@ -377,6 +463,7 @@ __global__ __launch_bounds__(THREADS) void k_fwd(
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[kk >> 2][kk & 3], b[kk], acc, 0, 0, 0);
+#endif
     if (CONCAT || h == H - 1) {  // end of the work item: bias, activation, store
       const int c = 32 * tc + l32;
       const int oc = (CONCAT ? h * C : 0) + c;
@@ -1214,7 +1301,7 @@ void attn_canon_bwd(int64_t B, hipStream_t st, const float* dy, const float* y, 
 // HEAD: + the layer output [32][OC + 1], two [32] row vectors and the head weights [OC]
 size_t attn_canon_fwd_lds(int n, int H, bool has_ae, bool edge_order, int head_oc) {
   const int nae = has_ae ? (edge_order ? n * (n - 1) : n * n) * H : 0;
-  return sizeof(float) * ((size_t)H * 32 * canon::PS + 2 * (size_t)H * 32 +
+  return sizeof(float) * ((size_t)canon::sp_floats(H) + 2 * (size_t)H * 32 +
                           (size_t)((nae + 3) & ~3) +
                           (head_oc > 0 ? (size_t)32 * (head_oc + 1) + 64 + head_oc : 0));
 }
@@ -1223,7 +1310,9 @@ size_t attn_canon_fwd_lds(int n, int H, bool has_ae, bool edge_order, int head_o
 // graph (its rows and columns all in one place) and the layer output fits LDS
 bool attn_canon_head_ok(int64_t B, int n, int H, int C, bool concat) {
   const int OC = concat ? H * C : C;
-  return n >= 1 && n <= 32 && canon_fwd_splits(B, H, C, concat) == 1 && OC <= 512;
+  // LDS with the layer output, for the larger (dense [n][n]) logit block
+  return n >= 1 && n <= 32 && canon_fwd_splits(B, H, C, concat) == 1 && OC <= 512 &&
+         attn_canon_fwd_lds(n, H, true, false, OC) <= 160 * 1024;
 }
 
 template <int ACT, bool CONCAT, bool KEEP, bool HEAD>
