@@ -192,7 +192,11 @@ def ptr(t: torch.Tensor | None) -> int | None:
 
 
 def stream_handle(device: torch.device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    """The raw hipStream_t of the device's current stream (torch's own accessor:
+    under torch.compile a resumed frame can see current_stream() as a generic
+    torch.Stream without .cuda_stream)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return torch._C._cuda_getCurrentRawStream(idx)
 
 
 def ptr_array(ptrs) -> ctypes.Array:

@@ -227,6 +227,8 @@ FWD_OVERLAP = os.environ.get("SV2N_FWD_OVERLAP", "auto")
 def _overlap_bwd(dev, bf16: bool) -> bool:
     if dev.type != "cuda" or BWD_OVERLAP == "off":
         return False
+    if torch.compiler.is_compiling():  # streams stay out of traced graphs
+        return False
     return BWD_OVERLAP == "on" or bf16
 
 

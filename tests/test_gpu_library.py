@@ -106,15 +106,18 @@ def test_opcheck_backward_ops(dev):
                           test_utils=UTILS)
 
 
-def test_torch_compile_matches_eager(dev):
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_torch_compile_matches_eager(dev, precision):
     """torch.compile(GATModel) (inductor) on a batch whose layout is attached:
     the sv2n ops appear in the traced graph as custom ops (no graph break
-    inside the GAT stack) and the forward / gradients equal eager."""
+    inside the GAT stack) and the forward / gradients equal eager.  bf16: the
+    eager backward runs on two streams (stack.BWD_OVERLAP), the traced one
+    on one."""
     import copy
 
     from spotv2net_amd import GATModel
     torch.manual_seed(2)
-    m1 = GATModel(60, 6, 2, 1, [8, 4], concat_heads=True).to(dev)
+    m1 = GATModel(60, 6, 2, 1, [8, 4], concat_heads=True).to(dev).set_precision(precision)
     m2 = copy.deepcopy(m1)
     d = _small(dev)
     torch._dynamo.reset()

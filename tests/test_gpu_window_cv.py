@@ -100,3 +100,37 @@ def test_other_edge_paths_refuse_a_cv_batch(dev, monkeypatch):
     with pytest.raises(RuntimeError, match="BatchNorm"):
         ms(part)
     m(part)  # the covariance-layout path takes it
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 17])
+def test_cv_batch_small_graphs_bitwise_full_batch(dev, n):
+    """Graph sizes whose last 16-pair tile reaches past the upper rows by
+    more than the lower rows (n = 2, 3, 5: pad > P) or by a partial tile
+    (n = 17): the columns the cv-only gather leaves NaN are never read —
+    forward and every gradient equal the full gather's bit for bit."""
+    from spotv2net_amd import GATModel, WindowDataset
+    from spotv2net_amd.data import synthetic_series
+    from spotv2net_amd.stack import cov_var_edges_only
+    V, W = synthetic_series(60 + S, n, seed=7)
+    ds = WindowDataset(V.to(dev), W.to(dev), S)
+    B = 12
+    idx = torch.arange(B, device=dev) * 4
+    full = ds.empty_batch(B)
+    ds.fill(full, idx)
+    part = ds.empty_batch(B, cov_var_only=True)
+    part.edge_attr.fill_(math.nan)
+    ds.fill(part, idx)
+    torch.manual_seed(11)
+    m = GATModel(n * S, 3 * S, 4, 1, [16, 8], concat_heads=True).to(dev)
+    assert cov_var_edges_only(list(m.gat_layers), n, S)
+    outs, grads = [], []
+    for b in (full, part):
+        m.zero_grad(set_to_none=True)
+        out = m(b)
+        (out ** 2).mean().backward()
+        outs.append(out.detach())
+        grads.append([p.grad.clone() for p in m.parameters()])
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
+    for (name, _), g0, g1 in zip(m.named_parameters(), *grads):
+        assert torch.equal(g0, g1), name
