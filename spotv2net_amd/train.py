@@ -83,22 +83,29 @@ def _host_staged(t: torch.Tensor, group) -> bool:
     return t.is_cuda and dist.get_backend(group) == "gloo"
 
 
-def allreduce_mean_(flat: torch.Tensor, group=None) -> None:
-    """Average a flat gradient buffer across the data-parallel group in place:
-    ONE all-reduce (RCCL over xGMI with the nccl backend; through a host copy
-    with gloo)."""
+def allreduce_sum_(flat: torch.Tensor, group=None) -> int:
+    """Sum a flat gradient buffer across the data-parallel group in place: ONE
+    all-reduce (RCCL over xGMI with the nccl backend; through a host copy with
+    gloo).  Returns the world size (1: nothing done)."""
     if not (dist.is_available() and dist.is_initialized()):
-        return
+        return 1
     ws = dist.get_world_size(group)
     if ws == 1:
-        return
+        return 1
     if _host_staged(flat, group):
         host = flat.cpu()
         dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
         flat.copy_(host)
     else:
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
-    flat.div_(ws)
+    return ws
+
+
+def allreduce_mean_(flat: torch.Tensor, group=None) -> None:
+    """Average a flat gradient buffer across the data-parallel group in place."""
+    ws = allreduce_sum_(flat, group)
+    if ws > 1:
+        flat.div_(ws)
 
 
 def broadcast_params_(module: torch.nn.Module, src: int = 0, group=None) -> None:
@@ -329,8 +336,12 @@ class TrainStep:
             sh.g_fb = torch.cuda.CUDAGraph()
             with torch.cuda.graph(sh.g_fb):
                 self._fwd_bwd(sh)
+            # the ÷ world size of the all-reduced sum rides in the optimizer
+            # graph (no eager launch between the collective and the replay)
+            ws = dist.get_world_size(self.group)
             sh.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(sh.g_opt):
+                self.flat.div_(ws)
                 self._opt_step()
         else:
             sh.g_fb = torch.cuda.CUDAGraph()
@@ -348,7 +359,7 @@ class TrainStep:
             return self.loss
         sh.g_fb.replay()
         if self.distributed:
-            allreduce_mean_(self.flat, self.group)
+            allreduce_sum_(self.flat, self.group)  # the mean's ÷ is inside g_opt
             sh.g_opt.replay()
         self.loss = sh.loss
         return self.loss
