@@ -62,6 +62,10 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 #ifndef SV2N_AGG_X3
 #define SV2N_AGG_X3 1
 #endif
+// backward: G = xs·dZᵀ (the softmax's dP) on bf16x3 as well (1) or exact f32 (0)
+#ifndef SV2N_BWD_G_X3
+#define SV2N_BWD_G_X3 1
+#endif
 constexpr int PBR = 40;  // bf16 row stride of a probability plane row (80 B: distinct b128 bank slots)
 // floats of the probability area sP of the forward: f32 rows, or three bf16 planes
 __host__ __device__ constexpr int sp_floats(int H) {
@@ -1011,7 +1015,29 @@ __global__ __launch_bounds__(THREADS) void k_bwd(
       }
       // G[j][i] += Σ_c xs[j][c] · dZ[i][c]    (step kk pairs columns kk and 16 + kk;
       // the chunk's columns past cw are staged zeros)
-      {
+      if constexpr (SV2N_BWD_G_X3 && ACT == ACT_ID && DEPTH <= 2) {
+        // bf16x3: K steps of 16 columns, lane (row, half) holds columns 16s +
+        // 8·half .. +7.  Identity-activation, two-chunk instances only: with
+        // the activation's operands live the extra planes cost the C3 kernel
+        // its second workgroup per CU, and at three chunks in flight (C2 L0)
+        // it measured no faster (27.6 -> 27.8-28.0 us; C2 L1 19.8-20.2 ->
+        // 18.7-18.9 us, profiles/r06_attn_bwd_g_bf16x3.txt)
+        const float* xr = sX + l32 * CS + 8 * half;
+        const float* zr = sZ + l32 * CS + 8 * half;
+#pragma unroll 1
+        for (int ks = 0; ks < 2; ++ks) {
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr + 16 * ks);
+          const f32x4 x1 = *reinterpret_cast<const f32x4*>(xr + 16 * ks + 4);
+          const f32x4 z0 = *reinterpret_cast<const f32x4*>(zr + 16 * ks);
+          const f32x4 z1 = *reinterpret_cast<const f32x4*>(zr + 16 * ks + 4);
+          const float xv[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+          const float zv[8] = {z0[0], z0[1], z0[2], z0[3], z1[0], z1[1], z1[2], z1[3]};
+          bf16x8 a3[3], b3[3];
+          split8_x3(xv, a3);
+          split8_x3(zv, b3);
+          G = mfma32_x3(a3, b3, G);
+        }
+      } else {
         const f32x4* xa = reinterpret_cast<const f32x4*>(sX + l32 * CS + 16 * half);
         const f32x4* zb = reinterpret_cast<const f32x4*>(sZ + l32 * CS + 16 * half);
         f32x4 a4[4], b4[4];
