@@ -16,6 +16,11 @@
 #   tools/measure.sh c3trace OUT                 kernel trace + stats of the C3 bf16 loop
 #   tools/measure.sh close   OUT                 tests, c2, step and configs in one call
 #
+# Same-box A/B of library builds (a build of the same sources with a -D switch,
+# loaded through SV2N_LIB; round 6): tools/ab_step.sh OUT lib... (traced C2
+# step per build), tools/ab_c3.sh (C3 line per build, C3LIBS="..."),
+# tools/ab_run.sh OUT lib... (C2 bench line per build).
+#
 # Every GPU step has its own time limit and the steps are chained: the first
 # failure ends the call (no retries on the box).
 set -o pipefail
