@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define SV2N_ABI_VERSION 20
+#define SV2N_ABI_VERSION 21
 #define SV2N_MAX_LAYERS 8   /* layers folded into one edge pass            */
 #define SV2N_MAX_N 32       /* nodes per graph on the one-workgroup-per-graph
                                attention path (sv2n_gat_attn_fwd/bwd)      */
@@ -670,8 +670,10 @@ int sv2n_window_gather_diag(const float* vol, const float* volvol, const float* 
  * past n·seq_length; NaN rows for windows outside the series) — the bf16
  * execution mode's projection operand (sv2n_gemm_bf16_a16) and its weight
  * gradient's (sv2n_gat_wgrad_node_bf16b) straight from the data builder
- * (ABI 15).  Row-kernel shapes only (n·seq_length % 4 == 0, 3·S·(n+1) floats
- * of LDS <= 64 KiB, future_steps <= 256); else SV2N_ERR_SHAPE. */
+ * (ABI 15).  x may be NULL (ABI 21): only the twin is written, for a
+ * consumer that reads x through it alone.  Row-kernel shapes only
+ * (n·seq_length % 4 == 0, 3·S·(n+1) floats of LDS <= 64 KiB, future_steps
+ * <= 256); else SV2N_ERR_SHAPE. */
 int sv2n_window_gather_bf16x(const float* vol, const float* volvol, const float* diag, int n,
                              int64_t num_matrices, const int64_t* starts, int64_t start_offset,
                              int64_t num_windows, int seq_length, int future_steps,
@@ -687,7 +689,8 @@ int sv2n_window_gather_bf16x(const float* vol, const float* volvol, const float*
  * (the even-S passes' last tile of 16 upper rows runs into them with zero
  * d-logits): what those passes read (≈ 1/6 of the edge bytes).  The rest of edge_attr
  * is left as it was; any other reader of it is the caller's error.  Windows
- * outside the series give NaN rows as in sv2n_window_gather_diag.  Row-kernel
+ * outside the series give NaN rows as in sv2n_window_gather_diag.  x may be
+ * NULL when x_bf16 is not (ABI 21, as sv2n_window_gather_bf16x).  Row-kernel
  * shapes only (see sv2n_window_gather_bf16x); else SV2N_ERR_SHAPE. */
 int sv2n_window_gather_cv(const float* vol, const float* volvol, const float* diag, int n,
                           int64_t num_matrices, const int64_t* starts, int64_t start_offset,

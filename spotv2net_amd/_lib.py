@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SV2N_LIB: an alternative build of the same library (diagnostic builds, e.g.
 # tools/stamps.py); default the in-tree one
 LIB_PATH = os.environ.get("SV2N_LIB") or os.path.join(_HERE, "libsv2n.so")
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 _c_f = ctypes.POINTER(ctypes.c_float)
 _p = ctypes.c_void_p

@@ -19,6 +19,10 @@
 // error that needs no host round trip; the op stays capturable).
 #include "sv2n_common.h"
 
+#ifndef SV2N_WINDOW_XCD
+#define SV2N_WINDOW_XCD 1
+#endif
+
 namespace sv2n {
 
 __global__ __launch_bounds__(256) void k_window_gather(
@@ -95,8 +99,19 @@ __global__ __launch_bounds__(256) void k_window_rows(
   float* sv = lds;             // [S][NP] vol[t][u][v]
   float* sw = sv + S * NP;     // [S][NP] volvol[t][u][v]
   float* sd = sw + S * NP;     // [S][NP] volvol[t][v][v]
-  const int u = blockIdx.x % n;
-  const int64_t b = blockIdx.x / n;
+#if SV2N_WINDOW_XCD
+  // XCD-aware order: blocks are dealt round-robin over the 8 XCDs, so block i
+  // takes the (i % 8)-th contiguous eighth of the (window, node) range — a
+  // window's n node blocks share one XCD's L2, and the series lines their rows
+  // share (row u and u+1 of a matrix meet inside one 128-B line; the diagonal
+  // every block reads) are fetched into one L2 instead of up to eight
+  const int G = gridDim.x, gq = G >> 3, gr = G & 7, gi = blockIdx.x & 7;
+  const int wb = gi * gq + min(gi, gr) + (blockIdx.x >> 3);
+#else
+  const int wb = blockIdx.x;
+#endif
+  const int u = wb % n;
+  const int64_t b = wb / n;
   const int t = threadIdx.x;
   const int64_t nn = (int64_t)n * n;
   const int64_t st = starts[b] < 0 ? -1 : starts[b] + soff;  // a negative index is out of range
@@ -104,8 +119,10 @@ __global__ __launch_bounds__(256) void k_window_rows(
   if (st < 0 || st + S + F > T) {  // window outside the series: NaN rows, no reads
     const float qnan = __builtin_nanf("");
     if (t < F) y[(b * n + u) * F + t] = qnan;
-    float* xr = x + (b * n + u) * (int64_t)n * S;
-    for (int j = t; j < n * S; j += 256) xr[j] = qnan;
+    if (x) {
+      float* xr = x + (b * n + u) * (int64_t)n * S;
+      for (int j = t; j < n * S; j += 256) xr[j] = qnan;
+    }
     if (xb)
       for (int j = t; j < ldxb; j += 256)
         xb[(b * n + u) * ldxb + j] = j < n * S ? (unsigned short)0x7fc0 : (unsigned short)0;
@@ -144,7 +161,8 @@ __global__ __launch_bounds__(256) void k_window_rows(
   if (t < F) y[(b * n + u) * F + t] = vol[(st + S + t) * nn + (int64_t)u * n + u];
   __syncthreads();
   // x[b*n+u][c*S + tt] = vol[tt][u][c]: 16-B stores when the row allows
-  float* xr = x + (b * n + u) * (int64_t)n * S;
+  // (x NULL with xb: only the bf16 twin, ABI 21)
+  float* xr = x ? x + (b * n + u) * (int64_t)n * S : nullptr;
   const int nxr = n * S;
   if ((nxr & 3) == 0 && (((uintptr_t)xr) & 15) == 0) {
     unsigned short* xbr = xb ? xb + (b * n + u) * ldxb : nullptr;
@@ -155,7 +173,7 @@ __global__ __launch_bounds__(256) void k_window_rows(
         const int j = 4 * j4 + k, c = j / S, tt = j - c * S;
         v[k] = sv[tt * NP + c];
       }
-      *reinterpret_cast<f32x4*>(xr + 4 * j4) = v;
+      if (xr) *reinterpret_cast<f32x4*>(xr + 4 * j4) = v;
       if (xbr) {  // bf16(x) beside it (round to nearest even, as the GEMMs' staging)
         typedef __bf16 b4 __attribute__((ext_vector_type(4)));
         *reinterpret_cast<b4*>(xbr + 4 * j4) = __builtin_convertvector(v, b4);
@@ -266,7 +284,7 @@ extern "C" int sv2n_window_gather_bf16x(const float* vol, const float* volvol,
                                         const uint16_t* canon, float* x, uint16_t* x_bf16,
                                         int64_t ld_xb, float* edge_attr, float* y,
                                         hipStream_t stream) {
-  if (!vol || !volvol || !starts || !canon || !x || !x_bf16 || !edge_attr || !y)
+  if (!vol || !volvol || !starts || !canon || !x_bf16 || !edge_attr || !y)
     return SV2N_ERR_ARG;
   if (n < 2 || n > SV2N_MAX_N_TILED || num_windows < 1 || seq_length < 1 || future_steps < 1 ||
       num_matrices < 1)
@@ -289,7 +307,8 @@ extern "C" int sv2n_window_gather_cv(const float* vol, const float* volvol, cons
                                      int future_steps, const uint16_t* canon, float* x,
                                      uint16_t* x_bf16, int64_t ld_xb, float* edge_attr, float* y,
                                      hipStream_t stream) {
-  if (!vol || !volvol || !starts || !canon || !x || !edge_attr || !y) return SV2N_ERR_ARG;
+  if (!vol || !volvol || !starts || !canon || (!x && !x_bf16) || !edge_attr || !y)
+    return SV2N_ERR_ARG;
   if (n < 2 || n > SV2N_MAX_N_TILED || num_windows < 1 || seq_length < 1 || future_steps < 1 ||
       num_matrices < 1)
     return SV2N_ERR_SHAPE;

@@ -63,6 +63,12 @@ class Data:
         return f"{self.__class__.__name__}({', '.join(parts)})"
 
 
+def twin_only_x(data) -> bool:
+    """Whether ``data.x`` is a ``WindowDataset.empty_batch(twin_only=True)``
+    buffer: NaN, never written by ``fill`` — x exists only as its bf16 twin."""
+    return bool(getattr(getattr(data, "x", None), "_sv2n_twin_only", False))
+
+
 def bf16_twin(data) -> Optional[torch.Tensor]:
     """bf16(data.x) [N][K rounded up to 64] when the batch carries one written
     together with x (``WindowDataset.empty_batch(bf16_x=True)``) and x is
@@ -250,7 +256,7 @@ class WindowDataset:
             if volvol.dtype == torch.float32 else None
 
     def empty_batch(self, batch_size: int, bf16_x: bool = False,
-                    cov_var_only: bool = False) -> Batch:
+                    cov_var_only: bool = False, twin_only: bool = False) -> Batch:
         """Static device buffers of one batch of ``batch_size`` windows (the
         layout of ``batch``), for ``fill``: a hipGraph-captured train step
         reads the same tensors every replay.  ``bf16_x``: ``fill`` also
@@ -261,7 +267,12 @@ class WindowDataset:
         (sv2n_window_gather_cv, ≈ 1/6 of its bytes) — for a consumer that
         reads it through those passes alone (``train.Fit`` when
         ``stack.cov_var_edges_only`` says so); any other edge path refuses the
-        batch (``layout.check_full_edge_attr``)."""
+        batch (``layout.check_full_edge_attr``).  ``twin_only`` (with
+        ``bf16_x``): ``fill`` writes only the bf16 twin; x stays NaN and is
+        marked (``twin_only_x``) — for a consumer whose layer-0 GEMMs read the
+        twin alone (``train.Fit`` when ``stack.twin_only_ok`` says so; the
+        stack refuses the batch on any path that would read x).  Ignored when
+        no twin is made."""
         B, n, S = batch_size, self.n, self.S
         E0 = n * (n - 1)
         dev = self.vol.device
@@ -277,6 +288,9 @@ class WindowDataset:
             if window_bf16x_supported(n, S, self.future_steps):
                 b._x_bf16 = torch.zeros(B * n, (n * S + 63) // 64 * 64, device=dev,
                                         dtype=torch.bfloat16)
+                if twin_only:
+                    b.x.fill_(float("nan"))
+                    b.x._sv2n_twin_only = True
                 b._x_bf16_of = (b.x.data_ptr(), b.x._version)
         if cov_var_only and dev.type == "cuda" and self.vol.dtype == torch.float32 and \
                 self.volvol.dtype == torch.float32 and 3 * S * (n + 1) * 4 <= 64 * 1024 and \
@@ -308,7 +322,7 @@ class WindowDataset:
                                          idx if idx.dtype == torch.long else idx.long(), S, Fs,
                                          canonical_table(n, self.vol.device), out.x,
                                          out.edge_attr, out.y_x, self.cut, self.diag, xb,
-                                         cv_only)
+                                         cv_only, xb is not None and twin_only_x(out))
             mark_cov_var(out.edge_attr, S)
             if cv_only:
                 mark_cov_var_only(out.edge_attr)

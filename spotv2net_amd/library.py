@@ -121,7 +121,7 @@ _SCHEMAS = {
     "window_gather": "(Tensor vol, Tensor volvol, Tensor starts, int seq_length, "
                      "int future_steps, Tensor canon, Tensor(a!) x, Tensor(b!) edge_attr, "
                      "Tensor(c!) y, int start_offset=0, Tensor? diag=None, "
-                     "Tensor(d!)? x_bf16=None, bool cov_var_only=False) -> ()",
+                     "Tensor(d!)? x_bf16=None, bool cov_var_only=False, bool skip_x=False) -> ()",
     "project_a16": "(Tensor a_bf16, int k, Tensor planes, Tensor w) -> Tensor",
 }
 for _name, _schema in _SCHEMAS.items():
@@ -1178,10 +1178,13 @@ def _adam_step_fake(param, grad, exp_avg, exp_avg_sq, step, ticket, lr, beta1, b
 
 @_impl("window_gather")
 def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y,
-                   start_offset=0, diag=None, x_bf16=None, cov_var_only=False):
+                   start_offset=0, diag=None, x_bf16=None, cov_var_only=False, skip_x=False):
     """``cov_var_only``: of edge_attr only what the covariance-layout edge
     passes read (sv2n_window_gather_cv); the caller vouches that nothing
-    else reads it (data.WindowDataset.empty_batch(cov_var_only=True))."""
+    else reads it (data.WindowDataset.empty_batch(cov_var_only=True)).
+    ``skip_x``: only the bf16 twin of x is written (x left as it was; ABI
+    21), for a batch whose x is read through the twin alone
+    (data.WindowDataset.empty_batch(twin_only=True))."""
     lib = _lib.load()
     _f32(vol, volvol, x, edge_attr, y)
     _need(vol.is_contiguous() and volvol.is_contiguous(), "series must be contiguous")
@@ -1197,6 +1200,8 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
     if diag is not None:  # the series' diagonal, diag[t][v] = volvol[t][v][v]
         _f32(diag)
         _need(diag.is_contiguous() and diag.shape == vol.shape[:2], "diag must be [T][n]")
+    _need(not skip_x or x_bf16 is not None, "skip_x needs x_bf16")
+    x_ptr = 0 if skip_x else x.data_ptr()
     if x_bf16 is not None:  # bf16(x) beside x (sv2n_window_gather_bf16x)
         _need(x_bf16.dtype == torch.bfloat16 and x_bf16.dim() == 2 and
               x_bf16.shape[0] == x.shape[0] and x_bf16.stride(1) == 1, "x_bf16 layout")
@@ -1204,7 +1209,7 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
         _lib.check(lib.sv2n_window_gather_cv(
             vol.data_ptr(), volvol.data_ptr(), _p(diag), vol.shape[1], vol.shape[0],
             starts.data_ptr(), start_offset, starts.numel(), seq_length, future_steps,
-            canon.data_ptr(), x.data_ptr(), _p(x_bf16),
+            canon.data_ptr(), x_ptr, _p(x_bf16),
             0 if x_bf16 is None else x_bf16.stride(0), edge_attr.data_ptr(), y.data_ptr(),
             _st(vol)), "sv2n_window_gather_cv")
         return
@@ -1212,7 +1217,7 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
         _lib.check(lib.sv2n_window_gather_bf16x(
             vol.data_ptr(), volvol.data_ptr(), _p(diag), vol.shape[1], vol.shape[0],
             starts.data_ptr(), start_offset, starts.numel(), seq_length, future_steps,
-            canon.data_ptr(), x.data_ptr(), x_bf16.data_ptr(), x_bf16.stride(0),
+            canon.data_ptr(), x_ptr, x_bf16.data_ptr(), x_bf16.stride(0),
             edge_attr.data_ptr(), y.data_ptr(), _st(vol)), "sv2n_window_gather_bf16x")
         return
     _lib.check(lib.sv2n_window_gather_diag(vol.data_ptr(), volvol.data_ptr(), _p(diag),
@@ -1225,7 +1230,8 @@ def _window_gather(vol, volvol, starts, seq_length, future_steps, canon, x, edge
 
 @_fake("window_gather")
 def _window_gather_fake(vol, volvol, starts, seq_length, future_steps, canon, x, edge_attr, y,
-                        start_offset=0, diag=None, x_bf16=None, cov_var_only=False):
+                        start_offset=0, diag=None, x_bf16=None, cov_var_only=False,
+                        skip_x=False):
     return None
 
 

@@ -28,7 +28,7 @@ from torch import nn
 
 from . import graphed, ops
 from .conv import GATConv
-from .data import bf16_twin
+from .data import bf16_twin, twin_only_x
 from .layout import GraphLayout, analyze_edge_index, check_full_edge_attr, declare_canonical
 from .stack import gat_stack, gat_train_head_mse, head_mse_loss, linear_head
 
@@ -126,6 +126,9 @@ class GATModel(nn.Module):
     def _hidden(self, data, layout: Optional[GraphLayout] = None) -> torch.Tensor:
         x, edge_index, edge_attr = data.x, data.edge_index, data.edge_attr
         if self.standardize:
+            if twin_only_x(data):
+                raise RuntimeError("GATModel's node BatchNorm (standardize) reads x, which this "
+                                   "batch holds only as its bf16 twin (empty_batch(twin_only=True))")
             x = self.bnorm_node(x)
             if edge_attr is not None:
                 check_full_edge_attr(edge_attr, "GATModel's edge BatchNorm (standardize)")

@@ -431,7 +431,12 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
             aes = [None] * L
 
     # 3) layers
+    # x of a twin-only batch (data.twin_only_x) is NaN: only the bf16 twin may
+    # be read, by the layer-0 projection and weight-gradient GEMMs
+    twin_only = bool(getattr(x, "_sv2n_twin_only", False))
     xin = _aligned(x)
+    if twin_only:
+        xin._sv2n_twin_only = True
     xb0 = None  # bf16(x) of layer 0 (bf16 mode, x without grad)
     saved_x, saved_xs, saved_y, saved_p, saved_keep, saved_drop = [], [], [], [], [], []
     saved_st = []
@@ -452,6 +457,9 @@ def stack_forward(x, edge_attr, convs, layout: GraphLayout, act: int, post_dropo
             # bf16 mode: the projection also leaves bf16(x) for the layer's
             # weight-gradient GEMM (sv2n_gemm_bf16_export)
             xs, xb0 = ops.project_bf16_export(xin, planes[l], waugs[l])
+        elif l == 0 and twin_only:
+            raise RuntimeError(_TWIN_ONLY_MSG.format("layer 0's projection (no bf16-twin GEMM "
+                                                     "for this model / batch)"))
         else:
             xs = ops.project(xin, planes[l], waugs[l], False, bf16)  # x · Waugᵀ
         if overlap is not None:
@@ -665,6 +673,8 @@ def stack_backward(saved, meta: _StackMeta, convs, layout: GraphLayout, dout, ne
                 meta.post_p[l] or 0.0)
         daes[l] = _opt(dae)
         if l == 0:
+            if getattr(xs_in[0], "_sv2n_twin_only", False):
+                raise RuntimeError(_TWIN_ONLY_MSG.format("layer 0's weight gradient (fp32 x)"))
             fork_edge()
         gW = grad_of(c.lin_src.weight)
         gas = grad_of(c.att_src)
@@ -731,6 +741,23 @@ def _a16_ok(x_bf16: torch.Tensor, xin: torch.Tensor, planes) -> bool:
             and x_bf16.shape[0] == xin.shape[0] and x_bf16.shape[1] >= xin.shape[1]
             and x_bf16.stride(1) == 1 and x_bf16.stride(0) % 8 == 0
             and x_bf16.data_ptr() % 16 == 0 and xin.shape[0] >= 1024 and planes.shape[-2] >= 384)
+
+
+_TWIN_ONLY_MSG = ("{} reads x, which this batch holds only as its bf16 twin "
+                  "(data.WindowDataset.empty_batch(twin_only=True))")
+
+
+def twin_only_ok(convs, rows: int) -> bool:
+    """Whether layer 0 of this stack reads a ``rows``-node bf16 batch's x
+    only through its bf16 twin (``_a16_ok``'s shape conditions, the bf16
+    operand path on, a weight that trains): ``train.Fit`` then has the
+    gather write the twin alone (data.WindowDataset.empty_batch(twin_only=True)).
+    The stack re-checks on the tensors and refuses a twin-only batch on any
+    other path."""
+    from .library import _ldx
+    c = convs[0]
+    return (BF16_OPERANDS == "on" and rows >= 1024 and _ldx(c.heads, c.out_channels) >= 384
+            and c.lin_src.weight.requires_grad)
 
 
 def _bf16_export_ok(bf16: bool, want: bool, xin: torch.Tensor, conv, other_path: bool) -> bool:

@@ -419,6 +419,9 @@ class ForwardStep:
 # device-memory budget of one captured test forward (Fit.eval_chunk): C3's
 # 432 test windows (~2 MB each) stay one forward
 EVAL_BYTES = int(os.environ.get("SV2N_EVAL_BYTES", 1 << 30))
+# "off": Fit's bf16 batches keep x written beside its bf16 twin (A/B switch)
+TWIN_ONLY = os.environ.get("SV2N_TWIN_ONLY", "on")
+
 
 class Fit:
     """5_train_SpotV2Net.py's loop over a device-resident WindowDataset:
@@ -454,6 +457,7 @@ class Fit:
         from .stack import cov_var_edges_only
         self._cv_only = bool(not getattr(model, "standardize", False) and
                              cov_var_edges_only(list(model.gat_layers), dataset.n, dataset.S))
+        self._bf16 = getattr(model, "precision", None) == "bf16"
         sizes = [self.bs] if self.n_train >= self.bs else []
         if self.n_train % self.bs:
             sizes.append(self.n_train % self.bs)
@@ -482,11 +486,20 @@ class Fit:
             self._idx[b] = torch.zeros(b, dtype=torch.long, device=self.dev)
             # the bf16 mode's layer-0 GEMMs read bf16(x) from the gather
             self._batch[b] = self.ds.empty_batch(
-                b, bf16_x=getattr(self.model, "precision", None) == "bf16",
-                cov_var_only=self._cv_only)
+                b, bf16_x=self._bf16, cov_var_only=self._cv_only, twin_only=self._twin_only(b))
             self.ds.fill(self._batch[b], self._idx[b])
         data, idx = self._batch[b], self._idx[b]
         return data, (lambda: self.ds.fill(data, idx))
+
+    def _twin_only(self, b: int) -> bool:
+        """Whether a ``b``-window batch's x is gathered as its bf16 twin alone
+        (data.WindowDataset.empty_batch(twin_only=True)): the bf16 mode, the
+        covariance-layout edge passes (a canonical batch on the unfused
+        attention) and a layer 0 that reads x only through the twin
+        (stack.twin_only_ok); SV2N_TWIN_ONLY=off keeps x written."""
+        from .stack import twin_only_ok
+        return bool(TWIN_ONLY == "on" and self._bf16 and self._cv_only and
+                    twin_only_ok(list(self.model.gat_layers), b * self.ds.n))
 
     def _window_bytes(self) -> int:
         """Device bytes one test window costs in the captured test forward:
@@ -527,8 +540,8 @@ class Fit:
                 # its index buffer every step)
                 idx = all_idx[:size].clone()
                 data = self.ds.empty_batch(
-                    size, bf16_x=getattr(self.model, "precision", None) == "bf16",
-                    cov_var_only=self._cv_only)
+                    size, bf16_x=self._bf16, cov_var_only=self._cv_only,
+                    twin_only=self._twin_only(size))
                 self.ds.fill(data, idx)
                 rows = data.x.shape[0] // size  # nodes per window
                 tot = self._tot_test

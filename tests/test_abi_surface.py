@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     for name in names:
         assert hasattr(lib, name), f"libsv2n.so lacks {name}"
     assert set(names) == set(_lib.EXPORTED_SYMBOLS), "ctypes table and header disagree"
-    assert lib.sv2n_abi_version() == _lib.ABI_VERSION == 20
+    assert lib.sv2n_abi_version() == _lib.ABI_VERSION == 21
     assert b"invalid argument" in lib.sv2n_strerror(-1)
 
 
