@@ -139,16 +139,22 @@ __global__ __launch_bounds__(256) void k_window_rows(
     int dst[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const int k = min(k0 + t + 256 * r, S * n - 1);
+      // past the end: no load at all (the lanes' requests, not clamped
+      // duplicates — at C3's S·n = 1260 three of the eight rounds are empty)
+      const int k = k0 + t + 256 * r;
       const int tt = k / n, v = k - tt * n;
       const int64_t base = (st + tt) * nn;
       dst[r] = tt * NP + v;
-      a[r] = vol[base + (int64_t)u * n + v];
-      w[r] = volvol[base + (int64_t)u * n + v];
-      // the diagonal is only read for the pairs (u, w > u); from the series'
-      // diagonal [T][n] when given (ABI 11: one line per matrix instead of
-      // one per element)
-      d[r] = v > u ? (diag ? diag[(st + tt) * n + v] : volvol[base + (int64_t)v * n + v]) : 0.f;
+      a[r] = w[r] = d[r] = 0.f;
+      if (k < S * n) {
+        a[r] = vol[base + (int64_t)u * n + v];
+        w[r] = volvol[base + (int64_t)u * n + v];
+        // the diagonal is only read for the pairs (u, w > u) — and of the
+        // covariance-only edge rows only by node 0; from the series' diagonal
+        // [T][n] when given (ABI 11: one line per matrix, not one per element)
+        if (v > u && (!cv_only || u == 0))
+          d[r] = diag ? diag[(st + tt) * n + v] : volvol[base + (int64_t)v * n + v];
+      }
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r)
